@@ -1,0 +1,149 @@
+"""Build the native modules in-tree.
+
+* ``_sphx_cpu``  — OpenMP reference path, compiled with g++ (same libgomp as PyTorch).
+* ``_sphx_hip``  — gfx950 kernels + host launchers, compiled with hipcc ``--offload-arch=gfx950``.
+* ``_sphx_io``   — H5Part-compatible HDF5 reader/writer linked against the image's serial libhdf5.
+
+Outputs land in ``sphexa_amd/_native/`` so they travel with the repository snapshot to the GPU box.
+Builds are incremental (object files are rebuilt only when a source or header is newer).
+"""
+
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+OUT = os.path.join(PKG, "_native")
+OBJ = os.path.join(OUT, "obj")
+EXT = sysconfig.get_config_var("EXT_SUFFIX")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HDF5_ROOT = os.environ.get("SPHX_HDF5_ROOT", "/opt/conda")
+ARCH = os.environ.get("SPHX_OFFLOAD_ARCH", "gfx950")
+
+
+def _py_includes():
+    import pybind11
+
+    return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, "include", "sphx", "*.hpp")) + glob.glob(os.path.join(CSRC, "*", "*.hpp"))
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def _compile_all(jobs, verbose):
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+        futs = {ex.submit(_run, cmd): out for cmd, out in jobs}
+        for f in cf.as_completed(futs):
+            f.result()
+            if verbose:
+                print(f"  built {os.path.basename(futs[f])}", flush=True)
+
+
+def _cpu_march():
+    try:
+        with open("/proc/cpuinfo") as f:
+            flags = f.read()
+        if " avx2 " in flags and " fma " in flags:
+            return ["-march=x86-64-v3"]
+    except OSError:
+        pass
+    return []
+
+
+def build_cpu(verbose=False):
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "cpu", "*.cpp")))
+    target = os.path.join(OUT, "_sphx_cpu" + EXT)
+    flags = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", f"-I{os.path.join(CSRC, 'include')}",
+             f"-I{os.path.join(CSRC, 'cpu')}"] + _cpu_march() + _py_includes()
+    hdrs = _headers()
+    jobs, objs = [], []
+    for s in srcs:
+        o = os.path.join(OBJ, "cpu_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if _newer(o, [s] + hdrs):
+            jobs.append((["g++", *flags, "-c", s, "-o", o], o))
+    _compile_all(jobs, verbose)
+    if jobs or _newer(target, objs):
+        _run(["g++", "-shared", "-fopenmp", *objs, "-o", target])
+    return target
+
+
+def build_hip(verbose=False):
+    os.makedirs(OBJ, exist_ok=True)
+    hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+    srcs = sorted(glob.glob(os.path.join(CSRC, "hip", "*.hip")) + glob.glob(os.path.join(CSRC, "hip", "*.cpp")))
+    target = os.path.join(OUT, "_sphx_hip" + EXT)
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             f"-I{os.path.join(CSRC, 'include')}", f"-I{os.path.join(CSRC, 'hip')}"] + _py_includes()
+    hdrs = _headers() + glob.glob(os.path.join(CSRC, "hip", "*.h"))
+    jobs, objs = [], []
+    for s in srcs:
+        o = os.path.join(OBJ, "hip_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if _newer(o, [s] + hdrs):
+            lang = ["-x", "hip"] if s.endswith(".hip") else []
+            jobs.append(([hipcc, *flags, *lang, "-c", s, "-o", o], o))
+    _compile_all(jobs, verbose)
+    if jobs or _newer(target, objs):
+        _run([hipcc, "-shared", f"--offload-arch={ARCH}", *objs, "-o", target,
+              f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"])
+    return target
+
+
+def build_io(verbose=False):
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "io", "*.cpp")))
+    if not srcs or not os.path.exists(os.path.join(HDF5_ROOT, "include", "hdf5.h")):
+        return None
+    target = os.path.join(OUT, "_sphx_io" + EXT)
+    flags = ["-O2", "-std=c++17", "-fPIC", f"-I{HDF5_ROOT}/include", f"-I{os.path.join(CSRC, 'include')}"] + \
+        _py_includes()
+    jobs, objs = [], []
+    for s in srcs:
+        o = os.path.join(OBJ, "io_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if _newer(o, [s] + _headers()):
+            jobs.append((["g++", *flags, "-c", s, "-o", o], o))
+    _compile_all(jobs, verbose)
+    if jobs or _newer(target, objs):
+        # link libhdf5 by full path with an rpath so that the conda lib directory is not put in front of the
+        # system libraries for everything else in the process
+        _run(["g++", "-shared", *objs, "-o", target, os.path.join(HDF5_ROOT, "lib", "libhdf5.so.103"),
+              f"-Wl,-rpath,{HDF5_ROOT}/lib"])
+    return target
+
+
+def build_all(verbose=False, hip=True):
+    out = [build_cpu(verbose), build_io(verbose)]
+    if hip:
+        out.append(build_hip(verbose))
+    return [o for o in out if o]
+
+
+if __name__ == "__main__":
+    skip_hip = "--no-hip" in sys.argv
+    for t in build_all(verbose=True, hip=not skip_hip):
+        print("ok", t)

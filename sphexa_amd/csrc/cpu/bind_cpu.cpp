@@ -1,0 +1,366 @@
+// pybind11 bindings of the OpenMP reference path. All buffers are passed as raw addresses of torch CPU tensors
+// owned by the Python layer; variable-size outputs (trees) are returned as numpy arrays.
+#include <array>
+#include <stdexcept>
+
+#include <omp.h>
+
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "cpu_api.hpp"
+
+namespace py = pybind11;
+using namespace sphx;
+
+namespace sphx::cpu
+{
+int64_t findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
+                      const TreeView& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, uint32_t* nc,
+                      bool iterateH);
+void xmass(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*, const double*,
+           const double*, const double*, const float*, const float*, const float*, float*);
+void veDefGradh(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*, const double*,
+                const double*, const double*, const float*, const float*, const float*, const float*, const float*,
+                float*, float*);
+void eosVe(int64_t, int64_t, const SphConsts&, const double*, const float*, const float*, const float*, const float*,
+           float*, float*, float*, float*);
+void eosStd(int64_t, int64_t, const SphConsts&, const double*, const float*, float*, float*, float*);
+void iad(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*, const double*,
+         const double*, const double*, const float*, const float*, const float*, const float*, float* const[6]);
+void divvCurlv(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*, const double*,
+               const double*, const double*, const float*, const float*, const float*, const float*,
+               const float* const[6], const float*, const float*, const float*, float*, float*, float* const[6]);
+void avSwitches(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*, const double*,
+                const double*, const double*, const float*, const float*, const float*, const float*, const float*,
+                const float* const[6], const float*, const float*, const float*, const float*, double, float*);
+double momentumEnergyVe(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*,
+                        const VeMomentumPtrs&, bool, float*, float*, float*, double*);
+double momentumEnergyStd(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*,
+                         const StdMomentumPtrs&, float*, float*, float*, double*);
+void updatePositions(int64_t, int64_t, double, double, double*, double*, double*, float*, float*, float*, float*,
+                     float*, float*, const float*, const float*, const float*, const float*, double*, double*,
+                     const double*, float*, double, const Box&);
+void updateSmoothingLength(int64_t, int64_t, unsigned, const uint32_t*, float*);
+void conservedQuantities(int64_t, int64_t, const double*, const double*, const double*, const float*, const float*,
+                         const float*, const float*, const double*, const double*, const int32_t*, double, double*);
+} // namespace sphx::cpu
+
+namespace
+{
+using BoxArr   = std::array<double, 9>;
+using ConstArr = std::array<double, 13>;
+using Ptr      = uintptr_t;
+
+template<class T>
+T* P(Ptr p)
+{
+    return reinterpret_cast<T*>(p);
+}
+
+Box toBox(const BoxArr& a)
+{
+    Box b;
+    for (int d = 0; d < 3; ++d)
+    {
+        b.lo[d] = a[d];
+        b.hi[d] = a[3 + d];
+        b.bc[d] = int(a[6 + d]);
+    }
+    return b;
+}
+
+SphConsts toConsts(const ConstArr& a)
+{
+    SphConsts s;
+    s.K             = a[0];
+    s.Kcour         = a[1];
+    s.Krho          = a[2];
+    s.gamma         = a[3];
+    s.muiConst      = a[4];
+    s.alphamin      = float(a[5]);
+    s.alphamax      = float(a[6]);
+    s.decayConstant = float(a[7]);
+    s.Atmin         = float(a[8]);
+    s.Atmax         = float(a[9]);
+    s.ramp          = float(a[10]);
+    s.ng0           = unsigned(a[11]);
+    s.ngmax         = unsigned(a[12]);
+    return s;
+}
+
+template<class T>
+py::array_t<T> toNumpy(const std::vector<T>& v)
+{
+    py::array_t<T> a(v.size());
+    std::copy(v.begin(), v.end(), a.mutable_data());
+    return a;
+}
+
+cpu::TreeView toView(int64_t numNodes, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr center, Ptr half)
+{
+    return cpu::TreeView{numNodes, P<const int32_t>(child), P<const int32_t>(n2l), P<const int32_t>(ns),
+                         P<const int32_t>(ne),     P<const double>(center), P<const double>(half)};
+}
+
+std::array<float*, 6> six(const std::array<Ptr, 6>& a)
+{
+    std::array<float*, 6> r;
+    for (int k = 0; k < 6; ++k)
+        r[k] = P<float>(a[k]);
+    return r;
+}
+
+} // namespace
+
+PYBIND11_MODULE(_sphx_cpu, m)
+{
+    m.doc() = "sphexa_amd OpenMP reference path";
+
+    m.def("num_threads", []() { return omp_get_max_threads(); });
+
+    m.def("compute_keys", [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, int kind, Ptr keys)
+          { cpu::computeKeys(n, P<double>(x), P<double>(y), P<double>(z), toBox(box), kind, P<KeyT>(keys)); });
+
+    m.def("sort_keys", [](int64_t n, Ptr keys, Ptr perm) { cpu::sortKeys(n, P<KeyT>(keys), P<int32_t>(perm)); });
+
+    m.def("gather", [](int64_t n, Ptr perm, Ptr src, Ptr dst, int elemSize)
+          { cpu::gatherBytes(n, P<int32_t>(perm), P<char>(src), P<char>(dst), elemSize); });
+
+    m.def("node_counts", [](Ptr tree, int64_t L, Ptr keys, int64_t n, Ptr counts)
+          { cpu::nodeCounts(P<KeyT>(tree), L, P<KeyT>(keys), n, P<uint32_t>(counts)); });
+
+    m.def("build_tree",
+          [](py::array_t<uint64_t> treeIn, Ptr keys, int64_t n, uint32_t bucket, int maxIter)
+          {
+              std::vector<KeyT> tree(treeIn.data(), treeIn.data() + treeIn.size());
+              std::vector<uint32_t> counts;
+              auto out = cpu::buildTree(tree, P<KeyT>(keys), n, bucket, counts, maxIter);
+              return py::make_tuple(toNumpy(out), toNumpy(counts));
+          });
+
+    m.def("rebalance",
+          [](py::array_t<uint64_t> treeIn, py::array_t<uint32_t> counts, uint32_t bucket)
+          {
+              std::vector<KeyT> tree(treeIn.data(), treeIn.data() + treeIn.size());
+              bool changed = cpu::rebalance(tree, counts.data(), bucket);
+              return py::make_tuple(toNumpy(tree), changed);
+          });
+
+    m.def("link_octree",
+          [](py::array_t<uint64_t> tree)
+          {
+              auto o = cpu::linkOctree(tree.data(), int64_t(tree.size()) - 1);
+              py::dict d;
+              d["num_nodes"]     = o.numNodes;
+              d["num_leaves"]    = o.numLeaves;
+              d["prefixes"]      = toNumpy(o.prefixes);
+              d["child_offsets"] = toNumpy(o.childOffsets);
+              d["parents"]       = toNumpy(o.parents);
+              d["node_to_leaf"]  = toNumpy(o.nodeToLeaf);
+              d["leaf_to_node"]  = toNumpy(o.leafToNode);
+              d["level_range"]   = toNumpy(o.levelRange);
+              return d;
+          });
+
+    m.def("node_props",
+          [](py::array_t<uint64_t> tree, Ptr keys, int64_t n, int64_t offset, Ptr x, Ptr y, Ptr z)
+          {
+              auto o    = cpu::linkOctree(tree.data(), int64_t(tree.size()) - 1);
+              int64_t N = o.numNodes;
+              py::array_t<int32_t> ns(N), ne(N);
+              py::array_t<double> center(3 * N), half(3 * N);
+              cpu::nodeRanges(o, P<KeyT>(keys), n, offset, ns.mutable_data(), ne.mutable_data());
+              cpu::tightBoxes(o, ns.data(), ne.data(), P<double>(x), P<double>(y), P<double>(z),
+                              center.mutable_data(), half.mutable_data());
+              py::dict d;
+              d["num_nodes"]     = o.numNodes;
+              d["num_leaves"]    = o.numLeaves;
+              d["prefixes"]      = toNumpy(o.prefixes);
+              d["child_offsets"] = toNumpy(o.childOffsets);
+              d["parents"]       = toNumpy(o.parents);
+              d["node_to_leaf"]  = toNumpy(o.nodeToLeaf);
+              d["leaf_to_node"]  = toNumpy(o.leafToNode);
+              d["level_range"]   = toNumpy(o.levelRange);
+              d["node_start"]    = ns;
+              d["node_end"]      = ne;
+              d["center"]        = center;
+              d["half"]          = half;
+              return d;
+          });
+
+    m.def("search_boxes",
+          [](int64_t N, Ptr child, Ptr n2l, std::vector<int64_t> levelRange, Ptr ns, Ptr ne, Ptr x, Ptr y, Ptr z,
+             Ptr h, double factor, Ptr center, Ptr half)
+          {
+              cpu::boxesWithRadius(N, P<int32_t>(child), P<int32_t>(n2l), levelRange.data(), P<int32_t>(ns),
+                                   P<int32_t>(ne), P<double>(x), P<double>(y), P<double>(z), P<float>(h), factor,
+                                   P<double>(center), P<double>(half));
+          });
+
+    m.def("mark_in_boxes",
+          [](int64_t nb, Ptr bc, Ptr bh, int64_t numNodes, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr center, Ptr half,
+             Ptr x, Ptr y, Ptr z, const BoxArr& box, Ptr flags)
+          {
+              auto t = toView(numNodes, child, n2l, ns, ne, center, half);
+              cpu::markInBoxes(nb, P<double>(bc), P<double>(bh), t, P<double>(x), P<double>(y), P<double>(z),
+                               toBox(box), P<uint8_t>(flags));
+          });
+
+    m.def("find_neighbors",
+          [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr h, int64_t numNodes, Ptr child, Ptr n2l, Ptr ns,
+             Ptr ne, Ptr center, Ptr half, const BoxArr& box, unsigned ng0, unsigned ngmax, Ptr nidx, Ptr nc,
+             bool iterateH)
+          {
+              auto t = toView(numNodes, child, n2l, ns, ne, center, half);
+              return cpu::findNeighbors(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(h), t,
+                                        toBox(box), ng0, ngmax, P<int32_t>(nidx), P<uint32_t>(nc), iterateH);
+          });
+
+    m.def("xmass", [](int64_t first, int64_t last, const ConstArr& sc, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x,
+                      Ptr y, Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr xm)
+          {
+              cpu::xmass(first, last, toConsts(sc), toBox(box), P<int32_t>(nidx), P<uint32_t>(nc), P<double>(x),
+                         P<double>(y), P<double>(z), P<float>(h), P<float>(mm), P<float>(wh), P<float>(xm));
+          });
+
+    m.def("ve_def_gradh",
+          [](int64_t first, int64_t last, const ConstArr& sc, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y,
+             Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr whd, Ptr xm, Ptr kx, Ptr gradh)
+          {
+              cpu::veDefGradh(first, last, toConsts(sc), toBox(box), P<int32_t>(nidx), P<uint32_t>(nc),
+                              P<double>(x), P<double>(y), P<double>(z), P<float>(h), P<float>(mm), P<float>(wh),
+                              P<float>(whd), P<float>(xm), P<float>(kx), P<float>(gradh));
+          });
+
+    m.def("eos_ve", [](int64_t first, int64_t last, const ConstArr& sc, Ptr temp, Ptr mm, Ptr kx, Ptr xm, Ptr gradh,
+                       Ptr prho, Ptr c, Ptr rho, Ptr p)
+          {
+              cpu::eosVe(first, last, toConsts(sc), P<double>(temp), P<float>(mm), P<float>(kx), P<float>(xm),
+                         P<float>(gradh), P<float>(prho), P<float>(c), P<float>(rho), P<float>(p));
+          });
+
+    m.def("eos_std", [](int64_t first, int64_t last, const ConstArr& sc, Ptr temp, Ptr mm, Ptr rho, Ptr p, Ptr c)
+          {
+              cpu::eosStd(first, last, toConsts(sc), P<double>(temp), P<float>(mm), P<float>(rho), P<float>(p),
+                          P<float>(c));
+          });
+
+    m.def("iad", [](int64_t first, int64_t last, const ConstArr& sc, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x,
+                    Ptr y, Ptr z, Ptr h, Ptr wh, Ptr numer, Ptr denom, const std::array<Ptr, 6>& cij)
+          {
+              auto c = six(cij);
+              cpu::iad(first, last, toConsts(sc), toBox(box), P<int32_t>(nidx), P<uint32_t>(nc), P<double>(x),
+                       P<double>(y), P<double>(z), P<float>(h), P<float>(wh), P<float>(numer), P<float>(denom),
+                       c.data());
+          });
+
+    m.def("divv_curlv",
+          [](int64_t first, int64_t last, const ConstArr& sc, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y,
+             Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr h, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
+             Ptr curlv, const std::array<Ptr, 6>& dV)
+          {
+              auto c = six(cij);
+              auto g = six(dV);
+              const float* cc[6];
+              for (int k = 0; k < 6; ++k)
+                  cc[k] = c[k];
+              cpu::divvCurlv(first, last, toConsts(sc), toBox(box), P<int32_t>(nidx), P<uint32_t>(nc),
+                             P<double>(x), P<double>(y), P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz),
+                             P<float>(h), cc, P<float>(wh), P<float>(kx), P<float>(xm), P<float>(divv),
+                             P<float>(curlv), g.data());
+          });
+
+    m.def("av_switches",
+          [](int64_t first, int64_t last, const ConstArr& sc, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y,
+             Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr c, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm,
+             Ptr divv, double dt, Ptr alpha)
+          {
+              auto cc6 = six(cij);
+              const float* cc[6];
+              for (int k = 0; k < 6; ++k)
+                  cc[k] = cc6[k];
+              cpu::avSwitches(first, last, toConsts(sc), toBox(box), P<int32_t>(nidx), P<uint32_t>(nc),
+                              P<double>(x), P<double>(y), P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz),
+                              P<float>(h), P<float>(c), cc, P<float>(wh), P<float>(kx), P<float>(xm),
+                              P<float>(divv), dt, P<float>(alpha));
+          });
+
+    m.def("momentum_energy_ve",
+          [](int64_t first, int64_t last, const ConstArr& sc, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y,
+             Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr prho, Ptr c, const std::array<Ptr, 6>& cij, Ptr kx,
+             Ptr xm, Ptr alpha, const std::array<Ptr, 6>& dV, Ptr wh, bool avClean, Ptr ax, Ptr ay, Ptr az, Ptr du)
+          {
+              VeMomentumPtrs p;
+              p.x = P<double>(x);
+              p.y = P<double>(y);
+              p.z = P<double>(z);
+              p.vx = P<float>(vx);
+              p.vy = P<float>(vy);
+              p.vz = P<float>(vz);
+              p.h = P<float>(h);
+              p.m = P<float>(mm);
+              p.prho = P<float>(prho);
+              p.c = P<float>(c);
+              for (int k = 0; k < 6; ++k)
+              {
+                  p.cij[k] = P<float>(cij[k]);
+                  p.dV[k]  = P<float>(dV[k]);
+              }
+              p.kx = P<float>(kx);
+              p.xm = P<float>(xm);
+              p.alpha = P<float>(alpha);
+              p.wh = P<float>(wh);
+              return cpu::momentumEnergyVe(first, last, toConsts(sc), toBox(box), P<int32_t>(nidx), P<uint32_t>(nc),
+                                           p, avClean, P<float>(ax), P<float>(ay), P<float>(az), P<double>(du));
+          });
+
+    m.def("momentum_energy_std",
+          [](int64_t first, int64_t last, const ConstArr& sc, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y,
+             Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr rho, Ptr p_, Ptr c, const std::array<Ptr, 6>& cij,
+             Ptr wh, Ptr ax, Ptr ay, Ptr az, Ptr du)
+          {
+              StdMomentumPtrs p;
+              p.x = P<double>(x);
+              p.y = P<double>(y);
+              p.z = P<double>(z);
+              p.vx = P<float>(vx);
+              p.vy = P<float>(vy);
+              p.vz = P<float>(vz);
+              p.h = P<float>(h);
+              p.m = P<float>(mm);
+              p.rho = P<float>(rho);
+              p.p = P<float>(p_);
+              p.c = P<float>(c);
+              for (int k = 0; k < 6; ++k)
+                  p.cij[k] = P<float>(cij[k]);
+              p.wh = P<float>(wh);
+              return cpu::momentumEnergyStd(first, last, toConsts(sc), toBox(box), P<int32_t>(nidx),
+                                            P<uint32_t>(nc), p, P<float>(ax), P<float>(ay), P<float>(az),
+                                            P<double>(du));
+          });
+
+    m.def("update_positions",
+          [](int64_t first, int64_t last, double dt, double dt_m1, Ptr x, Ptr y, Ptr z, Ptr vx, Ptr vy, Ptr vz,
+             Ptr xm1, Ptr ym1, Ptr zm1, Ptr ax, Ptr ay, Ptr az, Ptr h, Ptr temp, Ptr u, Ptr du, Ptr dum1, double cv,
+             const BoxArr& box)
+          {
+              cpu::updatePositions(first, last, dt, dt_m1, P<double>(x), P<double>(y), P<double>(z), P<float>(vx),
+                                   P<float>(vy), P<float>(vz), P<float>(xm1), P<float>(ym1), P<float>(zm1),
+                                   P<float>(ax), P<float>(ay), P<float>(az), P<float>(h), P<double>(temp),
+                                   P<double>(u), P<double>(du), P<float>(dum1), cv, toBox(box));
+          });
+
+    m.def("conserved_quantities",
+          [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr mm, Ptr temp, Ptr u, Ptr nc,
+             double cv, Ptr out)
+          {
+              cpu::conservedQuantities(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(vx),
+                                       P<float>(vy), P<float>(vz), P<float>(mm), P<double>(temp), P<double>(u),
+                                       P<int32_t>(nc), cv, P<double>(out));
+          });
+
+    m.def("update_h", [](int64_t first, int64_t last, unsigned ng0, Ptr nc, Ptr h)
+          { cpu::updateSmoothingLength(first, last, ng0, P<uint32_t>(nc), P<float>(h)); });
+}

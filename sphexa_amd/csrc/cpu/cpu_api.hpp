@@ -1,0 +1,57 @@
+// Declarations of the OpenMP reference path (module _sphx_cpu).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "sphx/box.hpp"
+#include "sphx/sph_math.hpp"
+
+namespace sphx::cpu
+{
+
+struct LinkedOctree
+{
+    int64_t numNodes{0};
+    int64_t numLeaves{0};
+    std::vector<KeyT> prefixes;        // placeholder codes, level-major, key-minor
+    std::vector<int32_t> childOffsets; // 0 for leaves
+    std::vector<int32_t> parents;      // per sibling group
+    std::vector<int32_t> nodeToLeaf;   // -1 for internal nodes
+    std::vector<int32_t> leafToNode;
+    std::vector<int64_t> levelRange;   // first node index of each level, size kMaxLevel+2
+};
+
+void computeKeys(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind, KeyT* keys);
+void sortKeys(int64_t n, KeyT* keys, int32_t* perm);
+void gatherBytes(int64_t n, const int32_t* perm, const char* src, char* dst, int elemSize);
+void nodeCounts(const KeyT* tree, int64_t L, const KeyT* keys, int64_t n, uint32_t* counts);
+bool rebalance(std::vector<KeyT>& tree, const uint32_t* counts, uint32_t bucket);
+std::vector<KeyT> buildTree(std::vector<KeyT> tree, const KeyT* keys, int64_t n, uint32_t bucket,
+                            std::vector<uint32_t>& counts, int maxIter);
+LinkedOctree linkOctree(const KeyT* tree, int64_t L);
+void nodeRanges(const LinkedOctree& o, const KeyT* keys, int64_t n, int64_t offset, int32_t* nodeStart,
+                int32_t* nodeEnd);
+void tightBoxes(const LinkedOctree& o, const int32_t* nodeStart, const int32_t* nodeEnd, const double* x,
+                const double* y, const double* z, double* center, double* half);
+
+void boxesWithRadius(int64_t N, const int32_t* childOffsets, const int32_t* nodeToLeaf, const int64_t* levelRange,
+                     const int32_t* nodeStart, const int32_t* nodeEnd, const double* x, const double* y,
+                     const double* z, const float* h, double factor, double* center, double* half);
+
+//! @brief flat view of a linked octree with tight node boxes, as used by the traversals
+struct TreeView
+{
+    int64_t numNodes;
+    const int32_t* childOffsets;
+    const int32_t* nodeToLeaf;
+    const int32_t* nodeStart;
+    const int32_t* nodeEnd;
+    const double* center;
+    const double* half;
+};
+
+void markInBoxes(int64_t numBoxes, const double* bc, const double* bh, const TreeView& t, const double* x,
+                 const double* y, const double* z, const Box& box, uint8_t* flags);
+
+} // namespace sphx::cpu

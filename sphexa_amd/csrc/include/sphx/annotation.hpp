@@ -1,0 +1,37 @@
+// Host/device annotations for math shared between the OpenMP reference path and the gfx950 kernels.
+// Parity: reference domain/include/cstone/cuda/annotation.hpp:36-52 (HOST_DEVICE_FUN).
+// There is exactly one device target (gfx950 through hipcc); the same headers compiled by g++ produce the
+// OpenMP CPU reference, so the only switch here is "compiled by hipcc or not".
+#pragma once
+
+#include <cstdint>
+#include <cmath>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define SPHX_HD __host__ __device__ inline
+#define SPHX_DEV __device__ inline
+#else
+#define SPHX_HD inline
+#endif
+
+namespace sphx
+{
+
+template<class T>
+SPHX_HD T smin(T a, T b)
+{
+    return a < b ? a : b;
+}
+
+template<class T>
+SPHX_HD T smax(T a, T b)
+{
+    return a < b ? b : a;
+}
+
+SPHX_HD int clz64(uint64_t x) { return x == 0 ? 64 : __builtin_clzll(x); }
+SPHX_HD int ctz64(uint64_t x) { return x == 0 ? 64 : __builtin_ctzll(x); }
+SPHX_HD int popcount64(uint64_t x) { return __builtin_popcountll(x); }
+
+} // namespace sphx

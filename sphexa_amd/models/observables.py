@@ -1,0 +1,74 @@
+"""Observables: globally conserved quantities and the per-iteration constants.txt rows.
+
+Parity: reference main/src/observables/conserved_quantities.hpp:49-177 (eKin, eInt, linear and angular momentum,
+neighbor sum; MPI_Reduce of 10 doubles), time_energies.hpp:40-66 (constants.txt columns), factory.hpp:45-69.
+The device reduction is one fused native pass (``_sphx_hip.conserved_quantities``) on the GPU, an OpenMP loop on the
+CPU; the cross-rank reduction is one allreduce of the 10-vector.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import _lib
+from ..ops.hydro_consts import ideal_gas_cv
+from ..parallel.comm import SUM
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def local_conserved(d, first: int, last: int) -> torch.Tensor:
+    """returns float64 tensor [eKin, eInt, 0, linmom(3), angmom(3), ncsum] on the data device"""
+    cv = ideal_gas_cv(d.muiConst, d.gamma)
+    temp = d["temp"] if d.is_allocated("temp") else None
+    u = d["u"] if d.is_allocated("u") else None
+    nc = d["nc"] if d.is_allocated("nc") else None
+    out = torch.zeros(10, dtype=torch.float64, device=d.device)
+    args = (first, last, d["x"].data_ptr(), d["y"].data_ptr(), d["z"].data_ptr(), d["vx"].data_ptr(),
+            d["vy"].data_ptr(), d["vz"].data_ptr(), d["m"].data_ptr(), 0 if temp is None else temp.data_ptr(),
+            0 if u is None else u.data_ptr(), 0 if nc is None else nc.data_ptr(), cv, out.data_ptr())
+    if d.device.type == "cuda":
+        _lib.hip().conserved_quantities(*args, _stream())
+    else:
+        _lib.cpu().conserved_quantities(*args)
+    return out
+
+
+def compute_conserved_quantities(d, first: int, last: int, comm):
+    q = local_conserved(d, first, last)
+    q[2] = d.egrav
+    comm.allreduce(q, SUM)
+    q = q.cpu().tolist()
+    d.ecin, d.eint, d.egrav = q[0], q[1], q[2]
+    d.etot = d.ecin + d.eint + d.egrav
+    d.linmom = math.sqrt(q[3] ** 2 + q[4] ** 2 + q[5] ** 2)
+    d.angmom = math.sqrt(q[6] ** 2 + q[7] ** 2 + q[8] ** 2)
+    d.totalNeighbors = int(q[9])
+
+
+class TimeAndEnergy:
+    """constants.txt writer: iteration, time, dt, etot, ecin, eint, egrav, linmom, angmom (time_energies.hpp)"""
+
+    def __init__(self, path: str | None, rank: int):
+        self.path = path
+        self.rank = rank
+        self._f = open(path, "a") if (path and rank == 0) else None
+
+    def extra_columns(self, d, domain):
+        return []
+
+    def compute_and_write(self, d, domain, comm):
+        compute_conserved_quantities(d, domain.start_index(), domain.end_index(), comm)
+        extra = self.extra_columns(d, domain)
+        if self._f:
+            cols = [d.iteration, d.ttot, d.minDt, d.etot, d.ecin, d.eint, d.egrav, d.linmom, d.angmom] + extra
+            self._f.write(" ".join(f"{c:.15g}" if isinstance(c, float) else str(c) for c in cols) + "\n")
+            self._f.flush()
+
+    def close(self):
+        if self._f:
+            self._f.close()

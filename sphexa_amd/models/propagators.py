@@ -1,0 +1,289 @@
+"""Time-step drivers ("propagators").
+
+Parity (reference main/src/propagator/):
+  ipropagator.hpp:44-126  interface: conservedFields, activateFields, sync, step, saveFields, save, load,
+                          writeMetrics, printIterationTimings ("### Check ###" lines)
+  ve_hydro.hpp:50-287     HydroVeProp<avClean>: the VE sequence with 4 halo exchanges
+  std_hydro.hpp:50-224    HydroProp: standard SPH
+  nbody.hpp:50-153        NbodyProp: gravity only
+  turb_ve.hpp:52-103      TurbVeProp: VE + turbulence stirring
+  factory.hpp:49-73       propagatorFactory(--prop {ve, std, nbody, turbulence, std-cooling})
+"""
+
+from __future__ import annotations
+
+import math
+import sys
+from typing import List
+
+import torch
+
+from ..ops import hydro as H
+from ..ops.neighbors import find_neighbors
+from ..parallel.comm import MIN
+from ..utils.timer import Timer
+
+
+class Propagator:
+    conserved: List[str] = []
+    dependent: List[str] = []
+
+    def __init__(self, out=sys.stdout, rank: int = 0, quiet: bool = False):
+        self.out = out if rank == 0 and not quiet else None
+        self.rank = rank
+        self.timer = Timer(self.out)
+        self.nl = None
+        self.gravity = None
+
+    # --------------------------------------------------------------------------------------------- interface
+    def conserved_fields(self) -> List[str]:
+        return ["x", "y", "z", "h", "m"] + list(self.conserved)
+
+    def activate_fields(self, d):
+        d.set_conserved("x", "y", "z", "h", "m")
+        d.set_dependent("keys")
+        d.set_conserved(*self.conserved)
+        d.set_dependent(*self.dependent)
+        self.timer.device = d.device
+
+    def sync(self, domain, d):
+        domain.sync(d, self.conserved_fields(), self.dependent)
+
+    def step(self, domain, d):
+        raise NotImplementedError
+
+    def save_fields(self, writer, first, last, d, box):
+        for name in d.outputFieldNames:
+            if d.is_allocated(name):
+                writer.write_field(name, d[name][first:last])
+
+    def save(self, writer):
+        pass
+
+    def load(self, path, reader):
+        pass
+
+    # ---------------------------------------------------------------------------------------------- shared
+    def _neighbors(self, domain, d):
+        first, last = domain.start_index(), domain.end_index()
+        self.nl = find_neighbors(d, domain.octree, domain.box, first, last,
+                                 nidx=self.nl.nidx if self.nl is not None else None)
+        return first, last
+
+    def _gravity(self, domain, d):
+        if d.g != 0.0:
+            if self.gravity is None:
+                from .gravity import MultipoleHolder
+
+                self.gravity = MultipoleHolder()
+            self.gravity.upsweep(d, domain)
+            self.timer.step("Upsweep")
+            self.gravity.traverse(d, domain)
+            self.timer.step("Gravity")
+
+    def compute_timestep(self, domain, d, *extra):
+        """min of Courant, rho, acceleration and 1.1x previous dt; global MIN (reference sph/timestep.hpp)"""
+        first, last = domain.start_index(), domain.end_index()
+        if d.minDtCourant is None:
+            d.minDtCourant = float(d.minDtCourant_dev.item())
+        dt_acc = math.inf
+        if d.g != 0.0 and last > first:
+            a2 = (d["ax"][first:last].double() ** 2 + d["ay"][first:last].double() ** 2 +
+                  d["az"][first:last].double() ** 2).max()
+            max_acc = math.sqrt(float(a2))
+            if max_acc > 0:
+                dt_acc = d.etaAcc * math.sqrt(d.eps / max_acc)
+        dt_loc = min([dt_acc, d.minDtCourant, d.minDtRho, d.maxDtIncrease * d.minDt] + list(extra))
+        dt = domain.comm.allreduce_scalar(dt_loc, MIN, device=d.device)
+        d.ttot += dt
+        d.minDt_m1 = d.minDt
+        d.minDt = dt
+
+    def rho_timestep(self, d, first, last):
+        if last <= first:
+            return math.inf
+        mx = float(d["divv"][first:last].max())
+        return d.Krho / abs(mx) if mx != 0 else math.inf
+
+    def print_iteration_timings(self, domain, d):
+        if self.out is None:
+            return
+        o = self.out
+        b = domain.box
+        print(f"### Check ### Global Tree Nodes: {domain.global_tree_size()}, Particles: {domain.n_particles()}, "
+              f"Halos: {domain.n_particles_with_halos() - domain.n_particles()}", file=o)
+        print(f"### Check ### Computational domain: {b.lo[0]} {b.hi[0]} {b.lo[1]} {b.hi[1]} {b.lo[2]} {b.hi[2]}",
+              file=o)
+        avg = d.totalNeighbors / max(d.numParticlesGlobal, 1)
+        print(f"### Check ### Total Neighbors: {d.totalNeighbors}, Avg neighbor count per particle: {avg:.6g}", file=o)
+        print(f"### Check ### Total time: {d.ttot}, current time-step: {d.minDt}", file=o)
+        print(f"### Check ### Total energy: {d.etot}, (internal: {d.eint}, kinetic: {d.ecin}, gravitational: "
+              f"{d.egrav})", file=o)
+        ot = domain.octree
+        print(f"### Check ### Focus Tree Nodes: {ot.num_leaves if ot else 0}, maxDepth {ot.max_depth() if ot else 0}",
+              file=o)
+        print(f"=== Total time for iteration({d.iteration}) {self.timer.sum_of_steps():.6f}s\n", file=o)
+
+
+class HydroVeProp(Propagator):
+    """volume-element SPH with AV switches (default ``--prop ve``), optional AV cleaning"""
+
+    conserved = ["temp", "vx", "vy", "vz", "x_m1", "y_m1", "z_m1", "du_m1", "alpha"]
+    dependent_base = ["ax", "ay", "az", "prho", "c", "du", "c11", "c12", "c13", "c22", "c23", "c33", "xm", "kx",
+                      "nc"]
+    gradv = ["dV11", "dV12", "dV13", "dV22", "dV23", "dV33"]
+
+    def __init__(self, out=sys.stdout, rank=0, av_clean: bool = False, quiet=False):
+        super().__init__(out, rank, quiet)
+        self.av_clean = av_clean
+        self.dependent = self.dependent_base + (self.gradv if av_clean else [])
+        if av_clean and self.out:
+            print("AV cleaning is activated", file=self.out)
+
+    def compute_forces(self, domain, d):
+        t = self.timer
+        t.start()
+        self.sync(domain, d)
+        t.step("domain::sync")
+        box = domain.box
+        first, last = self._neighbors(domain, d)
+        t.step("FindNeighbors")
+        nl = self.nl
+
+        H.compute_xmass(d, nl, box)
+        t.step("XMass")
+        domain.exchange_halos(d, ["xm"])
+        t.step("mpi::synchronizeHalos")
+
+        d.release("ay")
+        d.acquire("gradh")
+        H.compute_ve_def_gradh(d, nl, box)
+        t.step("Normalization & Gradh")
+        H.compute_eos_ve(d, first, last)
+        t.step("EquationOfState")
+        domain.exchange_halos(d, ["vx", "vy", "vz", "prho", "c", "kx"])
+        t.step("mpi::synchronizeHalos")
+
+        d.release("gradh", "az")
+        d.acquire("divv", "curlv")
+        H.compute_iad_divv_curlv(d, nl, box, self.av_clean)
+        d.minDtRho = self.rho_timestep(d, first, last)
+        t.step("IadVelocityDivCurl")
+        domain.exchange_halos(d, ["c11", "c12", "c13", "c22", "c23", "c33", "divv"])
+        t.step("mpi::synchronizeHalos")
+
+        H.compute_av_switches(d, nl, box)
+        t.step("AVswitches")
+        if self.av_clean:
+            domain.exchange_halos(d, ["dV11", "dV12", "dV22", "dV23", "dV33", "alpha"])
+        else:
+            domain.exchange_halos(d, ["alpha"])
+        t.step("mpi::synchronizeHalos")
+
+        d.release("divv", "curlv")
+        d.acquire("ay", "az")
+        H.compute_momentum_energy_ve(d, nl, box, self.av_clean)
+        t.step("MomentumAndEnergy")
+        self._gravity(domain, d)
+
+    def step(self, domain, d):
+        self.compute_forces(domain, d)
+        first, last = domain.start_index(), domain.end_index()
+        self.compute_timestep(domain, d)
+        self.timer.step("Timestep")
+        H.compute_positions(d, first, last, domain.box)
+        H.update_smoothing_length(d, first, last)
+        self.timer.step("UpdateQuantities")
+        self.timer.stop()
+
+    def save_fields(self, writer, first, last, d, box):
+        """three output passes as in the reference: allocated fields, then EOS products, then divv/curlv"""
+        todo = [n for n in d.outputFieldNames]
+        done = set()
+
+        def output():
+            for n in todo:
+                if n not in done and d.is_allocated(n):
+                    writer.write_field(n, d[n][first:last])
+                    done.add(n)
+
+        output()
+        if any(n in ("rho", "p", "gradh") for n in todo if n not in done):
+            d.release("ax", "ay", "az")
+            d.acquire("rho", "p", "gradh")
+            if self.nl is not None:
+                H.compute_ve_def_gradh(d, self.nl, box)
+            H.compute_eos_ve(d, first, last)
+            output()
+            d.release("rho", "p", "gradh")
+            d.acquire("ax", "ay", "az")
+        if any(n in ("divv", "curlv") for n in todo if n not in done):
+            d.release("ax", "ay")
+            d.acquire("divv", "curlv")
+            if self.nl is not None:
+                H.compute_iad_divv_curlv(d, self.nl, box, False)
+            output()
+            d.release("divv", "curlv")
+            d.acquire("ax", "ay")
+        missing = [n for n in todo if n not in done]
+        if missing and self.rank == 0:
+            print("WARNING: the following fields are not in use and therefore not output: " + ",".join(missing))
+
+
+class HydroProp(Propagator):
+    """standard SPH (``--prop std``)"""
+
+    conserved = ["temp", "vx", "vy", "vz", "x_m1", "y_m1", "z_m1", "du_m1"]
+    dependent = ["rho", "p", "c", "ax", "ay", "az", "du", "c11", "c12", "c13", "c22", "c23", "c33", "nc"]
+
+    def compute_forces(self, domain, d):
+        t = self.timer
+        box = domain.box
+        first, last = self._neighbors(domain, d)
+        t.step("FindNeighbors")
+        nl = self.nl
+        H.compute_density(d, nl, box)
+        t.step("Density")
+        H.compute_eos_std(d, first, last)
+        t.step("EquationOfState")
+        domain.exchange_halos(d, ["vx", "vy", "vz", "rho", "p", "c"])
+        t.step("mpi::synchronizeHalos")
+        H.compute_iad(d, nl, box, "m", "rho")
+        t.step("IAD")
+        domain.exchange_halos(d, ["c11", "c12", "c13", "c22", "c23", "c33"])
+        t.step("mpi::synchronizeHalos")
+        H.compute_momentum_energy_std(d, nl, box)
+        t.step("MomentumEnergyIAD")
+        self._gravity(domain, d)
+
+    def step(self, domain, d):
+        self.timer.start()
+        self.sync(domain, d)
+        self.timer.step("domain::sync")
+        self.compute_forces(domain, d)
+        first, last = domain.start_index(), domain.end_index()
+        self.compute_timestep(domain, d)
+        self.timer.step("Timestep")
+        H.compute_positions(d, first, last, domain.box)
+        H.update_smoothing_length(d, first, last)
+        self.timer.step("UpdateQuantities")
+        self.timer.stop()
+
+
+def propagator_factory(name: str, av_clean: bool, out, rank: int, quiet: bool = False) -> Propagator:
+    if name == "ve":
+        return HydroVeProp(out, rank, av_clean, quiet)
+    if name == "std":
+        return HydroProp(out, rank, quiet)
+    if name == "nbody":
+        from .nbody import NbodyProp
+
+        return NbodyProp(out, rank, quiet)
+    if name == "turbulence":
+        from .turbulence import TurbVeProp
+
+        return TurbVeProp(out, rank, av_clean, quiet)
+    if name == "std-cooling":
+        raise RuntimeError("--prop std-cooling requires the Grackle chemistry library, which is not available in "
+                           "this build")
+    raise ValueError(f"Unknown propagator choice: {name}")

@@ -1,0 +1,57 @@
+"""Loader for the in-tree native modules.
+
+The HIP module is mandatory whenever a GPU is present: an op on a CUDA(HIP) tensor never silently falls back to
+PyTorch or the CPU path — it raises if ``_sphx_hip`` cannot be loaded.
+"""
+
+from __future__ import annotations
+
+import importlib.util
+import os
+import sys
+import sysconfig
+
+_NATIVE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
+_EXT = sysconfig.get_config_var("EXT_SUFFIX")
+_cache: dict = {}
+
+
+def _load(name: str):
+    if name in _cache:
+        return _cache[name]
+    path = os.path.join(_NATIVE_DIR, name + _EXT)
+    if not os.path.exists(path):
+        # build on first use (CPU container or fresh checkout)
+        from .. import build_native
+
+        if name == "_sphx_cpu":
+            build_native.build_cpu()
+        elif name == "_sphx_hip":
+            build_native.build_hip()
+        elif name == "_sphx_io":
+            build_native.build_io()
+    if not os.path.exists(path):
+        raise ImportError(f"native module {name} not found at {path}")
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sys.modules[name] = mod
+    _cache[name] = mod
+    return mod
+
+
+def cpu():
+    return _load("_sphx_cpu")
+
+
+def hip():
+    return _load("_sphx_hip")
+
+
+def io():
+    return _load("_sphx_io")
+
+
+def native_paths():
+    """the .so files this process has loaded (for diagnostics / smoke tests)"""
+    return {k: getattr(v, "__file__", None) for k, v in _cache.items()}

@@ -1,0 +1,182 @@
+"""SPH hydrodynamics operators (VE and STD formulations), EOS, integration and smoothing-length update.
+
+Parity (reference sph/include/sph/):
+  hydro_ve/xmass*.{hpp,cu}, ve_def_gradh*, eos*, iad_divv_curlv*, av_switches*, momentum_energy*  (VE)
+  hydro_std/density.hpp, eos*, iad*, momentum_energy*                                             (STD)
+  positions*.{hpp,cu}, update_h*.{hpp,cu}, timestep.hpp
+Each op dispatches on the tensor device: HIP tensors go to the gfx950 kernels (_sphx_hip), CPU tensors to the
+OpenMP reference path (_sphx_cpu). There is no silent fallback between the two.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+from .neighbors import NeighborList
+from ..utils.box import Box
+
+CIJ = ("c11", "c12", "c13", "c22", "c23", "c33")
+DV = ("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _nl_args(nl: NeighborList, d):
+    return nl.nidx.data_ptr(), d["nc"].data_ptr()
+
+
+def _is_gpu(d):
+    return d.device.type == "cuda"
+
+
+def compute_xmass(d, nl: NeighborList, box: Box, out_field: str = "xm"):
+    first, last = nl.first, nl.last
+    nidx, nc = _nl_args(nl, d)
+    args = (first, last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+            d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d[out_field].data_ptr())
+    if _is_gpu(d):
+        _lib.hip().xmass(*args, _stream())
+    else:
+        _lib.cpu().xmass(*args)
+
+
+def compute_density(d, nl: NeighborList, box: Box):
+    """STD density: the XMass loop written into rho (volume element m/rho0), see hydro_std/density.hpp"""
+    compute_xmass(d, nl, box, out_field="rho")
+
+
+def compute_ve_def_gradh(d, nl: NeighborList, box: Box):
+    nidx, nc = _nl_args(nl, d)
+    args = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+            d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d.whd.data_ptr(),
+            d["xm"].data_ptr(), d["kx"].data_ptr(), d["gradh"].data_ptr())
+    if _is_gpu(d):
+        _lib.hip().ve_def_gradh(*args, _stream())
+    else:
+        _lib.cpu().ve_def_gradh(*args)
+
+
+def compute_eos_ve(d, first: int, last: int):
+    rho = d["rho"] if d.is_allocated("rho") else None
+    p = d["p"] if d.is_allocated("p") else None
+    args = (first, last, d.consts_array(), d["temp"].data_ptr(), d["m"].data_ptr(), d["kx"].data_ptr(),
+            d["xm"].data_ptr(), d["gradh"].data_ptr(), d["prho"].data_ptr(), d["c"].data_ptr(), _p(rho), _p(p))
+    if _is_gpu(d):
+        _lib.hip().eos_ve(*args, _stream())
+    else:
+        _lib.cpu().eos_ve(*args)
+
+
+def compute_eos_std(d, first: int, last: int):
+    args = (first, last, d.consts_array(), d["temp"].data_ptr(), d["m"].data_ptr(), d["rho"].data_ptr(),
+            d["p"].data_ptr(), d["c"].data_ptr())
+    if _is_gpu(d):
+        _lib.hip().eos_std(*args, _stream())
+    else:
+        _lib.cpu().eos_std(*args)
+
+
+def compute_iad(d, nl: NeighborList, box: Box, numer: str, denom: str):
+    """IAD matrices; VE uses volumes xm/kx, STD uses m/rho"""
+    nidx, nc = _nl_args(nl, d)
+    args = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+            d["z"].data_ptr(), d["h"].data_ptr(), d.wh.data_ptr(), d[numer].data_ptr(), d[denom].data_ptr(),
+            [d[c].data_ptr() for c in CIJ])
+    if _is_gpu(d):
+        _lib.hip().iad(*args, _stream())
+    else:
+        _lib.cpu().iad(*args)
+
+
+def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False):
+    compute_iad(d, nl, box, "xm", "kx")
+    nidx, nc = _nl_args(nl, d)
+    dv = [d[n].data_ptr() for n in DV] if av_clean else [0] * 6
+    args = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+            d["z"].data_ptr(), d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(), d["h"].data_ptr(),
+            [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["kx"].data_ptr(), d["xm"].data_ptr(),
+            d["divv"].data_ptr(), d["curlv"].data_ptr(), dv)
+    if _is_gpu(d):
+        _lib.hip().divv_curlv(*args, _stream())
+    else:
+        _lib.cpu().divv_curlv(*args)
+
+
+def compute_av_switches(d, nl: NeighborList, box: Box):
+    nidx, nc = _nl_args(nl, d)
+    args = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+            d["z"].data_ptr(), d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(), d["h"].data_ptr(),
+            d["c"].data_ptr(), [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["kx"].data_ptr(),
+            d["xm"].data_ptr(), d["divv"].data_ptr(), float(d.minDt), d["alpha"].data_ptr())
+    if _is_gpu(d):
+        _lib.hip().av_switches(*args, _stream())
+    else:
+        _lib.cpu().av_switches(*args)
+
+
+def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = False):
+    """accelerations (-grad P / rho + AV), du/dt and the per-particle Courant time-step minimum"""
+    nidx, nc = _nl_args(nl, d)
+    dv = [d[n].data_ptr() for n in DV] if av_clean else [d["c11"].data_ptr()] * 6
+    common = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+              d["z"].data_ptr(), d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(), d["h"].data_ptr(),
+              d["m"].data_ptr(), d["prho"].data_ptr(), d["c"].data_ptr(), [d[c].data_ptr() for c in CIJ],
+              d["kx"].data_ptr(), d["xm"].data_ptr(), d["alpha"].data_ptr(), dv, d.wh.data_ptr(), bool(av_clean),
+              d["ax"].data_ptr(), d["ay"].data_ptr(), d["az"].data_ptr(), d["du"].data_ptr())
+    if _is_gpu(d):
+        dt = torch.full((1,), math.inf, dtype=torch.float32, device=d.device)
+        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), _stream())
+        d.minDtCourant_dev = dt
+        d.minDtCourant = None
+    else:
+        d.minDtCourant = float(_lib.cpu().momentum_energy_ve(*common))
+
+
+def compute_momentum_energy_std(d, nl: NeighborList, box: Box):
+    nidx, nc = _nl_args(nl, d)
+    common = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+              d["z"].data_ptr(), d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(), d["h"].data_ptr(),
+              d["m"].data_ptr(), d["rho"].data_ptr(), d["p"].data_ptr(), d["c"].data_ptr(),
+              [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["ax"].data_ptr(), d["ay"].data_ptr(),
+              d["az"].data_ptr(), d["du"].data_ptr())
+    if _is_gpu(d):
+        dt = torch.full((1,), math.inf, dtype=torch.float32, device=d.device)
+        _lib.hip().momentum_energy_std(*common, dt.data_ptr(), _stream())
+        d.minDtCourant_dev = dt
+        d.minDtCourant = None
+    else:
+        d.minDtCourant = float(_lib.cpu().momentum_energy_std(*common))
+
+
+def compute_positions(d, first: int, last: int, box: Box):
+    """Press 2nd order positions + AB2 energy (temp or u), PBC wrap, fixed-boundary freeze"""
+    from .hydro_consts import ideal_gas_cv
+
+    temp = d["temp"] if d.is_allocated("temp") else None
+    u = d["u"] if (temp is None and d.is_allocated("u")) else None
+    cv = ideal_gas_cv(d.muiConst, d.gamma)
+    args = (first, last, float(d.minDt), float(d.minDt_m1), d["x"].data_ptr(), d["y"].data_ptr(), d["z"].data_ptr(),
+            d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(), d["x_m1"].data_ptr(), d["y_m1"].data_ptr(),
+            d["z_m1"].data_ptr(), d["ax"].data_ptr(), d["ay"].data_ptr(), d["az"].data_ptr(), d["h"].data_ptr(),
+            _p(temp), _p(u), d["du"].data_ptr(), d["du_m1"].data_ptr(), cv, box.to_array())
+    if _is_gpu(d):
+        _lib.hip().update_positions(*args, _stream())
+    else:
+        _lib.cpu().update_positions(*args)
+
+
+def update_smoothing_length(d, first: int, last: int):
+    args = (first, last, int(d.ng0), d["nc"].data_ptr(), d["h"].data_ptr())
+    if _is_gpu(d):
+        _lib.hip().update_h(*args, _stream())
+    else:
+        _lib.cpu().update_h(*args)

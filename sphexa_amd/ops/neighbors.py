@@ -1,0 +1,101 @@
+"""Neighbor search with the coupled smoothing-length iteration.
+
+Parity: reference domain/include/cstone/findneighbors.hpp:95-195 (CPU, per particle), traversal/find_neighbors.cuh
+(GPU warp traversal) and sph/include/sph/find_neighbors.hpp:12-56 + hydro_ve/xmass_gpu.cu:54-101 (h re-iteration
+while nc < ng0/4 or nc-1 > ngmax, at most 10 rounds). Neighbors are stored once per step and re-used by every SPH
+loop (the reference GPU path re-traverses the tree in each of its five kernels).
+
+Storage layouts
+  * CPU:  ``nidx[(i - first) * ngmax + k]``
+  * HIP:  target groups of 64 consecutive particles (one wave64 per group);
+          ``nidx[(g * ngmax + k) * 64 + lane]`` so that step k of the j-loop is one coalesced 256-B load per wave.
+``nc`` (a particle field) counts neighbors *including* self, as in the reference.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .octree import Octree
+from ..utils.box import Box
+
+GROUP = 64
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@dataclass
+class NeighborList:
+    nidx: torch.Tensor
+    first: int
+    last: int
+    ngmax: int
+    grouped: bool  # True: HIP wave64-interleaved layout
+
+    @property
+    def stride(self):
+        return GROUP if self.grouped else 1
+
+
+class NeighborSearchError(RuntimeError):
+    pass
+
+
+def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
+                   nidx: torch.Tensor | None = None) -> NeighborList:
+    """search neighbors of particles [first, last) within 2h, adjusting h towards ng0 neighbors"""
+    x, y, z, h, nc = d["x"], d["y"], d["z"], d["h"], d["nc"]
+    n = last - first
+    ngmax = d.ngmax
+    if d.ng0 > ngmax:
+        raise ValueError("ng0 should be smaller than ngmax")
+    if x.is_cuda:
+        hp = _lib.hip()
+        num_groups = (n + GROUP - 1) // GROUP
+        need = max(num_groups, 1) * GROUP * ngmax
+        if nidx is None or nidx.numel() < need:
+            nidx = torch.empty(need, dtype=torch.int32, device=x.device)
+        stats = torch.zeros(4, dtype=torch.int64, device=x.device)
+        hp.find_neighbors(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), tree.num_nodes,
+                          tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
+                          tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
+                          d.ng0, ngmax, nidx.data_ptr(), nc.data_ptr(), int(iterate_h), stats.data_ptr(), _stream())
+        st = stats.cpu()
+        if int(st[1]) > 0:
+            raise NeighborSearchError(f"GPU traversal stack overflow in {int(st[1])} groups")
+        d.nc_fail = int(st[0])
+        return NeighborList(nidx, first, last, ngmax, True)
+
+    need = max(n, 1) * ngmax
+    if nidx is None or nidx.numel() < need:
+        nidx = torch.empty(need, dtype=torch.int32)
+    fails = _lib.cpu().find_neighbors(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
+                                      tree.num_nodes, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
+                                      tree.node_start.data_ptr(), tree.node_end.data_ptr(), tree.center.data_ptr(),
+                                      tree.half.data_ptr(), box.to_array(), d.ng0, ngmax, nidx.data_ptr(),
+                                      nc.data_ptr(), bool(iterate_h))
+    d.nc_fail = int(fails)
+    return NeighborList(nidx, first, last, ngmax, False)
+
+
+def neighbor_lists_as_sets(nl: NeighborList, nc: torch.Tensor):
+    """debug/test helper: python sets of neighbor indices per target (capped lists)"""
+    out = []
+    nidx = nl.nidx.cpu()
+    ncc = nc.cpu()
+    for i in range(nl.first, nl.last):
+        cnt = min(int(ncc[i]) - 1, nl.ngmax)
+        if nl.grouped:
+            g, lane = divmod(i - nl.first, GROUP)
+            base = g * nl.ngmax * GROUP
+            s = {int(nidx[base + k * GROUP + lane]) for k in range(cnt)}
+        else:
+            base = (i - nl.first) * nl.ngmax
+            s = set(int(v) for v in nidx[base:base + cnt].tolist())
+        out.append(s)
+    return out

@@ -1,0 +1,191 @@
+"""Cornerstone octree build, linking and node properties.
+
+Parity: reference tree/csarray.hpp:202-534 + tree/csarray_gpu.cu:49-261 (node counts, rebalance, update until
+converged), tree/octree.hpp:71-620 + tree/octree_gpu.cu:55-170 (fully linked octree: placeholder codes, level-major
+node order, childOffsets, parents, levelRange, internal<->leaf maps), focus/source_center*.{hpp,cu} style per-node
+geometric data. Tight (particle) bounding boxes per node replace the reference's geometric centers/sizes in the
+neighbor search: same results, better pruning.
+
+HIP path: per-leaf binary-search counts, rebalance op kernel, hipCUB exclusive scan, emit kernel; linking via
+per-leaf internal-node counts (no radix tree), one radix sort of the placeholder codes, per-node child search;
+leaf boxes from particles and a per-level box upsweep.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+
+KEY_END = 1 << 63
+MAX_LEVEL = 21
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@dataclass
+class Octree:
+    tree: torch.Tensor            # cornerstone leaf keys (L+1), int64
+    counts: torch.Tensor          # particles per leaf (L), int32
+    num_nodes: int
+    num_leaves: int
+    prefixes: torch.Tensor        # placeholder codes (N), int64
+    child_offsets: torch.Tensor   # (N) int32, 0 for leaves
+    parents: torch.Tensor         # (N-1)/8+1 int32
+    node_to_leaf: torch.Tensor    # (N) int32, -1 internal
+    leaf_to_node: torch.Tensor    # (L) int32
+    level_range: List[int]        # (MAX_LEVEL+2)
+    node_start: torch.Tensor      # (N) int32 absolute particle index
+    node_end: torch.Tensor        # (N) int32
+    center: torch.Tensor          # (N*3) f64 tight box center
+    half: torch.Tensor            # (N*3) f64 tight box half size (negative: empty)
+    offset: int = 0               # index of the first particle covered by this tree
+
+    @property
+    def device(self):
+        return self.tree.device
+
+    def max_depth(self) -> int:
+        for l in range(MAX_LEVEL, -1, -1):
+            if self.level_range[l + 1] > self.level_range[l]:
+                return l
+        return 0
+
+    def node_levels(self) -> torch.Tensor:
+        lv = torch.empty(self.num_nodes, dtype=torch.int32, device=self.device)
+        for l in range(MAX_LEVEL + 1):
+            lv[self.level_range[l]:self.level_range[l + 1]] = l
+        return lv
+
+    def leaf_layout(self) -> torch.Tensor:
+        """first particle index of every leaf + end (L+1), absolute"""
+        ln = self.leaf_to_node.long()
+        return torch.cat([self.node_start[ln], self.node_end[ln[-1:]]])
+
+
+def update_tree(tree: Optional[torch.Tensor], keys: torch.Tensor, bucket: int, max_iter: int = 64):
+    """rebalance a cornerstone leaf array until every leaf has at most ``bucket`` particles (or max depth).
+
+    ``keys`` must be sorted. Returns (tree, counts).
+    """
+    dev = keys.device
+    n = keys.numel()
+    if keys.is_cuda:
+        h = _lib.hip()
+        if tree is None or tree.numel() < 2:
+            tree = _root_tree(dev)
+        for _ in range(max_iter):
+            L = tree.numel() - 1
+            counts = torch.empty(L, dtype=torch.int32, device=dev)
+            ops = torch.empty(L + 1, dtype=torch.int64, device=dev)
+            flag = torch.zeros(1, dtype=torch.int32, device=dev)
+            h.node_counts(tree.data_ptr(), L, keys.data_ptr(), n, counts.data_ptr(), _stream())
+            h.rebalance_ops(tree.data_ptr(), counts.data_ptr(), L, bucket, ops.data_ptr(), flag.data_ptr(), _stream())
+            if int(flag.item()) == 0:
+                return tree, counts
+            tmp = torch.empty(h.scan_temp_bytes(L + 1), dtype=torch.uint8, device=dev)
+            h.exclusive_scan_i64(ops.data_ptr(), ops.data_ptr(), L + 1, tmp.data_ptr(), tmp.numel(), _stream())
+            newL = int(ops[L].item())
+            out = torch.empty(newL + 1, dtype=torch.int64, device=dev)
+            h.emit_leaves(tree.data_ptr(), ops.data_ptr(), L, out.data_ptr(), newL, _stream())
+            tree = out
+        L = tree.numel() - 1
+        counts = torch.empty(L, dtype=torch.int32, device=dev)
+        h.node_counts(tree.data_ptr(), L, keys.data_ptr(), n, counts.data_ptr(), _stream())
+        return tree, counts
+
+    t_in = _root_np() if tree is None or tree.numel() < 2 else tree.numpy().view(np.uint64)
+    t_out, counts = _lib.cpu().build_tree(t_in, keys.data_ptr(), n, bucket, max_iter)
+    return torch.from_numpy(t_out.view(np.int64)), torch.from_numpy(counts.view(np.int32))
+
+
+def _root_np():
+    return np.array([0, KEY_END], dtype=np.uint64)
+
+
+def _root_tree(dev):
+    return torch.from_numpy(_root_np().view(np.int64)).to(dev)
+
+
+def root_tree(dev):
+    """the single-leaf cornerstone array [0, 2^63]"""
+    return _root_tree(dev)
+
+
+def node_counts(tree: torch.Tensor, keys: torch.Tensor) -> torch.Tensor:
+    """particles per leaf of ``tree`` for sorted ``keys`` (int32)"""
+    L = tree.numel() - 1
+    counts = torch.empty(L, dtype=torch.int32, device=keys.device)
+    if keys.is_cuda:
+        _lib.hip().node_counts(tree.data_ptr(), L, keys.data_ptr(), keys.numel(), counts.data_ptr(), _stream())
+    else:
+        _lib.cpu().node_counts(tree.data_ptr(), L, keys.data_ptr(), keys.numel(), counts.data_ptr())
+    return counts
+
+
+def build_octree(tree: torch.Tensor, counts: torch.Tensor, keys: torch.Tensor, x, y, z, offset: int = 0) -> Octree:
+    """link the leaf array into a fully linked octree and compute per-node particle ranges and tight boxes.
+
+    ``keys``/``x``/``y``/``z`` are the sorted particles covered by the tree, starting at absolute index ``offset``.
+    """
+    n = keys.numel()
+    if keys.is_cuda:
+        return _build_octree_hip(tree, counts, keys, x, y, z, offset)
+    d = _lib.cpu().node_props(tree.numpy().view(np.uint64), keys.data_ptr(), n, offset, x.data_ptr(), y.data_ptr(),
+                              z.data_ptr())
+    t = torch.from_numpy
+    return Octree(tree=tree, counts=counts, num_nodes=int(d["num_nodes"]), num_leaves=int(d["num_leaves"]),
+                  prefixes=t(d["prefixes"].view(np.int64)), child_offsets=t(d["child_offsets"]),
+                  parents=t(d["parents"]), node_to_leaf=t(d["node_to_leaf"]), leaf_to_node=t(d["leaf_to_node"]),
+                  level_range=[int(v) for v in d["level_range"]], node_start=t(d["node_start"]),
+                  node_end=t(d["node_end"]), center=t(d["center"]), half=t(d["half"]), offset=offset)
+
+
+def _build_octree_hip(tree, counts, keys, x, y, z, offset) -> Octree:
+    h = _lib.hip()
+    dev = keys.device
+    L = tree.numel() - 1
+    n = keys.numel()
+    s = _stream()
+    # internal node count per leaf -> exclusive scan
+    icount = torch.empty(L + 1, dtype=torch.int64, device=dev)
+    h.internal_counts(tree.data_ptr(), L, icount.data_ptr(), s)
+    tmp = torch.empty(h.scan_temp_bytes(L + 1), dtype=torch.uint8, device=dev)
+    h.exclusive_scan_i64(icount.data_ptr(), icount.data_ptr(), L + 1, tmp.data_ptr(), tmp.numel(), s)
+    Ni = int(icount[L].item())
+    N = Ni + L
+    codes = torch.empty(N, dtype=torch.int64, device=dev)
+    vals = torch.empty(N, dtype=torch.int32, device=dev)
+    h.make_codes(tree.data_ptr(), L, icount.data_ptr(), Ni, codes.data_ptr(), vals.data_ptr(), s)
+    codes_s = torch.empty_like(codes)
+    vals_s = torch.empty_like(vals)
+    tmp = torch.empty(h.sort_pairs_temp_bytes(N), dtype=torch.uint8, device=dev)
+    h.sort_pairs_i64_i32(N, codes.data_ptr(), codes_s.data_ptr(), vals.data_ptr(), vals_s.data_ptr(),
+                         tmp.data_ptr(), tmp.numel(), 0, 64, s)
+    child = torch.empty(N, dtype=torch.int32, device=dev)
+    parents = torch.full(((N - 1) // 8 + 1,), -1, dtype=torch.int32, device=dev)
+    leaf_to_node = torch.empty(L, dtype=torch.int32, device=dev)
+    level_range = torch.empty(MAX_LEVEL + 2, dtype=torch.int64, device=dev)
+    h.link_nodes(codes_s.data_ptr(), vals_s.data_ptr(), N, child.data_ptr(), parents.data_ptr(),
+                 leaf_to_node.data_ptr(), level_range.data_ptr(), s)
+    ns = torch.empty(N, dtype=torch.int32, device=dev)
+    ne = torch.empty(N, dtype=torch.int32, device=dev)
+    center = torch.empty(3 * N, dtype=torch.float64, device=dev)
+    half = torch.empty(3 * N, dtype=torch.float64, device=dev)
+    lr = [int(v) for v in level_range.cpu().tolist()]
+    h.node_ranges(codes_s.data_ptr(), N, keys.data_ptr(), n, offset, ns.data_ptr(), ne.data_ptr(), s)
+    h.leaf_boxes(vals_s.data_ptr(), N, ns.data_ptr(), ne.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(),
+                 center.data_ptr(), half.data_ptr(), s)
+    for l in range(MAX_LEVEL, -1, -1):
+        a, b = lr[l], lr[l + 1]
+        if b > a:
+            h.upsweep_boxes(a, b, vals_s.data_ptr(), child.data_ptr(), center.data_ptr(), half.data_ptr(), s)
+    return Octree(tree=tree, counts=counts, num_nodes=N, num_leaves=L, prefixes=codes_s, child_offsets=child,
+                  parents=parents, node_to_leaf=vals_s, leaf_to_node=leaf_to_node, level_range=lr, node_start=ns,
+                  node_end=ne, center=center, half=half, offset=offset)

@@ -1,0 +1,88 @@
+"""SFC keys, key sort (reorder map) and multi-field gather.
+
+Parity: reference sfc/sfc.hpp:282 + sfc/sfc_gpu.cu:38-54 (computeSfcKeys), primitives/gather.hpp:132-162 and
+primitives/gather.cuh:44-113 (SfcSorter / GpuSfcSorter: sort keys, keep the permutation, gather fields).
+HIP path: one thread per particle key kernel; hipCUB (rocPRIM onesweep) radix sort of (key, index) over the 63 used
+key bits; a multi-array gather kernel that reorders all fields of one dtype in a single launch.
+"""
+
+from __future__ import annotations
+
+from typing import Sequence
+
+import torch
+
+from . import _lib
+from ..utils.box import Box
+
+HILBERT, MORTON = 0, 1
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def compute_keys(x: torch.Tensor, y: torch.Tensor, z: torch.Tensor, box: Box, kind: int = HILBERT,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    n = x.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=x.device)
+    if n == 0:
+        return out
+    if x.is_cuda:
+        _lib.hip().compute_keys(n, x.data_ptr(), y.data_ptr(), z.data_ptr(), box.to_array(), kind, out.data_ptr(),
+                                _stream())
+    else:
+        _lib.cpu().compute_keys(n, x.data_ptr(), y.data_ptr(), z.data_ptr(), box.to_array(), kind, out.data_ptr())
+    return out
+
+
+def sort_keys(keys: torch.Tensor):
+    """returns (sorted keys, permutation int32) with sorted[i] = keys[perm[i]]"""
+    n = keys.numel()
+    perm = torch.empty(n, dtype=torch.int32, device=keys.device)
+    if n == 0:
+        return keys.clone(), perm
+    if keys.is_cuda:
+        h = _lib.hip()
+        out = torch.empty_like(keys)
+        tmp = torch.empty(h.sort_temp_bytes(n), dtype=torch.uint8, device=keys.device)
+        h.sort_keys(n, keys.data_ptr(), out.data_ptr(), perm.data_ptr(), tmp.data_ptr(), tmp.numel(), _stream())
+        return out, perm
+    out = keys.clone()
+    _lib.cpu().sort_keys(n, out.data_ptr(), perm.data_ptr())
+    return out, perm
+
+
+def gather(perm: torch.Tensor, src: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[i] = src[perm[i]] for i < perm.numel()"""
+    n = perm.numel()
+    if out is None:
+        out = torch.empty(n, dtype=src.dtype, device=src.device)
+    if n == 0:
+        return out
+    if src.is_cuda:
+        _lib.hip().gather(n, perm.data_ptr(), src.data_ptr(), out.data_ptr(), src.element_size(), _stream())
+    else:
+        _lib.cpu().gather(n, perm.data_ptr(), src.data_ptr(), out.data_ptr(), src.element_size())
+    return out
+
+
+def gather_many(perm: torch.Tensor, srcs: Sequence[torch.Tensor]):
+    """gather several fields with the same permutation; on the GPU all fields of one element size share a launch"""
+    n = perm.numel()
+    outs = [torch.empty(n, dtype=s.dtype, device=s.device) for s in srcs]
+    if n == 0 or not srcs:
+        return outs
+    if srcs[0].is_cuda:
+        h = _lib.hip()
+        for size in (4, 8):
+            idx = [i for i, s in enumerate(srcs) if s.element_size() == size]
+            for c in range(0, len(idx), 16):
+                chunk = idx[c:c + 16]
+                h.gather_multi(n, perm.data_ptr(), [srcs[i].data_ptr() for i in chunk],
+                               [outs[i].data_ptr() for i in chunk], size, _stream())
+    else:
+        for s, o in zip(srcs, outs):
+            _lib.cpu().gather(n, perm.data_ptr(), s.data_ptr(), o.data_ptr(), s.element_size())
+    return outs

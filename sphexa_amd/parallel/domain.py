@@ -1,0 +1,344 @@
+"""SFC domain decomposition, particle migration, halo discovery and halo exchange.
+
+Parity (reference domain/include/cstone/):
+  domain/domain.hpp:65-647               Domain facade: sync, syncGrav, exchangeHalos, startIndex/endIndex,
+                                         nParticles/nParticlesWithHalos, box, globalTree, layout
+  domain/assignment*.{hpp,cuh}           global SFC assignment: bbox -> keys -> sort -> replicated global tree with
+                                         allreduced leaf counts -> uniform bins -> send ranges -> exchange
+  domain/domaindecomp.hpp:49-166         uniformBins, SfcAssignment, limitBoundaryShifts
+  tree/update_mpi*.{hpp,cuh}             global tree update with MPI_Allreduce(SUM) of counts
+  halos/halos.hpp, halos/exchange_halos* halo discovery + exchange
+  sfc/box_mpi.hpp:83-118                 global bounding box (MIN/MAX allreduce of non-periodic extents)
+
+MI355X-native design:
+  * one process per GPU; every collective is a torch.distributed call on device tensors (RCCL over xGMI)
+  * particle migration = one count exchange + one all_to_all_single per conserved field group
+  * halo discovery is *push-based*: every rank all-gathers a coarse cut of the other ranks' search boxes (node
+    bounding boxes of x +- 2h) and sends exactly its particles that fall inside them. Because ranks own contiguous
+    SFC ranges and send in key order, [halos from lower ranks | own | halos from higher ranks] is globally
+    SFC-sorted without another sort, and the halo send/receive schedules are known sizes for all later exchanges
+    (no MPI_Probe analog needed).
+  * the local octree (neighbor search) covers own + halo particles.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ..ops import _lib
+from ..ops import octree as octree_ops
+from ..ops import sfc as sfc_ops
+from ..utils.box import Box, PERIODIC
+from .comm import Comm, MAX, MIN, SUM
+
+HALO_FIELDS = ("x", "y", "z", "h", "m")
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class Domain:
+    def __init__(self, comm: Comm, box: Box, bucket_size_focus: int = 64, bucket_size: Optional[int] = None,
+                 theta: float = 1.0, sfc_kind: int = sfc_ops.HILBERT, halo_cut_boxes: int = 4096):
+        self.comm = comm
+        self.rank, self.size = comm.rank, comm.size
+        self.box = box.copy()
+        self.bucket_size_focus = bucket_size_focus
+        self.bucket_size = bucket_size
+        self.theta = theta
+        self.sfc_kind = sfc_kind
+        self.halo_cut_boxes = halo_cut_boxes
+
+        self.start = 0
+        self.end = 0
+        self.n_with_halos = 0
+        self.global_tree: Optional[torch.Tensor] = None
+        self.global_counts: Optional[torch.Tensor] = None
+        self.assignment: Optional[List[int]] = None     # global-tree leaf index boundaries per rank
+        self.local_tree: Optional[torch.Tensor] = None
+        self.octree: Optional[octree_ops.Octree] = None
+        self.halo_send_idx: List[torch.Tensor] = []       # per destination rank: own particle indices (absolute)
+        self.halo_send_counts: List[int] = [0] * self.size
+        self.halo_recv_counts: List[int] = [0] * self.size
+        self.n_lo = 0
+        self.n_hi = 0
+        self.stats: Dict[str, float] = {}
+
+    # ------------------------------------------------------------------------------------------------ queries
+    def n_particles(self) -> int:
+        return self.end - self.start
+
+    def n_particles_with_halos(self) -> int:
+        return self.n_with_halos
+
+    def start_index(self) -> int:
+        return self.start
+
+    def end_index(self) -> int:
+        return self.end
+
+    # ------------------------------------------------------------------------------------------------- bbox
+    def update_box(self, x, y, z):
+        """recompute extents of non-periodic dimensions from the owned particles (global MIN/MAX allreduce)"""
+        if all(b == PERIODIC for b in self.box.bc):
+            return
+        coords = (x, y, z)
+        dev = x.device
+        mins = torch.stack([c.min() if c.numel() else torch.tensor(math.inf, dtype=c.dtype, device=dev)
+                            for c in coords])
+        maxs = torch.stack([c.max() if c.numel() else torch.tensor(-math.inf, dtype=c.dtype, device=dev)
+                            for c in coords])
+        ext = torch.cat([mins, -maxs])
+        self.comm.allreduce(ext, MIN)
+        ext = ext.cpu().tolist()
+        for d in range(3):
+            if self.box.bc[d] != PERIODIC:
+                lo, hi = ext[d], -ext[3 + d]
+                if hi <= lo:
+                    hi = lo + 1e-10
+                self.box.lo[d] = lo
+                self.box.hi[d] = hi
+
+    # --------------------------------------------------------------------------------------------- the sync
+    def sync(self, d, conserved: Sequence[str], dependent: Sequence[str] = ()):
+        """redistribute particles along the SFC, sort, discover and exchange halos, build the local octree.
+
+        ``d`` is a ParticlesData. ``conserved`` fields are carried along (x,y,z,h,m must be included); dependent
+        fields are only resized. After the call d.size == n_with_halos and own particles are [start, end).
+        """
+        if self.octree is None and self.end == 0:
+            # first call: everything held by this rank is owned (initial conditions / file read)
+            self.start, self.end = 0, d.size
+        s, e = self.start, self.end
+        own = {f: d[f][s:e] for f in conserved}
+        x, y, z = own["x"], own["y"], own["z"]
+
+        self.update_box(x, y, z)
+        keys = sfc_ops.compute_keys(x, y, z, self.box, self.sfc_kind)
+
+        if self.size > 1:
+            keys, own = self._distribute(keys, own, conserved)
+
+        skeys, perm = sfc_ops.sort_keys(keys)
+        names = list(own.keys())
+        reordered = sfc_ops.gather_many(perm, [own[f] for f in names])
+        own = dict(zip(names, reordered))
+        n_own = skeys.numel()
+
+        if self.size > 1:
+            self._discover_halos(skeys, own)
+        else:
+            self.n_lo = self.n_hi = 0
+            self.halo_send_idx = []
+
+        total = self.n_lo + n_own + self.n_hi
+        d.resize(total, keep=False)
+        self.start, self.end, self.n_with_halos = self.n_lo, self.n_lo + n_own, total
+        for f in names:
+            d.buffer(f)[self.start:self.end].copy_(own[f])
+        d.buffer("keys")[self.start:self.end].copy_(skeys)
+
+        if self.size > 1:
+            self.exchange_halos(d, [f for f in HALO_FIELDS])
+            hs = [slice(0, self.start), slice(self.end, total)]
+            for sl in hs:
+                if sl.stop > sl.start:
+                    sfc_ops.compute_keys(d["x"][sl], d["y"][sl], d["z"][sl], self.box, self.sfc_kind,
+                                         out=d["keys"][sl])
+
+        all_keys = d["keys"]
+        self.local_tree, counts = octree_ops.update_tree(self.local_tree, all_keys, self.bucket_size_focus)
+        self.octree = octree_ops.build_octree(self.local_tree, counts, all_keys, d["x"], d["y"], d["z"], 0)
+        self.stats["local_leaves"] = self.octree.num_leaves
+        self.stats["halos"] = total - n_own
+
+    # ------------------------------------------------------------------------------------ global assignment
+    def _global_bucket(self, n_global: int) -> int:
+        if self.bucket_size is not None:
+            return self.bucket_size
+        return max(64, n_global // (100 * self.size))
+
+    def _distribute(self, keys, own: Dict[str, torch.Tensor], conserved):
+        """assign SFC ranges to ranks by equal particle counts and migrate particles (alltoallv)"""
+        skeys, perm = sfc_ops.sort_keys(keys)
+        n_global = int(self.comm.allreduce_scalar(float(skeys.numel()), SUM, device=keys.device))
+        bucket = self._global_bucket(n_global)
+
+        tree = self.global_tree
+        if tree is None:
+            tree = octree_ops.root_tree(skeys.device)
+        for _ in range(64):
+            # local counts on the replicated tree -> global counts -> identical rebalance on every rank
+            gcounts = octree_ops.node_counts(tree, skeys).to(torch.int64)
+            self.comm.allreduce(gcounts, SUM)
+            new_tree, changed = _rebalance_replicated(tree, gcounts, bucket)
+            if not changed:
+                break
+            tree = new_tree
+        L = tree.numel() - 1
+        self.global_tree, self.global_counts = tree, gcounts
+
+        # uniform bins over leaf counts
+        csum = torch.cumsum(gcounts, 0).cpu()
+        targets = torch.tensor([round(r * n_global / self.size) for r in range(1, self.size)], dtype=torch.int64)
+        cuts = torch.searchsorted(csum, targets, right=False).tolist()
+        bounds = [0] + [min(c + 1, L) for c in cuts] + [L]
+        for r in range(1, self.size + 1):
+            bounds[r] = max(bounds[r], bounds[r - 1])
+        self.assignment = bounds
+        tree_cpu = tree.cpu()
+        bkeys = torch.stack([tree_cpu[b] for b in bounds[1:-1]]) if self.size > 1 else torch.empty(0, dtype=torch.int64)
+        # send ranges: lower_bound of boundary keys in the sorted local keys
+        pos = torch.searchsorted(skeys, bkeys.to(skeys.device)).cpu().tolist()
+        edges = [0] + pos + [skeys.numel()]
+        send_counts = [edges[r + 1] - edges[r] for r in range(self.size)]
+        recv_counts = self.comm.exchange_counts(send_counts)
+
+        names = list(own.keys())
+        sorted_fields = sfc_ops.gather_many(perm, [own[f] for f in names])
+        out = {}
+        for f, t in zip(names, sorted_fields):
+            out[f], _ = self.comm.alltoallv(t, send_counts, recv_counts)
+        new_keys, _ = self.comm.alltoallv(skeys, send_counts, recv_counts)
+        self.stats["migrated_out"] = sum(send_counts) - send_counts[self.rank]
+        return new_keys, out
+
+    # ------------------------------------------------------------------------------------------------ halos
+    def _discover_halos(self, skeys, own):
+        """push-based halo discovery against the other ranks' search boxes"""
+        x, y, z, h = own["x"], own["y"], own["z"], own["h"]
+        tree, counts = octree_ops.update_tree(None, skeys, self.bucket_size_focus)
+        ot = octree_ops.build_octree(tree, counts, skeys, x, y, z, 0)
+        c, hf = _search_boxes(ot, x, y, z, h, 2.0)
+        cut = _coarse_cut(ot, c, hf, self.halo_cut_boxes)
+        boxes = torch.cat([c.view(-1, 3)[cut], hf.view(-1, 3)[cut]], dim=1)  # (nb, 6)
+        all_boxes = self.comm.allgather_var(boxes)
+
+        send_idx: List[torch.Tensor] = []
+        for q in range(self.size):
+            if q == self.rank or all_boxes[q].shape[0] == 0 or skeys.numel() == 0:
+                send_idx.append(torch.empty(0, dtype=torch.int64, device=skeys.device))
+                continue
+            flags = _mark_in_boxes(ot, all_boxes[q], x, y, z, self.box)
+            send_idx.append(torch.nonzero(flags, as_tuple=False).flatten())
+        self.halo_send_counts = [int(t.numel()) for t in send_idx]
+        self.halo_recv_counts = self.comm.exchange_counts(self.halo_send_counts)
+        self.n_lo = sum(self.halo_recv_counts[: self.rank])
+        self.n_hi = sum(self.halo_recv_counts[self.rank + 1:])
+        self._halo_send_rel = send_idx  # relative to own block, converted to absolute below
+        self.halo_send_idx = [t + self.n_lo for t in send_idx]
+
+    def exchange_halos(self, d, fields: Sequence[str]):
+        """fill halo slots of ``fields`` from their owners. One packed all_to_all per call (all fields fused)."""
+        if self.size == 1:
+            return
+        if not fields:
+            return
+        send_idx = torch.cat(self.halo_send_idx) if self.halo_send_idx else None
+        tensors = [d[f] for f in fields]
+        packed = _pack_rows(tensors, send_idx)
+        rowbytes = packed.shape[1]
+        recv, _ = self.comm.alltoallv(packed, self.halo_send_counts, self.halo_recv_counts)
+        lo = recv[: self.n_lo]
+        hi = recv[self.n_lo:]
+        _unpack_rows(lo, tensors, 0)
+        _unpack_rows(hi, tensors, self.end)
+        del rowbytes
+
+    # ---------------------------------------------------------------------------------------- diagnostics
+    def global_tree_size(self) -> int:
+        return 0 if self.global_tree is None else self.global_tree.numel() - 1
+
+
+# -------------------------------------------------------------------------------------------------------------
+def _rebalance_replicated(tree: torch.Tensor, gcounts: torch.Tensor, bucket: int):
+    """identical, deterministic rebalance on every rank given the global counts"""
+    import numpy as np
+
+    t_np = tree.cpu().numpy().view(np.uint64)
+    c_np = gcounts.clamp(max=2**32 - 1).to(torch.int64).cpu().numpy().astype(np.uint32)
+    new, changed = _lib.cpu().rebalance(t_np, c_np, bucket)
+    return torch.from_numpy(new.view(np.int64)).to(tree.device), bool(changed)
+
+
+def _search_boxes(ot, x, y, z, h, factor: float):
+    """per-node bounding boxes of the search spheres x +- factor*h"""
+    N = ot.num_nodes
+    center = torch.empty(3 * N, dtype=torch.float64, device=x.device)
+    half = torch.empty(3 * N, dtype=torch.float64, device=x.device)
+    if x.is_cuda:
+        hp = _lib.hip()
+        s = _stream()
+        hp.leaf_boxes_h(ot.node_to_leaf.data_ptr(), N, ot.node_start.data_ptr(), ot.node_end.data_ptr(),
+                        x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), float(factor), center.data_ptr(),
+                        half.data_ptr(), s)
+        for l in range(octree_ops.MAX_LEVEL, -1, -1):
+            a, b = ot.level_range[l], ot.level_range[l + 1]
+            if b > a:
+                hp.upsweep_boxes(a, b, ot.node_to_leaf.data_ptr(), ot.child_offsets.data_ptr(), center.data_ptr(),
+                                 half.data_ptr(), s)
+    else:
+        _lib.cpu().search_boxes(N, ot.child_offsets.data_ptr(), ot.node_to_leaf.data_ptr(), ot.level_range,
+                                ot.node_start.data_ptr(), ot.node_end.data_ptr(), x.data_ptr(), y.data_ptr(),
+                                z.data_ptr(), h.data_ptr(), float(factor), center.data_ptr(), half.data_ptr())
+    return center, half
+
+
+def _coarse_cut(ot, center, half, max_boxes: int) -> torch.Tensor:
+    """node indices of a tree cut with at most ~max_boxes non-empty nodes (nodes at the cut level + shallower
+    leaves)"""
+    lv = ot.node_levels()
+    is_leaf = ot.node_to_leaf >= 0
+    nonempty = half.view(-1, 3)[:, 0] >= 0
+    best = None
+    for cut in range(0, octree_ops.MAX_LEVEL + 1):
+        sel = ((lv == cut) | (is_leaf & (lv < cut))) & nonempty
+        cnt = int(sel.sum().item())
+        if cnt > max_boxes and best is not None:
+            break
+        best = sel
+        if cut > ot.max_depth():
+            break
+    return torch.nonzero(best, as_tuple=False).flatten()
+
+
+def _mark_in_boxes(ot, boxes: torch.Tensor, x, y, z, box: Box) -> torch.Tensor:
+    """flags[i] = particle i lies inside any of ``boxes`` (rows: center[3], half[3]); PBC aware"""
+    n = x.numel()
+    flags = torch.zeros(n, dtype=torch.uint8, device=x.device)
+    bc = boxes[:, :3].contiguous().view(-1)
+    bh = boxes[:, 3:].contiguous().view(-1)
+    nb = boxes.shape[0]
+    args = (nb, bc.data_ptr(), bh.data_ptr(), ot.num_nodes, ot.child_offsets.data_ptr(),
+            ot.node_to_leaf.data_ptr(), ot.node_start.data_ptr(), ot.node_end.data_ptr(), ot.center.data_ptr(),
+            ot.half.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(), box.to_array(), flags.data_ptr())
+    if x.is_cuda:
+        _lib.hip().mark_in_boxes(*args, _stream())
+    else:
+        _lib.cpu().mark_in_boxes(*args)
+    return flags
+
+
+def _pack_rows(tensors: Sequence[torch.Tensor], idx: Optional[torch.Tensor]) -> torch.Tensor:
+    """gather rows idx of several 1-D fields into one (n, rowbytes) uint8 matrix"""
+    cols = []
+    for t in tensors:
+        sel = t.index_select(0, idx) if idx is not None else t
+        cols.append(sel.contiguous().view(torch.uint8).view(-1, t.element_size()))
+    return torch.cat(cols, dim=1) if cols else None
+
+
+def _unpack_rows(rows: torch.Tensor, tensors: Sequence[torch.Tensor], offset: int):
+    n = rows.shape[0]
+    if n == 0:
+        return
+    col = 0
+    for t in tensors:
+        es = t.element_size()
+        chunk = rows[:, col:col + es].contiguous().view(t.dtype).view(-1)
+        t[offset:offset + n].copy_(chunk)
+        col += es
