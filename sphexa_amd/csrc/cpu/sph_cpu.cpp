@@ -2,7 +2,7 @@
  *
  * Parity: reference domain/include/cstone/findneighbors.hpp:95-195 (per-particle octree search, radius 2h,
  * PBC minimum image, capped at ngmax, count excludes self), sph/include/sph/find_neighbors.hpp:12-56
- * (h re-iteration up to 10x until ng0/4 <= nc <= ngmax+1), hydro_ve/*.hpp and hydro_std/*.hpp wrappers,
+ * (h re-iteration up to 10x until ng0/4 <= nc <= ngmax+1), hydro_ve and hydro_std wrappers,
  * positions.hpp, update_h.hpp, timestep.hpp.
  */
 #include <cmath>

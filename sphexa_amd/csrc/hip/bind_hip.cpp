@@ -1,0 +1,313 @@
+// pybind11 bindings of the gfx950 module. Buffers are raw device addresses of torch HIP tensors; every launcher
+// takes the caller's stream (torch.cuda.current_stream()) so kernels are ordered with torch ops and RCCL.
+#include <array>
+#include <vector>
+
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "hip_api.h"
+
+namespace py = pybind11;
+using namespace sphx;
+using namespace sphx::hip;
+
+namespace
+{
+using BoxArr   = std::array<double, 9>;
+using ConstArr = std::array<double, 13>;
+using Ptr      = uintptr_t;
+
+template<class T>
+T* P(Ptr p)
+{
+    return reinterpret_cast<T*>(p);
+}
+
+hipStream_t St(Ptr s) { return reinterpret_cast<hipStream_t>(s); }
+
+Box toBox(const BoxArr& a)
+{
+    Box b;
+    for (int d = 0; d < 3; ++d)
+    {
+        b.lo[d] = a[d];
+        b.hi[d] = a[3 + d];
+        b.bc[d] = int(a[6 + d]);
+    }
+    return b;
+}
+
+SphConsts toConsts(const ConstArr& a)
+{
+    SphConsts s;
+    s.K             = a[0];
+    s.Kcour         = a[1];
+    s.Krho          = a[2];
+    s.gamma         = a[3];
+    s.muiConst      = a[4];
+    s.alphamin      = float(a[5]);
+    s.alphamax      = float(a[6]);
+    s.decayConstant = float(a[7]);
+    s.Atmin         = float(a[8]);
+    s.Atmax         = float(a[9]);
+    s.ramp          = float(a[10]);
+    s.ng0           = unsigned(a[11]);
+    s.ngmax         = unsigned(a[12]);
+    return s;
+}
+
+NbrArgs nbr(int64_t first, int64_t last, Ptr nidx, Ptr nc, const SphConsts& sc)
+{
+    return NbrArgs{first, last, P<const int32_t>(nidx), P<const int32_t>(nc), sc.ngmax};
+}
+
+std::array<float*, 6> six(const std::array<Ptr, 6>& a)
+{
+    std::array<float*, 6> r;
+    for (int k = 0; k < 6; ++k)
+        r[k] = P<float>(a[k]);
+    return r;
+}
+
+std::array<const float*, 6> csix(const std::array<Ptr, 6>& a)
+{
+    std::array<const float*, 6> r;
+    for (int k = 0; k < 6; ++k)
+        r[k] = P<const float>(a[k]);
+    return r;
+}
+
+} // namespace
+
+PYBIND11_MODULE(_sphx_hip, m)
+{
+    m.doc() = "sphexa_amd gfx950 kernels";
+
+    m.def("device_info",
+          []()
+          {
+              int dev = 0;
+              hipGetDevice(&dev);
+              hipDeviceProp_t p;
+              hipGetDeviceProperties(&p, dev);
+              py::dict d;
+              d["name"]      = std::string(p.name);
+              d["arch"]      = std::string(p.gcnArchName);
+              d["cus"]       = p.multiProcessorCount;
+              d["lds"]       = p.sharedMemPerMultiprocessor;
+              d["mem"]       = p.totalGlobalMem;
+              d["warp_size"] = p.warpSize;
+              return d;
+          });
+
+    // ---------------------------------------------------------------------------------------------- sfc / sort
+    m.def("compute_keys", [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, int kind, Ptr keys, Ptr s)
+          { computeKeys(n, P<double>(x), P<double>(y), P<double>(z), toBox(box), kind, P<KeyT>(keys), St(s)); });
+    m.def("sort_temp_bytes", [](int64_t n) { return sortPairsTempBytes(n); });
+    m.def("sort_pairs_temp_bytes", [](int64_t n) { return sortPairsTempBytes(n); });
+    m.def("sort_keys", [](int64_t n, Ptr kin, Ptr kout, Ptr perm, Ptr tmp, size_t tmpBytes, Ptr s)
+          { sortKeys(n, P<KeyT>(kin), P<KeyT>(kout), P<int32_t>(perm), P<void>(tmp), tmpBytes, St(s)); });
+    m.def("sort_pairs_i64_i32",
+          [](int64_t n, Ptr kin, Ptr kout, Ptr vin, Ptr vout, Ptr tmp, size_t tmpBytes, int b0, int b1, Ptr s)
+          {
+              sortPairs(n, P<KeyT>(kin), P<KeyT>(kout), P<int32_t>(vin), P<int32_t>(vout), P<void>(tmp), tmpBytes, b0,
+                        b1, St(s));
+          });
+    m.def("gather", [](int64_t n, Ptr perm, Ptr src, Ptr dst, int es, Ptr s)
+          { gather(n, P<int32_t>(perm), P<void>(src), P<void>(dst), es, St(s)); });
+    m.def("gather_multi",
+          [](int64_t n, Ptr perm, const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst, int es, Ptr s)
+          { gatherMulti(n, P<int32_t>(perm), src, dst, es, St(s)); });
+    m.def("scan_temp_bytes", [](int64_t n) { return scanTempBytes(n); });
+    m.def("exclusive_scan_i64", [](Ptr in, Ptr out, int64_t n, Ptr tmp, size_t tb, Ptr s)
+          { exclusiveScanI64(P<int64_t>(in), P<int64_t>(out), n, P<void>(tmp), tb, St(s)); });
+
+    // ---------------------------------------------------------------------------------------------- octree
+    m.def("node_counts", [](Ptr tree, int64_t L, Ptr keys, int64_t n, Ptr counts, Ptr s)
+          { nodeCounts(P<KeyT>(tree), L, P<KeyT>(keys), n, P<int32_t>(counts), St(s)); });
+    m.def("rebalance_ops", [](Ptr tree, Ptr counts, int64_t L, uint32_t bucket, Ptr ops, Ptr flag, Ptr s)
+          { rebalanceOps(P<KeyT>(tree), P<int32_t>(counts), L, bucket, P<int64_t>(ops), P<int>(flag), St(s)); });
+    m.def("emit_leaves", [](Ptr tree, Ptr ops, int64_t L, Ptr out, int64_t newL, Ptr s)
+          { emitLeavesLaunch(P<KeyT>(tree), P<int64_t>(ops), L, P<KeyT>(out), newL, St(s)); });
+    m.def("internal_counts", [](Ptr tree, int64_t L, Ptr icount, Ptr s)
+          { internalCounts(P<KeyT>(tree), L, P<int64_t>(icount), St(s)); });
+    m.def("make_codes", [](Ptr tree, int64_t L, Ptr ioff, int64_t Ni, Ptr codes, Ptr vals, Ptr s)
+          { makeCodes(P<KeyT>(tree), L, P<int64_t>(ioff), Ni, P<KeyT>(codes), P<int32_t>(vals), St(s)); });
+    m.def("link_nodes", [](Ptr codes, Ptr vals, int64_t N, Ptr child, Ptr parents, Ptr l2n, Ptr lr, Ptr s)
+          {
+              linkNodes(P<KeyT>(codes), P<int32_t>(vals), N, P<int32_t>(child), P<int32_t>(parents), P<int32_t>(l2n),
+                        P<int64_t>(lr), St(s));
+          });
+    m.def("node_ranges", [](Ptr codes, int64_t N, Ptr keys, int64_t n, int64_t off, Ptr ns, Ptr ne, Ptr s)
+          { nodeRanges(P<KeyT>(codes), N, P<KeyT>(keys), n, off, P<int32_t>(ns), P<int32_t>(ne), St(s)); });
+    m.def("leaf_boxes", [](Ptr n2l, int64_t N, Ptr ns, Ptr ne, Ptr x, Ptr y, Ptr z, Ptr c, Ptr hf, Ptr s)
+          {
+              leafBoxes(P<int32_t>(n2l), N, P<int32_t>(ns), P<int32_t>(ne), P<double>(x), P<double>(y), P<double>(z),
+                        nullptr, 0.0, P<double>(c), P<double>(hf), St(s));
+          });
+    m.def("leaf_boxes_h",
+          [](Ptr n2l, int64_t N, Ptr ns, Ptr ne, Ptr x, Ptr y, Ptr z, Ptr h, double factor, Ptr c, Ptr hf, Ptr s)
+          {
+              leafBoxes(P<int32_t>(n2l), N, P<int32_t>(ns), P<int32_t>(ne), P<double>(x), P<double>(y), P<double>(z),
+                        P<float>(h), factor, P<double>(c), P<double>(hf), St(s));
+          });
+    m.def("upsweep_boxes", [](int64_t a, int64_t b, Ptr n2l, Ptr child, Ptr c, Ptr hf, Ptr s)
+          { upsweepBoxes(a, b, P<int32_t>(n2l), P<int32_t>(child), P<double>(c), P<double>(hf), St(s)); });
+    m.def("mark_in_boxes",
+          [](int64_t nb, Ptr bc, Ptr bh, int64_t numNodes, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr center, Ptr half,
+             Ptr x, Ptr y, Ptr z, const BoxArr& box, Ptr flags, Ptr s)
+          {
+              (void)numNodes;
+              markInBoxes(nb, P<double>(bc), P<double>(bh), P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns),
+                          P<int32_t>(ne), P<double>(center), P<double>(half), P<double>(x), P<double>(y),
+                          P<double>(z), toBox(box), P<uint8_t>(flags), St(s));
+          });
+
+    // ---------------------------------------------------------------------------------------------- neighbors
+    m.def("find_neighbors",
+          [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr h, int64_t numNodes, Ptr child, Ptr n2l, Ptr ns,
+             Ptr ne, Ptr center, Ptr half, const BoxArr& box, unsigned ng0, unsigned ngmax, Ptr nidx, Ptr nc,
+             int iterateH, Ptr stats, Ptr s)
+          {
+              (void)numNodes;
+              NsTree t{P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne), P<double>(center),
+                       P<double>(half)};
+              findNeighbors(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(h), t, toBox(box), ng0,
+                            ngmax, P<int32_t>(nidx), P<int32_t>(nc), iterateH, P<unsigned long long>(stats), St(s));
+          });
+
+    // ---------------------------------------------------------------------------------------------- hydro
+    m.def("xmass", [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x,
+                      Ptr y, Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr xm, Ptr s)
+          {
+              auto sc = toConsts(c);
+              xmass(nbr(first, last, nidx, nc, sc), sc, toBox(box), P<double>(x), P<double>(y), P<double>(z),
+                    P<float>(h), P<float>(mm), P<float>(wh), P<float>(xm), St(s));
+          });
+    m.def("ve_def_gradh", [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc,
+                             Ptr x, Ptr y, Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr whd, Ptr xm, Ptr kx, Ptr gradh, Ptr s)
+          {
+              auto sc = toConsts(c);
+              veDefGradh(nbr(first, last, nidx, nc, sc), sc, toBox(box), P<double>(x), P<double>(y), P<double>(z),
+                         P<float>(h), P<float>(mm), P<float>(wh), P<float>(whd), P<float>(xm), P<float>(kx),
+                         P<float>(gradh), St(s));
+          });
+    m.def("eos_ve", [](int64_t first, int64_t last, const ConstArr& c, Ptr temp, Ptr mm, Ptr kx, Ptr xm, Ptr gradh,
+                       Ptr prho, Ptr cc, Ptr rho, Ptr p, Ptr s)
+          {
+              eosVe(first, last, toConsts(c), P<double>(temp), P<float>(mm), P<float>(kx), P<float>(xm),
+                    P<float>(gradh), P<float>(prho), P<float>(cc), P<float>(rho), P<float>(p), St(s));
+          });
+    m.def("eos_std", [](int64_t first, int64_t last, const ConstArr& c, Ptr temp, Ptr mm, Ptr rho, Ptr p, Ptr cc,
+                        Ptr s)
+          {
+              eosStd(first, last, toConsts(c), P<double>(temp), P<float>(mm), P<float>(rho), P<float>(p),
+                     P<float>(cc), St(s));
+          });
+    m.def("iad", [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y,
+                    Ptr z, Ptr h, Ptr wh, Ptr numer, Ptr denom, const std::array<Ptr, 6>& cij, Ptr s)
+          {
+              auto sc = toConsts(c);
+              auto cp = six(cij);
+              iad(nbr(first, last, nidx, nc, sc), sc, toBox(box), P<double>(x), P<double>(y), P<double>(z),
+                  P<float>(h), P<float>(wh), P<float>(numer), P<float>(denom), cp.data(), St(s));
+          });
+    m.def("divv_curlv",
+          [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
+             Ptr vx, Ptr vy, Ptr vz, Ptr h, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
+             Ptr curlv, const std::array<Ptr, 6>& dV, Ptr s)
+          {
+              auto sc = toConsts(c);
+              auto cp = csix(cij);
+              auto g  = six(dV);
+              divvCurlv(nbr(first, last, nidx, nc, sc), sc, toBox(box), P<double>(x), P<double>(y), P<double>(z),
+                        P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), cp.data(), P<float>(wh), P<float>(kx),
+                        P<float>(xm), P<float>(divv), P<float>(curlv), g.data(), St(s));
+          });
+    m.def("av_switches",
+          [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
+             Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr cs, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
+             double dt, Ptr alpha, Ptr s)
+          {
+              auto sc = toConsts(c);
+              auto cp = csix(cij);
+              avSwitches(nbr(first, last, nidx, nc, sc), sc, toBox(box), P<double>(x), P<double>(y), P<double>(z),
+                         P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(cs), cp.data(),
+                         P<float>(wh), P<float>(kx), P<float>(xm), P<float>(divv), dt, P<float>(alpha), St(s));
+          });
+    m.def("momentum_energy_ve",
+          [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
+             Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr prho, Ptr cs, const std::array<Ptr, 6>& cij, Ptr kx, Ptr xm,
+             Ptr alpha, const std::array<Ptr, 6>& dV, Ptr wh, bool avClean, Ptr ax, Ptr ay, Ptr az, Ptr du,
+             Ptr minDt, Ptr s)
+          {
+              auto sc = toConsts(c);
+              VeMomentumPtrs p;
+              p.x    = P<double>(x);
+              p.y    = P<double>(y);
+              p.z    = P<double>(z);
+              p.vx   = P<float>(vx);
+              p.vy   = P<float>(vy);
+              p.vz   = P<float>(vz);
+              p.h    = P<float>(h);
+              p.m    = P<float>(mm);
+              p.prho = P<float>(prho);
+              p.c    = P<float>(cs);
+              for (int k = 0; k < 6; ++k)
+              {
+                  p.cij[k] = P<float>(cij[k]);
+                  p.dV[k]  = P<float>(dV[k]);
+              }
+              p.kx    = P<float>(kx);
+              p.xm    = P<float>(xm);
+              p.alpha = P<float>(alpha);
+              p.wh    = P<float>(wh);
+              momentumEnergyVe(nbr(first, last, nidx, nc, sc), sc, toBox(box), p, avClean, P<float>(ax), P<float>(ay),
+                               P<float>(az), P<double>(du), P<float>(minDt), St(s));
+          });
+    m.def("momentum_energy_std",
+          [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
+             Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr rho, Ptr pp, Ptr cs, const std::array<Ptr, 6>& cij, Ptr wh,
+             Ptr ax, Ptr ay, Ptr az, Ptr du, Ptr minDt, Ptr s)
+          {
+              auto sc = toConsts(c);
+              StdMomentumPtrs p;
+              p.x   = P<double>(x);
+              p.y   = P<double>(y);
+              p.z   = P<double>(z);
+              p.vx  = P<float>(vx);
+              p.vy  = P<float>(vy);
+              p.vz  = P<float>(vz);
+              p.h   = P<float>(h);
+              p.m   = P<float>(mm);
+              p.rho = P<float>(rho);
+              p.p   = P<float>(pp);
+              p.c   = P<float>(cs);
+              for (int k = 0; k < 6; ++k)
+                  p.cij[k] = P<float>(cij[k]);
+              p.wh = P<float>(wh);
+              momentumEnergyStd(nbr(first, last, nidx, nc, sc), sc, toBox(box), p, P<float>(ax), P<float>(ay),
+                                P<float>(az), P<double>(du), P<float>(minDt), St(s));
+          });
+    m.def("update_positions",
+          [](int64_t first, int64_t last, double dt, double dtm1, Ptr x, Ptr y, Ptr z, Ptr vx, Ptr vy, Ptr vz,
+             Ptr xm1, Ptr ym1, Ptr zm1, Ptr ax, Ptr ay, Ptr az, Ptr h, Ptr temp, Ptr u, Ptr du, Ptr dum1, double cv,
+             const BoxArr& box, Ptr s)
+          {
+              PosArgs p{P<double>(x),  P<double>(y),  P<double>(z),  P<float>(vx), P<float>(vy), P<float>(vz),
+                        P<float>(xm1), P<float>(ym1), P<float>(zm1), P<float>(ax), P<float>(ay), P<float>(az),
+                        P<float>(h),   P<double>(temp), P<double>(u), P<double>(du), P<float>(dum1)};
+              updatePositions(first, last, dt, dtm1, p, cv, toBox(box), St(s));
+          });
+    m.def("update_h", [](int64_t first, int64_t last, unsigned ng0, Ptr nc, Ptr h, Ptr s)
+          { updateH(first, last, ng0, P<int32_t>(nc), P<float>(h), St(s)); });
+    m.def("conserved_quantities",
+          [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr mm, Ptr temp, Ptr u, Ptr nc,
+             double cv, Ptr out, Ptr s)
+          {
+              conservedQuantities(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(vx), P<float>(vy),
+                                  P<float>(vz), P<float>(mm), P<double>(temp), P<double>(u), P<int32_t>(nc), cv,
+                                  P<double>(out), St(s));
+          });
+}

@@ -1,0 +1,95 @@
+// Shared helpers for the gfx950 kernels: error checking, launch geometry, wave64 primitives.
+// Parity: reference domain/include/cstone/cuda/errorcheck.cuh (checkGpuErrors), gpu_config.cuh (warpSize 64 on
+// AMD), primitives/warpscan.cuh (ballot/shfl/scans) — written directly for wave64 / gfx950.
+#pragma once
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include <hip/hip_runtime.h>
+
+#include "sphx/annotation.hpp"
+
+#define SPHX_CHECK(expr)                                                                                              \
+    do                                                                                                                \
+    {                                                                                                                 \
+        hipError_t err_ = (expr);                                                                                     \
+        if (err_ != hipSuccess)                                                                                       \
+        {                                                                                                             \
+            throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(err_) + " at " + __FILE__ + ":" + \
+                                     std::to_string(__LINE__));                                                       \
+        }                                                                                                             \
+    } while (0)
+
+#define SPHX_LAUNCH_CHECK() SPHX_CHECK(hipGetLastError())
+
+namespace sphx::hip
+{
+
+constexpr int kWave = 64;
+
+inline unsigned gridFor(int64_t n, int block) { return unsigned((n + block - 1) / block); }
+
+inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+//! @brief lanes below this lane in a 64-bit mask
+__device__ __forceinline__ uint64_t lanemaskLt()
+{
+    unsigned lane = threadIdx.x & 63;
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ int laneId() { return int(threadIdx.x & 63); }
+
+//! @brief broadcast a double from lane k (wave-uniform k) through two v_readlane_b32
+__device__ __forceinline__ double readLaneD(double v, int k)
+{
+    int2 p;
+    p = *reinterpret_cast<int2*>(&v);
+    int lo = __builtin_amdgcn_readlane(p.x, k);
+    int hi = __builtin_amdgcn_readlane(p.y, k);
+    int2 q{lo, hi};
+    return *reinterpret_cast<double*>(&q);
+}
+
+__device__ __forceinline__ float readLaneF(float v, int k)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+
+__device__ __forceinline__ int readLaneI(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+
+template<class T>
+__device__ __forceinline__ T waveMin(T v)
+{
+    for (int o = 32; o > 0; o >>= 1)
+        v = sphx::smin(v, __shfl_xor(v, o));
+    return v;
+}
+
+template<class T>
+__device__ __forceinline__ T waveMax(T v)
+{
+    for (int o = 32; o > 0; o >>= 1)
+        v = sphx::smax(v, __shfl_xor(v, o));
+    return v;
+}
+
+template<class T>
+__device__ __forceinline__ T waveSum(T v)
+{
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o);
+    return v;
+}
+
+//! @brief atomic min for non-negative floats via integer ordering
+__device__ __forceinline__ void atomicMinPosFloat(float* addr, float v)
+{
+    atomicMin(reinterpret_cast<int*>(addr), __float_as_int(v));
+}
+
+} // namespace sphx::hip

@@ -1,0 +1,113 @@
+// Host-side API of the gfx950 module (_sphx_hip): argument structs and launcher declarations.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "sphx/box.hpp"
+#include "sphx/sph_math.hpp"
+
+namespace sphx::hip
+{
+
+struct NsTree
+{
+    const int32_t* child;
+    const int32_t* n2l;
+    const int32_t* ns;
+    const int32_t* ne;
+    const double* center;
+    const double* half;
+};
+
+struct NbrArgs
+{
+    int64_t first, last;
+    const int32_t* nidx;
+    const int32_t* nc;
+    unsigned ngmax;
+};
+
+struct PosArgs
+{
+    double *x, *y, *z;
+    float *vx, *vy, *vz, *xm1, *ym1, *zm1;
+    const float *ax, *ay, *az, *h;
+    double *temp, *u;
+    const double* du;
+    float* dum1;
+};
+
+// sfc_sort.hip
+void computeKeys(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind, KeyT* keys,
+                 hipStream_t s);
+size_t sortPairsTempBytes(int64_t n);
+void sortPairs(int64_t n, const KeyT* keysIn, KeyT* keysOut, const int32_t* valsIn, int32_t* valsOut, void* tmp,
+               size_t tmpBytes, int beginBit, int endBit, hipStream_t s);
+void sortKeys(int64_t n, const KeyT* keysIn, KeyT* keysOut, int32_t* perm, void* tmp, size_t tmpBytes, hipStream_t s);
+void gather(int64_t n, const int32_t* perm, const void* src, void* dst, int elemSize, hipStream_t s);
+void gatherMulti(int64_t n, const int32_t* perm, const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,
+                 int elemSize, hipStream_t s);
+size_t scanTempBytes(int64_t n);
+void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s);
+
+// octree.hip
+void nodeCounts(const KeyT* tree, int64_t L, const KeyT* keys, int64_t n, int32_t* counts, hipStream_t s);
+void rebalanceOps(const KeyT* tree, const int32_t* counts, int64_t L, uint32_t bucket, int64_t* ops, int* changed,
+                  hipStream_t s);
+void emitLeavesLaunch(const KeyT* tree, const int64_t* ops, int64_t L, KeyT* out, int64_t newL, hipStream_t s);
+void internalCounts(const KeyT* tree, int64_t L, int64_t* icount, hipStream_t s);
+void makeCodes(const KeyT* tree, int64_t L, const int64_t* ioff, int64_t Ni, KeyT* codes, int32_t* vals,
+               hipStream_t s);
+void linkNodes(const KeyT* codes, const int32_t* vals, int64_t N, int32_t* child, int32_t* parents,
+               int32_t* leafToNode, int64_t* levelRange, hipStream_t s);
+void nodeRanges(const KeyT* codes, int64_t N, const KeyT* keys, int64_t n, int64_t offset, int32_t* ns, int32_t* ne,
+                hipStream_t s);
+void leafBoxes(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
+               const double* y, const double* z, const float* h, double factor, double* center, double* half,
+               hipStream_t s);
+void upsweepBoxes(int64_t a, int64_t b, const int32_t* n2l, const int32_t* child, double* center, double* half,
+                  hipStream_t s);
+void markInBoxes(int64_t nb, const double* bc, const double* bh, const int32_t* child, const int32_t* n2l,
+                 const int32_t* ns, const int32_t* ne, const double* center, const double* half, const double* x,
+                 const double* y, const double* z, const Box& box, uint8_t* flags, hipStream_t s);
+
+// neighbors.hip
+void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
+                   const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int32_t* nc,
+                   int iterateH, unsigned long long* stats, hipStream_t s);
+
+// hydro.hip
+void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y, const double* z,
+           const float* h, const float* m, const float* wh, float* xm, hipStream_t s);
+void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y,
+                const double* z, const float* h, const float* m, const float* wh, const float* whd, const float* xm,
+                float* kx, float* gradh, hipStream_t s);
+void eosVe(int64_t first, int64_t last, const SphConsts& sc, const double* temp, const float* m, const float* kx,
+           const float* xm, const float* gradh, float* prho, float* c, float* rho, float* p, hipStream_t s);
+void eosStd(int64_t first, int64_t last, const SphConsts& sc, const double* temp, const float* m, float* rho,
+            float* p, float* c, hipStream_t s);
+void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y, const double* z,
+         const float* h, const float* wh, const float* numer, const float* denom, float* const cij[6], hipStream_t s);
+void divvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y,
+               const double* z, const float* vx, const float* vy, const float* vz, const float* h,
+               const float* const cij[6], const float* wh, const float* kx, const float* xm, float* divv,
+               float* curlv, float* const dV[6], hipStream_t s);
+void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y,
+                const double* z, const float* vx, const float* vy, const float* vz, const float* h, const float* c,
+                const float* const cij[6], const float* wh, const float* kx, const float* xm, const float* divv,
+                double dt, float* alpha, hipStream_t s);
+void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, const VeMomentumPtrs& p, bool avClean,
+                      float* ax, float* ay, float* az, double* du, float* minDt, hipStream_t s);
+void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, const StdMomentumPtrs& p, float* ax,
+                       float* ay, float* az, double* du, float* minDt, hipStream_t s);
+void updatePositions(int64_t first, int64_t last, double dt, double dt_m1, const PosArgs& p, double cv,
+                     const Box& box, hipStream_t s);
+void updateH(int64_t first, int64_t last, unsigned ng0, const int32_t* nc, float* h, hipStream_t s);
+void conservedQuantities(int64_t first, int64_t last, const double* x, const double* y, const double* z,
+                         const float* vx, const float* vy, const float* vz, const float* m, const double* temp,
+                         const double* u, const int32_t* nc, double cv, double* out, hipStream_t s);
+
+} // namespace sphx::hip

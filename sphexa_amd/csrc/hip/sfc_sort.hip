@@ -1,0 +1,152 @@
+/*! SFC keys, radix sort with reorder map, multi-field gather, scans (gfx950).
+ *
+ * Parity: reference sfc/sfc_gpu.cu:38-54 (computeSfcKeysKernel), primitives/primitives_gpu.cu:85-91,270-338
+ * (gatherGpu, sortByKeyGpu with CUB radix sort, exclusiveScanGpu), primitives/gather.cuh:44-113 (GpuSfcSorter).
+ * Radix sorts go through hipCUB (rocPRIM onesweep on gfx950); keys use 63 bits so the sort runs over [0, 63).
+ */
+#include <hipcub/hipcub.hpp>
+
+#include "common.h"
+#include "hip_api.h"
+#include "sphx/box.hpp"
+
+namespace sphx::hip
+{
+
+__global__ void computeKeysKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                                  const double* __restrict__ z, Box box, int kind, KeyT* __restrict__ keys)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) keys[i] = particleKey(kind, x[i], y[i], z[i], box);
+}
+
+void computeKeys(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind, KeyT* keys,
+                 hipStream_t s)
+{
+    if (n == 0) return;
+    computeKeysKernel<<<gridFor(n, 256), 256, 0, s>>>(n, x, y, z, box, kind, keys);
+    SPHX_LAUNCH_CHECK();
+}
+
+__global__ void iotaKernel(int64_t n, int32_t* out)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = int32_t(i);
+}
+
+size_t sortPairsTempBytes(int64_t n)
+{
+    size_t bytes = 0;
+    SPHX_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const KeyT*)nullptr, (KeyT*)nullptr,
+                                                  (const int32_t*)nullptr, (int32_t*)nullptr, int(n), 0, 64));
+    // room for the iota value array used by sortKeys
+    return bytes + size_t(n) * sizeof(int32_t) + 256;
+}
+
+void sortPairs(int64_t n, const KeyT* keysIn, KeyT* keysOut, const int32_t* valsIn, int32_t* valsOut, void* tmp,
+               size_t tmpBytes, int beginBit, int endBit, hipStream_t s)
+{
+    if (n == 0) return;
+    size_t bytes = tmpBytes;
+    SPHX_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, keysIn, keysOut, valsIn, valsOut, int(n), beginBit,
+                                                  endBit, s));
+}
+
+void sortKeys(int64_t n, const KeyT* keysIn, KeyT* keysOut, int32_t* perm, void* tmp, size_t tmpBytes,
+              hipStream_t s)
+{
+    if (n == 0) return;
+    // carve the iota array off the front of the workspace, hipCUB temp storage follows (256-B aligned)
+    size_t iotaBytes = (size_t(n) * sizeof(int32_t) + 255) & ~size_t(255);
+    int32_t* iota    = static_cast<int32_t*>(tmp);
+    iotaKernel<<<gridFor(n, 256), 256, 0, s>>>(n, iota);
+    sortPairs(n, keysIn, keysOut, iota, perm, static_cast<char*>(tmp) + iotaBytes, tmpBytes - iotaBytes, 0, 63, s);
+}
+
+template<class T>
+__global__ void gatherKernel(int64_t n, const int32_t* __restrict__ perm, const T* __restrict__ src,
+                             T* __restrict__ dst)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[perm[i]];
+}
+
+void gather(int64_t n, const int32_t* perm, const void* src, void* dst, int elemSize, hipStream_t s)
+{
+    if (n == 0) return;
+    if (elemSize == 4)
+        gatherKernel<<<gridFor(n, 256), 256, 0, s>>>(n, perm, (const uint32_t*)src, (uint32_t*)dst);
+    else if (elemSize == 8)
+        gatherKernel<<<gridFor(n, 256), 256, 0, s>>>(n, perm, (const uint64_t*)src, (uint64_t*)dst);
+    else if (elemSize == 1)
+        gatherKernel<<<gridFor(n, 256), 256, 0, s>>>(n, perm, (const uint8_t*)src, (uint8_t*)dst);
+    else throw std::runtime_error("gather: unsupported element size");
+    SPHX_LAUNCH_CHECK();
+}
+
+constexpr int kMaxGatherFields = 16;
+
+template<class T>
+struct FieldPtrs
+{
+    const T* src[kMaxGatherFields];
+    T* dst[kMaxGatherFields];
+};
+
+//! @brief reorder up to 16 fields of one element size with a single read of the permutation
+template<class T>
+__global__ void gatherMultiKernel(int64_t n, const int32_t* __restrict__ perm, FieldPtrs<T> f, int numFields)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t p = perm[i];
+#pragma unroll 4
+    for (int k = 0; k < numFields; ++k)
+        f.dst[k][i] = f.src[k][p];
+}
+
+void gatherMulti(int64_t n, const int32_t* perm, const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,
+                 int elemSize, hipStream_t s)
+{
+    if (n == 0 || src.empty()) return;
+    int nf = int(src.size());
+    if (nf > kMaxGatherFields) throw std::runtime_error("gatherMulti: too many fields");
+    if (elemSize == 4)
+    {
+        FieldPtrs<uint32_t> f;
+        for (int k = 0; k < nf; ++k)
+        {
+            f.src[k] = reinterpret_cast<const uint32_t*>(src[k]);
+            f.dst[k] = reinterpret_cast<uint32_t*>(dst[k]);
+        }
+        gatherMultiKernel<<<gridFor(n, 256), 256, 0, s>>>(n, perm, f, nf);
+    }
+    else if (elemSize == 8)
+    {
+        FieldPtrs<uint64_t> f;
+        for (int k = 0; k < nf; ++k)
+        {
+            f.src[k] = reinterpret_cast<const uint64_t*>(src[k]);
+            f.dst[k] = reinterpret_cast<uint64_t*>(dst[k]);
+        }
+        gatherMultiKernel<<<gridFor(n, 256), 256, 0, s>>>(n, perm, f, nf);
+    }
+    else throw std::runtime_error("gatherMulti: unsupported element size");
+    SPHX_LAUNCH_CHECK();
+}
+
+size_t scanTempBytes(int64_t n)
+{
+    size_t bytes = 0;
+    SPHX_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int64_t*)nullptr, (int64_t*)nullptr, int(n)));
+    return bytes + 256;
+}
+
+void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s)
+{
+    if (n == 0) return;
+    size_t bytes = tmpBytes;
+    SPHX_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, int(n), s));
+}
+
+} // namespace sphx::hip

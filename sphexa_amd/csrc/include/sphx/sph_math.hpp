@@ -4,8 +4,8 @@
  *   sph/include/sph/kernels.hpp            updateH, tsKCourant, artificial_viscosity, symv
  *   sph/include/sph/table_lookup.hpp       linear-interpolated kernel table over [0,2], 20000 points
  *   sph/include/sph/eos.hpp                ideal gas cv / EOS
- *   sph/include/sph/hydro_ve/*_kern.hpp    VE j-loops (xmass, kx/gradh, IAD, divv/curlv, AV switches, momentum)
- *   sph/include/sph/hydro_std/*_kern.hpp   STD j-loops (IAD, momentum)
+ *   sph/include/sph/hydro_ve/(xmass|ve_def_gradh|iad|divv_curlv|av_switches|momentum_energy)_kern.hpp  VE j-loops
+ *   sph/include/sph/hydro_std/(iad|momentum_energy)_kern.hpp                                          STD j-loops
  *   sph/include/sph/positions.hpp          Press position update, AB2 energy update
  *
  * The neighbor list accessor is (nbr, stride): neighbor k of the target is nbr[k*stride]. The CPU path uses

@@ -35,10 +35,13 @@ def init_sedov_fields(d, s):
     width2 = s["width"] ** 2
     d["m"] = m_part
     d["h"] = h_init
-    d["du_m1"] = 0.0
-    d["alpha"] = d.alphamin
+    d.fill_if_allocated("du_m1", 0.0)
+    d.fill_if_allocated("mui", d.muiConst)
+    d.fill_if_allocated("alpha", d.alphamin)
     for f in ("vx", "vy", "vz", "x_m1", "y_m1", "z_m1"):
-        d[f] = 0.0
+        d.fill_if_allocated(f, 0.0)
+    if not d.is_allocated("temp"):
+        return
     cv = ideal_gas_cv(d.muiConst, d.gamma)
     x, y, z = d["x"], d["y"], d["z"]
     r2 = x * x + y * y + z * z

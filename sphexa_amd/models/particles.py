@@ -184,6 +184,11 @@ class ParticlesData:
     def __setitem__(self, name: str, value):
         self[name].copy_(torch.as_tensor(value, dtype=FIELD_DTYPES[name]))
 
+    def fill_if_allocated(self, name: str, value):
+        """set a field if the active propagator uses it (initializers fill optional fields this way)"""
+        if self.is_allocated(name):
+            self[name] = value
+
     def buffer(self, name: str) -> torch.Tensor:
         """the full-capacity storage of a field (used to swap in reordered data)"""
         return self._buf[name]

@@ -1,0 +1,78 @@
+"""Neighbor search vs an N^2 oracle (reference domain/test/unit/neighbors/findneighbors.cpp, all_to_all.hpp)."""
+
+import numpy as np
+import pytest
+import torch
+
+from sphexa_amd.models import particles as P
+from sphexa_amd.ops import octree as O
+from sphexa_amd.ops import sfc
+from sphexa_amd.ops.neighbors import find_neighbors, neighbor_lists_as_sets
+from sphexa_amd.utils.box import Box, OPEN, PERIODIC
+
+
+def _dataset(n, h, box, seed=0):
+    d = P.ParticlesData("cpu")
+    d.set_conserved("x", "y", "z", "h", "m")
+    d.set_dependent("nc", "keys")
+    d.resize(n)
+    g = np.random.default_rng(seed)
+    X = g.uniform(box.lo[0], box.hi[0], size=(n, 3))
+    keys = sfc.compute_keys(*(torch.from_numpy(X[:, k].copy()) for k in range(3)), box)
+    s, p = sfc.sort_keys(keys)
+    X = X[p.numpy()]
+    for k, c in enumerate("xyz"):
+        d[c] = torch.from_numpy(X[:, k].copy())
+    d["h"] = h
+    d["keys"] = s
+    tree, counts = O.update_tree(None, s, 16)
+    ot = O.build_octree(tree, counts, s, d["x"], d["y"], d["z"])
+    return d, ot, X
+
+
+def _all2all(X, h, box):
+    n = len(X)
+    L = np.array(box.lengths())
+    out = []
+    for i in range(n):
+        dx = X - X[i]
+        for k in range(3):
+            if box.bc[k] == PERIODIC:
+                dx[:, k] -= L[k] * np.rint(dx[:, k] / L[k])
+        r2 = (dx * dx).sum(1)
+        nb = set(np.nonzero(r2 < np.float32(4.0) * np.float32(h) * np.float32(h))[0].tolist()) - {i}
+        out.append(nb)
+    return out
+
+
+@pytest.mark.parametrize("bc", [OPEN, PERIODIC])
+def test_neighbors_vs_all2all(bc):
+    box = Box.cube(0.0, 1.0, bc)
+    h = 0.05
+    d, ot, X = _dataset(2000, h, box)
+    d.ngmax = 300
+    nl = find_neighbors(d, ot, box, 0, d.size, iterate_h=False)
+    got = neighbor_lists_as_sets(nl, d["nc"])
+    ref = _all2all(X, np.float32(h), box)
+    assert got == ref
+
+
+def test_h_iteration_targets_ng0():
+    box = Box.cube(0.0, 1.0, PERIODIC)
+    d, ot, X = _dataset(4000, 0.01, box, seed=2)  # far too few neighbors initially
+    d.ng0, d.ngmax = 50, 150
+    find_neighbors(d, ot, box, 0, d.size, iterate_h=True)
+    nc = d["nc"].numpy()
+    assert (nc >= d.ng0 // 4).all() and (nc - 1 <= d.ngmax).all()
+    assert d.nc_fail == 0
+
+
+def test_ngmax_capping():
+    box = Box.cube(0.0, 1.0, OPEN)
+    d, ot, X = _dataset(1500, 0.15, box, seed=3)
+    d.ngmax = 20
+    nl = find_neighbors(d, ot, box, 0, d.size, iterate_h=False)
+    nc = d["nc"].numpy()
+    assert nc.max() - 1 > 20  # counts are not capped
+    sets = neighbor_lists_as_sets(nl, d["nc"])
+    assert max(len(s) for s in sets) == 20
