@@ -32,6 +32,9 @@ void iad(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const u
 void divvCurlv(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*, const double*,
                const double*, const double*, const float*, const float*, const float*, const float*,
                const float* const[6], const float*, const float*, const float*, float*, float*, float* const[6]);
+void iadDivvCurlv(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*, const double*,
+                  const double*, const double*, const float*, const float*, const float*, const float*,
+                  float* const[6], const float*, const float*, const float*, float*, float*, float* const[6]);
 void avSwitches(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*, const double*,
                 const double*, const double*, const float*, const float*, const float*, const float*, const float*,
                 const float* const[6], const float*, const float*, const float*, const float*, double, float*);
@@ -272,6 +275,19 @@ PYBIND11_MODULE(_sphx_cpu, m)
                              P<float>(curlv), g.data());
           });
 
+    m.def("iad_divv_curlv",
+          [](int64_t first, int64_t last, const ConstArr& sc, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y,
+             Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr h, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
+             Ptr curlv, const std::array<Ptr, 6>& dV)
+          {
+              auto c = six(cij);
+              auto g = six(dV);
+              cpu::iadDivvCurlv(first, last, toConsts(sc), toBox(box), P<int32_t>(nidx), P<uint32_t>(nc),
+                                P<double>(x), P<double>(y), P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz),
+                                P<float>(h), c.data(), P<float>(wh), P<float>(kx), P<float>(xm), P<float>(divv),
+                                P<float>(curlv), g.data());
+          });
+
     m.def("av_switches",
           [](int64_t first, int64_t last, const ConstArr& sc, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y,
              Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr c, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm,
@@ -292,7 +308,7 @@ PYBIND11_MODULE(_sphx_cpu, m)
              Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr prho, Ptr c, const std::array<Ptr, 6>& cij, Ptr kx,
              Ptr xm, Ptr alpha, const std::array<Ptr, 6>& dV, Ptr wh, bool avClean, Ptr ax, Ptr ay, Ptr az, Ptr du)
           {
-              VeMomentumPtrs p;
+              cpu::VeMomentumPtrs p;
               p.x = P<double>(x);
               p.y = P<double>(y);
               p.z = P<double>(z);
@@ -321,7 +337,7 @@ PYBIND11_MODULE(_sphx_cpu, m)
              Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr rho, Ptr p_, Ptr c, const std::array<Ptr, 6>& cij,
              Ptr wh, Ptr ax, Ptr ay, Ptr az, Ptr du)
           {
-              StdMomentumPtrs p;
+              cpu::StdMomentumPtrs p;
               p.x = P<double>(x);
               p.y = P<double>(y);
               p.z = P<double>(z);

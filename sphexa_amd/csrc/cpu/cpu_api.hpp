@@ -10,6 +10,25 @@
 namespace sphx::cpu
 {
 
+//! @brief SoA field pointers of the VE momentum loop (assembled into SrcMom records by SoaMom)
+struct VeMomentumPtrs
+{
+    const CT *x, *y, *z;
+    const HT *vx, *vy, *vz, *h, *m, *prho, *c;
+    const HT* cij[6];
+    const HT *kx, *xm, *alpha;
+    const HT* dV[6];
+    const HT* wh;
+};
+
+struct StdMomentumPtrs
+{
+    const CT *x, *y, *z;
+    const HT *vx, *vy, *vz, *h, *m, *rho, *p, *c;
+    const HT* cij[6];
+    const HT* wh;
+};
+
 struct LinkedOctree
 {
     int64_t numNodes{0};

@@ -3,7 +3,8 @@
  * Parity: reference domain/include/cstone/findneighbors.hpp:95-195 (per-particle octree search, radius 2h,
  * PBC minimum image, capped at ngmax, count excludes self), sph/include/sph/find_neighbors.hpp:12-56
  * (h re-iteration up to 10x until ng0/4 <= nc <= ngmax+1), hydro_ve and hydro_std wrappers,
- * positions.hpp, update_h.hpp, timestep.hpp.
+ * positions.hpp, update_h.hpp, timestep.hpp. The j-loop math is shared with the gfx950 kernels (sph_math.hpp);
+ * here sources are read through SoA loaders.
  */
 #include <cmath>
 #include <limits>
@@ -88,20 +89,22 @@ void xmass(int64_t first, int64_t last, const SphConsts& sc, const Box& box, con
            const double* x, const double* y, const double* z, const float* h, const float* m, const float* wh,
            float* xm)
 {
+    SoaPos ld{x, y, z, m, nullptr};
 #pragma omp parallel for schedule(static)
     for (int64_t i = first; i < last; ++i)
-        xm[i] = xmassJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), x, y,
-                           z, h, m, wh);
+        xm[i] = xmassJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i], ld,
+                           wh);
 }
 
 void veDefGradh(int64_t first, int64_t last, const SphConsts& sc, const Box& box, const int32_t* nidx,
                 const uint32_t* nc, const double* x, const double* y, const double* z, const float* h, const float* m,
                 const float* wh, const float* whd, const float* xm, float* kx, float* gradh)
 {
+    SoaPos ld{x, y, z, m, xm};
 #pragma omp parallel for schedule(static)
     for (int64_t i = first; i < last; ++i)
-        veDefGradhJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), x, y, z,
-                        h, m, wh, whd, xm, kx[i], gradh[i]);
+        veDefGradhJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i], ld,
+                        wh, whd, kx[i], gradh[i]);
 }
 
 void eosVe(int64_t first, int64_t last, const SphConsts& sc, const double* temp, const float* m, const float* kx,
@@ -139,12 +142,12 @@ void iad(int64_t first, int64_t last, const SphConsts& sc, const Box& box, const
          const double* x, const double* y, const double* z, const float* h, const float* wh, const float* numer,
          const float* denom, float* const cij[6])
 {
+    SoaIad ld{x, y, z, numer, denom, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 #pragma omp parallel for schedule(static)
     for (int64_t i = first; i < last; ++i)
     {
         float c[6];
-        iadJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), x, y, z, h, wh,
-                 numer, denom, c);
+        iadJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i], ld, wh, c);
         for (int k = 0; k < 6; ++k)
             cij[k][i] = c[k];
     }
@@ -156,15 +159,38 @@ void divvCurlv(int64_t first, int64_t last, const SphConsts& sc, const Box& box,
                const float* kx, const float* xm, float* divv, float* curlv, float* const dV[6])
 {
     bool doGrad = dV[0] != nullptr;
+    SoaIad ld{x, y, z, nullptr, nullptr, vx, vy, vz, xm, nullptr, nullptr};
 #pragma omp parallel for schedule(static)
     for (int64_t i = first; i < last; ++i)
     {
         float g[6];
-        divvCurlvJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), x, y, z,
-                       vx, vy, vz, h, cij, wh, kx, xm, divv[i], curlv[i], doGrad ? g : nullptr);
+        float ci[6] = {cij[0][i], cij[1][i], cij[2][i], cij[3][i], cij[4][i], cij[5][i]};
+        divvCurlvJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i], kx[i],
+                       ci, ld, wh, divv[i], curlv[i], doGrad ? g : nullptr);
         if (doGrad)
             for (int k = 0; k < 6; ++k)
                 dV[k][i] = g[k];
+    }
+}
+
+void iadDivvCurlv(int64_t first, int64_t last, const SphConsts& sc, const Box& box, const int32_t* nidx,
+                  const uint32_t* nc, const double* x, const double* y, const double* z, const float* vx,
+                  const float* vy, const float* vz, const float* h, float* const cij[6], const float* wh,
+                  const float* kx, const float* xm, float* divv, float* curlv, float* const dV[6])
+{
+    bool doGrad = dV[0] != nullptr;
+    SoaIad ld{x, y, z, xm, kx, vx, vy, vz, xm, nullptr, nullptr};
+#pragma omp parallel for schedule(static)
+    for (int64_t i = first; i < last; ++i)
+    {
+        float c[6], g[6];
+        iadDivvCurlvJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i],
+                          kx[i], ld, wh, c, divv[i], curlv[i], doGrad ? g : nullptr);
+        for (int k = 0; k < 6; ++k)
+        {
+            cij[k][i] = c[k];
+            if (doGrad) dV[k][i] = g[k];
+        }
     }
 }
 
@@ -173,17 +199,23 @@ void avSwitches(int64_t first, int64_t last, const SphConsts& sc, const Box& box
                 const float* vy, const float* vz, const float* h, const float* c, const float* const cij[6],
                 const float* wh, const float* kx, const float* xm, const float* divv, double dt, float* alpha)
 {
+    SoaIad ld{x, y, z, xm, kx, vx, vy, vz, xm, c, divv};
 #pragma omp parallel for schedule(static)
     for (int64_t i = first; i < last; ++i)
-        alpha[i] = avSwitchesJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax),
-                                   x, y, z, vx, vy, vz, h, c, cij, wh, kx, xm, divv, dt, sc.alphamin, sc.alphamax,
-                                   sc.decayConstant, alpha[i]);
+    {
+        float ci[6] = {cij[0][i], cij[1][i], cij[2][i], cij[3][i], cij[4][i], cij[5][i]};
+        alpha[i]    = avSwitchesJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax),
+                                      h[i], ci, ld, wh, dt, sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
+    }
 }
 
 double momentumEnergyVe(int64_t first, int64_t last, const SphConsts& sc, const Box& box, const int32_t* nidx,
                         const uint32_t* nc, const VeMomentumPtrs& p, bool avClean, float* ax, float* ay, float* az,
                         double* du)
 {
+    SoaMom ld{p.x,      p.y,      p.z,      p.vx,     p.vy,  p.vz, p.h,  p.cij[0], p.cij[1], p.cij[2],
+              p.cij[3], p.cij[4], p.cij[5], p.m,      p.c,   p.xm, p.kx, p.prho,   p.alpha};
+    SoaGradV ldg{{p.dV[0], p.dV[1], p.dV[2], p.dV[3], p.dV[4], p.dV[5]}};
     double minDt = std::numeric_limits<double>::infinity();
 #pragma omp parallel for schedule(static) reduction(min : minDt)
     for (int64_t i = first; i < last; ++i)
@@ -191,8 +223,10 @@ double momentumEnergyVe(int64_t first, int64_t last, const SphConsts& sc, const 
         float mvs;
         const int32_t* nb = nidx + (i - first) * sc.ngmax;
         unsigned n        = capped(nc, i, sc.ngmax);
-        if (avClean) momentumEnergyJLoop<true>(unsigned(i), sc, box, nb, 1, n, p, ax[i], ay[i], az[i], du[i], mvs);
-        else momentumEnergyJLoop<false>(unsigned(i), sc, box, nb, 1, n, p, ax[i], ay[i], az[i], du[i], mvs);
+        if (avClean)
+            momentumEnergyJLoop<true>(unsigned(i), sc, box, nb, 1, n, ld, ldg, p.wh, ax[i], ay[i], az[i], du[i], mvs);
+        else
+            momentumEnergyJLoop<false>(unsigned(i), sc, box, nb, 1, n, ld, ldg, p.wh, ax[i], ay[i], az[i], du[i], mvs);
         float dti = tsKCourant(mvs, p.h[i], p.c[i], float(sc.Kcour));
         minDt     = std::min(minDt, double(dti));
     }
@@ -202,13 +236,15 @@ double momentumEnergyVe(int64_t first, int64_t last, const SphConsts& sc, const 
 double momentumEnergyStd(int64_t first, int64_t last, const SphConsts& sc, const Box& box, const int32_t* nidx,
                          const uint32_t* nc, const StdMomentumPtrs& p, float* ax, float* ay, float* az, double* du)
 {
+    SoaStd ld{p.x,      p.y,      p.z,      p.vx,     p.vy,     p.vz, p.h,   p.cij[0], p.cij[1],
+              p.cij[2], p.cij[3], p.cij[4], p.cij[5], p.m,      p.rho, p.p,  p.c};
     double minDt = std::numeric_limits<double>::infinity();
 #pragma omp parallel for schedule(static) reduction(min : minDt)
     for (int64_t i = first; i < last; ++i)
     {
         float mvs;
-        momentumEnergyStdJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), p,
-                               ax[i], ay[i], az[i], du[i], mvs);
+        momentumEnergyStdJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), ld,
+                               p.wh, ax[i], ay[i], az[i], du[i], mvs);
         float dti = tsKCourant(mvs, p.h[i], p.c[i], float(sc.Kcour));
         minDt     = std::min(minDt, double(dti));
     }
@@ -280,11 +316,6 @@ void updateSmoothingLength(int64_t first, int64_t last, unsigned ng0, const uint
     for (int64_t i = first; i < last; ++i)
         h[i] = updateH(ng0, nc[i], h[i]);
 }
-
-} // namespace sphx::cpu
-
-namespace sphx::cpu
-{
 
 //! @brief [eKin, eInt, -, linmom xyz, angmom xyz, sum nc] over [first, last) (reference conserved_quantities.hpp)
 void conservedQuantities(int64_t first, int64_t last, const double* x, const double* y, const double* z,

@@ -178,20 +178,22 @@ PYBIND11_MODULE(_sphx_hip, m)
           });
 
     // ---------------------------------------------------------------------------------------------- hydro
+    // same argument lists as the OpenMP module, plus (ntot, record workspace(s), stream)
     m.def("xmass", [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x,
-                      Ptr y, Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr xm, Ptr s)
+                      Ptr y, Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr xm, int64_t ntot, Ptr rec, Ptr s)
           {
               auto sc = toConsts(c);
-              xmass(nbr(first, last, nidx, nc, sc), sc, toBox(box), P<double>(x), P<double>(y), P<double>(z),
-                    P<float>(h), P<float>(mm), P<float>(wh), P<float>(xm), St(s));
+              xmass(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y), P<double>(z),
+                    P<float>(h), P<float>(mm), P<float>(wh), P<void>(rec), P<float>(xm), St(s));
           });
     m.def("ve_def_gradh", [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc,
-                             Ptr x, Ptr y, Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr whd, Ptr xm, Ptr kx, Ptr gradh, Ptr s)
+                             Ptr x, Ptr y, Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr whd, Ptr xm, Ptr kx, Ptr gradh,
+                             int64_t ntot, Ptr rec, Ptr s)
           {
               auto sc = toConsts(c);
-              veDefGradh(nbr(first, last, nidx, nc, sc), sc, toBox(box), P<double>(x), P<double>(y), P<double>(z),
-                         P<float>(h), P<float>(mm), P<float>(wh), P<float>(whd), P<float>(xm), P<float>(kx),
-                         P<float>(gradh), St(s));
+              veDefGradh(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
+                         P<double>(z), P<float>(h), P<float>(mm), P<float>(wh), P<float>(whd), P<float>(xm),
+                         P<void>(rec), P<float>(kx), P<float>(gradh), St(s));
           });
     m.def("eos_ve", [](int64_t first, int64_t last, const ConstArr& c, Ptr temp, Ptr mm, Ptr kx, Ptr xm, Ptr gradh,
                        Ptr prho, Ptr cc, Ptr rho, Ptr p, Ptr s)
@@ -206,89 +208,91 @@ PYBIND11_MODULE(_sphx_hip, m)
                      P<float>(cc), St(s));
           });
     m.def("iad", [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y,
-                    Ptr z, Ptr h, Ptr wh, Ptr numer, Ptr denom, const std::array<Ptr, 6>& cij, Ptr s)
+                    Ptr z, Ptr h, Ptr wh, Ptr numer, Ptr denom, const std::array<Ptr, 6>& cij, int64_t ntot, Ptr rec,
+                    Ptr s)
           {
               auto sc = toConsts(c);
               auto cp = six(cij);
-              iad(nbr(first, last, nidx, nc, sc), sc, toBox(box), P<double>(x), P<double>(y), P<double>(z),
-                  P<float>(h), P<float>(wh), P<float>(numer), P<float>(denom), cp.data(), St(s));
+              iad(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y), P<double>(z),
+                  P<float>(h), P<float>(wh), P<float>(numer), P<float>(denom), P<void>(rec), cp.data(), St(s));
           });
-    m.def("divv_curlv",
+    m.def("iad_divv_curlv",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
-             Ptr curlv, const std::array<Ptr, 6>& dV, Ptr s)
+             Ptr curlv, const std::array<Ptr, 6>& dV, int64_t ntot, Ptr rec, Ptr s)
           {
               auto sc = toConsts(c);
-              auto cp = csix(cij);
+              auto cp = six(cij);
               auto g  = six(dV);
-              divvCurlv(nbr(first, last, nidx, nc, sc), sc, toBox(box), P<double>(x), P<double>(y), P<double>(z),
-                        P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), cp.data(), P<float>(wh), P<float>(kx),
-                        P<float>(xm), P<float>(divv), P<float>(curlv), g.data(), St(s));
+              iadDivvCurlv(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
+                           P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(wh),
+                           P<float>(kx), P<float>(xm), P<void>(rec), cp.data(), P<float>(divv), P<float>(curlv),
+                           g.data(), St(s));
           });
     m.def("av_switches",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr cs, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
-             double dt, Ptr alpha, Ptr s)
+             double dt, Ptr alpha, int64_t ntot, Ptr rec, Ptr s)
           {
               auto sc = toConsts(c);
-              auto cp = csix(cij);
-              avSwitches(nbr(first, last, nidx, nc, sc), sc, toBox(box), P<double>(x), P<double>(y), P<double>(z),
-                         P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(cs), cp.data(),
-                         P<float>(wh), P<float>(kx), P<float>(xm), P<float>(divv), dt, P<float>(alpha), St(s));
+              auto cp = six(cij);
+              avSwitches(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
+                         P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(cs), cp.data(),
+                         P<float>(wh), P<float>(kx), P<float>(xm), P<float>(divv), dt, P<void>(rec), P<float>(alpha),
+                         St(s));
           });
     m.def("momentum_energy_ve",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr prho, Ptr cs, const std::array<Ptr, 6>& cij, Ptr kx, Ptr xm,
              Ptr alpha, const std::array<Ptr, 6>& dV, Ptr wh, bool avClean, Ptr ax, Ptr ay, Ptr az, Ptr du,
-             Ptr minDt, Ptr s)
+             Ptr minDt, int64_t ntot, Ptr rec, Ptr rec2, Ptr s)
           {
               auto sc = toConsts(c);
-              VeMomentumPtrs p;
-              p.x    = P<double>(x);
-              p.y    = P<double>(y);
-              p.z    = P<double>(z);
-              p.vx   = P<float>(vx);
-              p.vy   = P<float>(vy);
-              p.vz   = P<float>(vz);
-              p.h    = P<float>(h);
-              p.m    = P<float>(mm);
-              p.prho = P<float>(prho);
-              p.c    = P<float>(cs);
+              MomFields f;
+              f.x    = P<double>(x);
+              f.y    = P<double>(y);
+              f.z    = P<double>(z);
+              f.vx   = P<float>(vx);
+              f.vy   = P<float>(vy);
+              f.vz   = P<float>(vz);
+              f.h    = P<float>(h);
+              f.m    = P<float>(mm);
+              f.prho = P<float>(prho);
+              f.c    = P<float>(cs);
               for (int k = 0; k < 6; ++k)
               {
-                  p.cij[k] = P<float>(cij[k]);
-                  p.dV[k]  = P<float>(dV[k]);
+                  f.cij[k] = P<float>(cij[k]);
+                  f.dV[k]  = P<float>(dV[k]);
               }
-              p.kx    = P<float>(kx);
-              p.xm    = P<float>(xm);
-              p.alpha = P<float>(alpha);
-              p.wh    = P<float>(wh);
-              momentumEnergyVe(nbr(first, last, nidx, nc, sc), sc, toBox(box), p, avClean, P<float>(ax), P<float>(ay),
-                               P<float>(az), P<double>(du), P<float>(minDt), St(s));
+              f.kx    = P<float>(kx);
+              f.xm    = P<float>(xm);
+              f.alpha = P<float>(alpha);
+              momentumEnergyVe(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, f, avClean, P<float>(wh),
+                               P<void>(rec), P<void>(rec2), P<float>(ax), P<float>(ay), P<float>(az), P<double>(du),
+                               P<float>(minDt), St(s));
           });
     m.def("momentum_energy_std",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr rho, Ptr pp, Ptr cs, const std::array<Ptr, 6>& cij, Ptr wh,
-             Ptr ax, Ptr ay, Ptr az, Ptr du, Ptr minDt, Ptr s)
+             Ptr ax, Ptr ay, Ptr az, Ptr du, Ptr minDt, int64_t ntot, Ptr rec, Ptr s)
           {
               auto sc = toConsts(c);
-              StdMomentumPtrs p;
-              p.x   = P<double>(x);
-              p.y   = P<double>(y);
-              p.z   = P<double>(z);
-              p.vx  = P<float>(vx);
-              p.vy  = P<float>(vy);
-              p.vz  = P<float>(vz);
-              p.h   = P<float>(h);
-              p.m   = P<float>(mm);
-              p.rho = P<float>(rho);
-              p.p   = P<float>(pp);
-              p.c   = P<float>(cs);
+              StdFields f;
+              f.x   = P<double>(x);
+              f.y   = P<double>(y);
+              f.z   = P<double>(z);
+              f.vx  = P<float>(vx);
+              f.vy  = P<float>(vy);
+              f.vz  = P<float>(vz);
+              f.h   = P<float>(h);
+              f.m   = P<float>(mm);
+              f.rho = P<float>(rho);
+              f.p   = P<float>(pp);
+              f.c   = P<float>(cs);
               for (int k = 0; k < 6; ++k)
-                  p.cij[k] = P<float>(cij[k]);
-              p.wh = P<float>(wh);
-              momentumEnergyStd(nbr(first, last, nidx, nc, sc), sc, toBox(box), p, P<float>(ax), P<float>(ay),
-                                P<float>(az), P<double>(du), P<float>(minDt), St(s));
+                  f.cij[k] = P<float>(cij[k]);
+              momentumEnergyStd(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, f, P<float>(wh), P<void>(rec),
+                                P<float>(ax), P<float>(ay), P<float>(az), P<double>(du), P<float>(minDt), St(s));
           });
     m.def("update_positions",
           [](int64_t first, int64_t last, double dt, double dtm1, Ptr x, Ptr y, Ptr z, Ptr vx, Ptr vy, Ptr vz,

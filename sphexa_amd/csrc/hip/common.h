@@ -33,6 +33,16 @@ inline unsigned gridFor(int64_t n, int block) { return unsigned((n + block - 1) 
 
 inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+/*! @brief XCD-aware block remap: blocks that the dispatcher deals to one XCD (b % 8 equal) get a contiguous range
+ *         of logical blocks, so spatially adjacent target groups (which share most neighbors) hit the same L2.
+ *         Bijective for any grid size (cdna_hip_programming.md T1, bijective variant).
+ */
+__device__ __forceinline__ unsigned xcdRemap(unsigned b, unsigned nb)
+{
+    unsigned xcd = b & 7u, q = nb >> 3, r = nb & 7u;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
 //! @brief lanes below this lane in a 64-bit mask
 __device__ __forceinline__ uint64_t lanemaskLt()
 {

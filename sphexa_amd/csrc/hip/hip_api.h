@@ -80,29 +80,48 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
                    int iterateH, unsigned long long* stats, hipStream_t s);
 
 // hydro.hip
-void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y, const double* z,
-           const float* h, const float* m, const float* wh, float* xm, hipStream_t s);
-void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y,
-                const double* z, const float* h, const float* m, const float* wh, const float* whd, const float* xm,
-                float* kx, float* gradh, hipStream_t s);
+struct MomFields
+{
+    const double *x, *y, *z;
+    const float *vx, *vy, *vz, *h, *m, *prho, *c;
+    const float* cij[6];
+    const float *kx, *xm, *alpha;
+    const float* dV[6];
+};
+
+struct StdFields
+{
+    const double *x, *y, *z;
+    const float *vx, *vy, *vz, *h, *m, *rho, *p, *c;
+    const float* cij[6];
+};
+
+void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x, const double* y,
+           const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s);
+void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
+                const double* y, const double* z, const float* h, const float* m, const float* wh, const float* whd,
+                const float* xm, void* rec, float* kx, float* gradh, hipStream_t s);
 void eosVe(int64_t first, int64_t last, const SphConsts& sc, const double* temp, const float* m, const float* kx,
            const float* xm, const float* gradh, float* prho, float* c, float* rho, float* p, hipStream_t s);
 void eosStd(int64_t first, int64_t last, const SphConsts& sc, const double* temp, const float* m, float* rho,
             float* p, float* c, hipStream_t s);
-void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y, const double* z,
-         const float* h, const float* wh, const float* numer, const float* denom, float* const cij[6], hipStream_t s);
-void divvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y,
-               const double* z, const float* vx, const float* vy, const float* vz, const float* h,
-               const float* const cij[6], const float* wh, const float* kx, const float* xm, float* divv,
-               float* curlv, float* const dV[6], hipStream_t s);
-void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y,
-                const double* z, const float* vx, const float* vy, const float* vz, const float* h, const float* c,
-                const float* const cij[6], const float* wh, const float* kx, const float* xm, const float* divv,
-                double dt, float* alpha, hipStream_t s);
-void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, const VeMomentumPtrs& p, bool avClean,
-                      float* ax, float* ay, float* az, double* du, float* minDt, hipStream_t s);
-void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, const StdMomentumPtrs& p, float* ax,
-                       float* ay, float* az, double* du, float* minDt, hipStream_t s);
+void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x, const double* y,
+         const double* z, const float* h, const float* wh, const float* numer, const float* denom, void* rec,
+         float* const cij[6], hipStream_t s);
+void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
+                  const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
+                  const float* wh, const float* kx, const float* xm, void* rec, float* const cij[6], float* divv,
+                  float* curlv, float* const dV[6], hipStream_t s);
+void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
+                const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
+                const float* c, float* const cij[6], const float* wh, const float* kx, const float* xm,
+                const float* divv, double dt, void* rec, float* alpha, hipStream_t s);
+void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const MomFields& f,
+                      bool avClean, const float* wh, void* rec, void* recGradV, float* ax, float* ay, float* az,
+                      double* du, float* minDt, hipStream_t s);
+void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const StdFields& f,
+                       const float* wh, void* rec, float* ax, float* ay, float* az, double* du, float* minDt,
+                       hipStream_t s);
 void updatePositions(int64_t first, int64_t last, double dt, double dt_m1, const PosArgs& p, double cv,
                      const Box& box, hipStream_t s);
 void updateH(int64_t first, int64_t last, unsigned ng0, const int32_t* nc, float* h, hipStream_t s);

@@ -1,9 +1,18 @@
 /*! SPH loops on gfx950: VE and STD formulations, EOS, integration, h update, conserved-quantity reductions.
  *
  * Parity: reference sph/include/sph/hydro_ve/(..)_gpu.cu, hydro_std/(..)_gpu.cu, positions_gpu.cu:38-108,
- * update_h_gpu.cu:77-96, observables/conserved_gpu.cu:53-107. The pair math is the shared sphx/sph_math.hpp used
- * by the OpenMP path too. Neighbor lists come from the wave64 search (lane-interleaved, stride 64), so a wave's
- * step-k index load is one coalesced 256-byte transaction.
+ * update_h_gpu.cu:77-96, observables/conserved_gpu.cu:53-107.
+ *
+ * MI355X design (vs the reference's one-thread-per-target loop that gathers every neighbor field separately):
+ *   * every neighbor loop first packs the source fields it needs into a 16-byte aligned array of records (one
+ *     streaming pass), so a neighbor costs 2-8 dwordx4 loads of one contiguous 32-128 B record instead of up to 21
+ *     scattered 4/8-byte gathers;
+ *   * neighbor lists come from the wave64 search, lane-interleaved, so the index load of step k is one coalesced
+ *     256-byte access per wave;
+ *   * blocks are remapped so each XCD walks a contiguous SFC range of target groups (shared neighbors stay in that
+ *     XCD's L2);
+ *   * IAD and the velocity divergence/curl run in one kernel (c_ij of the target is all divv needs).
+ * The pair math is sphx/sph_math.hpp, shared with the OpenMP path.
  */
 #include <cfloat>
 
@@ -14,10 +23,13 @@
 namespace sphx::hip
 {
 
+constexpr int kBlock = 256;
+
 __device__ __forceinline__ bool targetOf(const NbrArgs& a, int64_t& i, const int32_t*& nbr, unsigned& n)
 {
-    int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    i         = a.first + t;
+    unsigned lb = xcdRemap(blockIdx.x, gridDim.x);
+    int64_t t   = int64_t(lb) * kBlock + threadIdx.x;
+    i           = a.first + t;
     if (i >= a.last) return false;
     int64_t g = t >> 6;
     nbr       = a.nidx + g * int64_t(a.ngmax) * 64 + (t & 63);
@@ -26,33 +38,132 @@ __device__ __forceinline__ bool targetOf(const NbrArgs& a, int64_t& i, const int
     return true;
 }
 
-inline unsigned grid256(const NbrArgs& a) { return gridFor(a.last - a.first, 256); }
+inline unsigned gridT(const NbrArgs& a) { return gridFor(a.last - a.first, kBlock); }
 
-__global__ __launch_bounds__(256) void xmassKernel(NbrArgs a, SphConsts sc, Box box, const double* __restrict__ x,
-                                                   const double* __restrict__ y, const double* __restrict__ z,
-                                                   const float* __restrict__ h, const float* __restrict__ m,
-                                                   const float* __restrict__ wh, float* __restrict__ xm)
+// ------------------------------------------------------------------------------------------------- packing
+
+__global__ void packPosKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                              const double* __restrict__ z, const float* __restrict__ m,
+                              const float* __restrict__ xm, SrcPos* __restrict__ out)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcPos r;
+    r.x    = x[i];
+    r.y    = y[i];
+    r.z    = z[i];
+    r.m    = m[i];
+    r.xm   = xm ? xm[i] : 0.f;
+    out[i] = r;
+}
+
+__global__ void packIadKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                              const double* __restrict__ z, const float* __restrict__ numer,
+                              const float* __restrict__ denom, const float* __restrict__ vx,
+                              const float* __restrict__ vy, const float* __restrict__ vz,
+                              const float* __restrict__ xm, const float* __restrict__ c,
+                              const float* __restrict__ divv, SrcIad* __restrict__ out)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcIad r;
+    r.x    = x[i];
+    r.y    = y[i];
+    r.z    = z[i];
+    r.vol  = numer ? numer[i] / denom[i] : 0.f;
+    r.vx   = vx ? vx[i] : 0.f;
+    r.vy   = vy ? vy[i] : 0.f;
+    r.vz   = vz ? vz[i] : 0.f;
+    r.xm   = xm ? xm[i] : 0.f;
+    r.c    = c ? c[i] : 0.f;
+    r.divv = divv ? divv[i] : 0.f;
+    out[i] = r;
+}
+
+__global__ void packMomKernel(int64_t n, MomFields f, SrcMom* __restrict__ out, SrcGradV* __restrict__ gv)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcMom r;
+    r.x     = f.x[i];
+    r.y     = f.y[i];
+    r.z     = f.z[i];
+    r.vx    = f.vx[i];
+    r.vy    = f.vy[i];
+    r.vz    = f.vz[i];
+    r.h     = f.h[i];
+    r.c11   = f.cij[0][i];
+    r.c12   = f.cij[1][i];
+    r.c13   = f.cij[2][i];
+    r.c22   = f.cij[3][i];
+    r.c23   = f.cij[4][i];
+    r.c33   = f.cij[5][i];
+    r.m     = f.m[i];
+    r.c     = f.c[i];
+    r.xm    = f.xm[i];
+    r.rho   = f.kx[i] * f.m[i] / f.xm[i];
+    r.prho  = f.prho[i];
+    r.alpha = f.alpha[i];
+    out[i]  = r;
+    if (gv)
+    {
+        SrcGradV g;
+        for (int k = 0; k < 6; ++k)
+            g.dV[k] = f.dV[k][i];
+        g.pad[0] = g.pad[1] = 0.f;
+        gv[i]                = g;
+    }
+}
+
+__global__ void packStdKernel(int64_t n, StdFields f, SrcStd* __restrict__ out)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcStd r;
+    r.x    = f.x[i];
+    r.y    = f.y[i];
+    r.z    = f.z[i];
+    r.vx   = f.vx[i];
+    r.vy   = f.vy[i];
+    r.vz   = f.vz[i];
+    r.h    = f.h[i];
+    r.c11  = f.cij[0][i];
+    r.c12  = f.cij[1][i];
+    r.c13  = f.cij[2][i];
+    r.c22  = f.cij[3][i];
+    r.c23  = f.cij[4][i];
+    r.c33  = f.cij[5][i];
+    r.m    = f.m[i];
+    r.rho  = f.rho[i];
+    r.p    = f.p[i];
+    r.c    = f.c[i];
+    out[i] = r;
+}
+
+// ------------------------------------------------------------------------------------------------ VE loops
+
+__global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, Box box, const float* __restrict__ h,
+                                                      const SrcPos* __restrict__ rec, const float* __restrict__ wh,
+                                                      float* __restrict__ xm)
 {
     int64_t i;
     const int32_t* nbr;
     unsigned n;
     if (!targetOf(a, i, nbr, n)) return;
-    xm[i] = xmassJLoop(unsigned(i), sc.K, box, nbr, 64, n, x, y, z, h, m, wh);
+    xm[i] = xmassJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcPos>{rec}, wh);
 }
 
-__global__ __launch_bounds__(256) void veDefGradhKernel(NbrArgs a, SphConsts sc, Box box, const double* __restrict__ x,
-                                                        const double* __restrict__ y, const double* __restrict__ z,
-                                                        const float* __restrict__ h, const float* __restrict__ m,
-                                                        const float* __restrict__ wh, const float* __restrict__ whd,
-                                                        const float* __restrict__ xm, float* __restrict__ kx,
-                                                        float* __restrict__ gradh)
+__global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts sc, Box box,
+                                                           const float* __restrict__ h, const SrcPos* __restrict__ rec,
+                                                           const float* __restrict__ wh, const float* __restrict__ whd,
+                                                           float* __restrict__ kx, float* __restrict__ gradh)
 {
     int64_t i;
     const int32_t* nbr;
     unsigned n;
     if (!targetOf(a, i, nbr, n)) return;
     float k, g;
-    veDefGradhJLoop(unsigned(i), sc.K, box, nbr, 64, n, x, y, z, h, m, wh, whd, xm, k, g);
+    veDefGradhJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcPos>{rec}, wh, whd, k, g);
     kx[i]    = k;
     gradh[i] = g;
 }
@@ -92,43 +203,38 @@ struct Six
     float* p[6];
 };
 
-struct CSix
-{
-    const float* p[6];
-};
-
-__global__ __launch_bounds__(256) void iadKernel(NbrArgs a, SphConsts sc, Box box, const double* __restrict__ x,
-                                                 const double* __restrict__ y, const double* __restrict__ z,
-                                                 const float* __restrict__ h, const float* __restrict__ wh,
-                                                 const float* __restrict__ numer, const float* __restrict__ denom,
-                                                 Six cij)
+__global__ __launch_bounds__(kBlock) void iadKernel(NbrArgs a, SphConsts sc, Box box, const float* __restrict__ h,
+                                                    const SrcIad* __restrict__ rec, const float* __restrict__ wh,
+                                                    Six cij)
 {
     int64_t i;
     const int32_t* nbr;
     unsigned n;
     if (!targetOf(a, i, nbr, n)) return;
     float c[6];
-    iadJLoop(unsigned(i), sc.K, box, nbr, 64, n, x, y, z, h, wh, numer, denom, c);
+    iadJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcIad>{rec}, wh, c);
     for (int k = 0; k < 6; ++k)
         cij.p[k][i] = c[k];
 }
 
-__global__ __launch_bounds__(256) void divvCurlvKernel(NbrArgs a, SphConsts sc, Box box, const double* __restrict__ x,
-                                                       const double* __restrict__ y, const double* __restrict__ z,
-                                                       const float* __restrict__ vx, const float* __restrict__ vy,
-                                                       const float* __restrict__ vz, const float* __restrict__ h,
-                                                       CSix cij, const float* __restrict__ wh,
-                                                       const float* __restrict__ kx, const float* __restrict__ xm,
-                                                       float* __restrict__ divv, float* __restrict__ curlv, Six dV,
-                                                       int doGrad)
+//! @brief IAD matrix, then divv/curlv (+ velocity gradient) in the same kernel over the same neighbor list
+__global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConsts sc, Box box,
+                                                             const float* __restrict__ h,
+                                                             const float* __restrict__ kx,
+                                                             const SrcIad* __restrict__ rec,
+                                                             const float* __restrict__ wh, Six cij,
+                                                             float* __restrict__ divv, float* __restrict__ curlv,
+                                                             Six dV, int doGrad)
 {
     int64_t i;
     const int32_t* nbr;
     unsigned n;
     if (!targetOf(a, i, nbr, n)) return;
-    float g[6], dvi, cvi;
-    divvCurlvJLoop(unsigned(i), sc.K, box, nbr, 64, n, x, y, z, vx, vy, vz, h, cij.p, wh, kx, xm, dvi, cvi,
-                   doGrad ? g : nullptr);
+    RecLoader<SrcIad> ld{rec};
+    float c[6], g[6], dvi, cvi;
+    iadDivvCurlvJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], kx[i], ld, wh, c, dvi, cvi, doGrad ? g : nullptr);
+    for (int k = 0; k < 6; ++k)
+        cij.p[k][i] = c[k];
     divv[i]  = dvi;
     curlv[i] = cvi;
     if (doGrad)
@@ -136,46 +242,57 @@ __global__ __launch_bounds__(256) void divvCurlvKernel(NbrArgs a, SphConsts sc, 
             dV.p[k][i] = g[k];
 }
 
-__global__ __launch_bounds__(256) void avSwitchesKernel(NbrArgs a, SphConsts sc, Box box, const double* __restrict__ x,
-                                                        const double* __restrict__ y, const double* __restrict__ z,
-                                                        const float* __restrict__ vx, const float* __restrict__ vy,
-                                                        const float* __restrict__ vz, const float* __restrict__ h,
-                                                        const float* __restrict__ c, CSix cij,
-                                                        const float* __restrict__ wh, const float* __restrict__ kx,
-                                                        const float* __restrict__ xm, const float* __restrict__ divv,
-                                                        double dt, float* __restrict__ alpha)
+__global__ __launch_bounds__(kBlock) void avSwitchesKernel(NbrArgs a, SphConsts sc, Box box,
+                                                           const float* __restrict__ h, Six cij,
+                                                           const SrcIad* __restrict__ rec,
+                                                           const float* __restrict__ wh, double dt,
+                                                           float* __restrict__ alpha)
 {
     int64_t i;
     const int32_t* nbr;
     unsigned n;
     if (!targetOf(a, i, nbr, n)) return;
-    alpha[i] = avSwitchesJLoop(unsigned(i), sc.K, box, nbr, 64, n, x, y, z, vx, vy, vz, h, c, cij.p, wh, kx, xm, divv,
-                               dt, sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
+    float ci[6] = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
+    alpha[i]    = avSwitchesJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], ci, RecLoader<SrcIad>{rec}, wh, dt,
+                                  sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
 }
 
 //! @brief block min of the Courant time step, then one atomic per block
-__device__ inline void reduceMinDt(float dti, bool valid, float* minDt)
+__device__ inline void reduceMinDt(float dti, float* minDt)
 {
-    __shared__ float red[4];
-    float v = valid ? dti : FLT_MAX;
-    v       = waveMin(v);
+    __shared__ float red[kBlock / 64];
+    float v = waveMin(dti);
     int w   = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) red[w] = v;
     __syncthreads();
     if (threadIdx.x == 0)
     {
         float r = red[0];
-        for (int k = 1; k < int(blockDim.x >> 6); ++k)
+        for (int k = 1; k < kBlock / 64; ++k)
             r = fminf(r, red[k]);
         atomicMinPosFloat(minDt, r);
     }
 }
 
+struct GradVLoader
+{
+    const SrcGradV* r;
+    __device__ SrcGradV operator()(unsigned j) const
+    {
+        if (r) return r[j];
+        SrcGradV g{};
+        return g;
+    }
+};
+
 template<bool avClean>
-__global__ __launch_bounds__(256) void momentumEnergyVeKernel(NbrArgs a, SphConsts sc, Box box, VeMomentumPtrs p,
-                                                              float* __restrict__ ax, float* __restrict__ ay,
-                                                              float* __restrict__ az, double* __restrict__ du,
-                                                              float* __restrict__ minDt)
+__global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphConsts sc, Box box,
+                                                                 const SrcMom* __restrict__ rec,
+                                                                 const SrcGradV* __restrict__ gv,
+                                                                 const float* __restrict__ wh,
+                                                                 float* __restrict__ ax, float* __restrict__ ay,
+                                                                 float* __restrict__ az, double* __restrict__ du,
+                                                                 float* __restrict__ minDt)
 {
     int64_t i;
     const int32_t* nbr;
@@ -186,20 +303,24 @@ __global__ __launch_bounds__(256) void momentumEnergyVeKernel(NbrArgs a, SphCons
     {
         float mvs, axi, ayi, azi;
         double dui;
-        momentumEnergyJLoop<avClean>(unsigned(i), sc, box, nbr, 64, n, p, axi, ayi, azi, dui, mvs);
+        momentumEnergyJLoop<avClean>(unsigned(i), sc, box, nbr, 64, n, RecLoader<SrcMom>{rec}, GradVLoader{gv}, wh,
+                                     axi, ayi, azi, dui, mvs);
         ax[i] = axi;
         ay[i] = ayi;
         az[i] = azi;
         du[i] = dui;
-        dti   = tsKCourant(mvs, p.h[i], p.c[i], float(sc.Kcour));
+        SrcMom ri = rec[i];
+        dti       = tsKCourant(mvs, ri.h, ri.c, float(sc.Kcour));
     }
-    reduceMinDt(dti, valid, minDt);
+    reduceMinDt(dti, minDt);
 }
 
-__global__ __launch_bounds__(256) void momentumEnergyStdKernel(NbrArgs a, SphConsts sc, Box box, StdMomentumPtrs p,
-                                                               float* __restrict__ ax, float* __restrict__ ay,
-                                                               float* __restrict__ az, double* __restrict__ du,
-                                                               float* __restrict__ minDt)
+__global__ __launch_bounds__(kBlock) void momentumEnergyStdKernel(NbrArgs a, SphConsts sc, Box box,
+                                                                  const SrcStd* __restrict__ rec,
+                                                                  const float* __restrict__ wh,
+                                                                  float* __restrict__ ax, float* __restrict__ ay,
+                                                                  float* __restrict__ az, double* __restrict__ du,
+                                                                  float* __restrict__ minDt)
 {
     int64_t i;
     const int32_t* nbr;
@@ -210,14 +331,16 @@ __global__ __launch_bounds__(256) void momentumEnergyStdKernel(NbrArgs a, SphCon
     {
         float mvs, axi, ayi, azi;
         double dui;
-        momentumEnergyStdJLoop(unsigned(i), sc.K, box, nbr, 64, n, p, axi, ayi, azi, dui, mvs);
+        momentumEnergyStdJLoop(unsigned(i), sc.K, box, nbr, 64, n, RecLoader<SrcStd>{rec}, wh, axi, ayi, azi, dui,
+                               mvs);
         ax[i] = axi;
         ay[i] = ayi;
         az[i] = azi;
         du[i] = dui;
-        dti   = tsKCourant(mvs, p.h[i], p.c[i], float(sc.Kcour));
+        SrcStd ri = rec[i];
+        dti       = tsKCourant(mvs, ri.h, ri.c, float(sc.Kcour));
     }
-    reduceMinDt(dti, valid, minDt);
+    reduceMinDt(dti, minDt);
 }
 
 __global__ void updatePositionsKernel(int64_t first, int64_t last, double dt, double dt_m1, PosArgs p, double cv,
@@ -325,20 +448,22 @@ __global__ void conservedKernel(int64_t first, int64_t last, const double* __res
 
 // --------------------------------------------------------------------------------------------------- launchers
 
-void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y, const double* z,
-           const float* h, const float* m, const float* wh, float* xm, hipStream_t s)
+void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x, const double* y,
+           const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s)
 {
     if (a.last <= a.first) return;
-    xmassKernel<<<grid256(a), 256, 0, s>>>(a, sc, box, x, y, z, h, m, wh, xm);
+    packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, nullptr, (SrcPos*)rec);
+    xmassKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, h, (const SrcPos*)rec, wh, xm);
     SPHX_LAUNCH_CHECK();
 }
 
-void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y,
-                const double* z, const float* h, const float* m, const float* wh, const float* whd, const float* xm,
-                float* kx, float* gradh, hipStream_t s)
+void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
+                const double* y, const double* z, const float* h, const float* m, const float* wh, const float* whd,
+                const float* xm, void* rec, float* kx, float* gradh, hipStream_t s)
 {
     if (a.last <= a.first) return;
-    veDefGradhKernel<<<grid256(a), 256, 0, s>>>(a, sc, box, x, y, z, h, m, wh, whd, xm, kx, gradh);
+    packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, xm, (SrcPos*)rec);
+    veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, h, (const SrcPos*)rec, wh, whd, kx, gradh);
     SPHX_LAUNCH_CHECK();
 }
 
@@ -358,63 +483,76 @@ void eosStd(int64_t first, int64_t last, const SphConsts& sc, const double* temp
     SPHX_LAUNCH_CHECK();
 }
 
-void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y, const double* z,
-         const float* h, const float* wh, const float* numer, const float* denom, float* const cij[6], hipStream_t s)
+void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x, const double* y,
+         const double* z, const float* h, const float* wh, const float* numer, const float* denom, void* rec,
+         float* const cij[6], hipStream_t s)
 {
     if (a.last <= a.first) return;
+    packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, numer, denom, nullptr, nullptr, nullptr,
+                                                     nullptr, nullptr, nullptr, (SrcIad*)rec);
     Six c;
     for (int k = 0; k < 6; ++k)
         c.p[k] = cij[k];
-    iadKernel<<<grid256(a), 256, 0, s>>>(a, sc, box, x, y, z, h, wh, numer, denom, c);
+    iadKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, h, (const SrcIad*)rec, wh, c);
     SPHX_LAUNCH_CHECK();
 }
 
-void divvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y,
-               const double* z, const float* vx, const float* vy, const float* vz, const float* h,
-               const float* const cij[6], const float* wh, const float* kx, const float* xm, float* divv,
-               float* curlv, float* const dV[6], hipStream_t s)
+void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
+                  const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
+                  const float* wh, const float* kx, const float* xm, void* rec, float* const cij[6], float* divv,
+                  float* curlv, float* const dV[6], hipStream_t s)
 {
     if (a.last <= a.first) return;
-    CSix c;
-    Six g;
+    packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, nullptr, nullptr,
+                                                     (SrcIad*)rec);
+    Six c, g;
     for (int k = 0; k < 6; ++k)
     {
         c.p[k] = cij[k];
         g.p[k] = dV[k];
     }
-    divvCurlvKernel<<<grid256(a), 256, 0, s>>>(a, sc, box, x, y, z, vx, vy, vz, h, c, wh, kx, xm, divv, curlv, g,
-                                                dV[0] != nullptr);
+    iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, h, kx, (const SrcIad*)rec, wh, c, divv, curlv, g,
+                                                   dV[0] != nullptr);
     SPHX_LAUNCH_CHECK();
 }
 
-void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, const double* x, const double* y,
-                const double* z, const float* vx, const float* vy, const float* vz, const float* h, const float* c,
-                const float* const cij[6], const float* wh, const float* kx, const float* xm, const float* divv,
-                double dt, float* alpha, hipStream_t s)
+void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
+                const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
+                const float* c, float* const cij[6], const float* wh, const float* kx, const float* xm,
+                const float* divv, double dt, void* rec, float* alpha, hipStream_t s)
 {
     if (a.last <= a.first) return;
-    CSix cc;
+    packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, c, divv, (SrcIad*)rec);
+    Six cc;
     for (int k = 0; k < 6; ++k)
         cc.p[k] = cij[k];
-    avSwitchesKernel<<<grid256(a), 256, 0, s>>>(a, sc, box, x, y, z, vx, vy, vz, h, c, cc, wh, kx, xm, divv, dt, alpha);
+    avSwitchesKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, h, cc, (const SrcIad*)rec, wh, dt, alpha);
     SPHX_LAUNCH_CHECK();
 }
 
-void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, const VeMomentumPtrs& p, bool avClean,
-                      float* ax, float* ay, float* az, double* du, float* minDt, hipStream_t s)
+void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const MomFields& f,
+                      bool avClean, const float* wh, void* rec, void* recGradV, float* ax, float* ay, float* az,
+                      double* du, float* minDt, hipStream_t s)
 {
     if (a.last <= a.first) return;
+    SrcGradV* gv = avClean ? (SrcGradV*)recGradV : nullptr;
+    packMomKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, (SrcMom*)rec, gv);
     if (avClean)
-        momentumEnergyVeKernel<true><<<grid256(a), 256, 0, s>>>(a, sc, box, p, ax, ay, az, du, minDt);
-    else momentumEnergyVeKernel<false><<<grid256(a), 256, 0, s>>>(a, sc, box, p, ax, ay, az, du, minDt);
+        momentumEnergyVeKernel<true>
+            <<<gridT(a), kBlock, 0, s>>>(a, sc, box, (const SrcMom*)rec, gv, wh, ax, ay, az, du, minDt);
+    else
+        momentumEnergyVeKernel<false>
+            <<<gridT(a), kBlock, 0, s>>>(a, sc, box, (const SrcMom*)rec, nullptr, wh, ax, ay, az, du, minDt);
     SPHX_LAUNCH_CHECK();
 }
 
-void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, const StdMomentumPtrs& p, float* ax,
-                       float* ay, float* az, double* du, float* minDt, hipStream_t s)
+void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const StdFields& f,
+                       const float* wh, void* rec, float* ax, float* ay, float* az, double* du, float* minDt,
+                       hipStream_t s)
 {
     if (a.last <= a.first) return;
-    momentumEnergyStdKernel<<<grid256(a), 256, 0, s>>>(a, sc, box, p, ax, ay, az, du, minDt);
+    packStdKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, (SrcStd*)rec);
+    momentumEnergyStdKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, (const SrcStd*)rec, wh, ax, ay, az, du, minDt);
     SPHX_LAUNCH_CHECK();
 }
 

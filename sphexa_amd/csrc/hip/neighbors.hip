@@ -9,9 +9,11 @@
  *   2. breadth-first traversal of the octree; each lane tests one frontier node against the group box, leaves are
  *      compacted into an LDS leaf list and internal hits expand into the next LDS frontier (ballot + mbcnt
  *      compaction, deterministic order)
- *   3. for every candidate leaf, lanes load up to 64 source particles (coalesced) and broadcast them one by one
- *      with v_readlane (no LDS round trip); each lane tests its own target with the reference criterion
- *      |x_i - x_j|^2 < 4h_i^2 (fp64 minimum image) and appends j to its lane-interleaved list
+ *   3. per candidate leaf: a ballot skips leaves that no lane's search sphere touches; lanes then load up to 64
+ *      source particles (coalesced), convert them to fp32 coordinates relative to the group center (periodic
+ *      images folded once per candidate, not per pair) and broadcast them one by one with v_readlane. Each lane
+ *      tests |x_i - x_j|^2 < 4h_i^2 in fp32; candidates inside a rounding band around the radius are re-tested in
+ *      fp64 with the reference's minimum-image formula, so the neighbor sets equal the fp64 CPU search exactly
  *   4. lanes whose count is out of [ng0/4, ngmax+1] update h and the wave repeats
  */
 #include "common.h"
@@ -26,6 +28,12 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kFrontCap      = 512;
 constexpr int kLeafCap       = 1024;
 
+//! @brief fold a coordinate difference into [-L/2, L/2] in periodic dimensions
+__device__ __forceinline__ double foldMin(double dx, const Box& b, int d)
+{
+    return b.bc[d] == kPeriodic ? dx - b.len(d) * rint(dx * b.ilen(d)) : dx;
+}
+
 __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_t last, const double* __restrict__ x,
                                                            const double* __restrict__ y,
                                                            const double* __restrict__ z, float* __restrict__ h,
@@ -39,8 +47,9 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
 
     const int wave  = threadIdx.x >> 6;
     const int lane  = threadIdx.x & 63;
-    const int64_t g = int64_t(blockIdx.x) * kWavesPerBlock + wave;
     const int64_t numGroups = (last - first + 63) / 64;
+    const unsigned lb       = xcdRemap(blockIdx.x, gridDim.x);
+    const int64_t g         = int64_t(lb) * kWavesPerBlock + wave;
     if (g >= numGroups) return;
 
     const int64_t i  = first + g * 64 + lane;
@@ -56,7 +65,6 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
     }
     int32_t* nlist = nidx + g * int64_t(ngmax) * 64 + lane;
     const unsigned ngmin = ng0 / 4;
-    const bool pbc = box.anyPeriodic();
 
     unsigned ncSph = 1;
     bool overflow  = false;
@@ -126,39 +134,58 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
         }
         if (overflow) break;
 
-        // 3. candidate tests
-        unsigned cnt    = 0;
-        double radiusSq = double(4.0f * hi * hi);
+        // 3. candidate tests in group-relative fp32 with an fp64 band check
+        // the fp32 path is valid if the folded group neighborhood cannot alias across a periodic boundary
+        bool relOk = true;
+        double R   = 0;
+        for (int d = 0; d < 3; ++d)
+        {
+            R = fmax(R, gs[d]);
+            if (box.bc[d] == kPeriodic && 2.0 * gs[d] > 0.45 * box.len(d)) relOk = false;
+        }
+        const float xir = float(foldMin(xi - gc[0], box, 0));
+        const float yir = float(foldMin(yi - gc[1], box, 1));
+        const float zir = float(foldMin(zi - gc[2], box, 2));
+        const float r2f = 4.0f * hi * hi;
+        // rounding of the fp32 distance^2 around the radius: coordinates carry |err| <= delta each
+        const float delta = float(R) * 6.0e-7f + 1e-30f;
+        const float band  = relOk ? 8.0f * hi * delta + 4.0f * delta * delta : 3.4e38f;
+        const double radiusSq = double(r2f);
+        const double ip[3]    = {xi, yi, zi};
+
+        unsigned cnt = 0;
         for (int l = 0; l < nLeaves; ++l)
         {
             int32_t nd = leaves[wave][l];
-            int32_t a  = t.ns[nd];
-            int32_t b  = t.ne[nd];
+            // skip leaves outside every lane's sphere (same strict test as the CPU traversal)
+            bool touch = valid && pointBoxDistSq(ip, t.center + 3 * nd, t.half + 3 * nd, box) < radiusSq;
+            if (!ballot(touch)) continue;
+            int32_t a = t.ns[nd];
+            int32_t b = t.ne[nd];
             for (int32_t c0 = a; c0 < b; c0 += 64)
             {
-                int32_t j  = c0 + lane;
-                int m      = min(64, b - c0);
-                double xj0 = 0, yj0 = 0, zj0 = 0;
+                int32_t j = c0 + lane;
+                int m     = min(64, b - c0);
+                float xr = 0, yr = 0, zr = 0;
                 if (j < b)
                 {
-                    xj0 = x[j];
-                    yj0 = y[j];
-                    zj0 = z[j];
+                    xr = float(foldMin(x[j] - gc[0], box, 0));
+                    yr = float(foldMin(y[j] - gc[1], box, 1));
+                    zr = float(foldMin(z[j] - gc[2], box, 2));
                 }
                 for (int k = 0; k < m; ++k)
                 {
-                    double xj = readLaneD(xj0, k);
-                    double yj = readLaneD(yj0, k);
-                    double zj = readLaneD(zj0, k);
-                    double d2;
-                    if (pbc) { d2 = distanceSqPbc(xj, yj, zj, xi, yi, zi, box); }
-                    else
-                    {
-                        double dx = xj - xi, dy = yj - yi, dz = zj - zi;
-                        d2 = dx * dx + dy * dy + dz * dz;
-                    }
+                    float dx = readLaneF(xr, k) - xir;
+                    float dy = readLaneF(yr, k) - yir;
+                    float dz = readLaneF(zr, k) - zir;
+                    float d2 = dx * dx + dy * dy + dz * dz;
                     int64_t jj = int64_t(c0) + k;
-                    if (valid && jj != i && d2 < radiusSq)
+                    bool hit   = d2 < r2f - band;
+                    if (!hit && d2 <= r2f + band)
+                    {
+                        hit = distanceSqPbc(x[jj], y[jj], z[jj], xi, yi, zi, box) < radiusSq;
+                    }
+                    if (valid && hit && jj != i)
                     {
                         if (cnt < ngmax) nlist[int64_t(cnt) * 64] = int32_t(jj);
                         cnt++;

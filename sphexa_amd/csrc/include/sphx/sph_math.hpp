@@ -8,8 +8,12 @@
  *   sph/include/sph/hydro_std/(iad|momentum_energy)_kern.hpp                                          STD j-loops
  *   sph/include/sph/positions.hpp          Press position update, AB2 energy update
  *
- * The neighbor list accessor is (nbr, stride): neighbor k of the target is nbr[k*stride]. The CPU path uses
- * stride 1 (per-particle rows), the GPU path stride 64 (one wave64 target group interleaved lane-major).
+ * Data access is decoupled from the math: every j-loop reads source particles through a *loader* returning a
+ * small record (SrcPos, SrcIad, ...). The OpenMP path assembles records from the SoA fields; the gfx950 path reads
+ * 16-byte aligned array-of-records buffers packed once per loop, so one neighbor costs 2-8 dwordx4 loads from one
+ * or two cache lines instead of up to 21 scattered 4-byte gathers. Fields that the reference derives per pair
+ * (xm/kx, kx*m/xm) are packed already derived — bit-identical because the same fp32 operations are applied.
+ * The neighbor list accessor is (nbr, stride): neighbor k is nbr[k*stride]; stride 1 on the CPU, 64 on the GPU.
  */
 #pragma once
 
@@ -116,37 +120,93 @@ SPHX_HD double energyUpdate(double u_old, double dt, double dt_m1, double du, do
 }
 
 // ---------------------------------------------------------------------------------------------------------
+// source records
+// ---------------------------------------------------------------------------------------------------------
+
+//! @brief position + mass (xmass, kx/gradh): 32 B
+struct alignas(16) SrcPos
+{
+    CT x, y, z;
+    HT m;
+    HT xm;
+};
+
+//! @brief IAD + divv/curlv + AV switches: 48 B; vol = xm/kx (VE) or m/rho (STD)
+struct alignas(16) SrcIad
+{
+    CT x, y, z;
+    HT vol;
+    HT vx, vy, vz;
+    HT xm;
+    HT c;
+    HT divv;
+};
+
+//! @brief VE momentum/energy: 96 B (+ velocity gradient for AV cleaning: 128 B)
+struct alignas(16) SrcMom
+{
+    CT x, y, z;
+    HT vx, vy, vz;
+    HT h;
+    HT c11, c12, c13, c22, c23, c33;
+    HT m, c, xm, rho;
+    HT prho, alpha;
+};
+
+struct alignas(16) SrcGradV
+{
+    HT dV[6];
+    HT pad[2];
+};
+
+//! @brief STD momentum/energy: 80 B
+struct alignas(16) SrcStd
+{
+    CT x, y, z;
+    HT vx, vy, vz, h;
+    HT c11, c12, c13, c22, c23, c33;
+    HT m, rho, p, c;
+};
+
+//! @brief pair separation (i - j) in hydro precision with the j-loop periodic fold at 2h_i
+SPHX_HD void pairDelta(CT xi, CT yi, CT zi, CT xj, CT yj, CT zj, HT hi, const Box& box, HT& rx, HT& ry, HT& rz)
+{
+    rx = HT(xi - xj);
+    ry = HT(yi - yj);
+    rz = HT(zi - zj);
+    foldPbc(box, HT(2) * hi, rx, ry, rz);
+}
+
+// ---------------------------------------------------------------------------------------------------------
 // VE formulation
 // ---------------------------------------------------------------------------------------------------------
 
-//! @brief xm_i = m_i / rho0_i, rho0_i = K h^-3 sum_j W_ij m_j including self
-template<class Idx>
-SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, const CT* x,
-                      const CT* y, const CT* z, const HT* h, const HT* m, const HT* wh)
+//! @brief xm_i = m_i / rho0_i, rho0_i = K h^-3 sum_j W_ij m_j including self (reference xmass_kern.hpp)
+template<class Idx, class Ld>
+SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
+                      const Ld& ld, const HT* wh)
 {
-    CT xi = x[i], yi = y[i], zi = z[i];
-    HT hi = h[i], mi = m[i];
+    SrcPos pi = ld(i);
     HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv;
-    HT rho0 = mi;
+    HT rho0 = pi.m;
     for (unsigned k = 0; k < nc; ++k)
     {
-        unsigned j = nbr[k * stride];
-        HT rx = HT(xi - x[j]), ry = HT(yi - y[j]), rz = HT(zi - z[j]);
-        foldPbc(box, HT(2) * hi, rx, ry, rz);
+        SrcPos pj = ld(unsigned(nbr[k * stride]));
+        HT rx, ry, rz;
+        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
-        rho0 += tableLookup(wh, dist * hInv) * m[j];
+        rho0 += tableLookup(wh, dist * hInv) * pj.m;
     }
-    return mi / (rho0 * HT(K) * h3Inv);
+    return pi.m / (rho0 * HT(K) * h3Inv);
 }
 
-//! @brief kx (VE normalization) and grad-h term
-template<class Idx>
-SPHX_HD void veDefGradhJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc,
-                             const CT* x, const CT* y, const CT* z, const HT* h, const HT* m, const HT* wh,
-                             const HT* whd, const HT* xm, HT& kxOut, HT& gradhOut)
+//! @brief kx (VE normalization) and grad-h term (reference ve_def_gradh_kern.hpp)
+template<class Idx, class Ld>
+SPHX_HD void veDefGradhJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
+                             const Ld& ld, const HT* wh, const HT* whd, HT& kxOut, HT& gradhOut)
 {
-    CT xi = x[i], yi = y[i], zi = z[i];
-    HT hi = h[i], mi = m[i], xmi = xm[i];
+    SrcPos pi = ld(i);
+    HT mi = pi.m, xmi = pi.xm;
     HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv;
 
     HT kxi      = xmi;
@@ -154,18 +214,18 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const Box& box, const Idx* nb
     HT wrho0i   = -HT(3) * mi;
     for (unsigned k = 0; k < nc; ++k)
     {
-        unsigned j = nbr[k * stride];
-        HT rx = HT(xi - x[j]), ry = HT(yi - y[j]), rz = HT(zi - z[j]);
-        foldPbc(box, HT(2) * hi, rx, ry, rz);
+        SrcPos pj = ld(unsigned(nbr[k * stride]));
+        HT rx, ry, rz;
+        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist  = sqrt(rx * rx + ry * ry + rz * rz);
         HT v     = dist * hInv;
         HT w     = tableLookup(wh, v);
         HT dw    = tableLookup(whd, v);
         HT dterh = -(HT(3) * w + v * dw);
-        HT xmj   = xm[j];
+        HT xmj   = pj.xm;
         kxi += w * xmj;
         whomegai += dterh * xmj;
-        wrho0i += dterh * m[j];
+        wrho0i += dterh * pj.m;
     }
     HT Kf = HT(K);
     kxi *= Kf * h3Inv;
@@ -198,24 +258,22 @@ SPHX_HD void invertTau(HT tau[6], HT hi, double K, HT c[6])
     c[5]      = (t11 * t22 - t12 * t12) * factor;
 }
 
-/*! @brief IAD matrix with generalized volume elements xm/kx (VE) or m/rho (STD: pass vol = m/rho via xm=m,
- *         kx=rho)
- */
-template<class Idx>
-SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, const CT* x,
-                      const CT* y, const CT* z, const HT* h, const HT* wh, const HT* numer, const HT* denom, HT c[6])
+//! @brief IAD matrix with volumes vol_j (VE: xm/kx, STD: m/rho) (reference hydro_ve/iad_kern.hpp, hydro_std)
+template<class Idx, class Ld>
+SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
+                      const Ld& ld, const HT* wh, HT c[6])
 {
     HT tau[6] = {0, 0, 0, 0, 0, 0};
-    CT xi = x[i], yi = y[i], zi = z[i];
-    HT hi = h[i], hInv = HT(1) / hi;
+    SrcIad pi = ld(i);
+    HT hInv   = HT(1) / hi;
     for (unsigned k = 0; k < nc; ++k)
     {
-        unsigned j = nbr[k * stride];
-        HT rx = HT(xi - x[j]), ry = HT(yi - y[j]), rz = HT(zi - z[j]);
-        foldPbc(box, HT(2) * hi, rx, ry, rz);
+        SrcIad pj = ld(unsigned(nbr[k * stride]));
+        HT rx, ry, rz;
+        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
         HT w    = tableLookup(wh, dist * hInv);
-        HT vw   = numer[j] / denom[j] * w;
+        HT vw   = pj.vol * w;
         tau[0] += rx * rx * vw;
         tau[1] += rx * ry * vw;
         tau[2] += rx * rz * vw;
@@ -226,31 +284,27 @@ SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
     invertTau(tau, hi, K, c);
 }
 
-//! @brief velocity divergence, |curl|, and optionally the symmetric velocity gradient (reference divv_curlv_kern.hpp)
-template<class Idx>
-SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc,
-                            const CT* x, const CT* y, const CT* z, const HT* vx, const HT* vy, const HT* vz,
-                            const HT* h, const HT* const cij[6], const HT* wh, const HT* kx, const HT* xm,
-                            HT& divvOut, HT& curlvOut, HT dV[6])
+//! @brief velocity divergence, |curl|, optional symmetric velocity gradient (reference divv_curlv_kern.hpp)
+template<class Idx, class Ld>
+SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
+                            HT kxi, const HT ci[6], const Ld& ld, const HT* wh, HT& divvOut, HT& curlvOut, HT* dV)
 {
-    CT xi = x[i], yi = y[i], zi = z[i];
-    HT vxi = vx[i], vyi = vy[i], vzi = vz[i];
-    HT hi = h[i], kxi = kx[i];
+    SrcIad pi = ld(i);
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
-    HT c11 = cij[0][i], c12 = cij[1][i], c13 = cij[2][i], c22 = cij[3][i], c23 = cij[4][i], c33 = cij[5][i];
+    HT c11 = ci[0], c12 = ci[1], c13 = ci[2], c22 = ci[3], c23 = ci[4], c33 = ci[5];
     HT dVx[3] = {0, 0, 0}, dVy[3] = {0, 0, 0}, dVz[3] = {0, 0, 0};
     for (unsigned k = 0; k < nc; ++k)
     {
-        unsigned j = nbr[k * stride];
-        HT rx = HT(xi - x[j]), ry = HT(yi - y[j]), rz = HT(zi - z[j]);
-        foldPbc(box, HT(2) * hi, rx, ry, rz);
+        SrcIad pj = ld(unsigned(nbr[k * stride]));
+        HT rx, ry, rz;
+        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
-        HT vxji = vx[j] - vxi, vyji = vy[j] - vyi, vzji = vz[j] - vzi;
+        HT vxji = pj.vx - pi.vx, vyji = pj.vy - pi.vy, vzji = pj.vz - pi.vz;
         HT W    = tableLookup(wh, dist * hInv);
         HT tA0  = -(c11 * rx + c12 * ry + c13 * rz) * W;
         HT tA1  = -(c12 * rx + c22 * ry + c23 * rz) * W;
         HT tA2  = -(c13 * rx + c23 * ry + c33 * rz) * W;
-        HT xmj  = xm[j];
+        HT xmj  = pj.xm;
         HT ax = vxji * xmj, ay = vyji * xmj, az = vzji * xmj;
         dVx[0] += ax * tA0;
         dVx[1] += ax * tA1;
@@ -277,38 +331,100 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
     }
 }
 
-//! @brief Cullen-Dehnen style AV switch (reference av_switches_kern.hpp)
-template<class Idx>
-SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc,
-                           const CT* x, const CT* y, const CT* z, const HT* vx, const HT* vy, const HT* vz,
-                           const HT* h, const HT* c, const HT* const cij[6], const HT* wh, const HT* kx,
-                           const HT* xm, const HT* divv, double dt, HT alphamin, HT alphamax, HT decayConstant,
-                           HT alpha_i)
+/*! @brief IAD matrix and velocity divergence/curl in ONE pass over the neighbors
+ *
+ * The reference (iad_divv_curlv_gpu.cu) runs the IAD loop, inverts tau into c_i, then runs a second loop where every
+ * term is -(c_i . r_ij) W_ij v_ji xm_j. Because c_i is constant over j, the second loop equals -c_i . M with
+ * M[a][b] = sum_j v_ji[a] xm_j W_ij r_ij[b], so M is accumulated together with tau and the neighbor data is read
+ * once. Mathematically identical; rounding differs from the two-pass form at the 1e-7 relative level.
+ */
+template<class Idx, class Ld>
+SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
+                               HT kxi, const Ld& ld, const HT* wh, HT c[6], HT& divvOut, HT& curlvOut, HT* dV)
 {
-    CT xi = x[i], yi = y[i], zi = z[i];
-    HT vxi = vx[i], vyi = vy[i], vzi = vz[i];
-    HT hi = h[i], ci = c[i];
-    HT c11 = cij[0][i], c12 = cij[1][i], c13 = cij[2][i], c22 = cij[3][i], c23 = cij[4][i], c33 = cij[5][i];
-    HT vsig = HT(1.e-40) * ci;
+    HT tau[6]  = {0, 0, 0, 0, 0, 0};
+    HT M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    SrcIad pi  = ld(i);
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
-    HT divvi = divv[i];
+    for (unsigned k = 0; k < nc; ++k)
+    {
+        SrcIad pj = ld(unsigned(nbr[k * stride]));
+        HT rx, ry, rz;
+        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
+        HT dist = sqrt(rx * rx + ry * ry + rz * rz);
+        HT w    = tableLookup(wh, dist * hInv);
+        HT vw   = pj.vol * w;
+        tau[0] += rx * rx * vw;
+        tau[1] += rx * ry * vw;
+        tau[2] += rx * rz * vw;
+        tau[3] += ry * ry * vw;
+        tau[4] += ry * rz * vw;
+        tau[5] += rz * rz * vw;
+        HT xw = pj.xm * w;
+        HT ax = (pj.vx - pi.vx) * xw, ay = (pj.vy - pi.vy) * xw, az = (pj.vz - pi.vz) * xw;
+        M[0][0] += ax * rx;
+        M[0][1] += ax * ry;
+        M[0][2] += ax * rz;
+        M[1][0] += ay * rx;
+        M[1][1] += ay * ry;
+        M[1][2] += ay * rz;
+        M[2][0] += az * rx;
+        M[2][1] += az * ry;
+        M[2][2] += az * rz;
+    }
+    invertTau(tau, hi, K, c);
+    // dV_a[k] = -sum_b c[k][b] M[a][b], c symmetric (c11 c12 c13 c22 c23 c33)
+    HT dVv[3][3];
+    for (int a = 0; a < 3; ++a)
+    {
+        dVv[a][0] = -(c[0] * M[a][0] + c[1] * M[a][1] + c[2] * M[a][2]);
+        dVv[a][1] = -(c[1] * M[a][0] + c[3] * M[a][1] + c[4] * M[a][2]);
+        dVv[a][2] = -(c[2] * M[a][0] + c[4] * M[a][1] + c[5] * M[a][2]);
+    }
+    HT nk   = HT(K) * hInv3 / kxi;
+    divvOut = nk * (dVv[0][0] + dVv[1][1] + dVv[2][2]);
+    HT cx = dVv[2][1] - dVv[1][2], cy = dVv[0][2] - dVv[2][0], cz = dVv[1][0] - dVv[0][1];
+    curlvOut = nk * sqrt(cx * cx + cy * cy + cz * cz);
+    if (dV)
+    {
+        dV[0] = nk * dVv[0][0];
+        dV[1] = nk * (dVv[0][1] + dVv[1][0]);
+        dV[2] = nk * (dVv[0][2] + dVv[2][0]);
+        dV[3] = nk * dVv[1][1];
+        dV[4] = nk * (dVv[1][2] + dVv[2][1]);
+        dV[5] = nk * dVv[2][2];
+    }
+}
+
+//! @brief Cullen-Dehnen style AV switch (reference av_switches_kern.hpp)
+template<class Idx, class Ld>
+SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
+                           const HT ci6[6], const Ld& ld, const HT* wh, double dt, HT alphamin, HT alphamax,
+                           HT decayConstant, HT alpha_i)
+{
+    SrcIad pi = ld(i);
+    HT ci     = pi.c;
+    HT c11 = ci6[0], c12 = ci6[1], c13 = ci6[2], c22 = ci6[3], c23 = ci6[4], c33 = ci6[5];
+    HT vsig  = HT(1.e-40) * ci;
+    HT hInv  = HT(1) / hi, hInv3 = hInv * hInv * hInv;
+    HT divvi = pi.divv;
     HT gx = 0, gy = 0, gz = 0;
     for (unsigned k = 0; k < nc; ++k)
     {
-        unsigned j = nbr[k * stride];
-        HT rx = HT(xi - x[j]), ry = HT(yi - y[j]), rz = HT(zi - z[j]);
-        foldPbc(box, HT(2) * hi, rx, ry, rz);
+        SrcIad pj = ld(unsigned(nbr[k * stride]));
+        HT rx, ry, rz;
+        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
-        HT vxij = vxi - vx[j], vyij = vyi - vy[j], vzij = vzi - vz[j];
+        HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
         HT rv   = rx * vxij + ry * vyij + rz * vzij;
         HT vsij = HT(0);
-        if (rv < HT(0)) { vsij = ci + c[j] - HT(3) * rv / dist; }
+        if (rv < HT(0)) { vsij = ci + pj.c - HT(3) * rv / dist; }
         vsig   = smax(vsig, vsij);
         HT W   = HT(K) * hInv3 * tableLookup(wh, dist * hInv);
         HT tA0 = -(c11 * rx + c12 * ry + c13 * rz) * W;
         HT tA1 = -(c12 * rx + c22 * ry + c23 * rz) * W;
         HT tA2 = -(c13 * rx + c23 * ry + c33 * rz) * W;
-        HT f   = xm[j] / kx[j] * (divvi - divv[j]);
+        HT f   = pj.vol * (divvi - pj.divv);
         gx += f * tA0;
         gy += f * tA1;
         gz += f * tA2;
@@ -354,35 +470,22 @@ SPHX_HD HT avRvCorrection(HT rx, HT ry, HT rz, HT eta_ab, HT eta_crit, const HT 
     return -phi * (d1 + d2);
 }
 
-struct VeMomentumPtrs
-{
-    const CT *x, *y, *z;
-    const HT *vx, *vy, *vz, *h, *m, *prho, *c;
-    const HT* cij[6];
-    const HT *kx, *xm, *alpha;
-    const HT* dV[6];
-    const HT* wh;
-};
-
 //! @brief VE momentum and energy equations (reference hydro_ve/momentum_energy_kern.hpp)
-template<bool avClean, class Idx>
+template<bool avClean, class Idx, class Ld, class LdG>
 SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box, const Idx* nbr, int stride,
-                                 unsigned nc, const VeMomentumPtrs& p, HT& axOut, HT& ayOut, HT& azOut,
-                                 double& duOut, HT& maxvsignalOut)
+                                 unsigned nc, const Ld& ld, const LdG& ldg, const HT* wh, HT& axOut, HT& ayOut,
+                                 HT& azOut, double& duOut, HT& maxvsignalOut)
 {
-    CT xi = p.x[i], yi = p.y[i], zi = p.z[i];
-    HT vxi = p.vx[i], vyi = p.vy[i], vzi = p.vz[i];
-    HT hi = p.h[i], mi = p.m[i], ci = p.c[i], kxi = p.kx[i];
-    HT alphai = p.alpha[i], xmi = p.xm[i];
-    HT rhoi = kxi * mi / xmi, prhoi = p.prho[i];
+    SrcMom pi = ld(i);
+    HT hi = pi.h, ci = pi.c, alphai = pi.alpha, xmi = pi.xm;
+    HT rhoi = pi.rho, prhoi = pi.prho;
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
-    HT c11i = p.cij[0][i], c12i = p.cij[1][i], c13i = p.cij[2][i], c22i = p.cij[3][i], c23i = p.cij[4][i],
-       c33i = p.cij[5][i];
     HT gVi[6] = {0, 0, 0, 0, 0, 0};
     if (avClean)
     {
+        SrcGradV g = ldg(i);
         for (int k = 0; k < 6; ++k)
-            gVi[k] = p.dV[k][i];
+            gVi[k] = g.dV[k];
     }
     HT etaCrit = cbrt(HT(32) * HT(M_PI) / HT(3) / HT(nc + 1));
 
@@ -391,38 +494,34 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
 
     for (unsigned k = 0; k < nc; ++k)
     {
-        unsigned j = nbr[k * stride];
-        HT rx = HT(xi - p.x[j]), ry = HT(yi - p.y[j]), rz = HT(zi - p.z[j]);
-        foldPbc(box, HT(2) * hi, rx, ry, rz);
+        unsigned j = unsigned(nbr[k * stride]);
+        SrcMom pj  = ld(j);
+        HT rx, ry, rz;
+        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
-        HT vxij = vxi - p.vx[j], vyij = vyi - p.vy[j], vzij = vzi - p.vz[j];
-        HT hj = p.h[j], hjInv = HT(1) / hj;
+        HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
+        HT hjInv = HT(1) / pj.h;
         HT v1 = dist * hInv, v2 = dist * hjInv;
-        HT Wi = hInv3 * tableLookup(p.wh, v1);
-        HT Wj = hjInv * hjInv * hjInv * tableLookup(p.wh, v2);
+        HT Wi = hInv3 * tableLookup(wh, v1);
+        HT Wj = hjInv * hjInv * hjInv * tableLookup(wh, v2);
 
-        HT tAi0 = -(c11i * rx + c12i * ry + c13i * rz) * Wi;
-        HT tAi1 = -(c12i * rx + c22i * ry + c23i * rz) * Wi;
-        HT tAi2 = -(c13i * rx + c23i * ry + c33i * rz) * Wi;
-        HT c11j = p.cij[0][j], c12j = p.cij[1][j], c13j = p.cij[2][j], c22j = p.cij[3][j], c23j = p.cij[4][j],
-           c33j = p.cij[5][j];
-        HT tAj0 = -(c11j * rx + c12j * ry + c13j * rz) * Wj;
-        HT tAj1 = -(c12j * rx + c22j * ry + c23j * rz) * Wj;
-        HT tAj2 = -(c13j * rx + c23j * ry + c33j * rz) * Wj;
+        HT tAi0 = -(pi.c11 * rx + pi.c12 * ry + pi.c13 * rz) * Wi;
+        HT tAi1 = -(pi.c12 * rx + pi.c22 * ry + pi.c23 * rz) * Wi;
+        HT tAi2 = -(pi.c13 * rx + pi.c23 * ry + pi.c33 * rz) * Wi;
+        HT tAj0 = -(pj.c11 * rx + pj.c12 * ry + pj.c13 * rz) * Wj;
+        HT tAj1 = -(pj.c12 * rx + pj.c22 * ry + pj.c23 * rz) * Wj;
+        HT tAj2 = -(pj.c13 * rx + pj.c23 * ry + pj.c33 * rz) * Wj;
 
-        HT mj = p.m[j], cj = p.c[j], xmj = p.xm[j];
-        HT rhoj = p.kx[j] * mj / xmj;
+        HT mj = pj.m, cj = pj.c, xmj = pj.xm, rhoj = pj.rho;
 
         HT rv = rx * vxij + ry * vyij + rz * vzij;
         if (avClean)
         {
-            HT gVj[6];
-            for (int q = 0; q < 6; ++q)
-                gVj[q] = p.dV[q][j];
-            rv += avRvCorrection(rx, ry, rz, smin(v1, v2), etaCrit, gVi, gVj);
+            SrcGradV gj = ldg(j);
+            rv += avRvCorrection(rx, ry, rz, smin(v1, v2), etaCrit, gVi, gj.dV);
         }
         HT wij  = rv / dist;
-        HT visc = artificialViscosity(alphai, p.alpha[j], ci, cj, wij);
+        HT visc = artificialViscosity(alphai, pj.alpha, ci, cj, wij);
         HT vs   = HT(0.5) * (ci + cj) - HT(2) * wij;
         maxvs   = vs > maxvs ? vs : maxvs;
 
@@ -455,7 +554,7 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
         energy += mj * a_mom * (vxij * tAi0 + vyij * tAi1 + vzij * tAi2);
 
         HT momi = mj * prhoi * a_mom;
-        HT momj = mj * p.prho[j] * b_mom;
+        HT momj = mj * pj.prho * b_mom;
         mx += momi * tAi0 + momj * tAj0 + avx;
         my += momi * tAi1 + momj * tAj1 + avy;
         mz += momi * tAi2 + momj * tAj2 + avz;
@@ -469,59 +568,46 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
     maxvsignalOut = maxvs;
 }
 
-struct StdMomentumPtrs
-{
-    const CT *x, *y, *z;
-    const HT *vx, *vy, *vz, *h, *m, *rho, *p, *c;
-    const HT* cij[6];
-    const HT* wh;
-};
-
-//! @brief standard SPH momentum and energy with constant alpha=1 AV (reference hydro_std/momentum_energy_kern.hpp)
-template<class Idx>
+//! @brief standard SPH momentum and energy, constant alpha=1 AV (reference hydro_std/momentum_energy_kern.hpp)
+template<class Idx, class Ld>
 SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc,
-                                    const StdMomentumPtrs& p, HT& axOut, HT& ayOut, HT& azOut, double& duOut,
+                                    const Ld& ld, const HT* wh, HT& axOut, HT& ayOut, HT& azOut, double& duOut,
                                     HT& maxvsignalOut)
 {
-    CT xi = p.x[i], yi = p.y[i], zi = p.z[i];
-    HT vxi = p.vx[i], vyi = p.vy[i], vzi = p.vz[i];
-    HT hi = p.h[i], roi = p.rho[i], pri = p.p[i], ci = p.c[i];
-    HT mi_roi = p.m[i] / roi;
+    SrcStd pi = ld(i);
+    HT hi = pi.h, roi = pi.rho, pri = pi.p, ci = pi.c;
+    HT mi_roi = pi.m / roi;
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
-    HT c11i = p.cij[0][i], c12i = p.cij[1][i], c13i = p.cij[2][i], c22i = p.cij[3][i], c23i = p.cij[4][i],
-       c33i = p.cij[5][i];
     HT maxvs = 0, mx = 0, my = 0, mz = 0, energy = 0;
     for (unsigned k = 0; k < nc; ++k)
     {
-        unsigned j = nbr[k * stride];
-        HT rx = HT(xi - p.x[j]), ry = HT(yi - p.y[j]), rz = HT(zi - p.z[j]);
-        foldPbc(box, HT(2) * hi, rx, ry, rz);
+        SrcStd pj = ld(unsigned(nbr[k * stride]));
+        HT rx, ry, rz;
+        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
-        HT vxij = vxi - p.vx[j], vyij = vyi - p.vy[j], vzij = vzi - p.vz[j];
-        HT hj = p.h[j], hjInv = HT(1) / hj;
+        HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
+        HT hjInv = HT(1) / pj.h;
         HT v1 = dist * hInv, v2 = dist * hjInv;
         HT rv = rx * vxij + ry * vyij + rz * vzij;
-        HT Wi = hInv3 * tableLookup(p.wh, v1);
-        HT Wj = hjInv * hjInv * hjInv * tableLookup(p.wh, v2);
-        HT tAi0 = c11i * rx + c12i * ry + c13i * rz;
-        HT tAi1 = c12i * rx + c22i * ry + c23i * rz;
-        HT tAi2 = c13i * rx + c23i * ry + c33i * rz;
-        HT c11j = p.cij[0][j], c12j = p.cij[1][j], c13j = p.cij[2][j], c22j = p.cij[3][j], c23j = p.cij[4][j],
-           c33j = p.cij[5][j];
-        HT tAj0 = c11j * rx + c12j * ry + c13j * rz;
-        HT tAj1 = c12j * rx + c22j * ry + c23j * rz;
-        HT tAj2 = c13j * rx + c23j * ry + c33j * rz;
-        HT roj = p.rho[j], cj = p.c[j];
+        HT Wi = hInv3 * tableLookup(wh, v1);
+        HT Wj = hjInv * hjInv * hjInv * tableLookup(wh, v2);
+        HT tAi0 = pi.c11 * rx + pi.c12 * ry + pi.c13 * rz;
+        HT tAi1 = pi.c12 * rx + pi.c22 * ry + pi.c23 * rz;
+        HT tAi2 = pi.c13 * rx + pi.c23 * ry + pi.c33 * rz;
+        HT tAj0 = pj.c11 * rx + pj.c12 * ry + pj.c13 * rz;
+        HT tAj1 = pj.c12 * rx + pj.c22 * ry + pj.c23 * rz;
+        HT tAj2 = pj.c13 * rx + pj.c23 * ry + pj.c33 * rz;
+        HT roj = pj.rho, cj = pj.c;
         HT wij  = rv / dist;
         HT visc = HT(0.5) * artificialViscosity(HT(1), HT(1), ci, cj, wij);
         HT vs   = ci + cj - HT(3) * wij;
         maxvs   = vs > maxvs ? vs : maxvs;
-        HT mj = p.m[j];
+        HT mj      = pj.m;
         HT mjrojWj = mj / roj * Wj;
         HT mjproi  = mj * pri / (roi * roi);
         {
             HT a = Wi * (mjproi + visc * mi_roi);
-            HT b = mjrojWj * (p.p[j] / roj + visc);
+            HT b = mjrojWj * (pj.p / roj + visc);
             mx += a * tAi0 + b * tAj0;
             my += a * tAi1 + b * tAj1;
             mz += a * tAi2 + b * tAj2;
@@ -539,5 +625,117 @@ SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const 
     azOut         = Kf * mz;
     maxvsignalOut = maxvs;
 }
+
+// ---------------------------------------------------------------------------------------------------------
+// record loaders
+// ---------------------------------------------------------------------------------------------------------
+
+//! @brief loader from a packed array of records (gfx950 path)
+template<class R>
+struct RecLoader
+{
+    const R* r;
+    SPHX_HD R operator()(unsigned j) const { return r[j]; }
+};
+
+//! @brief SoA loaders (OpenMP path): assemble the record from separate fields
+struct SoaPos
+{
+    const CT *x, *y, *z;
+    const HT *m, *xm;
+    SPHX_HD SrcPos operator()(unsigned j) const { return {x[j], y[j], z[j], m[j], xm ? xm[j] : HT(0)}; }
+};
+
+struct SoaIad
+{
+    const CT *x, *y, *z;
+    const HT *numer, *denom, *vx, *vy, *vz, *xm, *c, *divv;
+    SPHX_HD SrcIad operator()(unsigned j) const
+    {
+        SrcIad r;
+        r.x    = x[j];
+        r.y    = y[j];
+        r.z    = z[j];
+        r.vol  = numer ? numer[j] / denom[j] : HT(0);
+        r.vx   = vx ? vx[j] : HT(0);
+        r.vy   = vy ? vy[j] : HT(0);
+        r.vz   = vz ? vz[j] : HT(0);
+        r.xm   = xm ? xm[j] : HT(0);
+        r.c    = c ? c[j] : HT(0);
+        r.divv = divv ? divv[j] : HT(0);
+        return r;
+    }
+};
+
+struct SoaMom
+{
+    const CT *x, *y, *z;
+    const HT *vx, *vy, *vz, *h, *c11, *c12, *c13, *c22, *c23, *c33, *m, *c, *xm, *kx, *prho, *alpha;
+    SPHX_HD SrcMom operator()(unsigned j) const
+    {
+        SrcMom r;
+        r.x = x[j];
+        r.y = y[j];
+        r.z = z[j];
+        r.vx = vx[j];
+        r.vy = vy[j];
+        r.vz = vz[j];
+        r.h = h[j];
+        r.c11 = c11[j];
+        r.c12 = c12[j];
+        r.c13 = c13[j];
+        r.c22 = c22[j];
+        r.c23 = c23[j];
+        r.c33 = c33[j];
+        r.m = m[j];
+        r.c = c[j];
+        r.xm = xm[j];
+        r.rho = kx[j] * m[j] / xm[j];
+        r.prho = prho[j];
+        r.alpha = alpha[j];
+        return r;
+    }
+};
+
+struct SoaGradV
+{
+    const HT* dV[6];
+    SPHX_HD SrcGradV operator()(unsigned j) const
+    {
+        SrcGradV g;
+        for (int k = 0; k < 6; ++k)
+            g.dV[k] = dV[k] ? dV[k][j] : HT(0);
+        g.pad[0] = g.pad[1] = 0;
+        return g;
+    }
+};
+
+struct SoaStd
+{
+    const CT *x, *y, *z;
+    const HT *vx, *vy, *vz, *h, *c11, *c12, *c13, *c22, *c23, *c33, *m, *rho, *p, *c;
+    SPHX_HD SrcStd operator()(unsigned j) const
+    {
+        SrcStd r;
+        r.x = x[j];
+        r.y = y[j];
+        r.z = z[j];
+        r.vx = vx[j];
+        r.vy = vy[j];
+        r.vz = vz[j];
+        r.h = h[j];
+        r.c11 = c11[j];
+        r.c12 = c12[j];
+        r.c13 = c13[j];
+        r.c22 = c22[j];
+        r.c23 = c23[j];
+        r.c33 = c33[j];
+        r.m = m[j];
+        r.rho = rho[j];
+        r.p = p[j];
+        r.c = c[j];
+        return r;
+    }
+};
 
 } // namespace sphx

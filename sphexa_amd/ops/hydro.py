@@ -6,6 +6,8 @@ Parity (reference sph/include/sph/):
   positions*.{hpp,cu}, update_h*.{hpp,cu}, timestep.hpp
 Each op dispatches on the tensor device: HIP tensors go to the gfx950 kernels (_sphx_hip), CPU tensors to the
 OpenMP reference path (_sphx_cpu). There is no silent fallback between the two.
+The GPU loops take a record workspace (see csrc/include/sphx/sph_math.hpp): sources are packed into 32-128 B
+records once per loop so every neighbor is a few 16-byte loads.
 """
 
 from __future__ import annotations
@@ -20,6 +22,8 @@ from ..utils.box import Box
 
 CIJ = ("c11", "c12", "c13", "c22", "c23", "c33")
 DV = ("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")
+
+REC_BYTES = 128  # largest source record (SrcMom 96 B, SrcGradV 32 B in a second buffer)
 
 
 def _stream():
@@ -38,13 +42,28 @@ def _is_gpu(d):
     return d.device.type == "cuda"
 
 
+def _rec(d, which: int = 0):
+    """per-dataset record workspace on the GPU (grown with the particle count incl. halos)"""
+    name = "_rec%d" % which
+    need = d.size * (REC_BYTES if which == 0 else 32)
+    buf = getattr(d, name, None)
+    if buf is None or buf.numel() < need:
+        buf = torch.empty(int(need * 1.05) + 4096, dtype=torch.uint8, device=d.device)
+        setattr(d, name, buf)
+    return buf
+
+
+def _gpu_tail(d, which=(0,)):
+    return (d.size,) + tuple(_rec(d, w).data_ptr() for w in which) + (_stream(),)
+
+
 def compute_xmass(d, nl: NeighborList, box: Box, out_field: str = "xm"):
     first, last = nl.first, nl.last
     nidx, nc = _nl_args(nl, d)
     args = (first, last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d[out_field].data_ptr())
     if _is_gpu(d):
-        _lib.hip().xmass(*args, _stream())
+        _lib.hip().xmass(*args, *_gpu_tail(d))
     else:
         _lib.cpu().xmass(*args)
 
@@ -60,7 +79,7 @@ def compute_ve_def_gradh(d, nl: NeighborList, box: Box):
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d.whd.data_ptr(),
             d["xm"].data_ptr(), d["kx"].data_ptr(), d["gradh"].data_ptr())
     if _is_gpu(d):
-        _lib.hip().ve_def_gradh(*args, _stream())
+        _lib.hip().ve_def_gradh(*args, *_gpu_tail(d))
     else:
         _lib.cpu().ve_def_gradh(*args)
 
@@ -92,13 +111,13 @@ def compute_iad(d, nl: NeighborList, box: Box, numer: str, denom: str):
             d["z"].data_ptr(), d["h"].data_ptr(), d.wh.data_ptr(), d[numer].data_ptr(), d[denom].data_ptr(),
             [d[c].data_ptr() for c in CIJ])
     if _is_gpu(d):
-        _lib.hip().iad(*args, _stream())
+        _lib.hip().iad(*args, *_gpu_tail(d))
     else:
         _lib.cpu().iad(*args)
 
 
 def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False):
-    compute_iad(d, nl, box, "xm", "kx")
+    """VE IAD matrices, velocity divergence and curl (+ velocity gradient for AV cleaning), fused"""
     nidx, nc = _nl_args(nl, d)
     dv = [d[n].data_ptr() for n in DV] if av_clean else [0] * 6
     args = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
@@ -106,9 +125,9 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
             [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["kx"].data_ptr(), d["xm"].data_ptr(),
             d["divv"].data_ptr(), d["curlv"].data_ptr(), dv)
     if _is_gpu(d):
-        _lib.hip().divv_curlv(*args, _stream())
+        _lib.hip().iad_divv_curlv(*args, *_gpu_tail(d))
     else:
-        _lib.cpu().divv_curlv(*args)
+        _lib.cpu().iad_divv_curlv(*args)
 
 
 def compute_av_switches(d, nl: NeighborList, box: Box):
@@ -118,7 +137,7 @@ def compute_av_switches(d, nl: NeighborList, box: Box):
             d["c"].data_ptr(), [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["kx"].data_ptr(),
             d["xm"].data_ptr(), d["divv"].data_ptr(), float(d.minDt), d["alpha"].data_ptr())
     if _is_gpu(d):
-        _lib.hip().av_switches(*args, _stream())
+        _lib.hip().av_switches(*args, *_gpu_tail(d))
     else:
         _lib.cpu().av_switches(*args)
 
@@ -134,7 +153,7 @@ def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = F
               d["ax"].data_ptr(), d["ay"].data_ptr(), d["az"].data_ptr(), d["du"].data_ptr())
     if _is_gpu(d):
         dt = torch.full((1,), math.inf, dtype=torch.float32, device=d.device)
-        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), _stream())
+        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), *_gpu_tail(d, (0, 1)))
         d.minDtCourant_dev = dt
         d.minDtCourant = None
     else:
@@ -150,7 +169,7 @@ def compute_momentum_energy_std(d, nl: NeighborList, box: Box):
               d["az"].data_ptr(), d["du"].data_ptr())
     if _is_gpu(d):
         dt = torch.full((1,), math.inf, dtype=torch.float32, device=d.device)
-        _lib.hip().momentum_energy_std(*common, dt.data_ptr(), _stream())
+        _lib.hip().momentum_energy_std(*common, dt.data_ptr(), *_gpu_tail(d))
         d.minDtCourant_dev = dt
         d.minDtCourant = None
     else:

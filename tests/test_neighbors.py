@@ -70,7 +70,7 @@ def test_h_iteration_targets_ng0():
 def test_ngmax_capping():
     box = Box.cube(0.0, 1.0, OPEN)
     d, ot, X = _dataset(1500, 0.15, box, seed=3)
-    d.ngmax = 20
+    d.ng0, d.ngmax = 10, 20
     nl = find_neighbors(d, ot, box, 0, d.size, iterate_h=False)
     nc = d["nc"].numpy()
     assert nc.max() - 1 > 20  # counts are not capped
