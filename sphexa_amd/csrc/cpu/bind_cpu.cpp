@@ -377,6 +377,32 @@ PYBIND11_MODULE(_sphx_cpu, m)
                                        P<int32_t>(nc), cv, P<double>(out));
           });
 
+    m.def("gravity_upsweep",
+          [](int64_t N, Ptr child, Ptr n2l, std::vector<int64_t> levelRange, Ptr prefixes, Ptr ns, Ptr ne, Ptr x,
+             Ptr y, Ptr z, Ptr mm, const BoxArr& box, int kind, double invTheta, Ptr centers, Ptr mp)
+          {
+              cpu::gravityUpsweep(N, P<int32_t>(child), P<int32_t>(n2l), levelRange.data(), P<KeyT>(prefixes),
+                                  P<int32_t>(ns), P<int32_t>(ne), P<double>(x), P<double>(y), P<double>(z),
+                                  P<float>(mm), toBox(box), kind, invTheta, P<double>(centers),
+                                  P<Quadrupole>(mp));
+          });
+    m.def("compute_gravity",
+          [](int64_t first, int64_t last, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr centers, Ptr mp, Ptr x, Ptr y,
+             Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay, Ptr az, Ptr ugrav)
+          {
+              return cpu::computeGravity(first, last, P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns),
+                                         P<int32_t>(ne), P<double>(centers), P<Quadrupole>(mp), P<double>(x),
+                                         P<double>(y), P<double>(z), P<float>(h), P<float>(mm), G, P<float>(ax),
+                                         P<float>(ay), P<float>(az), P<double>(ugrav));
+          });
+    m.def("direct_sum",
+          [](int64_t first, int64_t last, int64_t n, Ptr x, Ptr y, Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay,
+             Ptr az, Ptr ugrav)
+          {
+              return cpu::directSum(first, last, n, P<double>(x), P<double>(y), P<double>(z), P<float>(h),
+                                    P<float>(mm), G, P<float>(ax), P<float>(ay), P<float>(az), P<double>(ugrav));
+          });
+
     m.def("update_h", [](int64_t first, int64_t last, unsigned ng0, Ptr nc, Ptr h)
           { cpu::updateSmoothingLength(first, last, ng0, P<uint32_t>(nc), P<float>(h)); });
 }

@@ -74,3 +74,21 @@ void markInBoxes(int64_t numBoxes, const double* bc, const double* bh, const Tre
                  const double* y, const double* z, const Box& box, uint8_t* flags);
 
 } // namespace sphx::cpu
+
+#include "sphx/gravity.hpp"
+
+namespace sphx::cpu
+{
+
+void gravityUpsweep(int64_t N, const int32_t* child, const int32_t* n2l, const int64_t* levelRange,
+                    const KeyT* prefixes, const int32_t* ns, const int32_t* ne, const double* x, const double* y,
+                    const double* z, const float* m, const Box& box, int kind, double invTheta, double* centers,
+                    Quadrupole* mp);
+double computeGravity(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
+                      const int32_t* ne, const double* centers, const Quadrupole* mp, const double* x,
+                      const double* y, const double* z, const float* h, const float* m, double G, float* ax,
+                      float* ay, float* az, double* ugrav);
+double directSum(int64_t first, int64_t last, int64_t n, const double* x, const double* y, const double* z,
+                 const float* h, const float* m, double G, float* ax, float* ay, float* az, double* ugrav);
+
+} // namespace sphx::cpu
