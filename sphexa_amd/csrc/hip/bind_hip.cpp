@@ -294,6 +294,37 @@ PYBIND11_MODULE(_sphx_hip, m)
               momentumEnergyStd(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, f, P<float>(wh), P<void>(rec),
                                 P<float>(ax), P<float>(ay), P<float>(az), P<double>(du), P<float>(minDt), St(s));
           });
+    // ---------------------------------------------------------------------------------------------- gravity
+    m.def("gravity_leaves", [](Ptr n2l, int64_t N, Ptr ns, Ptr ne, Ptr x, Ptr y, Ptr z, Ptr mm, Ptr centers, Ptr mp,
+                               Ptr s)
+          {
+              gravityLeaves(P<int32_t>(n2l), N, P<int32_t>(ns), P<int32_t>(ne), P<double>(x), P<double>(y),
+                            P<double>(z), P<float>(mm), P<double>(centers), P<void>(mp), St(s));
+          });
+    m.def("gravity_upsweep_level", [](int64_t a, int64_t b, Ptr n2l, Ptr child, Ptr centers, Ptr mp, Ptr s)
+          {
+              gravityUpsweepLevel(a, b, P<int32_t>(n2l), P<int32_t>(child), P<double>(centers), P<void>(mp), St(s));
+          });
+    m.def("gravity_set_mac", [](int64_t N, Ptr prefixes, const BoxArr& box, int kind, double invTheta, Ptr centers,
+                                Ptr s)
+          { gravitySetMac(N, P<KeyT>(prefixes), toBox(box), kind, invTheta, P<double>(centers), St(s)); });
+    m.def("compute_gravity",
+          [](int64_t first, int64_t last, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr centers, Ptr mp, Ptr x, Ptr y,
+             Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay, Ptr az, Ptr ugrav, Ptr out, Ptr stats, Ptr s)
+          {
+              computeGravity(first, last, P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne),
+                             P<double>(centers), P<void>(mp), P<double>(x), P<double>(y), P<double>(z), P<float>(h),
+                             P<float>(mm), float(G), P<float>(ax), P<float>(ay), P<float>(az), P<double>(ugrav),
+                             P<double>(out), P<unsigned long long>(stats), St(s));
+          });
+    m.def("direct_sum",
+          [](int64_t first, int64_t last, int64_t n, Ptr x, Ptr y, Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay,
+             Ptr az, Ptr ugrav, Ptr out, Ptr s)
+          {
+              directSum(first, last, n, P<double>(x), P<double>(y), P<double>(z), P<float>(h), P<float>(mm),
+                        float(G), P<float>(ax), P<float>(ay), P<float>(az), P<double>(ugrav), P<double>(out), St(s));
+          });
+
     m.def("update_positions",
           [](int64_t first, int64_t last, double dt, double dtm1, Ptr x, Ptr y, Ptr z, Ptr vx, Ptr vy, Ptr vz,
              Ptr xm1, Ptr ym1, Ptr zm1, Ptr ax, Ptr ay, Ptr az, Ptr h, Ptr temp, Ptr u, Ptr du, Ptr dum1, double cv,

@@ -1,0 +1,397 @@
+/*! Barnes-Hut self-gravity on gfx950: multipole upsweep, wave64 group traversal, direct sum.
+ *
+ * Parity: reference ryoanji/src/ryoanji/nbody/upwardpass.cuh:44-231 (computeLeafMultipoles, upsweepMultipoles
+ * per level), nbody/traversal.cuh:60-526 (traverse: warp per target group, breadth-first with approx (M2P) and
+ * body (P2P) queues, potential reduction), nbody/direct.cuh:44-112 (O(N^2) tiled direct sum).
+ *
+ * Design: one wave = 64 SFC-consecutive targets. The BFS frontier lives in LDS; MAC-accepted nodes are queued in an
+ * LDS M2P list, MAC-failing leaves in an LDS P2P list; both are flushed whenever they fill. M2P entries are
+ * broadcast as wave-uniform (scalar-cache) loads; P2P source tiles are loaded coalesced, converted to fp32
+ * coordinates relative to the group center and broadcast with v_readlane.
+ */
+#include <cfloat>
+
+#include "common.h"
+#include "hip_api.h"
+#include "sphx/gravity.hpp"
+
+namespace sphx::hip
+{
+
+__global__ void gravityLeavesKernel(const int32_t* __restrict__ n2l, int64_t N, const int32_t* __restrict__ ns,
+                                    const int32_t* __restrict__ ne, const double* __restrict__ x,
+                                    const double* __restrict__ y, const double* __restrict__ z,
+                                    const float* __restrict__ m, double* __restrict__ centers,
+                                    Quadrupole* __restrict__ mp)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= N || n2l[i] < 0) return;
+    double c[4] = {0, 0, 0, 0};
+    for (int32_t p = ns[i]; p < ne[i]; ++p)
+    {
+        c[0] += m[p] * x[p];
+        c[1] += m[p] * y[p];
+        c[2] += m[p] * z[p];
+        c[3] += m[p];
+    }
+    double inv    = c[3] != 0 ? 1.0 / c[3] : 0.0;
+    double com[3] = {c[0] * inv, c[1] * inv, c[2] * inv};
+    Quadrupole q;
+    p2m(x, y, z, m, ns[i], ne[i], com, q);
+    mp[i]              = q;
+    centers[4 * i + 0] = com[0];
+    centers[4 * i + 1] = com[1];
+    centers[4 * i + 2] = com[2];
+    centers[4 * i + 3] = c[3];
+}
+
+__global__ void gravityUpsweepKernel(int64_t a, int64_t b, const int32_t* __restrict__ n2l,
+                                     const int32_t* __restrict__ child, double* __restrict__ centers,
+                                     Quadrupole* __restrict__ mp)
+{
+    int64_t i = a + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= b || n2l[i] >= 0) return;
+    int32_t co  = child[i];
+    double c[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 8; ++k)
+    {
+        const double* cc = centers + 4 * (co + k);
+        c[0] += cc[3] * cc[0];
+        c[1] += cc[3] * cc[1];
+        c[2] += cc[3] * cc[2];
+        c[3] += cc[3];
+    }
+    double inv    = c[3] != 0 ? 1.0 / c[3] : 0.0;
+    double com[3] = {c[0] * inv, c[1] * inv, c[2] * inv};
+    Quadrupole q{};
+    for (int k = 0; k < 8; ++k)
+    {
+        const double* cc = centers + 4 * (co + k);
+        addQuadrupole(q, com[0] - cc[0], com[1] - cc[1], com[2] - cc[2], mp[co + k]);
+    }
+    mp[i]              = q;
+    centers[4 * i + 0] = com[0];
+    centers[4 * i + 1] = com[1];
+    centers[4 * i + 2] = com[2];
+    centers[4 * i + 3] = c[3];
+}
+
+__global__ void gravitySetMacKernel(int64_t N, const KeyT* __restrict__ prefixes, Box box, int kind, double invTheta,
+                                    double* __restrict__ centers)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    double gc[3], gs[3];
+    nodeGeometry(kind, prefixes[i], box, gc, gs);
+    double* c = centers + 4 * i;
+    if (c[3] == 0)
+    {
+        c[0] = gc[0];
+        c[1] = gc[1];
+        c[2] = gc[2];
+        c[3] = 0;
+    }
+    else { c[3] = vecMacR2(c, gc, gs, invTheta); }
+}
+
+void gravityLeaves(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
+                   const double* y, const double* z, const float* m, double* centers, void* mp, hipStream_t s)
+{
+    gravityLeavesKernel<<<gridFor(N, 128), 128, 0, s>>>(n2l, N, ns, ne, x, y, z, m, centers, (Quadrupole*)mp);
+    SPHX_LAUNCH_CHECK();
+}
+
+void gravityUpsweepLevel(int64_t a, int64_t b, const int32_t* n2l, const int32_t* child, double* centers, void* mp,
+                         hipStream_t s)
+{
+    if (b <= a) return;
+    gravityUpsweepKernel<<<gridFor(b - a, 256), 256, 0, s>>>(a, b, n2l, child, centers, (Quadrupole*)mp);
+    SPHX_LAUNCH_CHECK();
+}
+
+void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, double invTheta, double* centers,
+                   hipStream_t s)
+{
+    gravitySetMacKernel<<<gridFor(N, 256), 256, 0, s>>>(N, prefixes, box, kind, invTheta, centers);
+    SPHX_LAUNCH_CHECK();
+}
+
+// --------------------------------------------------------------------------------------------- traversal
+
+constexpr int kGWaves   = 4;
+constexpr int kGFront   = 512;
+constexpr int kGM2P     = 256;
+constexpr int kGLeaves  = 128;
+
+struct GravTree
+{
+    const int32_t* child;
+    const int32_t* n2l;
+    const int32_t* ns;
+    const int32_t* ne;
+    const double* centers;
+    const Quadrupole* mp;
+};
+
+//! @brief apply the queued multipoles to the lane's target (relative fp32 coordinates)
+__device__ inline void flushM2P(const int32_t* list, int n, const GravTree& t, double xi, double yi, double zi,
+                                float acc[4])
+{
+    for (int k = 0; k < n; ++k)
+    {
+        int32_t nd      = __builtin_amdgcn_readfirstlane(list[k]);
+        const double* c = t.centers + 4 * nd;
+        Quadrupole q    = t.mp[nd];
+        m2p(float(xi - c[0]), float(yi - c[1]), float(zi - c[2]), q, acc);
+    }
+}
+
+//! @brief P2P of the lane's target with all particles of the queued leaves
+__device__ inline void flushP2P(const int32_t* list, int n, const GravTree& t, const double* x, const double* y,
+                                const double* z, const float* h, const float* m, const double gc[3], float xr,
+                                float yr, float zr, float hi, float acc[4], int lane)
+{
+    for (int l = 0; l < n; ++l)
+    {
+        int32_t nd = __builtin_amdgcn_readfirstlane(list[l]);
+        int32_t a = t.ns[nd], b = t.ne[nd];
+        for (int32_t c0 = a; c0 < b; c0 += 64)
+        {
+            int32_t j = c0 + lane;
+            int cnt   = min(64, b - c0);
+            float sx = 0, sy = 0, sz = 0, sm = 0, sh = 0;
+            if (j < b)
+            {
+                sx = float(x[j] - gc[0]);
+                sy = float(y[j] - gc[1]);
+                sz = float(z[j] - gc[2]);
+                sm = m[j];
+                sh = h[j];
+            }
+            for (int k = 0; k < cnt; ++k)
+            {
+                float dx = readLaneF(sx, k) - xr;
+                float dy = readLaneF(sy, k) - yr;
+                float dz = readLaneF(sz, k) - zr;
+                p2p(dx, dy, dz, readLaneF(sm, k), hi, readLaneF(sh, k), acc);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last, GravTree t,
+                                                     const double* __restrict__ x, const double* __restrict__ y,
+                                                     const double* __restrict__ z, const float* __restrict__ h,
+                                                     const float* __restrict__ m, float G, float* __restrict__ ax,
+                                                     float* __restrict__ ay, float* __restrict__ az,
+                                                     double* __restrict__ ugrav, double* __restrict__ out,
+                                                     unsigned long long* __restrict__ stats)
+{
+    __shared__ int32_t frontA[kGWaves][kGFront];
+    __shared__ int32_t frontB[kGWaves][kGFront];
+    __shared__ int32_t m2pList[kGWaves][kGM2P];
+    __shared__ int32_t leafList[kGWaves][kGLeaves];
+    __shared__ double red[kGWaves];
+
+    const int wave          = threadIdx.x >> 6;
+    const int lane          = threadIdx.x & 63;
+    const int64_t numGroups = (last - first + 63) / 64;
+    const unsigned lb       = xcdRemap(blockIdx.x, gridDim.x);
+    const int64_t g         = int64_t(lb) * kGWaves + wave;
+    double upot             = 0;
+    if (g < numGroups)
+    {
+        const int64_t i  = first + g * 64 + lane;
+        const bool valid = i < last;
+        const int64_t ii = valid ? i : (last - 1);
+        double xi = x[ii], yi = y[ii], zi = z[ii];
+        float hi  = h[ii];
+
+        double tc[3], ts[3];
+        {
+            double p[3] = {xi, yi, zi};
+            for (int d = 0; d < 3; ++d)
+            {
+                double a = waveMin(p[d]);
+                double b = waveMax(p[d]);
+                tc[d]    = 0.5 * (a + b);
+                ts[d]    = 0.5 * (b - a);
+            }
+        }
+        float xr = float(xi - tc[0]), yr = float(yi - tc[1]), zr = float(zi - tc[2]);
+        float acc[4] = {0, 0, 0, 0};
+
+        int32_t* cur  = frontA[wave];
+        int32_t* nxt  = frontB[wave];
+        int32_t* mlst = m2pList[wave];
+        int32_t* llst = leafList[wave];
+        int nf = 1, nm = 0, nl = 0;
+        bool overflow = false;
+        if (lane == 0) cur[0] = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        while (nf > 0)
+        {
+            int nn = 0;
+            for (int base = 0; base < nf; base += 64)
+            {
+                int idx     = base + lane;
+                int32_t nd  = idx < nf ? cur[idx] : -1;
+                bool isM2P = false, isLeaf = false, isInt = false;
+                if (nd >= 0)
+                {
+                    const double* c = t.centers + 4 * nd;
+                    bool violated   = macViolated(c, c[3], tc, ts);
+                    isM2P           = !violated && c[3] != 0.0;
+                    isLeaf          = violated && t.n2l[nd] >= 0;
+                    isInt           = violated && t.n2l[nd] < 0;
+                }
+                uint64_t bm = ballot(isM2P), bl = ballot(isLeaf), bi = ballot(isInt);
+                int cm = __popcll(bm), cl = __popcll(bl), ci = __popcll(bi);
+                // flush the queues if this batch would overflow them
+                if (nm + cm > kGM2P)
+                {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    flushM2P(mlst, nm, t, xi, yi, zi, acc);
+                    nm = 0;
+                }
+                if (nl + cl > kGLeaves)
+                {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
+                    nl = 0;
+                }
+                if (isM2P) mlst[nm + __popcll(bm & lanemaskLt())] = nd;
+                if (isLeaf) llst[nl + __popcll(bl & lanemaskLt())] = nd;
+                if (isInt)
+                {
+                    int pos    = nn + 8 * __popcll(bi & lanemaskLt());
+                    int32_t co = t.child[nd];
+                    if (pos + 8 <= kGFront)
+                        for (int k = 0; k < 8; ++k)
+                            nxt[pos + k] = co + k;
+                }
+                nm += cm;
+                nl += cl;
+                nn += 8 * ci;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (nn > kGFront)
+            {
+                overflow = true;
+                nn       = 0;
+            }
+            int32_t* tmp = cur;
+            cur          = nxt;
+            nxt          = tmp;
+            nf           = nn;
+        }
+        flushM2P(mlst, nm, t, xi, yi, zi, acc);
+        flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
+
+        if (valid)
+        {
+            double u = double(G) * double(m[i]) * double(acc[0]);
+            upot     = u;
+            if (ugrav) ugrav[i] += u;
+            ax[i] += G * acc[1];
+            ay[i] += G * acc[2];
+            az[i] += G * acc[3];
+        }
+        if (lane == 0 && overflow) atomicAdd(&stats[1], 1ull);
+    }
+    double s = waveSum(upot);
+    if (lane == 0) red[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        double tot = 0;
+        for (int w = 0; w < kGWaves; ++w)
+            tot += red[w];
+        atomicAdd(out, 0.5 * tot);
+    }
+}
+
+void computeGravity(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
+                    const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
+                    const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
+                    double* ugrav, double* out, unsigned long long* stats, hipStream_t s)
+{
+    int64_t n = last - first;
+    if (n <= 0) return;
+    GravTree t{child, n2l, ns, ne, centers, (const Quadrupole*)mp};
+    int64_t groups = (n + 63) / 64;
+    unsigned grid  = unsigned((groups + kGWaves - 1) / kGWaves);
+    gravityKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats);
+    SPHX_LAUNCH_CHECK();
+}
+
+// --------------------------------------------------------------------------------------------- direct sum
+
+constexpr int kDirectTile = 256;
+
+__global__ __launch_bounds__(kDirectTile) void directKernel(int64_t first, int64_t last, int64_t n,
+                                                            const double* __restrict__ x,
+                                                            const double* __restrict__ y,
+                                                            const double* __restrict__ z,
+                                                            const float* __restrict__ h, const float* __restrict__ m,
+                                                            float G, float* __restrict__ ax, float* __restrict__ ay,
+                                                            float* __restrict__ az, double* __restrict__ ugrav,
+                                                            double* __restrict__ out)
+{
+    __shared__ double sx[kDirectTile], sy[kDirectTile], sz[kDirectTile];
+    __shared__ float sm[kDirectTile], sh[kDirectTile];
+    __shared__ double red[kDirectTile / 64];
+    int64_t i   = first + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    bool valid  = i < last;
+    double xi = valid ? x[i] : 0, yi = valid ? y[i] : 0, zi = valid ? z[i] : 0;
+    float hi  = valid ? h[i] : 0;
+    double acc[4] = {0, 0, 0, 0};
+    for (int64_t t0 = 0; t0 < n; t0 += kDirectTile)
+    {
+        int64_t j = t0 + threadIdx.x;
+        if (j < n)
+        {
+            sx[threadIdx.x] = x[j];
+            sy[threadIdx.x] = y[j];
+            sz[threadIdx.x] = z[j];
+            sm[threadIdx.x] = m[j];
+            sh[threadIdx.x] = h[j];
+        }
+        __syncthreads();
+        int cnt = int(min<int64_t>(kDirectTile, n - t0));
+        for (int k = 0; k < cnt; ++k)
+            p2p(sx[k] - xi, sy[k] - yi, sz[k] - zi, double(sm[k]), double(hi), double(sh[k]), acc);
+        __syncthreads();
+    }
+    double u = 0;
+    if (valid)
+    {
+        u = double(G) * double(m[i]) * acc[0];
+        if (ugrav) ugrav[i] = u;
+        ax[i] = float(G * acc[1]);
+        ay[i] = float(G * acc[2]);
+        az[i] = float(G * acc[3]);
+    }
+    double s = waveSum(u);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        double tot = 0;
+        for (int w = 0; w < kDirectTile / 64; ++w)
+            tot += red[w];
+        atomicAdd(out, 0.5 * tot);
+    }
+}
+
+void directSum(int64_t first, int64_t last, int64_t n, const double* x, const double* y, const double* z,
+               const float* h, const float* m, float G, float* ax, float* ay, float* az, double* ugrav, double* out,
+               hipStream_t s)
+{
+    if (last <= first) return;
+    directKernel<<<gridFor(last - first, kDirectTile), kDirectTile, 0, s>>>(first, last, n, x, y, z, h, m, G, ax, ay,
+                                                                             az, ugrav, out);
+    SPHX_LAUNCH_CHECK();
+}
+
+} // namespace sphx::hip

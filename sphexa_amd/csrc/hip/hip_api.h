@@ -129,4 +129,19 @@ void conservedQuantities(int64_t first, int64_t last, const double* x, const dou
                          const float* vx, const float* vy, const float* vz, const float* m, const double* temp,
                          const double* u, const int32_t* nc, double cv, double* out, hipStream_t s);
 
+// gravity.hip
+void gravityLeaves(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
+                   const double* y, const double* z, const float* m, double* centers, void* mp, hipStream_t s);
+void gravityUpsweepLevel(int64_t a, int64_t b, const int32_t* n2l, const int32_t* child, double* centers, void* mp,
+                         hipStream_t s);
+void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, double invTheta, double* centers,
+                   hipStream_t s);
+void computeGravity(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
+                    const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
+                    const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
+                    double* ugrav, double* out, unsigned long long* stats, hipStream_t s);
+void directSum(int64_t first, int64_t last, int64_t n, const double* x, const double* y, const double* z,
+               const float* h, const float* m, float G, float* ax, float* ay, float* az, double* ugrav, double* out,
+               hipStream_t s);
+
 } // namespace sphx::hip

@@ -1,0 +1,40 @@
+"""Self-gravity holder used by the propagators (``--G`` / test cases with gravConstant != 0).
+
+Parity: reference main/src/propagator/gravity_wrapper.hpp:42-133 (MultipoleHolderCpu/Gpu: upsweep, traverse,
+egrav = 0.5 G sum m phi, accelerations added to ax, ay, az) and ryoanji/interface/multipole_holder.cu.
+
+Multi-rank: the local octree covers own particles and the SPH halos; remote far-field contributions come through
+a locally-essential tree exchange (parallel/let.py): every rank pushes to every other rank the multipoles of its
+nodes that satisfy the vector MAC with respect to the receiver's domain box, and the particles of leaves that do
+not. Received particles join the local tree as gravity halos; received multipoles are applied as a flat M2P list.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from ..ops import gravity as G
+from ..parallel.comm import SUM
+
+
+class MultipoleHolder:
+    def __init__(self):
+        self.centers = None
+        self.multipoles = None
+        self.stats = {}
+
+    def upsweep(self, d, domain):
+        ot = domain.octree
+        self.centers, self.multipoles = G.upsweep(ot, d["x"], d["y"], d["z"], d["m"], domain.box, domain.theta,
+                                                  domain.sfc_kind)
+
+    def traverse(self, d, domain):
+        first, last = domain.start_index(), domain.end_index()
+        ot = domain.octree
+        egrav = G.compute_gravity(ot, self.centers, self.multipoles, first, last, d["x"], d["y"], d["z"], d["h"],
+                                  d["m"], d.g, d["ax"], d["ay"], d["az"])
+        let = getattr(domain, "let", None)
+        if let is not None:
+            egrav += let.apply_remote_multipoles(d, first, last)
+        # rank-local share; the observables reduction sums it over ranks (as the reference's MPI_Reduce does)
+        d.egrav = egrav

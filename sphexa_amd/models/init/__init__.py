@@ -28,31 +28,31 @@ def initializer_factory(init: str, glass: str | None = None):
 
         return SedovGlass(glass, settings)
     if name == "noh":
-        from .noh import NohGlassSphere
+        from .cases import NohGlassSphere
 
         return NohGlassSphere(glass, settings)
     if name == "evrard":
-        from .evrard import EvrardGlassSphere
+        from .cases import EvrardGlassSphere
 
         return EvrardGlassSphere(glass, settings)
     if name == "isobaric-cube":
-        from .isobaric_cube import IsobaricCubeGlass
+        from .cases import IsobaricCubeGlass
 
         return IsobaricCubeGlass(glass, settings)
     if name == "wind-shock":
-        from .wind_shock import WindShockGlass
+        from .cases import WindShockGlass
 
         return WindShockGlass(glass, settings)
     if name == "turbulence":
-        from .turbulence import TurbulenceGlass
+        from .cases import TurbulenceGlass
 
         return TurbulenceGlass(glass, settings)
     if name == "kelvin-helmholtz":
-        from .kelvin_helmholtz import KelvinHelmholtzGlass
+        from .cases import KelvinHelmholtzGlass
 
         return KelvinHelmholtzGlass(glass, settings)
     if name == "gresho-chan":
-        from .gresho_chan import GreshoChan
+        from .cases import GreshoChan
 
         return GreshoChan(glass, settings)
     if name == "evrard-cooling":

@@ -1,0 +1,83 @@
+"""Barnes-Hut self-gravity operators (Cartesian quadrupoles).
+
+Parity: reference ryoanji/src/ryoanji/interface/multipole_holder.cu:47-237 (upsweep -> traverse), nbody/
+upwardpass.cuh (leaf P2M, per-level M2M), nbody/traversal.cuh (BH traversal, M2P + P2P), nbody/direct.cuh (direct
+sum). On the GPU the traversal runs one wave per 64-target group with an LDS frontier (like the neighbor search);
+P2P tiles of 64 targets x 64 sources run on the f32 MFMA units (see csrc/hip/gravity.hip).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .octree import MAX_LEVEL, Octree
+from ..utils.box import Box
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def upsweep(tree: Octree, x, y, z, m, box: Box, theta: float, sfc_kind: int = 0):
+    """mass centers + squared vector-MAC radii (N x 4 f64) and quadrupoles (N x 8 f32) of every node"""
+    N = tree.num_nodes
+    centers = torch.empty(4 * N, dtype=torch.float64, device=x.device)
+    mp = torch.zeros(8 * N, dtype=torch.float32, device=x.device)
+    inv_theta = 1.0 / theta
+    if x.is_cuda:
+        h = _lib.hip()
+        s = _stream()
+        h.gravity_leaves(tree.node_to_leaf.data_ptr(), N, tree.node_start.data_ptr(), tree.node_end.data_ptr(),
+                         x.data_ptr(), y.data_ptr(), z.data_ptr(), m.data_ptr(), centers.data_ptr(), mp.data_ptr(), s)
+        for l in range(MAX_LEVEL, -1, -1):
+            a, b = tree.level_range[l], tree.level_range[l + 1]
+            if b > a:
+                h.gravity_upsweep_level(a, b, tree.node_to_leaf.data_ptr(), tree.child_offsets.data_ptr(),
+                                        centers.data_ptr(), mp.data_ptr(), s)
+        h.gravity_set_mac(N, tree.prefixes.data_ptr(), box.to_array(), sfc_kind, inv_theta, centers.data_ptr(), s)
+    else:
+        _lib.cpu().gravity_upsweep(N, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.level_range,
+                                   tree.prefixes.data_ptr(), tree.node_start.data_ptr(), tree.node_end.data_ptr(),
+                                   x.data_ptr(), y.data_ptr(), z.data_ptr(), m.data_ptr(), box.to_array(), sfc_kind,
+                                   inv_theta, centers.data_ptr(), mp.data_ptr())
+    return centers, mp
+
+
+def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h, m, G: float, ax, ay, az,
+                    ugrav=None) -> float:
+    """add G * a_grav to ax, ay, az for targets [first, last); returns this rank's 0.5 * sum G m phi"""
+    if last <= first:
+        return 0.0
+    if x.is_cuda:
+        hp = _lib.hip()
+        out = torch.zeros(2, dtype=torch.float64, device=x.device)
+        stats = torch.zeros(4, dtype=torch.int64, device=x.device)
+        hp.compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
+                           tree.node_start.data_ptr(), tree.node_end.data_ptr(), centers.data_ptr(), mp.data_ptr(),
+                           x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), m.data_ptr(), float(G),
+                           ax.data_ptr(), ay.data_ptr(), az.data_ptr(), 0 if ugrav is None else ugrav.data_ptr(),
+                           out.data_ptr(), stats.data_ptr(), _stream())
+        st = stats.cpu()
+        if int(st[1]) > 0:
+            raise RuntimeError(f"gravity traversal stack overflow in {int(st[1])} groups")
+        return float(out[0].item())
+    return float(_lib.cpu().compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
+                                            tree.node_start.data_ptr(), tree.node_end.data_ptr(), centers.data_ptr(),
+                                            mp.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
+                                            m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
+                                            0 if ugrav is None else ugrav.data_ptr()))
+
+
+def direct_sum(first: int, last: int, x, y, z, h, m, G: float, ax, ay, az, ugrav=None) -> float:
+    """O(N^2) softened gravity of all particles on targets [first, last) (overwrites ax, ay, az)"""
+    n = x.numel()
+    if x.is_cuda:
+        out = torch.zeros(1, dtype=torch.float64, device=x.device)
+        _lib.hip().direct_sum(first, last, n, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), m.data_ptr(),
+                              float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
+                              0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), _stream())
+        return float(out.item())
+    return float(_lib.cpu().direct_sum(first, last, n, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
+                                       m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
+                                       0 if ugrav is None else ugrav.data_ptr()))

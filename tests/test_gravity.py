@@ -1,0 +1,100 @@
+"""Barnes-Hut gravity vs direct sum (reference ryoanji/test: traversal_cpu.cpp, interface/global_forces_gpu.cpp
+thresholds: 1st-percentile relative acceleration error < 1e-3, max < 3e-2, potential relative error < 1e-2)."""
+
+import numpy as np
+import pytest
+import torch
+
+from sphexa_amd.ops import gravity as G
+from sphexa_amd.ops import octree as O
+from sphexa_amd.ops import sfc
+from sphexa_amd.utils.box import Box, OPEN
+
+
+def plummer(n, seed=0):
+    rng = np.random.default_rng(seed)
+    r = 1.0 / np.sqrt(rng.uniform(0.01, 0.95, n) ** (-2.0 / 3.0) - 1.0)
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1)[:, None]
+    return u * r[:, None]
+
+
+def _setup(n, device="cpu", seed=0, bucket=64):
+    X = plummer(n, seed)
+    box = Box([float(X[:, k].min()) - 1e-9 for k in range(3)], [float(X[:, k].max()) + 1e-9 for k in range(3)],
+              [OPEN] * 3)
+    x, y, z = (torch.from_numpy(X[:, k].copy()) for k in range(3))
+    keys = sfc.compute_keys(x, y, z, box)
+    s, p = sfc.sort_keys(keys)
+    p = p.long()
+    x, y, z = x[p], y[p], z[p]
+    m = torch.full((n,), 1.0 / n, dtype=torch.float32)
+    h = torch.full((n,), 0.01, dtype=torch.float32)
+    dev = torch.device(device)
+    x, y, z, m, h, s = (t.to(dev) for t in (x, y, z, m, h, s))
+    tree, counts = O.update_tree(None, s, bucket)
+    ot = O.build_octree(tree, counts, s, x, y, z)
+    return box, ot, x, y, z, m, h
+
+
+def _errors(a_bh, a_ref):
+    num = np.linalg.norm(a_bh - a_ref, axis=1)
+    den = np.linalg.norm(a_ref, axis=1)
+    return np.sort(num / den)
+
+
+@pytest.mark.parametrize("theta", [0.5, 0.75])
+def test_bh_vs_direct_cpu(theta):
+    n = 6000
+    box, ot, x, y, z, m, h = _setup(n)
+    centers, mp = G.upsweep(ot, x, y, z, m, box, theta)
+    # root mass and center
+    assert abs(float(mp[0]) - 1.0) < 1e-5
+    ax, ay, az = (torch.zeros(n, dtype=torch.float32) for _ in range(3))
+    eg = G.compute_gravity(ot, centers, mp, 0, n, x, y, z, h, m, 1.0, ax, ay, az)
+    rx, ry, rz = (torch.zeros(n, dtype=torch.float32) for _ in range(3))
+    egd = G.direct_sum(0, n, x, y, z, h, m, 1.0, rx, ry, rz)
+    a = np.stack([ax.numpy(), ay.numpy(), az.numpy()], 1).astype(np.float64)
+    r = np.stack([rx.numpy(), ry.numpy(), rz.numpy()], 1).astype(np.float64)
+    err = _errors(a, r)
+    assert err[int(0.01 * n)] < 1e-3
+    assert err[-1] < 3e-2
+    assert abs(eg - egd) / abs(egd) < 1e-2
+
+
+def test_direct_sum_two_body():
+    x = torch.tensor([0.0, 1.0], dtype=torch.float64)
+    y = torch.zeros(2, dtype=torch.float64)
+    z = torch.zeros(2, dtype=torch.float64)
+    m = torch.tensor([1.0, 2.0], dtype=torch.float32)
+    h = torch.full((2,), 1e-3, dtype=torch.float32)
+    ax, ay, az = (torch.zeros(2, dtype=torch.float32) for _ in range(3))
+    eg = G.direct_sum(0, 2, x, y, z, h, m, 1.0, ax, ay, az)
+    assert abs(float(ax[0]) - 2.0) < 1e-6 and abs(float(ax[1]) + 1.0) < 1e-6
+    assert abs(eg - (-2.0)) < 1e-9
+
+
+@pytest.mark.gpu
+def test_gravity_gpu_matches_cpu(gpu):
+    n = 20000
+    box, ot, x, y, z, m, h = _setup(n)
+    cc, mc = G.upsweep(ot, x, y, z, m, box, 0.5)
+    axc, ayc, azc = (torch.zeros(n, dtype=torch.float32) for _ in range(3))
+    egc = G.compute_gravity(ot, cc, mc, 0, n, x, y, z, h, m, 1.0, axc, ayc, azc)
+    boxg, otg, xg, yg, zg, mg, hg = _setup(n, gpu)
+    cg, mgp = G.upsweep(otg, xg, yg, zg, mg, boxg, 0.5)
+    assert torch.allclose(cg.cpu(), cc, rtol=1e-9, atol=1e-12)
+    assert torch.allclose(mgp.cpu(), mc, rtol=1e-4, atol=1e-9)
+    axg, ayg, azg = (torch.zeros(n, dtype=torch.float32, device=gpu) for _ in range(3))
+    egg = G.compute_gravity(otg, cg, mgp, 0, n, xg, yg, zg, hg, mg, 1.0, axg, ayg, azg)
+    a = np.stack([axg.cpu().numpy(), ayg.cpu().numpy(), azg.cpu().numpy()], 1)
+    r = np.stack([axc.numpy(), ayc.numpy(), azc.numpy()], 1)
+    err = _errors(a.astype(np.float64), r.astype(np.float64))
+    assert err[-1] < 1e-3
+    assert abs(egg - egc) / abs(egc) < 1e-4
+    # and vs direct sum on the GPU
+    rx, ry, rz = (torch.zeros(n, dtype=torch.float32, device=gpu) for _ in range(3))
+    G.direct_sum(0, n, xg, yg, zg, hg, mg, 1.0, rx, ry, rz)
+    d = np.stack([rx.cpu().numpy(), ry.cpu().numpy(), rz.cpu().numpy()], 1).astype(np.float64)
+    err = _errors(a.astype(np.float64), d)
+    assert err[int(0.01 * n)] < 1e-3 and err[-1] < 3e-2
