@@ -94,7 +94,7 @@ def main(argv=None) -> int:
 
     writer = sio.file_writer_factory(ascii, comm)
     sim_init = initializer_factory(init_cond, glass)
-    propagator = propagator_factory(prop, av_clean, out, rank, quiet)
+    propagator = propagator_factory(prop, av_clean, out, rank, quiet, sim_init.constants())
     observables = _observables_factory(sim_init.constants(), const_path, rank, init_cond)
 
     t_total = time.perf_counter()

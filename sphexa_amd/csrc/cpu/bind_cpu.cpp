@@ -126,6 +126,20 @@ PYBIND11_MODULE(_sphx_cpu, m)
     m.def("compute_keys", [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, int kind, Ptr keys)
           { cpu::computeKeys(n, P<double>(x), P<double>(y), P<double>(z), toBox(box), kind, P<KeyT>(keys)); });
 
+    m.def("decode_keys",
+          [](int64_t n, Ptr keys, int kind, Ptr ix, Ptr iy, Ptr iz)
+          {
+              const KeyT* k = P<KeyT>(keys);
+              int32_t *a = P<int32_t>(ix), *b = P<int32_t>(iy), *c = P<int32_t>(iz);
+#pragma omp parallel for schedule(static)
+              for (int64_t i = 0; i < n; ++i)
+              {
+                  uint32_t u, v, w;
+                  sfcDecode(kind, k[i], u, v, w);
+                  a[i] = int32_t(u), b[i] = int32_t(v), c[i] = int32_t(w);
+              }
+          });
+
     m.def("sort_keys", [](int64_t n, Ptr keys, Ptr perm) { cpu::sortKeys(n, P<KeyT>(keys), P<int32_t>(perm)); });
 
     m.def("gather", [](int64_t n, Ptr perm, Ptr src, Ptr dst, int elemSize)
@@ -405,4 +419,13 @@ PYBIND11_MODULE(_sphx_cpu, m)
 
     m.def("update_h", [](int64_t first, int64_t last, unsigned ng0, Ptr nc, Ptr h)
           { cpu::updateSmoothingLength(first, last, ng0, P<uint32_t>(nc), P<float>(h)); });
+
+    m.def("compute_stirring",
+          [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr ax, Ptr ay, Ptr az, int64_t numModes, Ptr modes,
+             Ptr re, Ptr im, Ptr amp, double norm)
+          {
+              cpu::computeStirring(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(ax), P<float>(ay),
+                                   P<float>(az), numModes, P<double>(modes), P<double>(re), P<double>(im),
+                                   P<double>(amp), norm);
+          });
 }

@@ -92,3 +92,13 @@ double directSum(int64_t first, int64_t last, int64_t n, const double* x, const 
                  const float* h, const float* m, double G, float* ax, float* ay, float* az, double* ugrav);
 
 } // namespace sphx::cpu
+
+namespace sphx::cpu
+{
+
+//! turbulence stirring: a_i += norm * sum_m amp_m (Re_m cos(k_m.x_i) - Im_m sin(k_m.x_i)), modes as (kx,ky,kz)
+void computeStirring(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* ax,
+                     float* ay, float* az, int64_t numModes, const double* modes, const double* phaseRe,
+                     const double* phaseIm, const double* amplitudes, double norm);
+
+} // namespace sphx::cpu

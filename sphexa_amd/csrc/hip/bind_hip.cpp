@@ -345,4 +345,12 @@ PYBIND11_MODULE(_sphx_hip, m)
                                   P<float>(vz), P<float>(mm), P<double>(temp), P<double>(u), P<int32_t>(nc), cv,
                                   P<double>(out), St(s));
           });
+
+    m.def("compute_stirring",
+          [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr ax, Ptr ay, Ptr az, int numModes, Ptr modes,
+             double norm, Ptr s)
+          {
+              computeStirring(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(ax), P<float>(ay),
+                              P<float>(az), numModes, P<void>(modes), float(norm), St(s));
+          });
 }

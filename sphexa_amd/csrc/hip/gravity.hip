@@ -147,14 +147,16 @@ __device__ inline void flushM2P(const int32_t* list, int n, const GravTree& t, d
 }
 
 //! @brief P2P of the lane's target with all particles of the queued leaves
-__device__ inline void flushP2P(const int32_t* list, int n, const GravTree& t, const double* x, const double* y,
-                                const double* z, const float* h, const float* m, const double gc[3], float xr,
-                                float yr, float zr, float hi, float acc[4], int lane)
+__device__ inline int flushP2P(const int32_t* list, int n, const GravTree& t, const double* x, const double* y,
+                               const double* z, const float* h, const float* m, const double gc[3], float xr,
+                               float yr, float zr, float hi, float acc[4], int lane)
 {
+    int numP2P = 0;
     for (int l = 0; l < n; ++l)
     {
         int32_t nd = __builtin_amdgcn_readfirstlane(list[l]);
         int32_t a = t.ns[nd], b = t.ne[nd];
+        numP2P += b - a;
         for (int32_t c0 = a; c0 < b; c0 += 64)
         {
             int32_t j = c0 + lane;
@@ -177,6 +179,7 @@ __device__ inline void flushP2P(const int32_t* list, int n, const GravTree& t, c
             }
         }
     }
+    return numP2P;
 }
 
 __global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last, GravTree t,
@@ -227,6 +230,7 @@ __global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last
         int32_t* llst = leafList[wave];
         int nf = 1, nm = 0, nl = 0;
         bool overflow = false;
+        unsigned long long totM2P = 0, totP2P = 0;
         if (lane == 0) cur[0] = 0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         while (nf > 0)
@@ -257,7 +261,7 @@ __global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last
                 if (nl + cl > kGLeaves)
                 {
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
+                    totP2P += flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
                     nl = 0;
                 }
                 if (isM2P) mlst[nm + __popcll(bm & lanemaskLt())] = nd;
@@ -272,6 +276,7 @@ __global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last
                 }
                 nm += cm;
                 nl += cl;
+                totM2P += cm;
                 nn += 8 * ci;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -286,7 +291,7 @@ __global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last
             nf           = nn;
         }
         flushM2P(mlst, nm, t, xi, yi, zi, acc);
-        flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
+        totP2P += flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
 
         if (valid)
         {
@@ -297,7 +302,16 @@ __global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last
             ay[i] += G * acc[2];
             az[i] += G * acc[3];
         }
-        if (lane == 0 && overflow) atomicAdd(&stats[1], 1ull);
+        if (lane == 0)
+        {
+            // stats: [0] sum of P2P per target, [1] overflowed groups, [2] sum of M2P, [3] max P2P, [4] max M2P
+            auto nv = (unsigned long long)(min(int64_t(64), last - (first + g * 64)));
+            if (overflow) atomicAdd(&stats[1], 1ull);
+            atomicAdd(&stats[0], totP2P * nv);
+            atomicAdd(&stats[2], totM2P * nv);
+            atomicMax(&stats[3], totP2P);
+            atomicMax(&stats[4], totM2P);
+        }
     }
     double s = waveSum(upot);
     if (lane == 0) red[wave] = s;

@@ -144,4 +144,8 @@ void directSum(int64_t first, int64_t last, int64_t n, const double* x, const do
                const float* h, const float* m, float G, float* ax, float* ay, float* az, double* ugrav, double* out,
                hipStream_t s);
 
+// turbulence.hip: modes = numModes records of 10 floats {kx, ky, kz, pad, amp*Re[3], amp*Im[3]}
+void computeStirring(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* ax,
+                     float* ay, float* az, int numModes, const void* modes, float norm, hipStream_t s);
+
 } // namespace sphx::hip

@@ -130,7 +130,7 @@ py::dict readAttrs(hid_t loc)
         hid_t space = H5Aget_space(attr);
         hssize_t np = H5Sget_simple_extent_npoints(space);
         char code   = codeOf(ftype);
-        py::array out(dtypeOf(code), {np});
+        py::array out(dtypeOf(code), std::vector<py::ssize_t>{py::ssize_t(np)});
         check(H5Aread(attr, memType(code), out.mutable_data()), "attr read");
         d[py::str(n)] = out;
         H5Sclose(space);
@@ -250,7 +250,7 @@ PYBIND11_MODULE(_sphx_io, m)
               char code   = as.empty() ? codeOf(ftype) : as[0];
               hid_t fs    = H5Dget_space(ds);
               hsize_t off = hsize_t(offset), cnt = hsize_t(count);
-              py::array out(dtypeOf(code), {count});
+              py::array out(dtypeOf(code), std::vector<py::ssize_t>{py::ssize_t(count)});
               if (cnt > 0)
               {
                   check(H5Sselect_hyperslab(fs, H5S_SELECT_SET, &off, nullptr, &cnt, nullptr), "hyperslab");

@@ -32,7 +32,7 @@ class MultipoleHolder:
         first, last = domain.start_index(), domain.end_index()
         ot = domain.octree
         egrav = G.compute_gravity(ot, self.centers, self.multipoles, first, last, d["x"], d["y"], d["z"], d["h"],
-                                  d["m"], d.g, d["ax"], d["ay"], d["az"])
+                                  d["m"], d.g, d["ax"], d["ay"], d["az"], stats=self.stats)
         let = getattr(domain, "let", None)
         if let is not None:
             egrav += let.apply_remote_multipoles(d, first, last)

@@ -175,7 +175,8 @@ class HydroVeProp(Propagator):
         H.compute_av_switches(d, nl, box)
         t.step("AVswitches")
         if self.av_clean:
-            domain.exchange_halos(d, ["dV11", "dV12", "dV22", "dV23", "dV33", "alpha"])
+            # all six gradient components: the reference (ve_hydro.hpp:186) leaves dV13 halos stale
+            domain.exchange_halos(d, ["dV11", "dV12", "dV13", "dV22", "dV23", "dV33", "alpha"])
         else:
             domain.exchange_halos(d, ["alpha"])
         t.step("mpi::synchronizeHalos")
@@ -270,7 +271,7 @@ class HydroProp(Propagator):
         self.timer.stop()
 
 
-def propagator_factory(name: str, av_clean: bool, out, rank: int, quiet: bool = False) -> Propagator:
+def propagator_factory(name: str, av_clean: bool, out, rank: int, quiet: bool = False, settings=None) -> Propagator:
     if name == "ve":
         return HydroVeProp(out, rank, av_clean, quiet)
     if name == "std":
@@ -282,7 +283,9 @@ def propagator_factory(name: str, av_clean: bool, out, rank: int, quiet: bool = 
     if name == "turbulence":
         from .turbulence import TurbVeProp
 
-        return TurbVeProp(out, rank, av_clean, quiet)
+        if settings is None or "solWeight" not in settings:
+            raise RuntimeError("--prop turbulence needs the turbulence settings (use --init turbulence)")
+        return TurbVeProp(out, rank, av_clean, quiet, settings)
     if name == "std-cooling":
         raise RuntimeError("--prop std-cooling requires the Grackle chemistry library, which is not available in "
                            "this build")

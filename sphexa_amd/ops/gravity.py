@@ -45,20 +45,23 @@ def upsweep(tree: Octree, x, y, z, m, box: Box, theta: float, sfc_kind: int = 0)
 
 
 def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h, m, G: float, ax, ay, az,
-                    ugrav=None) -> float:
-    """add G * a_grav to ax, ay, az for targets [first, last); returns this rank's 0.5 * sum G m phi"""
+                    ugrav=None, stats: dict | None = None) -> float:
+    """add G * a_grav to ax, ay, az for targets [first, last); returns this rank's 0.5 * sum G m phi.
+    On the GPU ``stats`` (if given) receives p2p/m2p (summed over targets) and max_p2p/max_m2p (per target)."""
     if last <= first:
         return 0.0
     if x.is_cuda:
         hp = _lib.hip()
         out = torch.zeros(2, dtype=torch.float64, device=x.device)
-        stats = torch.zeros(4, dtype=torch.int64, device=x.device)
+        st_dev = torch.zeros(5, dtype=torch.int64, device=x.device)
         hp.compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
                            tree.node_start.data_ptr(), tree.node_end.data_ptr(), centers.data_ptr(), mp.data_ptr(),
                            x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), m.data_ptr(), float(G),
                            ax.data_ptr(), ay.data_ptr(), az.data_ptr(), 0 if ugrav is None else ugrav.data_ptr(),
-                           out.data_ptr(), stats.data_ptr(), _stream())
-        st = stats.cpu()
+                           out.data_ptr(), st_dev.data_ptr(), _stream())
+        st = st_dev.cpu()
+        if stats is not None:
+            stats.update(p2p=int(st[0]), m2p=int(st[2]), max_p2p=int(st[3]), max_m2p=int(st[4]))
         if int(st[1]) > 0:
             raise RuntimeError(f"gravity traversal stack overflow in {int(st[1])} groups")
         return float(out[0].item())

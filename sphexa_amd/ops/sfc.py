@@ -37,6 +37,19 @@ def compute_keys(x: torch.Tensor, y: torch.Tensor, z: torch.Tensor, box: Box, ki
     return out
 
 
+MAX_COORD = 1 << 21
+
+
+def decode_keys(keys: torch.Tensor, box: Box | None = None, kind: int = HILBERT):
+    """integer grid coordinates (0 .. 2^21-1) of the cell lower corner of each key (sfc.hpp decodeSfc); host only"""
+    k = keys.detach().cpu().contiguous()
+    n = k.numel()
+    ix, iy, iz = (torch.empty(n, dtype=torch.int32) for _ in range(3))
+    if n:
+        _lib.cpu().decode_keys(n, k.data_ptr(), kind, ix.data_ptr(), iy.data_ptr(), iz.data_ptr())
+    return ix, iy, iz
+
+
 def sort_keys(keys: torch.Tensor):
     """returns (sorted keys, permutation int32) with sorted[i] = keys[perm[i]]"""
     n = keys.numel()
