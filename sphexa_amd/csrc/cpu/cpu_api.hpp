@@ -90,6 +90,11 @@ double computeGravity(int64_t first, int64_t last, const int32_t* child, const i
                       float* ay, float* az, double* ugrav);
 double directSum(int64_t first, int64_t last, int64_t n, const double* x, const double* y, const double* z,
                  const float* h, const float* m, double G, float* ax, float* ay, float* az, double* ugrav);
+void markLet(int64_t nb, const double* bc, const double* bh, const int32_t* child, const int32_t* n2l,
+             const double* tcenter, const double* thalf, const double* gcenters, const Box& box, uint8_t* failed);
+double m2pFlat(int64_t first, int64_t last, const double* x, const double* y, const double* z, const float* m,
+               int64_t M, const double* mc, const Quadrupole* mp, double G, float* ax, float* ay, float* az,
+               double* ugrav);
 
 } // namespace sphx::cpu
 

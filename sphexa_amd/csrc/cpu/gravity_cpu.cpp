@@ -185,3 +185,40 @@ double directSum(int64_t first, int64_t last, int64_t n, const double* x, const 
 }
 
 } // namespace sphx::cpu
+
+namespace sphx::cpu
+{
+
+void markLet(int64_t nb, const double* bc, const double* bh, const int32_t* child, const int32_t* n2l,
+             const double* tcenter, const double* thalf, const double* gcenters, const Box& box, uint8_t* failed)
+{
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t b = 0; b < nb; ++b)
+    {
+        // concurrent stores of the value 1 to the same flag are benign
+        markLetBox(bc + 3 * b, bh + 3 * b, child, n2l, tcenter, thalf, gcenters, box, failed);
+    }
+}
+
+double m2pFlat(int64_t first, int64_t last, const double* x, const double* y, const double* z, const float* m,
+               int64_t M, const double* mc, const Quadrupole* mp, double G, float* ax, float* ay, float* az,
+               double* ugrav)
+{
+    double egrav = 0;
+#pragma omp parallel for schedule(static) reduction(+ : egrav)
+    for (int64_t i = first; i < last; ++i)
+    {
+        double acc[4] = {0, 0, 0, 0};
+        for (int64_t k = 0; k < M; ++k)
+            m2p<double>(x[i] - mc[3 * k], y[i] - mc[3 * k + 1], z[i] - mc[3 * k + 2], mp[k], acc);
+        double u = G * double(m[i]) * acc[0];
+        if (ugrav) ugrav[i] += u;
+        egrav += u;
+        ax[i] += float(G * acc[1]);
+        ay[i] += float(G * acc[2]);
+        az[i] += float(G * acc[3]);
+    }
+    return 0.5 * egrav;
+}
+
+} // namespace sphx::cpu

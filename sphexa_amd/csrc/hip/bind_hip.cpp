@@ -353,4 +353,20 @@ PYBIND11_MODULE(_sphx_hip, m)
               computeStirring(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(ax), P<float>(ay),
                               P<float>(az), numModes, P<void>(modes), float(norm), St(s));
           });
+
+    m.def("mark_let",
+          [](int64_t nb, Ptr bc, Ptr bh, Ptr child, Ptr n2l, Ptr tc, Ptr th, Ptr gc, const BoxArr& box, Ptr failed,
+             Ptr s)
+          {
+              markLet(nb, P<double>(bc), P<double>(bh), P<int32_t>(child), P<int32_t>(n2l), P<double>(tc),
+                      P<double>(th), P<double>(gc), toBox(box), P<uint8_t>(failed), St(s));
+          });
+    m.def("m2p_flat",
+          [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr mm, int64_t M, Ptr mc, Ptr mp, double G, Ptr ax,
+             Ptr ay, Ptr az, Ptr ugrav, Ptr out, Ptr s)
+          {
+              m2pFlat(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(mm), M, P<double>(mc),
+                      P<void>(mp), float(G), P<float>(ax), P<float>(ay), P<float>(az), P<double>(ugrav),
+                      P<double>(out), St(s));
+          });
 }

@@ -409,3 +409,97 @@ void directSum(int64_t first, int64_t last, int64_t n, const double* x, const do
 }
 
 } // namespace sphx::hip
+
+// --------------------------------------------------------------------------------------- LET selection / M2P
+
+namespace sphx::hip
+{
+
+__global__ void markLetKernel(int64_t nb, const double* __restrict__ bc, const double* __restrict__ bh,
+                              const int32_t* __restrict__ child, const int32_t* __restrict__ n2l,
+                              const double* __restrict__ tc, const double* __restrict__ th,
+                              const double* __restrict__ gc, Box box, uint8_t* failed)
+{
+    int64_t b = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    markLetBox(bc + 3 * b, bh + 3 * b, child, n2l, tc, th, gc, box, failed);
+}
+
+void markLet(int64_t nb, const double* bc, const double* bh, const int32_t* child, const int32_t* n2l,
+             const double* tc, const double* th, const double* gc, const Box& box, uint8_t* failed, hipStream_t s)
+{
+    if (nb == 0) return;
+    markLetKernel<<<gridFor(nb, 64), 64, 0, s>>>(nb, bc, bh, child, n2l, tc, th, gc, box, failed);
+    SPHX_LAUNCH_CHECK();
+}
+
+constexpr int kFlatBlock = 256;
+
+/*! @brief every target against every remote multipole (all of them pass the MAC by construction of the LET);
+ *         multipoles are staged through LDS in chunks shared by the block, r = target - center in fp32
+ */
+__global__ __launch_bounds__(kFlatBlock) void m2pFlatKernel(int64_t first, int64_t last, const double* __restrict__ x,
+                                                            const double* __restrict__ y,
+                                                            const double* __restrict__ z,
+                                                            const float* __restrict__ m, int64_t M,
+                                                            const double* __restrict__ mc,
+                                                            const Quadrupole* __restrict__ mp, float G,
+                                                            float* __restrict__ ax, float* __restrict__ ay,
+                                                            float* __restrict__ az, double* __restrict__ ugrav,
+                                                            double* __restrict__ out)
+{
+    __shared__ double sc[kFlatBlock][3];
+    __shared__ Quadrupole sq[kFlatBlock];
+    __shared__ double red[kFlatBlock / 64];
+    int64_t i   = first + int64_t(blockIdx.x) * kFlatBlock + threadIdx.x;
+    bool valid  = i < last;
+    double xi = valid ? x[i] : 0, yi = valid ? y[i] : 0, zi = valid ? z[i] : 0;
+    float acc[4] = {0, 0, 0, 0};
+    for (int64_t base = 0; base < M; base += kFlatBlock)
+    {
+        int cnt = int(min(int64_t(kFlatBlock), M - base));
+        __syncthreads();
+        if (int(threadIdx.x) < cnt)
+        {
+            int64_t k = base + threadIdx.x;
+            sc[threadIdx.x][0] = mc[3 * k];
+            sc[threadIdx.x][1] = mc[3 * k + 1];
+            sc[threadIdx.x][2] = mc[3 * k + 2];
+            sq[threadIdx.x]    = mp[k];
+        }
+        __syncthreads();
+        for (int k = 0; k < cnt; ++k)
+            m2p(float(xi - sc[k][0]), float(yi - sc[k][1]), float(zi - sc[k][2]), sq[k], acc);
+    }
+    double u = 0;
+    if (valid)
+    {
+        u = double(G) * double(m[i]) * double(acc[0]);
+        if (ugrav) ugrav[i] += u;
+        ax[i] += G * acc[1];
+        ay[i] += G * acc[2];
+        az[i] += G * acc[3];
+    }
+    double s = waveSum(u);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        double tot = 0;
+        for (int w = 0; w < kFlatBlock / 64; ++w)
+            tot += red[w];
+        atomicAdd(out, 0.5 * tot);
+    }
+}
+
+void m2pFlat(int64_t first, int64_t last, const double* x, const double* y, const double* z, const float* m,
+             int64_t M, const double* mc, const void* mp, float G, float* ax, float* ay, float* az, double* ugrav,
+             double* out, hipStream_t s)
+{
+    if (last <= first || M == 0) return;
+    m2pFlatKernel<<<gridFor(last - first, kFlatBlock), kFlatBlock, 0, s>>>(
+        first, last, x, y, z, m, M, mc, (const Quadrupole*)mp, G, ax, ay, az, ugrav, out);
+    SPHX_LAUNCH_CHECK();
+}
+
+} // namespace sphx::hip

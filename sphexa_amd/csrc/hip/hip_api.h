@@ -144,6 +144,12 @@ void directSum(int64_t first, int64_t last, int64_t n, const double* x, const do
                const float* h, const float* m, float G, float* ax, float* ay, float* az, double* ugrav, double* out,
                hipStream_t s);
 
+void markLet(int64_t nb, const double* bc, const double* bh, const int32_t* child, const int32_t* n2l,
+             const double* tc, const double* th, const double* gc, const Box& box, uint8_t* failed, hipStream_t s);
+void m2pFlat(int64_t first, int64_t last, const double* x, const double* y, const double* z, const float* m,
+             int64_t M, const double* mc, const void* mp, float G, float* ax, float* ay, float* az, double* ugrav,
+             double* out, hipStream_t s);
+
 // turbulence.hip: modes = numModes records of 10 floats {kx, ky, kz, pad, amp*Re[3], amp*Im[3]}
 void computeStirring(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* ax,
                      float* ay, float* az, int numModes, const void* modes, float norm, hipStream_t s);

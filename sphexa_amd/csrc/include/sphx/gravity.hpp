@@ -156,4 +156,39 @@ SPHX_HD double vecMacR2(const double com[3], const double gc[3], const double gs
     return mac * mac;
 }
 
+/*! @brief locally-essential-tree selection for one receiver box (center qc, half size qs).
+ *
+ * Walks the sender's tree from the root and flags every node the receiver must not see as a single multipole:
+ * the node's tight particle box overlaps the receiver box (SPH halo candidates) or the receiver box violates the
+ * node's vector MAC (minimum image in periodic dimensions). The flags of all receiver boxes are OR-ed into
+ * @p failed; a flagged node always has flagged ancestors, so along every root-to-leaf path the flagged nodes form
+ * a prefix: the first unflagged node is sent as a multipole, flagged leaves are sent as particles.
+ * Parity: the role of reference focus/octree_focus_mpi.hpp (focus tree MAC refinement) + domain.hpp:246-313
+ * (syncGrav: nodes failing the MAC become halos), as a push-based per-receiver selection.
+ */
+SPHX_HD void markLetBox(const double qc[3], const double qs[3], const int32_t* child, const int32_t* n2l,
+                               const double* tcenter, const double* thalf, const double* gcenters, const Box& box,
+                               uint8_t* failed)
+{
+    int32_t stack[192];
+    int sp      = 0;
+    stack[sp++] = 0;
+    while (sp > 0)
+    {
+        int32_t node = stack[--sp];
+        if (thalf[3 * node] < 0) continue; // empty
+        const double* g = gcenters + 4 * node;
+        bool open = boxesOverlap(qc, qs, tcenter + 3 * node, thalf + 3 * node, box) ||
+                    pointBoxDistSq(g, qc, qs, box) < fabs(g[3]);
+        if (!open) continue;
+        failed[node] = 1;
+        if (n2l[node] < 0)
+        {
+            int32_t co = child[node];
+            for (int k = 7; k >= 0; --k)
+                stack[sp++] = co + k;
+        }
+    }
+}
+
 } // namespace sphx

@@ -3,10 +3,10 @@
 Parity: reference main/src/propagator/gravity_wrapper.hpp:42-133 (MultipoleHolderCpu/Gpu: upsweep, traverse,
 egrav = 0.5 G sum m phi, accelerations added to ax, ay, az) and ryoanji/interface/multipole_holder.cu.
 
-Multi-rank: the local octree covers own particles and the SPH halos; remote far-field contributions come through
-a locally-essential tree exchange (parallel/let.py): every rank pushes to every other rank the multipoles of its
-nodes that satisfy the vector MAC with respect to the receiver's domain box, and the particles of leaves that do
-not. Received particles join the local tree as gravity halos; received multipoles are applied as a flat M2P list.
+Multi-rank: the local octree covers own particles and the halos; remote far-field contributions come through the
+locally-essential tree exchange done in Domain.sync(gravity=True) (parallel/domain.py): every rank pushes to every
+other rank the multipoles of its nodes that satisfy the vector MAC with respect to the receiver's boxes, and the
+particles of leaves that do not (they arrive as halos). Received multipoles are applied as a flat M2P list.
 """
 
 from __future__ import annotations
@@ -33,8 +33,8 @@ class MultipoleHolder:
         ot = domain.octree
         egrav = G.compute_gravity(ot, self.centers, self.multipoles, first, last, d["x"], d["y"], d["z"], d["h"],
                                   d["m"], d.g, d["ax"], d["ay"], d["az"], stats=self.stats)
-        let = getattr(domain, "let", None)
-        if let is not None:
-            egrav += let.apply_remote_multipoles(d, first, last)
+        if domain.size > 1 and domain.remote_centers is not None:
+            egrav += G.m2p_flat(first, last, d["x"], d["y"], d["z"], d["m"], domain.remote_centers,
+                                domain.remote_quads, d.g, d["ax"], d["ay"], d["az"])
         # rank-local share; the observables reduction sums it over ranks (as the reference's MPI_Reduce does)
         d.egrav = egrav

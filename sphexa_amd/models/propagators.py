@@ -47,7 +47,7 @@ class Propagator:
         self.timer.device = d.device
 
     def sync(self, domain, d):
-        domain.sync(d, self.conserved_fields(), self.dependent)
+        domain.sync(d, self.conserved_fields(), self.dependent, gravity=d.g != 0.0)
 
     def step(self, domain, d):
         raise NotImplementedError

@@ -84,3 +84,55 @@ def direct_sum(first: int, last: int, x, y, z, h, m, G: float, ax, ay, az, ugrav
     return float(_lib.cpu().direct_sum(first, last, n, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
                                        m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
                                        0 if ugrav is None else ugrav.data_ptr()))
+
+
+def mark_let(tree: Octree, boxes: torch.Tensor, centers: torch.Tensor, box: Box) -> torch.Tensor:
+    """per-node flags (uint8): node must be opened for a receiver whose particles lie in ``boxes`` (rows
+    center[3], half[3]) — its tight box overlaps one of them or one of them violates its vector MAC"""
+    N = tree.num_nodes
+    failed = torch.zeros(N, dtype=torch.uint8, device=centers.device)
+    nb = boxes.shape[0]
+    if nb == 0:
+        return failed
+    bc = boxes[:, :3].contiguous().view(-1)
+    bh = boxes[:, 3:].contiguous().view(-1)
+    args = (nb, bc.data_ptr(), bh.data_ptr(), tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
+            tree.center.data_ptr(), tree.half.data_ptr(), centers.data_ptr(), box.to_array(), failed.data_ptr())
+    if centers.is_cuda:
+        _lib.hip().mark_let(*args, _stream())
+    else:
+        _lib.cpu().mark_let(*args)
+    return failed
+
+
+def let_selection(tree: Octree, failed: torch.Tensor, mp: torch.Tensor):
+    """(particle flags over the tree's particles, node indices whose multipoles are sent) from the open flags"""
+    N = tree.num_nodes
+    f = failed.bool()
+    leaf_open = f[tree.leaf_to_node.long()]
+    pflags = torch.repeat_interleave(leaf_open, tree.counts.long())
+    mass = mp.view(-1, 8)[:, 0]
+    send = ~f & (mass > 0)
+    if N > 1:
+        parent = tree.parents.long()[torch.div(torch.arange(1, N, device=f.device) - 1, 8, rounding_mode="floor")]
+        send[1:] &= f[parent]
+    return pflags, torch.nonzero(send, as_tuple=False).flatten()
+
+
+def m2p_flat(first: int, last: int, x, y, z, m, mcenters: torch.Tensor, mquads: torch.Tensor, G: float, ax, ay, az,
+             ugrav=None) -> float:
+    """apply M remote multipoles (centers (M,3) f64, quadrupoles (M,8) f32) to every target in [first, last)"""
+    M = mcenters.shape[0]
+    if M == 0 or last <= first:
+        return 0.0
+    mc = mcenters.contiguous()
+    mq = mquads.contiguous()
+    if x.is_cuda:
+        out = torch.zeros(1, dtype=torch.float64, device=x.device)
+        _lib.hip().m2p_flat(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), m.data_ptr(), M, mc.data_ptr(),
+                            mq.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
+                            0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), _stream())
+        return float(out.item())
+    return float(_lib.cpu().m2p_flat(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), m.data_ptr(), M,
+                                     mc.data_ptr(), mq.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(),
+                                     az.data_ptr(), 0 if ugrav is None else ugrav.data_ptr()))

@@ -19,6 +19,14 @@ MI355X-native design:
     SFC-sorted without another sort, and the halo send/receive schedules are known sizes for all later exchanges
     (no MPI_Probe analog needed).
   * the local octree (neighbor search) covers own + halo particles.
+  * self-gravity (``sync(..., gravity=True)``, reference syncGrav, domain.hpp:246-313 + focus/LET machinery
+    octree_focus_mpi.hpp): a push-based locally-essential tree. Every sender walks its own-particle tree against
+    each receiver's boxes (ops.gravity.mark_let): nodes whose particle box overlaps a receiver box or whose vector
+    MAC the box violates are opened; particles of opened leaves become the receiver's halos (a superset of the
+    SPH halos), the first unopened node on every root-to-leaf path is sent as one quadrupole. Received
+    quadrupoles (``remote_centers``/``remote_quads``) pass the MAC for every local target by construction and
+    are applied as a flat M2P; the local octree over own + halos provides the rest, so every remote particle's
+    mass is counted exactly once.
 """
 
 from __future__ import annotations
@@ -66,6 +74,8 @@ class Domain:
         self.halo_recv_counts: List[int] = [0] * self.size
         self.n_lo = 0
         self.n_hi = 0
+        self.remote_centers: Optional[torch.Tensor] = None  # (M, 3) f64 remote multipole expansion centers
+        self.remote_quads: Optional[torch.Tensor] = None    # (M, 8) f32 remote quadrupoles
         self.stats: Dict[str, float] = {}
 
     # ------------------------------------------------------------------------------------------------ queries
@@ -104,7 +114,7 @@ class Domain:
                 self.box.hi[d] = hi
 
     # --------------------------------------------------------------------------------------------- the sync
-    def sync(self, d, conserved: Sequence[str], dependent: Sequence[str] = ()):
+    def sync(self, d, conserved: Sequence[str], dependent: Sequence[str] = (), gravity: bool = False):
         """redistribute particles along the SFC, sort, discover and exchange halos, build the local octree.
 
         ``d`` is a ParticlesData. ``conserved`` fields are carried along (x,y,z,h,m must be included); dependent
@@ -130,7 +140,7 @@ class Domain:
         n_own = skeys.numel()
 
         if self.size > 1:
-            self._discover_halos(skeys, own)
+            self._discover_halos(skeys, own, gravity)
         else:
             self.n_lo = self.n_hi = 0
             self.halo_send_idx = []
@@ -208,8 +218,8 @@ class Domain:
         return new_keys, out
 
     # ------------------------------------------------------------------------------------------------ halos
-    def _discover_halos(self, skeys, own):
-        """push-based halo discovery against the other ranks' search boxes"""
+    def _discover_halos(self, skeys, own, gravity: bool = False):
+        """push-based halo discovery against the other ranks' search boxes (+ LET selection with gravity)"""
         x, y, z, h = own["x"], own["y"], own["z"], own["h"]
         tree, counts = octree_ops.update_tree(None, skeys, self.bucket_size_focus)
         ot = octree_ops.build_octree(tree, counts, skeys, x, y, z, 0)
@@ -218,19 +228,44 @@ class Domain:
         boxes = torch.cat([c.view(-1, 3)[cut], hf.view(-1, 3)[cut]], dim=1)  # (nb, 6)
         all_boxes = self.comm.allgather_var(boxes)
 
+        if gravity:
+            from ..ops import gravity as grav_ops
+
+            gcenters, gquads = grav_ops.upsweep(ot, x, y, z, own["m"], self.box, self.theta, self.sfc_kind)
         send_idx: List[torch.Tensor] = []
+        mp_send: List[torch.Tensor] = []
         for q in range(self.size):
             if q == self.rank or all_boxes[q].shape[0] == 0 or skeys.numel() == 0:
                 send_idx.append(torch.empty(0, dtype=torch.int64, device=skeys.device))
+                mp_send.append(torch.empty(0, dtype=torch.int64, device=skeys.device))
                 continue
-            flags = _mark_in_boxes(ot, all_boxes[q], x, y, z, self.box)
-            send_idx.append(torch.nonzero(flags, as_tuple=False).flatten())
+            if gravity:
+                failed = grav_ops.mark_let(ot, all_boxes[q], gcenters, self.box)
+                pflags, nodes = grav_ops.let_selection(ot, failed, gquads)
+                send_idx.append(torch.nonzero(pflags, as_tuple=False).flatten())
+                mp_send.append(nodes)
+            else:
+                flags = _mark_in_boxes(ot, all_boxes[q], x, y, z, self.box)
+                send_idx.append(torch.nonzero(flags, as_tuple=False).flatten())
+        if gravity:
+            self._exchange_multipoles(mp_send, gcenters, gquads)
         self.halo_send_counts = [int(t.numel()) for t in send_idx]
         self.halo_recv_counts = self.comm.exchange_counts(self.halo_send_counts)
         self.n_lo = sum(self.halo_recv_counts[: self.rank])
         self.n_hi = sum(self.halo_recv_counts[self.rank + 1:])
         self._halo_send_rel = send_idx  # relative to own block, converted to absolute below
         self.halo_send_idx = [t + self.n_lo for t in send_idx]
+
+    def _exchange_multipoles(self, mp_send, gcenters, gquads):
+        """one alltoallv of (center xyz f64, quadrupole 8 x f32) rows for the LET far field"""
+        idx = torch.cat(mp_send)
+        rows = torch.cat([gcenters.view(-1, 4)[idx, :3], gquads.view(-1, 8)[idx].contiguous().view(torch.float64)],
+                         dim=1)
+        counts = [int(t.numel()) for t in mp_send]
+        recv, _ = self.comm.alltoallv(rows, counts)
+        self.remote_centers = recv[:, :3].contiguous()
+        self.remote_quads = recv[:, 3:].contiguous().view(torch.float32).view(-1, 8)
+        self.stats["remote_multipoles"] = recv.shape[0]
 
     def exchange_halos(self, d, fields: Sequence[str]):
         """fill halo slots of ``fields`` from their owners. One packed all_to_all per call (all fields fused)."""

@@ -1,0 +1,153 @@
+"""Multi-rank Barnes-Hut through the locally-essential-tree exchange vs the direct sum of all particles.
+
+Reference: ryoanji/test/interface/global_forces_gpu.cpp:52-66,181-197 (Gaussian/Plummer cloud on several ranks:
+1st-percentile relative acceleration error < 1e-3, max < 3e-2, relative potential-energy error < 1e-2)."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+N = 12000
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def plummer(n, seed=3):
+    rng = np.random.default_rng(seed)
+    r = 1.0 / np.sqrt(rng.uniform(0.01, 0.95, n) ** (-2.0 / 3.0) - 1.0)
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1)[:, None]
+    return u * r[:, None]
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sphexa_amd.models import particles as P
+        from sphexa_amd.models.gravity import MultipoleHolder
+        from sphexa_amd.models.init.base import partition_range
+        from sphexa_amd.parallel.comm import Comm
+        from sphexa_amd.parallel.domain import Domain
+        from sphexa_amd.utils.box import Box, OPEN
+
+        X = plummer(N)
+        a, b = partition_range(N, rank, world)
+        d = P.ParticlesData("cpu")
+        d.set_conserved("x", "y", "z", "h", "m")
+        d.set_dependent("keys", "ax", "ay", "az")
+        d.resize(b - a)
+        for k, c in enumerate("xyz"):
+            d[c] = torch.from_numpy(X[a:b, k].copy())
+        d["m"] = 1.0 / N
+        d["h"] = 0.02
+        d.g = 1.0
+        box = Box([-1.0] * 3, [1.0] * 3, [OPEN] * 3)
+        dom = Domain(Comm(), box, bucket_size_focus=32, bucket_size=64, theta=0.5)
+        dom.sync(d, ["x", "y", "z", "h", "m"], ["ax", "ay", "az"], gravity=True)
+        s, e = dom.start_index(), dom.end_index()
+        for f in ("ax", "ay", "az"):
+            d[f][:] = 0.0
+        mh = MultipoleHolder()
+        mh.upsweep(d, dom)
+        mh.traverse(d, dom)
+        res = dict(x=d["x"][s:e].numpy().copy(), y=d["y"][s:e].numpy().copy(), z=d["z"][s:e].numpy().copy(),
+                   a=np.stack([d[f][s:e].numpy() for f in ("ax", "ay", "az")], 1).copy(), egrav=d.egrav,
+                   nremote=int(dom.stats.get("remote_multipoles", 0)), halos=dom.n_particles_with_halos() - (e - s))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, res = q.get(timeout=600)
+        out[r] = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return [out[r] for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_let_gravity_vs_direct(world):
+    from sphexa_amd.ops import gravity as G
+
+    res = _run(world)
+    assert all(r["nremote"] > 0 for r in res)
+    x = np.concatenate([r["x"] for r in res])
+    y = np.concatenate([r["y"] for r in res])
+    z = np.concatenate([r["z"] for r in res])
+    a = np.concatenate([r["a"] for r in res]).astype(np.float64)
+    assert x.size == N
+    xt, yt, zt = (torch.from_numpy(v.copy()) for v in (x, y, z))
+    m = torch.full((N,), 1.0 / N, dtype=torch.float32)
+    h = torch.full((N,), 0.02, dtype=torch.float32)
+    rx, ry, rz = (torch.zeros(N, dtype=torch.float32) for _ in range(3))
+    egd = G.direct_sum(0, N, xt, yt, zt, h, m, 1.0, rx, ry, rz)
+    ref = np.stack([rx.numpy(), ry.numpy(), rz.numpy()], 1).astype(np.float64)
+    err = np.sort(np.linalg.norm(a - ref, axis=1) / np.linalg.norm(ref, axis=1))
+    assert err[int(0.01 * N)] < 1e-3
+    assert err[-1] < 3e-2
+    eg = sum(r["egrav"] for r in res)
+    assert abs(eg - egd) / abs(egd) < 1e-2
+
+
+def _evrard_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sphexa_amd.app.simulation import Simulation
+
+        sim = Simulation("evrard", n=16, device="cpu")
+        sim.run(2)
+        c = sim.conserved()
+        q.put((rank, dict(c, dt=sim.d.minDt, n=sim.domain.n_particles())))
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_evrard_two_ranks_matches_one():
+    ctx = mp.get_context("spawn")
+    out = {}
+    for world in (1, 2):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_evrard_worker, args=(r, world, port, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = dict(q.get(timeout=600) for _ in range(world))
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        out[world] = res
+    one, two = out[1][0], out[2][0]
+    assert out[2][0]["n"] + out[2][1]["n"] == one["n"]
+    # Barnes-Hut with different trees: energies agree to the BH accuracy
+    assert abs(two["egrav"] - one["egrav"]) < 2e-3 * abs(one["egrav"])
+    assert abs(two["etot"] - one["etot"]) < 2e-3 * abs(one["etot"])
+    assert abs(two["nsum"] - one["nsum"]) <= 1e-3 * one["nsum"]
