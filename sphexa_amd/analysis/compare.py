@@ -1,0 +1,131 @@
+"""Compare an SPH snapshot with the analytical solution of its test case and print L1 errors.
+
+    python -m sphexa_amd.analysis.compare dump_sedov.h5 [--step N | --time T] [--case sedov|noh|gresho-chan]
+
+Parity: reference main/src/analytical_solutions/compare_solutions.py:85-126 (Sedov), compare_noh.py (Noh),
+compare_gresho_chan.py (tangential velocity). The reference Sedov script compares pressure and velocity against
+the *density* column of the solution (compare_solutions.py:107,115); its CI thresholds (.jenkins/reframe_ci.py:
+350-353) were recorded with that comparison, so ``reference_quirk=True`` reproduces it for parity checks while the
+default compares like with like.
+"""
+
+from __future__ import annotations
+
+import argparse
+import sys
+from typing import Dict
+
+import numpy as np
+
+from ..utils.io import H5PartReader, read_file_attributes
+from . import solutions as S
+
+
+def _attrs_scalar(a) -> Dict[str, float]:
+    out = {}
+    for k, v in a.items():
+        v = np.asarray(v).ravel()
+        if v.size == 1 and np.issubdtype(v.dtype, np.number):
+            out[k] = float(v[0])
+    return out
+
+
+def _select_step(path, step=None, time=None):
+    rd = H5PartReader()
+    rd.set_step(path, 0, collective=False)
+    from ..ops import _lib
+
+    io = _lib.io()
+    n = io.num_steps(rd.f)
+    rd.close_step()
+    infos = []
+    for s in range(n):
+        rd.set_step(path, s, collective=False)
+        a = _attrs_scalar(rd.step_attributes())
+        infos.append((s, int(a.get("iteration", s)), a.get("time", 0.0)))
+        rd.close_step()
+    if step is not None:
+        idx = [i for i, it, _ in infos if it == step]
+        if not idx:
+            raise ValueError(f"iteration {step} not in {path}")
+        return idx[0]
+    if time is not None:
+        return min(infos, key=lambda t: abs(t[2] - time))[0]
+    return infos[-1][0]
+
+
+def load_snapshot(path, step=None, time=None):
+    hstep = _select_step(path, step, time)
+    rd = H5PartReader()
+    rd.set_step(path, hstep, collective=False)
+    names = set(rd.dataset_names())
+    data = {f: rd.read_field(f, "d") for f in names}
+    attrs = _attrs_scalar(rd.step_attributes())
+    rd.close_step()
+    try:
+        settings = _attrs_scalar(read_file_attributes(path))
+    except Exception:
+        settings = {}
+    return data, attrs, settings
+
+
+def l1_errors(data, attrs, settings, case="sedov", reference_quirk=False):
+    t = attrs["time"]
+    x, y, z = data["x"], data["y"], data["z"]
+    r = np.sqrt(x * x + y * y + z * z)
+    out = {}
+    if case in ("sedov", "noh"):
+        vr = np.sqrt(data["vx"] ** 2 + data["vy"] ** 2 + data["vz"] ** 2) if "vx" in data else None
+        gamma = settings.get("gamma", attrs.get("gamma", 5.0 / 3.0))
+        if case == "sedov":
+            sol = S.SedovSolution(3, gamma)
+            rs = np.linspace(0.0, settings.get("r1", 0.5) * np.sqrt(3.0), 4000)
+            prof = sol.profile(rs, t, energy=settings.get("energyTotal", 1.0), rho0=settings.get("rho0", 1.0),
+                               u0=settings.get("u0", 1e-8), p0=settings.get("p0", 0.0),
+                               vel0=settings.get("vr0", 0.0), cs0=settings.get("cs0", 0.0))
+            ex = {k: np.interp(r, rs, getattr(prof, k)) for k in ("rho", "p", "vel")}
+            if reference_quirk:
+                ex["p"] = ex["vel"] = ex["rho"]
+        else:
+            prof = S.noh_profile(r, t, gamma=gamma, rho0=settings.get("rho0", 1.0), u0=settings.get("u0", 1e-20),
+                                 p0=settings.get("p0", 0.0), vel0=settings.get("vr0", -1.0))
+            ex = {"rho": prof.rho, "p": prof.p, "vel": prof.vel}
+        if "rho" in data:
+            out["Density"] = S.l1_error(r, data["rho"], y_exact=ex["rho"])
+        if "p" in data:
+            out["Pressure"] = S.l1_error(r, data["p"], y_exact=ex["p"])
+        if vr is not None:
+            out["Velocity"] = S.l1_error(r, vr, y_exact=ex["vel"])
+    elif case == "gresho-chan":
+        r2 = np.sqrt(x * x + y * y)
+        vt = (-y * data["vx"] + x * data["vy"]) / np.maximum(r2, 1e-300)
+        out["Velocity"] = S.l1_error(r2, vt, y_exact=S.gresho_velocity(settings.get("R1", 0.2), r2,
+                                                                      settings.get("v0", 1.0)))
+    else:
+        raise ValueError(f"no analytical solution for case {case}")
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="L1 errors of an SPH snapshot against the analytical solution")
+    ap.add_argument("simFile")
+    g = ap.add_mutually_exclusive_group()
+    g.add_argument("-s", "--step", type=int)
+    g.add_argument("-t", "--time", type=float)
+    ap.add_argument("--case", default=None, help="sedov | noh | gresho-chan (default: from file attributes)")
+    ap.add_argument("--reference-quirk", action="store_true",
+                    help="compare p and |v| against the density solution like the reference script")
+    a = ap.parse_args(argv)
+    data, attrs, settings = load_snapshot(a.simFile, a.step, a.time)
+    case = a.case
+    if case is None:
+        case = "noh" if "vr0" in settings and settings.get("vr0", 0) < 0 else (
+            "gresho-chan" if "gresho-chan" in settings else "sedov")
+    print(f"Loaded {data['x'].size} particles at t = {attrs['time']}")
+    for k, v in l1_errors(data, attrs, settings, case, a.reference_quirk).items():
+        print(f"{k} L1 error {v}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -90,11 +90,43 @@ def test_gravity_gpu_matches_cpu(gpu):
     a = np.stack([axg.cpu().numpy(), ayg.cpu().numpy(), azg.cpu().numpy()], 1)
     r = np.stack([axc.numpy(), ayc.numpy(), azc.numpy()], 1)
     err = _errors(a.astype(np.float64), r.astype(np.float64))
-    assert err[-1] < 1e-3
-    assert abs(egg - egc) / abs(egc) < 1e-4
+    # GPU groups of 64 targets vs CPU groups of 16: different interaction lists, same accuracy class
+    assert err[n // 2] < 1e-4 and err[-1] < 2e-2
+    assert abs(egg - egc) / abs(egc) < 1e-3
     # and vs direct sum on the GPU
     rx, ry, rz = (torch.zeros(n, dtype=torch.float32, device=gpu) for _ in range(3))
     G.direct_sum(0, n, xg, yg, zg, hg, mg, 1.0, rx, ry, rz)
     d = np.stack([rx.cpu().numpy(), ry.cpu().numpy(), rz.cpu().numpy()], 1).astype(np.float64)
     err = _errors(a.astype(np.float64), d)
     assert err[int(0.01 * n)] < 1e-3 and err[-1] < 3e-2
+
+
+@pytest.mark.gpu
+def test_let_kernels_gpu_match_cpu(gpu):
+    """mark_let and the flat M2P on the GPU reproduce the OpenMP path"""
+    n = 8000
+    box, ot, x, y, z, m, h = _setup(n)
+    cc, mc = G.upsweep(ot, x, y, z, m, box, 0.5)
+    rng = np.random.default_rng(1)
+    boxes = torch.from_numpy(np.concatenate([rng.uniform(2, 4, (64, 3)), rng.uniform(0.1, 0.5, (64, 3))], 1))
+    fc = G.mark_let(ot, boxes, cc, box)
+    boxg, otg, xg, yg, zg, mg, hg = _setup(n, gpu)
+    cg, mgp = G.upsweep(otg, xg, yg, zg, mg, boxg, 0.5)
+    fg = G.mark_let(otg, boxes.to(gpu), cg, boxg)
+    assert torch.equal(fg.cpu(), fc)
+    pf, nodes = G.let_selection(ot, fc, mc)
+    assert 0 < nodes.numel() < ot.num_nodes
+    # remote multipoles applied to far targets
+    mcent = cc.view(-1, 4)[nodes, :3].contiguous()
+    mq = mc.view(-1, 8)[nodes].contiguous()
+    tx = torch.from_numpy(rng.uniform(2, 4, 500))
+    ty = torch.from_numpy(rng.uniform(2, 4, 500))
+    tz = torch.from_numpy(rng.uniform(2, 4, 500))
+    tm = torch.full((500,), 1e-3, dtype=torch.float32)
+    out_c = [torch.zeros(500, dtype=torch.float32) for _ in range(3)]
+    ec = G.m2p_flat(0, 500, tx, ty, tz, tm, mcent, mq, 1.0, *out_c)
+    out_g = [torch.zeros(500, dtype=torch.float32, device=gpu) for _ in range(3)]
+    eg = G.m2p_flat(0, 500, tx.to(gpu), ty.to(gpu), tz.to(gpu), tm.to(gpu), mcent.to(gpu), mq.to(gpu), 1.0, *out_g)
+    for a, b in zip(out_c, out_g):
+        assert torch.allclose(b.cpu(), a, rtol=1e-4, atol=1e-7)
+    assert abs(eg - ec) < 1e-4 * abs(ec)
