@@ -165,16 +165,18 @@ PYBIND11_MODULE(_sphx_hip, m)
           });
 
     // ---------------------------------------------------------------------------------------------- neighbors
+    m.def("neighbor_scratch_bytes", [](int64_t n) { return neighborScratchBytes(n); });
     m.def("find_neighbors",
           [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr h, int64_t numNodes, Ptr child, Ptr n2l, Ptr ns,
              Ptr ne, Ptr center, Ptr half, const BoxArr& box, unsigned ng0, unsigned ngmax, Ptr nidx, Ptr nc,
-             int iterateH, Ptr stats, Ptr s)
+             int iterateH, Ptr stats, Ptr scratch, int testFrontCap, Ptr s)
           {
               (void)numNodes;
               NsTree t{P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne), P<double>(center),
                        P<double>(half)};
               findNeighbors(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(h), t, toBox(box), ng0,
-                            ngmax, P<int32_t>(nidx), P<int32_t>(nc), iterateH, P<unsigned long long>(stats), St(s));
+                            ngmax, P<int32_t>(nidx), P<int32_t>(nc), iterateH, P<unsigned long long>(stats), P<void>(scratch),
+                            testFrontCap, St(s));
           });
 
     // ---------------------------------------------------------------------------------------------- hydro
@@ -310,13 +312,16 @@ PYBIND11_MODULE(_sphx_hip, m)
           { gravitySetMac(N, P<KeyT>(prefixes), toBox(box), kind, invTheta, P<double>(centers), St(s)); });
     m.def("compute_gravity",
           [](int64_t first, int64_t last, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr centers, Ptr mp, Ptr x, Ptr y,
-             Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay, Ptr az, Ptr ugrav, Ptr out, Ptr stats, Ptr s)
+             Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay, Ptr az, Ptr ugrav, Ptr out, Ptr stats, Ptr scratch,
+             int testFrontCap, Ptr s)
           {
               computeGravity(first, last, P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne),
                              P<double>(centers), P<void>(mp), P<double>(x), P<double>(y), P<double>(z), P<float>(h),
                              P<float>(mm), float(G), P<float>(ax), P<float>(ay), P<float>(az), P<double>(ugrav),
-                             P<double>(out), P<unsigned long long>(stats), St(s));
+                             P<double>(out), P<unsigned long long>(stats), P<void>(scratch), testFrontCap,
+                             St(s));
           });
+    m.def("gravity_scratch_bytes", [](int64_t n) { return gravityScratchBytes(n); });
     m.def("direct_sum",
           [](int64_t first, int64_t last, int64_t n, Ptr x, Ptr y, Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay,
              Ptr az, Ptr ugrav, Ptr out, Ptr s)

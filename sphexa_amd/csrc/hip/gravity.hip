@@ -182,13 +182,163 @@ __device__ inline int flushP2P(const int32_t* list, int n, const GravTree& t, co
     return numP2P;
 }
 
+template<bool kSpill>
+__device__ __forceinline__ void gWaveSync()
+{
+    if constexpr (kSpill) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
+    else { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+}
+
+template<bool kSpill>
+__device__ __forceinline__ int32_t gLoad(const int32_t* p)
+{
+    if constexpr (kSpill) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+    else { return *p; }
+}
+
+/*! @brief Barnes-Hut traversal of one 64-target group (one wave): breadth-first over the tree with the vector MAC
+ *         against the group's bounding box; accepted nodes queue in the LDS M2P list, opened leaves in the LDS
+ *         leaf list, both flushed when full. Returns false (nothing written) if the frontier overflows
+ *         @p frontCap — the group is then redone by the spill kernel with a global-memory frontier.
+ */
+template<bool kSpill>
+__device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t last, const GravTree& t,
+                                             const double* __restrict__ x, const double* __restrict__ y,
+                                             const double* __restrict__ z, const float* __restrict__ h,
+                                             const float* __restrict__ m, float G, float* __restrict__ ax,
+                                             float* __restrict__ ay, float* __restrict__ az,
+                                             double* __restrict__ ugrav, unsigned long long* __restrict__ stats,
+                                             int32_t* frontA, int32_t* frontB, int32_t* mlst, int32_t* llst,
+                                             int frontCap, double& upot)
+{
+    const int lane   = threadIdx.x & 63;
+    const int64_t i  = first + g * 64 + lane;
+    const bool valid = i < last;
+    const int64_t ii = valid ? i : (last - 1);
+    double xi = x[ii], yi = y[ii], zi = z[ii];
+    float hi  = h[ii];
+
+    double tc[3], ts[3];
+    {
+        double p[3] = {xi, yi, zi};
+        for (int d = 0; d < 3; ++d)
+        {
+            double a = waveMin(p[d]);
+            double b = waveMax(p[d]);
+            tc[d]    = 0.5 * (a + b);
+            ts[d]    = 0.5 * (b - a);
+        }
+    }
+    float xr = float(xi - tc[0]), yr = float(yi - tc[1]), zr = float(zi - tc[2]);
+    float acc[4] = {0, 0, 0, 0};
+
+    int32_t* cur = frontA;
+    int32_t* nxt = frontB;
+    int nf = 1, nm = 0, nl = 0;
+    unsigned long long totM2P = 0, totP2P = 0;
+    if (lane == 0) cur[0] = 0;
+    gWaveSync<kSpill>();
+    while (nf > 0)
+    {
+        int nn = 0;
+        for (int base = 0; base < nf; base += 64)
+        {
+            int idx    = base + lane;
+            int32_t nd = idx < nf ? gLoad<kSpill>(cur + idx) : -1;
+            bool isM2P = false, isLeaf = false, isInt = false;
+            if (nd >= 0)
+            {
+                const double* c = t.centers + 4 * nd;
+                bool violated   = macViolated(c, c[3], tc, ts);
+                isM2P           = !violated && c[3] != 0.0;
+                isLeaf          = violated && t.n2l[nd] >= 0;
+                isInt           = violated && t.n2l[nd] < 0;
+            }
+            uint64_t bm = ballot(isM2P), bl = ballot(isLeaf), bi = ballot(isInt);
+            int cm = __popcll(bm), cl = __popcll(bl), ci = __popcll(bi);
+            // flush the queues if this batch would overflow them
+            if (nm + cm > kGM2P)
+            {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                flushM2P(mlst, nm, t, xi, yi, zi, acc);
+                nm = 0;
+            }
+            if (nl + cl > kGLeaves)
+            {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                totP2P += flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
+                nl = 0;
+            }
+            if (isM2P) mlst[nm + __popcll(bm & lanemaskLt())] = nd;
+            if (isLeaf) llst[nl + __popcll(bl & lanemaskLt())] = nd;
+            if (isInt)
+            {
+                int pos    = nn + 8 * __popcll(bi & lanemaskLt());
+                int32_t co = t.child[nd];
+                if (pos + 8 <= frontCap)
+                    for (int k = 0; k < 8; ++k)
+                        nxt[pos + k] = co + k;
+            }
+            nm += cm;
+            nl += cl;
+            totM2P += cm;
+            nn += 8 * ci;
+        }
+        gWaveSync<kSpill>();
+        if (nn > frontCap) return false;
+        int32_t* tmp = cur;
+        cur          = nxt;
+        nxt          = tmp;
+        nf           = nn;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    flushM2P(mlst, nm, t, xi, yi, zi, acc);
+    totP2P += flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
+
+    if (valid)
+    {
+        double u = double(G) * double(m[i]) * double(acc[0]);
+        upot     = u;
+        if (ugrav) ugrav[i] += u;
+        ax[i] += G * acc[1];
+        ay[i] += G * acc[2];
+        az[i] += G * acc[3];
+    }
+    if (lane == 0)
+    {
+        // stats: [0] sum of P2P per target, [1] failed groups, [2] sum of M2P, [3] max P2P, [4] max M2P,
+        //        [5] spilled groups (queued for the global-frontier kernel)
+        auto nv = (unsigned long long)(min(int64_t(64), last - (first + g * 64)));
+        atomicAdd(&stats[0], totP2P * nv);
+        atomicAdd(&stats[2], totM2P * nv);
+        atomicMax(&stats[3], totP2P);
+        atomicMax(&stats[4], totM2P);
+    }
+    return true;
+}
+
+__device__ __forceinline__ void blockEnergy(double upot, double* red, int nw, double* out)
+{
+    double s = waveSum(upot);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        double tot = 0;
+        for (int w = 0; w < nw; ++w)
+            tot += red[w];
+        atomicAdd(out, 0.5 * tot);
+    }
+}
+
 __global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last, GravTree t,
                                                      const double* __restrict__ x, const double* __restrict__ y,
                                                      const double* __restrict__ z, const float* __restrict__ h,
                                                      const float* __restrict__ m, float G, float* __restrict__ ax,
                                                      float* __restrict__ ay, float* __restrict__ az,
                                                      double* __restrict__ ugrav, double* __restrict__ out,
-                                                     unsigned long long* __restrict__ stats)
+                                                     unsigned long long* __restrict__ stats,
+                                                     int32_t* __restrict__ spillList, int frontCap)
 {
     __shared__ int32_t frontA[kGWaves][kGFront];
     __shared__ int32_t frontB[kGWaves][kGFront];
@@ -197,145 +347,75 @@ __global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last
     __shared__ double red[kGWaves];
 
     const int wave          = threadIdx.x >> 6;
-    const int lane          = threadIdx.x & 63;
     const int64_t numGroups = (last - first + 63) / 64;
     const unsigned lb       = xcdRemap(blockIdx.x, gridDim.x);
     const int64_t g         = int64_t(lb) * kGWaves + wave;
     double upot             = 0;
     if (g < numGroups)
     {
-        const int64_t i  = first + g * 64 + lane;
-        const bool valid = i < last;
-        const int64_t ii = valid ? i : (last - 1);
-        double xi = x[ii], yi = y[ii], zi = z[ii];
-        float hi  = h[ii];
-
-        double tc[3], ts[3];
-        {
-            double p[3] = {xi, yi, zi};
-            for (int d = 0; d < 3; ++d)
-            {
-                double a = waveMin(p[d]);
-                double b = waveMax(p[d]);
-                tc[d]    = 0.5 * (a + b);
-                ts[d]    = 0.5 * (b - a);
-            }
-        }
-        float xr = float(xi - tc[0]), yr = float(yi - tc[1]), zr = float(zi - tc[2]);
-        float acc[4] = {0, 0, 0, 0};
-
-        int32_t* cur  = frontA[wave];
-        int32_t* nxt  = frontB[wave];
-        int32_t* mlst = m2pList[wave];
-        int32_t* llst = leafList[wave];
-        int nf = 1, nm = 0, nl = 0;
-        bool overflow = false;
-        unsigned long long totM2P = 0, totP2P = 0;
-        if (lane == 0) cur[0] = 0;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        while (nf > 0)
-        {
-            int nn = 0;
-            for (int base = 0; base < nf; base += 64)
-            {
-                int idx     = base + lane;
-                int32_t nd  = idx < nf ? cur[idx] : -1;
-                bool isM2P = false, isLeaf = false, isInt = false;
-                if (nd >= 0)
-                {
-                    const double* c = t.centers + 4 * nd;
-                    bool violated   = macViolated(c, c[3], tc, ts);
-                    isM2P           = !violated && c[3] != 0.0;
-                    isLeaf          = violated && t.n2l[nd] >= 0;
-                    isInt           = violated && t.n2l[nd] < 0;
-                }
-                uint64_t bm = ballot(isM2P), bl = ballot(isLeaf), bi = ballot(isInt);
-                int cm = __popcll(bm), cl = __popcll(bl), ci = __popcll(bi);
-                // flush the queues if this batch would overflow them
-                if (nm + cm > kGM2P)
-                {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    flushM2P(mlst, nm, t, xi, yi, zi, acc);
-                    nm = 0;
-                }
-                if (nl + cl > kGLeaves)
-                {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    totP2P += flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
-                    nl = 0;
-                }
-                if (isM2P) mlst[nm + __popcll(bm & lanemaskLt())] = nd;
-                if (isLeaf) llst[nl + __popcll(bl & lanemaskLt())] = nd;
-                if (isInt)
-                {
-                    int pos    = nn + 8 * __popcll(bi & lanemaskLt());
-                    int32_t co = t.child[nd];
-                    if (pos + 8 <= kGFront)
-                        for (int k = 0; k < 8; ++k)
-                            nxt[pos + k] = co + k;
-                }
-                nm += cm;
-                nl += cl;
-                totM2P += cm;
-                nn += 8 * ci;
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (nn > kGFront)
-            {
-                overflow = true;
-                nn       = 0;
-            }
-            int32_t* tmp = cur;
-            cur          = nxt;
-            nxt          = tmp;
-            nf           = nn;
-        }
-        flushM2P(mlst, nm, t, xi, yi, zi, acc);
-        totP2P += flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
-
-        if (valid)
-        {
-            double u = double(G) * double(m[i]) * double(acc[0]);
-            upot     = u;
-            if (ugrav) ugrav[i] += u;
-            ax[i] += G * acc[1];
-            ay[i] += G * acc[2];
-            az[i] += G * acc[3];
-        }
-        if (lane == 0)
-        {
-            // stats: [0] sum of P2P per target, [1] overflowed groups, [2] sum of M2P, [3] max P2P, [4] max M2P
-            auto nv = (unsigned long long)(min(int64_t(64), last - (first + g * 64)));
-            if (overflow) atomicAdd(&stats[1], 1ull);
-            atomicAdd(&stats[0], totP2P * nv);
-            atomicAdd(&stats[2], totM2P * nv);
-            atomicMax(&stats[3], totP2P);
-            atomicMax(&stats[4], totM2P);
-        }
+        bool ok = gravityGroup<false>(g, first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, stats, frontA[wave],
+                                      frontB[wave], m2pList[wave], leafList[wave], frontCap, upot);
+        if (!ok && (threadIdx.x & 63) == 0) spillList[atomicAdd(&stats[5], 1ull)] = int32_t(g);
     }
-    double s = waveSum(upot);
-    if (lane == 0) red[wave] = s;
-    __syncthreads();
-    if (threadIdx.x == 0)
+    blockEnergy(upot, red, kGWaves, out);
+}
+
+constexpr int kGSpillWaves = 128;
+constexpr int kGSpillFront = 32768;
+
+__global__ __launch_bounds__(64) void gravitySpillKernel(int64_t first, int64_t last, GravTree t,
+                                                         const double* __restrict__ x, const double* __restrict__ y,
+                                                         const double* __restrict__ z, const float* __restrict__ h,
+                                                         const float* __restrict__ m, float G, float* __restrict__ ax,
+                                                         float* __restrict__ ay, float* __restrict__ az,
+                                                         double* __restrict__ ugrav, double* __restrict__ out,
+                                                         unsigned long long* __restrict__ stats,
+                                                         const int32_t* __restrict__ spillList,
+                                                         int32_t* __restrict__ scratch)
+{
+    __shared__ int32_t m2pList[kGM2P];
+    __shared__ int32_t leafList[kGLeaves];
+    __shared__ double red[1];
+    const int64_t numSpill = int64_t(__hip_atomic_load(&stats[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    int32_t* frontA = scratch + int64_t(blockIdx.x) * 2 * kGSpillFront;
+    int32_t* frontB = frontA + kGSpillFront;
+    double upot     = 0;
+    for (int64_t k = blockIdx.x; k < numSpill; k += gridDim.x)
     {
-        double tot = 0;
-        for (int w = 0; w < kGWaves; ++w)
-            tot += red[w];
-        atomicAdd(out, 0.5 * tot);
+        double u = 0;
+        bool ok  = gravityGroup<true>(spillList[k], first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, stats,
+                                      frontA, frontB, m2pList, leafList, kGSpillFront, u);
+        upot += u;
+        if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
     }
+    blockEnergy(upot, red, 1, out);
+}
+
+size_t gravityScratchBytes(int64_t n)
+{
+    int64_t groups = (n + 63) / 64;
+    return size_t((groups + 63) / 64 * 64) * sizeof(int32_t) +
+           size_t(kGSpillWaves) * 2 * kGSpillFront * sizeof(int32_t);
 }
 
 void computeGravity(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
                     const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
                     const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
-                    double* ugrav, double* out, unsigned long long* stats, hipStream_t s)
+                    double* ugrav, double* out, unsigned long long* stats, void* scratch, int testFrontCap,
+                    hipStream_t s)
 {
     int64_t n = last - first;
     if (n <= 0) return;
     GravTree t{child, n2l, ns, ne, centers, (const Quadrupole*)mp};
-    int64_t groups = (n + 63) / 64;
-    unsigned grid  = unsigned((groups + kGWaves - 1) / kGWaves);
-    gravityKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats);
+    int64_t groups     = (n + 63) / 64;
+    int32_t* spillList = static_cast<int32_t*>(scratch);
+    int32_t* spillMem  = spillList + (groups + 63) / 64 * 64;
+    unsigned grid      = unsigned((groups + kGWaves - 1) / kGWaves);
+    gravityKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
+                                               spillList, testFrontCap > 0 ? min(testFrontCap, kGFront) : kGFront);
+    SPHX_LAUNCH_CHECK();
+    gravitySpillKernel<<<kGSpillWaves, 64, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
+                                                   spillList, spillMem);
     SPHX_LAUNCH_CHECK();
 }
 

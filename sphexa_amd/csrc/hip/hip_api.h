@@ -75,9 +75,11 @@ void markInBoxes(int64_t nb, const double* bc, const double* bh, const int32_t* 
                  const double* y, const double* z, const Box& box, uint8_t* flags, hipStream_t s);
 
 // neighbors.hip
+// stats: [0] h-iteration failures, [1] groups overflowing even the spill storage, [2] spilled groups
+size_t neighborScratchBytes(int64_t n);
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int32_t* nc,
-                   int iterateH, unsigned long long* stats, hipStream_t s);
+                   int iterateH, unsigned long long* stats, void* scratch, int testFrontCap, hipStream_t s);
 
 // hydro.hip
 struct MomFields
@@ -139,7 +141,9 @@ void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, do
 void computeGravity(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
                     const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
                     const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
-                    double* ugrav, double* out, unsigned long long* stats, hipStream_t s);
+                    double* ugrav, double* out, unsigned long long* stats, void* scratch, int testFrontCap,
+                    hipStream_t s);
+size_t gravityScratchBytes(int64_t n);
 void directSum(int64_t first, int64_t last, int64_t n, const double* x, const double* y, const double* z,
                const float* h, const float* m, float G, float* ax, float* ay, float* az, double* ugrav, double* out,
                hipStream_t s);

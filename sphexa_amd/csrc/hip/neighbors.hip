@@ -34,24 +34,34 @@ __device__ __forceinline__ double foldMin(double dx, const Box& b, int d)
     return b.bc[d] == kPeriodic ? dx - b.len(d) * rint(dx * b.ilen(d)) : dx;
 }
 
-__global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_t last, const double* __restrict__ x,
-                                                           const double* __restrict__ y,
-                                                           const double* __restrict__ z, float* __restrict__ h,
-                                                           NsTree t, Box box, unsigned ng0, unsigned ngmax,
-                                                           int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
-                                                           int iterateH, unsigned long long* __restrict__ stats)
+//! @brief ordering point between lanes of one wave exchanging data through the frontier/leaf storage
+template<bool kSpill>
+__device__ __forceinline__ void waveSync()
 {
-    __shared__ int32_t frontA[kWavesPerBlock][kFrontCap];
-    __shared__ int32_t frontB[kWavesPerBlock][kFrontCap];
-    __shared__ int32_t leaves[kWavesPerBlock][kLeafCap];
+    if constexpr (kSpill) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
+    else { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+}
 
-    const int wave  = threadIdx.x >> 6;
-    const int lane  = threadIdx.x & 63;
-    const int64_t numGroups = (last - first + 63) / 64;
-    const unsigned lb       = xcdRemap(blockIdx.x, gridDim.x);
-    const int64_t g         = int64_t(lb) * kWavesPerBlock + wave;
-    if (g >= numGroups) return;
+//! @brief frontier/leaf loads: LDS in the fast path, L2-coherent (device scope) global loads in the spill path
+template<bool kSpill>
+__device__ __forceinline__ int32_t ldList(const int32_t* p)
+{
+    if constexpr (kSpill) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+    else { return *p; }
+}
 
+/*! @brief search of one target group (one wave). Returns false if the frontier or the leaf list overflowed the
+ *         given capacities (nothing is written then, the group is retried by the spill kernel).
+ */
+template<bool kSpill>
+__device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t last, const double* __restrict__ x,
+                                            const double* __restrict__ y, const double* __restrict__ z,
+                                            float* __restrict__ h, const NsTree& t, const Box& box, unsigned ng0,
+                                            unsigned ngmax, int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
+                                            int iterateH, unsigned long long* __restrict__ stats, int32_t* frontA,
+                                            int32_t* frontB, int32_t* leaves, int frontCap, int leafCap)
+{
+    const int lane   = threadIdx.x & 63;
     const int64_t i  = first + g * 64 + lane;
     const bool valid = i < last;
     double xi = 0, yi = 0, zi = 0;
@@ -67,7 +77,6 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
     const unsigned ngmin = ng0 / 4;
 
     unsigned ncSph = 1;
-    bool overflow  = false;
     int round      = 0;
     for (;; ++round)
     {
@@ -85,19 +94,19 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
         }
 
         // 2. breadth-first traversal
-        int32_t* cur = frontA[wave];
-        int32_t* nxt = frontB[wave];
+        int32_t* cur = frontA;
+        int32_t* nxt = frontB;
         int nf       = 1;
         int nLeaves  = 0;
         if (lane == 0) cur[0] = 0;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        waveSync<kSpill>();
         while (nf > 0)
         {
             int nn = 0;
             for (int base = 0; base < nf; base += 64)
             {
                 int idx     = base + lane;
-                int32_t nd  = idx < nf ? cur[idx] : -1;
+                int32_t nd  = idx < nf ? ldList<kSpill>(cur + idx) : -1;
                 bool hit    = nd >= 0 && boxesOverlap(gc, gs, t.center + 3 * nd, t.half + 3 * nd, box);
                 bool isLeaf = hit && t.n2l[nd] >= 0;
                 bool isInt  = hit && !isLeaf;
@@ -108,31 +117,26 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
                 if (isLeaf)
                 {
                     int pos = nLeaves + pl;
-                    if (pos < kLeafCap) leaves[wave][pos] = nd;
+                    if (pos < leafCap) leaves[pos] = nd;
                 }
                 if (isInt)
                 {
                     int pos    = nn + 8 * pi;
                     int32_t co = t.child[nd];
-                    if (pos + 8 <= kFrontCap)
+                    if (pos + 8 <= frontCap)
                         for (int k = 0; k < 8; ++k)
                             nxt[pos + k] = co + k;
                 }
                 nLeaves += __popcll(ml);
                 nn += 8 * __popcll(mi);
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (nn > kFrontCap || nLeaves > kLeafCap)
-            {
-                overflow = true;
-                nn       = 0;
-            }
+            waveSync<kSpill>();
+            if (nn > frontCap || nLeaves > leafCap) { return false; }
             int32_t* tmp = cur;
             cur          = nxt;
             nxt          = tmp;
             nf           = nn;
         }
-        if (overflow) break;
 
         // 3. candidate tests in group-relative fp32 with an fp64 band check
         // the fp32 path is valid if the folded group neighborhood cannot alias across a periodic boundary
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
         unsigned cnt = 0;
         for (int l = 0; l < nLeaves; ++l)
         {
-            int32_t nd = leaves[wave][l];
+            int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + l));
             // skip leaves outside every lane's sphere (same strict test as the CPU traversal)
             bool touch = valid && pointBoxDistSq(ip, t.center + 3 * nd, t.half + 3 * nd, box) < radiusSq;
             if (!ballot(touch)) continue;
@@ -201,28 +205,95 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
         if (repeat) hi = sphx::updateH<float>(ng0, ncSph, hi);
     }
 
-    if (lane == 0)
-    {
-        if (overflow) atomicAdd(&stats[1], 1ull);
-        if (round >= 10) atomicAdd(&stats[0], 1ull);
-    }
+    if (lane == 0 && round >= 10) atomicAdd(&stats[0], 1ull);
     if (valid)
     {
         nc[i] = int32_t(ncSph);
         h[i]  = hi;
     }
+    return true;
+}
+
+//! fast path: frontier and leaf list in LDS; overflowing groups are queued for the spill kernel
+__global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_t last, const double* __restrict__ x,
+                                                           const double* __restrict__ y,
+                                                           const double* __restrict__ z, float* __restrict__ h,
+                                                           NsTree t, Box box, unsigned ng0, unsigned ngmax,
+                                                           int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
+                                                           int iterateH, unsigned long long* __restrict__ stats,
+                                                           int32_t* __restrict__ spillList, int frontCap)
+{
+    __shared__ int32_t frontA[kWavesPerBlock][kFrontCap];
+    __shared__ int32_t frontB[kWavesPerBlock][kFrontCap];
+    __shared__ int32_t leaves[kWavesPerBlock][kLeafCap];
+
+    const int wave          = threadIdx.x >> 6;
+    const int64_t numGroups = (last - first + 63) / 64;
+    const unsigned lb       = xcdRemap(blockIdx.x, gridDim.x);
+    const int64_t g         = int64_t(lb) * kWavesPerBlock + wave;
+    if (g >= numGroups) return;
+
+    bool ok = searchGroup<false>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
+                                 frontA[wave], frontB[wave], leaves[wave], frontCap, kLeafCap);
+    if (!ok && (threadIdx.x & 63) == 0)
+    {
+        unsigned long long slot = atomicAdd(&stats[2], 1ull);
+        spillList[slot] = int32_t(g);
+    }
+}
+
+/*! spill path: persistent waves take the queued groups and redo them with frontier/leaf storage in global
+ *  memory (kSpillFront / kSpillLeaves entries per wave); a group that overflows even these counts in stats[1]
+ */
+constexpr int kSpillWaves  = 128;
+constexpr int kSpillFront  = 16384;
+constexpr int kSpillLeaves = 65536;
+
+__global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, int64_t last,
+                                                               const double* __restrict__ x,
+                                                               const double* __restrict__ y,
+                                                               const double* __restrict__ z, float* __restrict__ h,
+                                                               NsTree t, Box box, unsigned ng0, unsigned ngmax,
+                                                               int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
+                                                               int iterateH, unsigned long long* __restrict__ stats,
+                                                               const int32_t* __restrict__ spillList,
+                                                               int32_t* __restrict__ scratch)
+{
+    const int64_t numSpill = int64_t(__hip_atomic_load(&stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    int32_t* frontA = scratch + int64_t(blockIdx.x) * (2 * kSpillFront + kSpillLeaves);
+    int32_t* frontB = frontA + kSpillFront;
+    int32_t* leaves = frontB + kSpillFront;
+    for (int64_t k = blockIdx.x; k < numSpill; k += gridDim.x)
+    {
+        int64_t g = spillList[k];
+        bool ok   = searchGroup<true>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
+                                      frontA, frontB, leaves, kSpillFront, kSpillLeaves);
+        if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
+    }
+}
+
+size_t neighborScratchBytes(int64_t n)
+{
+    int64_t groups = (n + 63) / 64;
+    return size_t(groups) * sizeof(int32_t) + size_t(kSpillWaves) * (2 * kSpillFront + kSpillLeaves) * sizeof(int32_t);
 }
 
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int32_t* nc,
-                   int iterateH, unsigned long long* stats, hipStream_t s)
+                   int iterateH, unsigned long long* stats, void* scratch, int testFrontCap, hipStream_t s)
 {
     int64_t n = last - first;
     if (n <= 0) return;
-    int64_t groups = (n + 63) / 64;
-    unsigned grid  = unsigned((groups + kWavesPerBlock - 1) / kWavesPerBlock);
+    int64_t groups     = (n + 63) / 64;
+    int32_t* spillList = static_cast<int32_t*>(scratch);
+    int32_t* spillMem  = spillList + ((groups + 63) / 64) * 64;
+    unsigned grid      = unsigned((groups + kWavesPerBlock - 1) / kWavesPerBlock);
     findNeighborsKernel<<<grid, 64 * kWavesPerBlock, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc,
-                                                             iterateH, stats);
+                                                             iterateH, stats, spillList,
+                                                             testFrontCap > 0 ? min(testFrontCap, kFrontCap) : kFrontCap);
+    SPHX_LAUNCH_CHECK();
+    findNeighborsSpillKernel<<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc,
+                                                        iterateH, stats, spillList, spillMem);
     SPHX_LAUNCH_CHECK();
 }
 

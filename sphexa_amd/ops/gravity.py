@@ -19,6 +19,10 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+# test hook: >0 shrinks the LDS frontier of the GPU traversal so that groups take the global-memory spill path
+TEST_FRONT_CAP = 0
+
+
 def upsweep(tree: Octree, x, y, z, m, box: Box, theta: float, sfc_kind: int = 0):
     """mass centers + squared vector-MAC radii (N x 4 f64) and quadrupoles (N x 8 f32) of every node"""
     N = tree.num_nodes
@@ -53,15 +57,19 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
     if x.is_cuda:
         hp = _lib.hip()
         out = torch.zeros(2, dtype=torch.float64, device=x.device)
-        st_dev = torch.zeros(5, dtype=torch.int64, device=x.device)
+        st_dev = torch.zeros(6, dtype=torch.int64, device=x.device)
+        from .neighbors import _scratch
+
+        scratch = _scratch(hp.gravity_scratch_bytes(last - first), x.device)
         hp.compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
                            tree.node_start.data_ptr(), tree.node_end.data_ptr(), centers.data_ptr(), mp.data_ptr(),
                            x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), m.data_ptr(), float(G),
                            ax.data_ptr(), ay.data_ptr(), az.data_ptr(), 0 if ugrav is None else ugrav.data_ptr(),
-                           out.data_ptr(), st_dev.data_ptr(), _stream())
+                           out.data_ptr(), st_dev.data_ptr(), scratch.data_ptr(), TEST_FRONT_CAP, _stream())
         st = st_dev.cpu()
         if stats is not None:
-            stats.update(p2p=int(st[0]), m2p=int(st[2]), max_p2p=int(st[3]), max_m2p=int(st[4]))
+            stats.update(p2p=int(st[0]), m2p=int(st[2]), max_p2p=int(st[3]), max_m2p=int(st[4]),
+                         spilled=int(st[5]))
         if int(st[1]) > 0:
             raise RuntimeError(f"gravity traversal stack overflow in {int(st[1])} groups")
         return float(out[0].item())

@@ -46,6 +46,20 @@ class NeighborSearchError(RuntimeError):
     pass
 
 
+_SCRATCH: dict = {}
+# test hook: >0 shrinks the LDS frontier of the GPU search so that groups take the global-memory spill path
+TEST_FRONT_CAP = 0
+
+
+def _scratch(nbytes: int, device) -> torch.Tensor:
+    """grow-only device workspace of the neighbor search spill path (overflow queue + global frontiers)"""
+    t = _SCRATCH.get(device)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _SCRATCH[device] = t
+    return t
+
+
 def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
                    nidx: torch.Tensor | None = None) -> NeighborList:
     """search neighbors of particles [first, last) within 2h, adjusting h towards ng0 neighbors"""
@@ -61,14 +75,17 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         if nidx is None or nidx.numel() < need:
             nidx = torch.empty(need, dtype=torch.int32, device=x.device)
         stats = torch.zeros(4, dtype=torch.int64, device=x.device)
+        scratch = _scratch(hp.neighbor_scratch_bytes(n), x.device)
         hp.find_neighbors(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), tree.num_nodes,
                           tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
                           tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
-                          d.ng0, ngmax, nidx.data_ptr(), nc.data_ptr(), int(iterate_h), stats.data_ptr(), _stream())
+                          d.ng0, ngmax, nidx.data_ptr(), nc.data_ptr(), int(iterate_h), stats.data_ptr(),
+                          scratch.data_ptr(), TEST_FRONT_CAP, _stream())
         st = stats.cpu()
         if int(st[1]) > 0:
             raise NeighborSearchError(f"GPU traversal stack overflow in {int(st[1])} groups")
         d.nc_fail = int(st[0])
+        d.nc_spilled = int(st[2])
         return NeighborList(nidx, first, last, ngmax, True)
 
     need = max(n, 1) * ngmax
