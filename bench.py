@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
-"""Headline benchmark: particle-updates/s of the VE-SPH Sedov blast, ``--init sedov -n 400`` (64 M particles).
+"""Headline benchmark: particle-updates/s of the reference's test cases (BASELINE.json).
+
+Default: VE-SPH Sedov blast ``--init sedov -n 400`` (64 M particles, regular-lattice initial conditions).
+``--init evrard -n 200`` runs the second headline config (Evrard collapse with Barnes-Hut self-gravity, glass ICs).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 the driver starts one process per
 GPU with torch.distributed.run. W untimed steps, then exactly K timed steps bracketed by barrier + device sync,
 max over ranks, rank 0 prints one JSON line. The whole time step is inside the timed region: domain sync (SFC keys,
-sort, octree, halo discovery), neighbor search with h iteration, the five VE loops, EOS, four halo exchanges,
-global dt reduction and the position/energy/h update.
+sort, octree, migration, halo discovery + LET), neighbor search with h iteration, the five VE loops, EOS, four halo
+exchanges, gravity (upsweep, traversal, remote multipoles), global dt reduction and the position/energy/h update.
 
-Scaling: the problem (64 M particles) is fixed as N grows -> strong scaling.
+Scaling: the problem size is fixed as N grows -> strong scaling.
 """
 
 from __future__ import annotations
@@ -22,6 +25,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+METRIC = "particle-updates/sec (whole node), Sedov -n 400 and Evrard+gravity -n 200"
 BASELINE_VALUE = None  # the reference publishes no throughput numbers
 
 
@@ -30,16 +34,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("-n", type=int, default=400, help="particles per dimension (n^3 total)")
+    ap.add_argument("--init", default="sedov", help="test case (sedov, evrard, noh, ...)")
+    ap.add_argument("-n", type=int, default=None, help="particles per dimension (default 400 sedov, 200 evrard)")
     ap.add_argument("--prop", default="ve")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
+    n = args.n if args.n is not None else (200 if args.init == "evrard" else 400)
 
-    from sphexa_amd.models import particles as P
-    from sphexa_amd.models.init.sedov import SedovGrid
-    from sphexa_amd.models.propagators import propagator_factory
+    from sphexa_amd.app.simulation import Simulation
     from sphexa_amd.parallel.comm import init_distributed
-    from sphexa_amd.parallel.domain import Domain
 
     comm = init_distributed("nccl" if torch.cuda.is_available() else "gloo")
     rank, size = comm.rank, comm.size
@@ -50,29 +53,20 @@ def main():
     else:
         device = torch.device("cpu")
 
-    d = P.ParticlesData(device)
-    prop = propagator_factory(args.prop, False, sys.stdout if (args.verbose and rank == 0) else None, rank, True)
-    prop.activate_fields(d)
+    sim = Simulation(args.init, n=n, prop=args.prop, device=device, comm=comm,
+                     out=sys.stdout if (args.verbose and rank == 0) else None, quiet=not args.verbose)
+    prop, d = sim.propagator, sim.d
     prop.timer.sync = args.verbose
-    init = SedovGrid()
-    box = init.init(rank, size, args.n, d)
-    bucket = max(64, d.numParticlesGlobal // (100 * size))
-    domain = Domain(comm, box, bucket_size_focus=64, bucket_size=bucket)
-    prop.sync(domain, d)
-
-    def step():
-        prop.step(domain, d)
-        d.iteration += 1
 
     for _ in range(args.warmup):
-        step()
+        sim.step()
 
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        sim.step()
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
@@ -82,8 +76,10 @@ def main():
     ms = 1000.0 * dt / max(args.steps, 1)
     value = d.numParticlesGlobal * args.steps / dt
     if rank == 0:
+        grav = " + Barnes-Hut self-gravity" if d.g != 0 else ""
+        ic = "glass" if args.init != "sedov" else "lattice"
         out = {
-            "metric": "particle-updates/sec (whole node), Sedov -n 400",
+            "metric": METRIC,
             "value": value,
             "unit": "particle-updates/s",
             "n_gpus": size,
@@ -94,9 +90,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "fp64 coordinates + fp32 hydro (reference precision mix)",
-            "data": "synthetic (built-in Sedov lattice initial conditions)",
-            "config": {"model": f"sedov-ve -n {args.n} ({d.numParticlesGlobal} particles)",
-                       "global_batch": d.numParticlesGlobal, "seq_len": 1,
+            "data": f"synthetic (built-in {args.init} {ic} initial conditions)",
+            "config": {"model": f"{args.init} -n {n} --prop {args.prop}{grav} ({int(d.numParticlesGlobal)} particles)",
+                       "global_batch": int(d.numParticlesGlobal), "seq_len": 1,
                        "parallelism": f"sfc-domain-decomposition x{size}"},
         }
         print(json.dumps(out), flush=True)
@@ -104,6 +100,8 @@ def main():
             nsteps = max(prop.timer.num_accum, 1)
             for k, v in prop.timer.accum.items():
                 print(f"# substep {k:28s} {1000.0 * v / nsteps:10.3f} ms/step", file=sys.stderr)
+            if prop.gravity is not None and prop.gravity.stats:
+                print(f"# gravity stats {prop.gravity.stats}", file=sys.stderr)
             if device.type == "cuda":
                 print(f"# max memory allocated {torch.cuda.max_memory_allocated() / 2**30:.2f} GiB", file=sys.stderr)
 
