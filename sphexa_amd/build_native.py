@@ -91,17 +91,21 @@ def build_cpu(verbose=False):
     return target
 
 
-def build_hip(verbose=False):
-    os.makedirs(OBJ, exist_ok=True)
+def build_hip(verbose=False, variant=None, defines=()):
+    """``variant``/``defines``: tuning build into _native/variants/<variant>/ with extra -D flags (loaded when
+    SPHX_HIP_VARIANT=<variant> is set)"""
+    out_dir = os.path.join(OUT, "variants", variant) if variant else OUT
+    obj_dir = os.path.join(out_dir, "obj") if variant else OBJ
+    os.makedirs(obj_dir, exist_ok=True)
     hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
     srcs = sorted(glob.glob(os.path.join(CSRC, "hip", "*.hip")) + glob.glob(os.path.join(CSRC, "hip", "*.cpp")))
-    target = os.path.join(OUT, "_sphx_hip" + EXT)
+    target = os.path.join(out_dir, "_sphx_hip" + EXT)
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-             f"-I{os.path.join(CSRC, 'include')}", f"-I{os.path.join(CSRC, 'hip')}"] + _py_includes()
+             f"-I{os.path.join(CSRC, 'include')}", f"-I{os.path.join(CSRC, 'hip')}"] + list(defines) + _py_includes()
     hdrs = _headers() + glob.glob(os.path.join(CSRC, "hip", "*.h"))
     jobs, objs = [], []
     for s in srcs:
-        o = os.path.join(OBJ, "hip_" + os.path.basename(s) + ".o")
+        o = os.path.join(obj_dir, "hip_" + os.path.basename(s) + ".o")
         objs.append(o)
         if _newer(o, [s] + hdrs):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
@@ -144,6 +148,12 @@ def build_all(verbose=False, hip=True):
 
 
 if __name__ == "__main__":
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        tag = sys.argv[i + 1]
+        defs = [a for a in sys.argv[i + 2:] if a.startswith("-D")]
+        print("ok", build_hip(verbose=True, variant=tag, defines=defs))
+        sys.exit(0)
     skip_hip = "--no-hip" in sys.argv
     for t in build_all(verbose=True, hip=not skip_hip):
         print("ok", t)

@@ -156,6 +156,8 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         const float band  = relOk ? 8.0f * hi * delta + 4.0f * delta * delta : 3.4e38f;
         const double radiusSq = double(r2f);
         const double ip[3]    = {xi, yi, zi};
+        // group search box half sizes in the relative fp32 frame, widened by the coordinate rounding
+        const float gsf[3] = {float(gs[0]) + 2.0f * delta, float(gs[1]) + 2.0f * delta, float(gs[2]) + 2.0f * delta};
 
         unsigned cnt = 0;
         for (int l = 0; l < nLeaves; ++l)
@@ -169,21 +171,24 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
             for (int32_t c0 = a; c0 < b; c0 += 64)
             {
                 int32_t j = c0 + lane;
-                int m     = min(64, b - c0);
                 float xr = 0, yr = 0, zr = 0;
+                bool inBox = false;
                 if (j < b)
                 {
                     xr = float(foldMin(x[j] - gc[0], box, 0));
                     yr = float(foldMin(y[j] - gc[1], box, 1));
                     zr = float(foldMin(z[j] - gc[2], box, 2));
+                    // only sources inside the group search box can be a neighbor of any lane
+                    inBox = !relOk || (fabsf(xr) <= gsf[0] && fabsf(yr) <= gsf[1] && fabsf(zr) <= gsf[2]);
                 }
-                for (int k = 0; k < m; ++k)
+                for (uint64_t mask = ballot(inBox); mask; mask &= mask - 1)
                 {
+                    const int k = __builtin_ctzll(mask);
                     float dx = readLaneF(xr, k) - xir;
                     float dy = readLaneF(yr, k) - yir;
                     float dz = readLaneF(zr, k) - zir;
                     float d2 = dx * dx + dy * dy + dz * dz;
-                    int64_t jj = int64_t(c0) + k;
+                    const int64_t jj = int64_t(c0) + k;
                     bool hit   = d2 < r2f - band;
                     if (!hit && d2 <= r2f + band)
                     {

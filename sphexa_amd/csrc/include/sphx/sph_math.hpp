@@ -181,6 +181,59 @@ SPHX_HD void pairDelta(CT xi, CT yi, CT zi, CT xj, CT yj, CT zj, HT hi, const Bo
 // VE formulation
 // ---------------------------------------------------------------------------------------------------------
 
+
+// gathers in flight per lane and loop kind (tuned on MI355X; see profiles/)
+#ifndef SPHX_BATCH_POS
+#define SPHX_BATCH_POS 4
+#endif
+#ifndef SPHX_BATCH_IAD
+#define SPHX_BATCH_IAD 2
+#endif
+#ifndef SPHX_BATCH_MOM
+#define SPHX_BATCH_MOM 2
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+constexpr bool kDeviceBatching = true;
+#else
+constexpr bool kDeviceBatching = false;
+#endif
+
+/*! @brief neighbor loop with memory-level parallelism: on the GPU, B indices and then B source records are loaded
+ *         before the B pair evaluations run, so every wave keeps B independent gathers in flight (the pair loops
+ *         are latency bound otherwise: one dependent index->record->math chain per iteration). The OpenMP build
+ *         evaluates one neighbor at a time. Evaluation order (and hence the floating-point sums) is unchanged.
+ */
+template<int B, class Idx, class Ld, class F>
+SPHX_HD void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const Ld& ld, F&& f)
+{
+    using Rec  = decltype(ld(0u));
+    unsigned k = 0;
+    if constexpr (kDeviceBatching && B > 1)
+    {
+        for (; k + B <= nc; k += B)
+        {
+            unsigned j[B];
+            Rec r[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                j[u] = unsigned(nbr[(k + u) * stride]);
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                r[u] = ld(j[u]);
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                f(j[u], r[u]);
+        }
+    }
+#pragma nounroll
+    for (; k < nc; ++k)
+    {
+        unsigned j = unsigned(nbr[k * stride]);
+        f(j, ld(j));
+    }
+}
+
 //! @brief xm_i = m_i / rho0_i, rho0_i = K h^-3 sum_j W_ij m_j including self (reference xmass_kern.hpp)
 template<class Idx, class Ld>
 SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
@@ -189,14 +242,12 @@ SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
     SrcPos pi = ld(i);
     HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv;
     HT rho0 = pi.m;
-    for (unsigned k = 0; k < nc; ++k)
-    {
-        SrcPos pj = ld(unsigned(nbr[k * stride]));
+    forEachNeighbor<SPHX_BATCH_POS>(nbr, stride, nc, ld, [&](unsigned j, const SrcPos& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
         rho0 += tableLookup(wh, dist * hInv) * pj.m;
-    }
+    });
     return pi.m / (rho0 * HT(K) * h3Inv);
 }
 
@@ -212,9 +263,7 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const Box& box, const Idx* nb
     HT kxi      = xmi;
     HT whomegai = -HT(3) * xmi;
     HT wrho0i   = -HT(3) * mi;
-    for (unsigned k = 0; k < nc; ++k)
-    {
-        SrcPos pj = ld(unsigned(nbr[k * stride]));
+    forEachNeighbor<SPHX_BATCH_POS>(nbr, stride, nc, ld, [&](unsigned j, const SrcPos& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist  = sqrt(rx * rx + ry * ry + rz * rz);
@@ -226,7 +275,7 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const Box& box, const Idx* nb
         kxi += w * xmj;
         whomegai += dterh * xmj;
         wrho0i += dterh * pj.m;
-    }
+    });
     HT Kf = HT(K);
     kxi *= Kf * h3Inv;
     whomegai *= Kf * h3Inv * hInv;
@@ -266,9 +315,7 @@ SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
     HT tau[6] = {0, 0, 0, 0, 0, 0};
     SrcIad pi = ld(i);
     HT hInv   = HT(1) / hi;
-    for (unsigned k = 0; k < nc; ++k)
-    {
-        SrcIad pj = ld(unsigned(nbr[k * stride]));
+    forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
@@ -280,7 +327,7 @@ SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
         tau[3] += ry * ry * vw;
         tau[4] += ry * rz * vw;
         tau[5] += rz * rz * vw;
-    }
+    });
     invertTau(tau, hi, K, c);
 }
 
@@ -293,9 +340,7 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
     HT c11 = ci[0], c12 = ci[1], c13 = ci[2], c22 = ci[3], c23 = ci[4], c33 = ci[5];
     HT dVx[3] = {0, 0, 0}, dVy[3] = {0, 0, 0}, dVz[3] = {0, 0, 0};
-    for (unsigned k = 0; k < nc; ++k)
-    {
-        SrcIad pj = ld(unsigned(nbr[k * stride]));
+    forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
@@ -315,7 +360,7 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
         dVz[0] += az * tA0;
         dVz[1] += az * tA1;
         dVz[2] += az * tA2;
-    }
+    });
     HT nk   = HT(K) * hInv3 / kxi;
     divvOut = nk * (dVx[0] + dVy[1] + dVz[2]);
     HT cx = dVz[1] - dVy[2], cy = dVx[2] - dVz[0], cz = dVy[0] - dVx[1];
@@ -346,9 +391,7 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* 
     HT M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
     SrcIad pi  = ld(i);
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
-    for (unsigned k = 0; k < nc; ++k)
-    {
-        SrcIad pj = ld(unsigned(nbr[k * stride]));
+    forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
@@ -371,7 +414,7 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* 
         M[2][0] += az * rx;
         M[2][1] += az * ry;
         M[2][2] += az * rz;
-    }
+    });
     invertTau(tau, hi, K, c);
     // dV_a[k] = -sum_b c[k][b] M[a][b], c symmetric (c11 c12 c13 c22 c23 c33)
     HT dVv[3][3];
@@ -409,9 +452,7 @@ SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const Box& box, const Idx* nbr,
     HT hInv  = HT(1) / hi, hInv3 = hInv * hInv * hInv;
     HT divvi = pi.divv;
     HT gx = 0, gy = 0, gz = 0;
-    for (unsigned k = 0; k < nc; ++k)
-    {
-        SrcIad pj = ld(unsigned(nbr[k * stride]));
+    forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
@@ -428,7 +469,7 @@ SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const Box& box, const Idx* nbr,
         gx += f * tA0;
         gy += f * tA1;
         gz += f * tA2;
-    }
+    });
     HT graddivv = sqrt(gx * gx + gy * gy + gz * gz);
     HT alphaloc = 0;
     if (divvi < HT(0))
@@ -492,10 +533,7 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
     HT maxvs = 0, mx = 0, my = 0, mz = 0, energy = 0, aviscE = 0;
     const HT Atmin = sc.Atmin, Atmax = sc.Atmax, ramp = sc.ramp;
 
-    for (unsigned k = 0; k < nc; ++k)
-    {
-        unsigned j = unsigned(nbr[k * stride]);
-        SrcMom pj  = ld(j);
+    forEachNeighbor<SPHX_BATCH_MOM>(nbr, stride, nc, ld, [&](unsigned j, const SrcMom& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
@@ -558,7 +596,7 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
         mx += momi * tAi0 + momj * tAj0 + avx;
         my += momi * tAi1 + momj * tAj1 + avy;
         mz += momi * tAi2 + momj * tAj2 + avz;
-    }
+    });
     aviscE        = smax(HT(0), aviscE);
     HT Kf         = HT(sc.K);
     duOut         = double(Kf * (prhoi * energy + HT(0.5) * aviscE));
@@ -579,9 +617,7 @@ SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const 
     HT mi_roi = pi.m / roi;
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
     HT maxvs = 0, mx = 0, my = 0, mz = 0, energy = 0;
-    for (unsigned k = 0; k < nc; ++k)
-    {
-        SrcStd pj = ld(unsigned(nbr[k * stride]));
+    forEachNeighbor<SPHX_BATCH_MOM>(nbr, stride, nc, ld, [&](unsigned j, const SrcStd& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
@@ -617,7 +653,7 @@ SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const 
             HT b = visc * mjrojWj;
             energy += vxij * (a * tAi0 + b * tAj0) + vyij * (a * tAi1 + b * tAj1) + vzij * (a * tAi2 + b * tAj2);
         }
-    }
+    });
     HT Kf         = HT(K);
     duOut         = double(-Kf * HT(0.5) * energy);
     axOut         = Kf * mx;

@@ -20,6 +20,12 @@ def _load(name: str):
     if name in _cache:
         return _cache[name]
     path = os.path.join(_NATIVE_DIR, name + _EXT)
+    variant = os.environ.get("SPHX_HIP_VARIANT") if name == "_sphx_hip" else None
+    if variant:
+        # tuning builds: sphexa_amd/_native/variants/<tag>/_sphx_hip*.so (build_native --variant tag -DNAME=V ...)
+        path = os.path.join(_NATIVE_DIR, "variants", variant, name + _EXT)
+        if not os.path.exists(path):
+            raise ImportError(f"HIP variant {variant} not built: {path}")
     if not os.path.exists(path):
         # build on first use (CPU container or fresh checkout)
         from .. import build_native
