@@ -48,6 +48,8 @@ Where possible options are:
     --avclean           Use AV cleaning
     --duration          Maximum wall-clock run time of the simulation in seconds [MAX_INT]
     --profile [FREQ]    Write substep timings to a "profile" file every FREQ iterations
+    --pmroot PATH       Energy counters directory (Cray pm_counters layout) sampled with --profile
+                        [/sys/cray/pm_counters]; the amdgpu hwmon sensor is used for the GPU when absent
     -o PATH             Location of generated output files
     --device DEV        cuda (default when a GPU is present) or cpu (OpenMP reference path)
 """
@@ -97,6 +99,15 @@ def main(argv=None) -> int:
     propagator = propagator_factory(prop, av_clean, out, rank, quiet, sim_init.constants())
     observables = _observables_factory(sim_init.constants(), const_path, rank, init_cond)
 
+    if prof_enabled:
+        from ..utils.pm_reader import PmReader
+
+        pm = PmReader(rank)
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        per_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(max(torch.cuda.device_count(), 1))))
+        pm.add_counters(parser.get("--pmroot", "/sys/cray/pm_counters"), per_node, local)
+        propagator.timer.pm = pm
+
     t_total = time.perf_counter()
     comm.barrier()
 
@@ -139,6 +150,10 @@ def main(argv=None) -> int:
             write_step(writer, out_file, d, domain, propagator)
         if prof_enabled and (is_output_step(d.iteration, prof_freq) or wall_reached):
             write_profile(propagator, comm, os.path.join(os.path.dirname(out_file) or ".", "profile"))
+            if propagator.timer.pm is not None and not ascii:
+                propagator.timer.pm.write_timings(sio.file_writer_factory(False, comm),
+                                                  os.path.join(os.path.dirname(out_file) or ".", "energy"),
+                                                  comm.size)
         if wall_reached:
             d.iteration += 1
             break

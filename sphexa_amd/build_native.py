@@ -100,7 +100,10 @@ def build_hip(verbose=False, variant=None, defines=()):
     hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
     srcs = sorted(glob.glob(os.path.join(CSRC, "hip", "*.hip")) + glob.glob(os.path.join(CSRC, "hip", "*.cpp")))
     target = os.path.join(out_dir, "_sphx_hip" + EXT)
+    # fp32 division/sqrt as the hardware rcp/sqrt (<= 1 ulp) instead of the IEEE correctly-rounded expansions
+    # (~10 VALU each): the SPH pair loops are VALU-bound on MI355X (profiles/), the results stay fp32-accurate
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-fno-hip-fp32-correctly-rounded-divide-sqrt",
              f"-I{os.path.join(CSRC, 'include')}", f"-I{os.path.join(CSRC, 'hip')}"] + list(defines) + _py_includes()
     hdrs = _headers() + glob.glob(os.path.join(CSRC, "hip", "*.h"))
     jobs, objs = [], []

@@ -91,7 +91,7 @@ __global__ void packMomKernel(int64_t n, MomFields f, SrcMom* __restrict__ out, 
     r.vx    = f.vx[i];
     r.vy    = f.vy[i];
     r.vz    = f.vz[i];
-    r.h     = f.h[i];
+    r.ih    = 1.0f / f.h[i];
     r.c11   = f.cij[0][i];
     r.c12   = f.cij[1][i];
     r.c13   = f.cij[2][i];
@@ -104,6 +104,7 @@ __global__ void packMomKernel(int64_t n, MomFields f, SrcMom* __restrict__ out, 
     r.rho   = f.kx[i] * f.m[i] / f.xm[i];
     r.prho  = f.prho[i];
     r.alpha = f.alpha[i];
+    r.mrho  = f.m[i] / r.rho;
     out[i]  = r;
     if (gv)
     {
@@ -126,7 +127,7 @@ __global__ void packStdKernel(int64_t n, StdFields f, SrcStd* __restrict__ out)
     r.vx   = f.vx[i];
     r.vy   = f.vy[i];
     r.vz   = f.vz[i];
-    r.h    = f.h[i];
+    r.ih   = 1.0f / f.h[i];
     r.c11  = f.cij[0][i];
     r.c12  = f.cij[1][i];
     r.c13  = f.cij[2][i];
@@ -310,7 +311,7 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphC
         az[i] = azi;
         du[i] = dui;
         SrcMom ri = rec[i];
-        dti       = tsKCourant(mvs, ri.h, ri.c, float(sc.Kcour));
+        dti       = tsKCourant(mvs, 1.0f / ri.ih, ri.c, float(sc.Kcour));
     }
     reduceMinDt(dti, minDt);
 }
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyStdKernel(NbrArgs a, Sph
         az[i] = azi;
         du[i] = dui;
         SrcStd ri = rec[i];
-        dti       = tsKCourant(mvs, ri.h, ri.c, float(sc.Kcour));
+        dti       = tsKCourant(mvs, 1.0f / ri.ih, ri.c, float(sc.Kcour));
     }
     reduceMinDt(dti, minDt);
 }

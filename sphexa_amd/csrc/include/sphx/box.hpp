@@ -54,25 +54,22 @@ SPHX_HD double distanceSqPbc(double x1, double y1, double z1, double x2, double 
     return dx * dx + dy * dy + dz * dz;
 }
 
-//! @brief single periodic fold when the component exceeds r (the SPH j-loop convention)
+//! @brief single periodic fold when the component exceeds r (the SPH j-loop convention); select-based, so the
+//!        GPU pair loops stay branch free (the component is at most one box length off)
+template<class T>
+SPHX_HD T foldOne(T v, T r, T L, bool periodic)
+{
+    T lo = v > r ? v - L : v;
+    T hi = v < -r ? v + L : lo;
+    return periodic ? hi : v;
+}
+
 template<class T>
 SPHX_HD void foldPbc(const Box& b, T r, T& xx, T& yy, T& zz)
 {
-    if (b.bc[0] == kPeriodic)
-    {
-        if (xx > r) xx -= T(b.len(0));
-        else if (xx < -r) xx += T(b.len(0));
-    }
-    if (b.bc[1] == kPeriodic)
-    {
-        if (yy > r) yy -= T(b.len(1));
-        else if (yy < -r) yy += T(b.len(1));
-    }
-    if (b.bc[2] == kPeriodic)
-    {
-        if (zz > r) zz -= T(b.len(2));
-        else if (zz < -r) zz += T(b.len(2));
-    }
+    xx = foldOne(xx, r, T(b.len(0)), b.bc[0] == kPeriodic);
+    yy = foldOne(yy, r, T(b.len(1)), b.bc[1] == kPeriodic);
+    zz = foldOne(zz, r, T(b.len(2)), b.bc[2] == kPeriodic);
 }
 
 //! @brief fold a coordinate back into the box for periodic dimensions (one image shift)

@@ -53,9 +53,11 @@ SPHX_HD T tableLookup(const T* table, T v)
     constexpr T dx     = T(2.0) / nInt;
     constexpr T invDx  = T(1) / dx;
     int idx            = int(v * invDx);
-    if (idx >= nInt) return T(0);
-    T d = (table[idx + 1] - table[idx]) * invDx;
-    return table[idx] + d * (v - T(idx) * dx);
+    bool inside        = idx < nInt;
+    idx                = inside ? idx : nInt - 1;
+    T t0 = table[idx], t1 = table[idx + 1];
+    T r  = t0 + (t1 - t0) * invDx * (v - T(idx) * dx);
+    return inside ? r : T(0);
 }
 
 //! @brief smoothing length update targeting ng0 neighbors (reference kernels.hpp updateH)
@@ -142,15 +144,16 @@ struct alignas(16) SrcIad
     HT divv;
 };
 
-//! @brief VE momentum/energy: 96 B (+ velocity gradient for AV cleaning: 128 B)
+//! @brief VE momentum/energy: 96 B (+ velocity gradient for AV cleaning: 128 B). Per-particle factors of the pair
+//!        terms are precomputed at pack time (1/h, m/rho) so the pair loop has no divisions.
 struct alignas(16) SrcMom
 {
     CT x, y, z;
     HT vx, vy, vz;
-    HT h;
+    HT ih;
     HT c11, c12, c13, c22, c23, c33;
     HT m, c, xm, rho;
-    HT prho, alpha;
+    HT prho, alpha, mrho;
 };
 
 struct alignas(16) SrcGradV
@@ -163,7 +166,7 @@ struct alignas(16) SrcGradV
 struct alignas(16) SrcStd
 {
     CT x, y, z;
-    HT vx, vy, vz, h;
+    HT vx, vy, vz, ih;
     HT c11, c12, c13, c22, c23, c33;
     HT m, rho, p, c;
 };
@@ -175,6 +178,16 @@ SPHX_HD void pairDelta(CT xi, CT yi, CT zi, CT xj, CT yj, CT zj, HT hi, const Bo
     ry = HT(yi - yj);
     rz = HT(zi - zj);
     foldPbc(box, HT(2) * hi, rx, ry, rz);
+}
+
+//! @brief 1/sqrt(x): the hardware reciprocal square root on the GPU, IEEE sqrt + division on the host
+SPHX_HD HT rsqrtH(HT x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return rsqrtf(x);
+#else
+    return HT(1) / std::sqrt(x);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -190,7 +203,7 @@ SPHX_HD void pairDelta(CT xi, CT yi, CT zi, CT xj, CT yj, CT zj, HT hi, const Bo
 #define SPHX_BATCH_IAD 2
 #endif
 #ifndef SPHX_BATCH_MOM
-#define SPHX_BATCH_MOM 2
+#define SPHX_BATCH_MOM 1
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -455,11 +468,13 @@ SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const Box& box, const Idx* nbr,
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
-        HT dist = sqrt(rx * rx + ry * ry + rz * rz);
+        HT r2      = rx * rx + ry * ry + rz * rz;
+        HT invDist = rsqrtH(r2);
+        HT dist    = r2 * invDist;
         HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
         HT rv   = rx * vxij + ry * vyij + rz * vzij;
         HT vsij = HT(0);
-        if (rv < HT(0)) { vsij = ci + pj.c - HT(3) * rv / dist; }
+        if (rv < HT(0)) { vsij = ci + pj.c - HT(3) * rv * invDist; }
         vsig   = smax(vsig, vsij);
         HT W   = HT(K) * hInv3 * tableLookup(wh, dist * hInv);
         HT tA0 = -(c11 * rx + c12 * ry + c13 * rz) * W;
@@ -518,9 +533,9 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
                                  HT& azOut, double& duOut, HT& maxvsignalOut)
 {
     SrcMom pi = ld(i);
-    HT hi = pi.h, ci = pi.c, alphai = pi.alpha, xmi = pi.xm;
-    HT rhoi = pi.rho, prhoi = pi.prho;
-    HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
+    HT hInv = pi.ih, hi = HT(1) / hInv, ci = pi.c, alphai = pi.alpha, xmi = pi.xm;
+    HT rhoi = pi.rho, prhoi = pi.prho, invRhoi = HT(1) / rhoi, log2xmi = log2(xmi);
+    HT hInv3 = hInv * hInv * hInv;
     HT gVi[6] = {0, 0, 0, 0, 0, 0};
     if (avClean)
     {
@@ -536,9 +551,11 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
     forEachNeighbor<SPHX_BATCH_MOM>(nbr, stride, nc, ld, [&](unsigned j, const SrcMom& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
-        HT dist = sqrt(rx * rx + ry * ry + rz * rz);
+        HT r2      = rx * rx + ry * ry + rz * rz;
+        HT invDist = rsqrtH(r2);
+        HT dist    = r2 * invDist;
         HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
-        HT hjInv = HT(1) / pj.h;
+        HT hjInv = pj.ih;
         HT v1 = dist * hInv, v2 = dist * hjInv;
         HT Wi = hInv3 * tableLookup(wh, v1);
         HT Wj = hjInv * hjInv * hjInv * tableLookup(wh, v2);
@@ -558,32 +575,35 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
             SrcGradV gj = ldg(j);
             rv += avRvCorrection(rx, ry, rz, smin(v1, v2), etaCrit, gVi, gj.dV);
         }
-        HT wij  = rv / dist;
+        HT wij  = rv * invDist;
         HT visc = artificialViscosity(alphai, pj.alpha, ci, cj, wij);
         HT vs   = HT(0.5) * (ci + cj) - HT(2) * wij;
         maxvs   = vs > maxvs ? vs : maxvs;
 
+        // generalized volume elements with the Atwood ramp; Atwood = |rho_i - rho_j| / (rho_i + rho_j)
         HT a_mom, b_mom;
-        HT Atwood = fabs(rhoi - rhoj) / (rhoi + rhoj);
-        if (Atwood < Atmin)
+        HT dRho = fabs(rhoi - rhoj), sRho = rhoi + rhoj;
+        if (dRho < Atmin * sRho)
         {
             a_mom = xmi * xmi;
             b_mom = xmj * xmj;
         }
-        else if (Atwood > Atmax)
+        else if (dRho > Atmax * sRho)
         {
             a_mom = xmi * xmj;
             b_mom = a_mom;
         }
         else
         {
-            HT sigma = ramp * (Atwood - Atmin);
-            a_mom    = pow(xmi, HT(2) - sigma) * pow(xmj, sigma);
-            b_mom    = pow(xmj, HT(2) - sigma) * pow(xmi, sigma);
+            // xmi^(2-s) xmj^s = xmi^2 (xmj/xmi)^s and xmj^(2-s) xmi^s = xmj^2 (xmj/xmi)^-s
+            HT sigma = ramp * (dRho / sRho - Atmin);
+            HT q     = exp2(sigma * (log2(xmj) - log2xmi));
+            a_mom    = xmi * xmi * q;
+            b_mom    = xmj * xmj / q;
         }
 
-        HT av  = mj / rhoi * visc;
-        HT bv  = mj / rhoj * visc;
+        HT av  = mj * invRhoi * visc;
+        HT bv  = pj.mrho * visc;
         HT avx = HT(0.5) * (av * tAi0 + bv * tAj0);
         HT avy = HT(0.5) * (av * tAi1 + bv * tAj1);
         HT avz = HT(0.5) * (av * tAi2 + bv * tAj2);
@@ -613,16 +633,18 @@ SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const 
                                     HT& maxvsignalOut)
 {
     SrcStd pi = ld(i);
-    HT hi = pi.h, roi = pi.rho, pri = pi.p, ci = pi.c;
+    HT hInv = pi.ih, hi = HT(1) / hInv, roi = pi.rho, pri = pi.p, ci = pi.c;
     HT mi_roi = pi.m / roi;
-    HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
+    HT hInv3 = hInv * hInv * hInv;
     HT maxvs = 0, mx = 0, my = 0, mz = 0, energy = 0;
     forEachNeighbor<SPHX_BATCH_MOM>(nbr, stride, nc, ld, [&](unsigned j, const SrcStd& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
-        HT dist = sqrt(rx * rx + ry * ry + rz * rz);
+        HT r2      = rx * rx + ry * ry + rz * rz;
+        HT invDist = rsqrtH(r2);
+        HT dist    = r2 * invDist;
         HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
-        HT hjInv = HT(1) / pj.h;
+        HT hjInv = pj.ih;
         HT v1 = dist * hInv, v2 = dist * hjInv;
         HT rv = rx * vxij + ry * vyij + rz * vzij;
         HT Wi = hInv3 * tableLookup(wh, v1);
@@ -634,7 +656,7 @@ SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const 
         HT tAj1 = pj.c12 * rx + pj.c22 * ry + pj.c23 * rz;
         HT tAj2 = pj.c13 * rx + pj.c23 * ry + pj.c33 * rz;
         HT roj = pj.rho, cj = pj.c;
-        HT wij  = rv / dist;
+        HT wij  = rv * invDist;
         HT visc = HT(0.5) * artificialViscosity(HT(1), HT(1), ci, cj, wij);
         HT vs   = ci + cj - HT(3) * wij;
         maxvs   = vs > maxvs ? vs : maxvs;
@@ -716,7 +738,7 @@ struct SoaMom
         r.vx = vx[j];
         r.vy = vy[j];
         r.vz = vz[j];
-        r.h = h[j];
+        r.ih = HT(1) / h[j];
         r.c11 = c11[j];
         r.c12 = c12[j];
         r.c13 = c13[j];
@@ -729,6 +751,7 @@ struct SoaMom
         r.rho = kx[j] * m[j] / xm[j];
         r.prho = prho[j];
         r.alpha = alpha[j];
+        r.mrho = m[j] / r.rho;
         return r;
     }
 };
@@ -759,7 +782,7 @@ struct SoaStd
         r.vx = vx[j];
         r.vy = vy[j];
         r.vz = vz[j];
-        r.h = h[j];
+        r.ih = HT(1) / h[j];
         r.c11 = c11[j];
         r.c12 = c12[j];
         r.c13 = c13[j];

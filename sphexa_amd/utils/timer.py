@@ -43,6 +43,7 @@ class Timer:
         self.steps: "OrderedDict[str, float]" = OrderedDict()
         self.accum: Dict[str, float] = OrderedDict()
         self.num_accum = 0
+        self.pm = None  # optional utils.pm_reader.PmReader sampled at every boundary
 
     def _now(self):
         if self.sync and self.device is not None and self.device.type == "cuda":
@@ -52,12 +53,16 @@ class Timer:
     def start(self):
         self.steps.clear()
         self.t0 = self.last = self._now()
+        if self.pm is not None:
+            self.pm.start()
         r = _roctx()
         if r:
             r.roctxRangePushA(b"step")
 
     def step(self, name: str):
         now = self._now()
+        if self.pm is not None:
+            self.pm.step()
         dt = now - self.last
         self.last = now
         self.steps[name] = self.steps.get(name, 0.0) + dt

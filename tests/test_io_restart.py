@@ -68,3 +68,21 @@ def test_ascii_output(tmp_path):
     assert files
     rows = np.loadtxt(files[0])
     assert rows.shape == (8**3, 4)
+
+
+def test_profile_and_energy_counters(tmp_path):
+    """--profile writes substep timings; --pmroot counters (Cray layout) are sampled at every substep boundary"""
+    pm = tmp_path / "pm"
+    pm.mkdir()
+    (pm / "energy").write_text("1000 J 5000000 us\n")
+    (pm / "accel0_energy").write_text("200 J 5000000 us\n")
+    out = str(tmp_path / "dump.h5")
+    _run_cli(["--init", "sedov", "-n", "8", "-s", "2", "--profile", "1", "--pmroot", str(pm), "-o", out,
+              "--device", "cpu", "--quiet"])
+    prof = (tmp_path / "profile").read_text().split("\n")
+    assert prof[0].startswith("numRanks 1") and "MomentumAndEnergy" in prof[1]
+    rd = H5PartReader()
+    rd.set_step(str(tmp_path / "energy.h5"), -1, collective=False)
+    names = set(rd.dataset_names())
+    rd.close_step()
+    assert {"node", "node_timeStamps"} <= names or {"acc", "acc_timeStamps"} <= names
