@@ -67,6 +67,7 @@ class Domain:
         self.global_tree: Optional[torch.Tensor] = None
         self.global_counts: Optional[torch.Tensor] = None
         self.assignment: Optional[List[int]] = None     # global-tree leaf index boundaries per rank
+        self.assignment_keys: Optional[List[int]] = None  # SFC key boundaries per rank (after shift limiting)
         self.local_tree: Optional[torch.Tensor] = None
         self.octree: Optional[octree_ops.Octree] = None
         self.halo_send_idx: List[torch.Tensor] = []       # per destination rank: own particle indices (absolute)
@@ -201,7 +202,15 @@ class Domain:
             bounds[r] = max(bounds[r], bounds[r - 1])
         self.assignment = bounds
         tree_cpu = tree.cpu()
-        bkeys = torch.stack([tree_cpu[b] for b in bounds[1:-1]]) if self.size > 1 else torch.empty(0, dtype=torch.int64)
+        keys_b = [int(tree_cpu[b]) & 0xFFFFFFFFFFFFFFFF for b in bounds]  # the end key 2^63 is stored as int64 min
+        old = self.assignment_keys
+        if old is not None and len(old) == len(keys_b):
+            # limitBoundaryShifts (reference domaindecomp.hpp:140-166): a rank can only grow into the old ranges
+            # of its two neighbors, so particles move at most one rank per step
+            for r in range(1, self.size):
+                keys_b[r] = min(max(keys_b[r], old[r - 1]), old[r + 1])
+        self.assignment_keys = keys_b
+        bkeys = torch.tensor(keys_b[1:-1], dtype=torch.int64)
         # send ranges: lower_bound of boundary keys in the sorted local keys
         pos = torch.searchsorted(skeys, bkeys.to(skeys.device)).cpu().tolist()
         edges = [0] + pos + [skeys.numel()]
