@@ -34,4 +34,16 @@ SPHX_HD int clz64(uint64_t x) { return x == 0 ? 64 : __builtin_clzll(x); }
 SPHX_HD int ctz64(uint64_t x) { return x == 0 ? 64 : __builtin_ctzll(x); }
 SPHX_HD int popcount64(uint64_t x) { return __builtin_popcountll(x); }
 
+//! @brief 1/sqrt(x): hardware reciprocal square root (v_rsq_f32) on the GPU, sqrt + division on the host
+SPHX_HD float rsqrtF(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rsqf(x);
+#else
+    return 1.0f / std::sqrt(x);
+#endif
+}
+
+SPHX_HD double rsqrtF(double x) { return 1.0 / std::sqrt(x); }
+
 } // namespace sphx

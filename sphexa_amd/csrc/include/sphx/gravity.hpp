@@ -85,7 +85,7 @@ template<class T>
 SPHX_HD void m2p(T rx, T ry, T rz, const Quadrupole& mp, T acc[4])
 {
     T r2   = rx * rx + ry * ry + rz * rz;
-    T rm1  = T(1) / sqrt(r2);
+    T rm1  = rsqrtF(r2);
     T rm2  = rm1 * rm1;
     T rm5  = rm2 * rm2 * rm1;
     T Qrx  = rx * mp.q[qXX] + ry * mp.q[qXY] + rz * mp.q[qXZ];
@@ -108,7 +108,7 @@ SPHX_HD void p2p(T dx, T dy, T dz, T mj, T hi, T hj, T acc[4])
     T hij   = hi + hj;
     T hij2  = hij * hij;
     T R2eff = R2 < hij2 ? hij2 : R2;
-    T invR  = T(1) / sqrt(R2eff);
+    T invR  = rsqrtF(R2eff);
     T invR2 = invR * invR;
     T w     = mj * invR * invR2;
     acc[0] -= w * R2;

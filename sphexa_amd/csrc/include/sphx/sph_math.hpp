@@ -180,15 +180,8 @@ SPHX_HD void pairDelta(CT xi, CT yi, CT zi, CT xj, CT yj, CT zj, HT hi, const Bo
     foldPbc(box, HT(2) * hi, rx, ry, rz);
 }
 
-//! @brief 1/sqrt(x): the hardware reciprocal square root on the GPU, IEEE sqrt + division on the host
-SPHX_HD HT rsqrtH(HT x)
-{
-#if defined(__HIP_DEVICE_COMPILE__)
-    return rsqrtf(x);
-#else
-    return HT(1) / std::sqrt(x);
-#endif
-}
+//! @brief 1/sqrt(x) in hydro precision (annotation.hpp rsqrtF)
+SPHX_HD HT rsqrtH(HT x) { return rsqrtF(x); }
 
 // ---------------------------------------------------------------------------------------------------------
 // VE formulation
