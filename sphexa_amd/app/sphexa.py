@@ -52,6 +52,7 @@ Where possible options are:
                         [/sys/cray/pm_counters]; the amdgpu hwmon sensor is used for the GPU when absent
     -o PATH             Location of generated output files
     --device DEV        cuda (default when a GPU is present) or cpu (OpenMP reference path)
+    --insitu MOD[:FN]   In-situ adaptor module called every iteration with the local particle fields
 """
 
 
@@ -135,6 +136,9 @@ def main(argv=None) -> int:
     propagator.sync(domain, d)
     if rank == 0:
         print(f"Domain synchronized, nLocalParticles {domain.n_particles()}", flush=True)
+    from .insitu import InsituHook
+
+    viz = InsituHook(parser.get("--insitu", None), sim_init.constants())
 
     start_iteration = d.iteration
     while not stop_simulation(d.iteration - 1, d.ttot, max_step):
@@ -142,6 +146,7 @@ def main(argv=None) -> int:
         box = domain.box
         observables.compute_and_write(d, domain, comm)
         propagator.print_iteration_timings(domain, d)
+        viz.execute(d, domain)
 
         wall_reached = (time.perf_counter() - t_total) > duration
         if (is_output_step(d.iteration, write_freq) or is_output_time(d.ttot - d.minDt, d.ttot, write_freq)
@@ -164,6 +169,7 @@ def main(argv=None) -> int:
         print(f"# Total execution time of {d.iteration - start_iteration} iterations of {init_cond} up to t = "
               f"{d.ttot:.6f}: {elapsed:.6f}s", file=out, flush=True)
     observables.close()
+    viz.finalize()
     return 0
 
 

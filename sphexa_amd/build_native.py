@@ -154,7 +154,7 @@ if __name__ == "__main__":
     if "--variant" in sys.argv:
         i = sys.argv.index("--variant")
         tag = sys.argv[i + 1]
-        defs = [a for a in sys.argv[i + 2:] if a.startswith("-D")]
+        defs = [a for a in sys.argv[i + 2:] if a.startswith(("-D", "-f", "-m"))]
         print("ok", build_hip(verbose=True, variant=tag, defines=defs))
         sys.exit(0)
     skip_hip = "--no-hip" in sys.argv

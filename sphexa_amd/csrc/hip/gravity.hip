@@ -119,7 +119,7 @@ void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, do
 // --------------------------------------------------------------------------------------------- traversal
 
 constexpr int kGWaves   = 4;
-constexpr int kGFront   = 512;
+constexpr int kGStack   = 2048;
 constexpr int kGM2P     = 256;
 constexpr int kGLeaves  = 128;
 
@@ -196,10 +196,13 @@ __device__ __forceinline__ int32_t gLoad(const int32_t* p)
     else { return *p; }
 }
 
-/*! @brief Barnes-Hut traversal of one 64-target group (one wave): breadth-first over the tree with the vector MAC
- *         against the group's bounding box; accepted nodes queue in the LDS M2P list, opened leaves in the LDS
- *         leaf list, both flushed when full. Returns false (nothing written) if the frontier overflows
- *         @p frontCap — the group is then redone by the spill kernel with a global-memory frontier.
+/*! @brief Barnes-Hut traversal of one 64-target group (one wave): last-in-first-out over chunks of up to 64 nodes
+ *         (each lane tests one node against the vector MAC of the group's bounding box); accepted nodes queue in
+ *         the LDS M2P list, opened leaves in the LDS leaf list, both flushed in batches; children of opened
+ *         internal nodes are pushed on the stack. Popping the most recently pushed nodes first keeps the stack
+ *         at O(depth x 8 x 64) entries instead of a whole tree level (breadth-first). Returns false (nothing
+ *         written) if the stack overflows @p stackCap — the group is then redone by the spill kernel with a
+ *         global-memory stack.
  */
 template<bool kSpill>
 __device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t last, const GravTree& t,
@@ -208,8 +211,7 @@ __device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t l
                                              const float* __restrict__ m, float G, float* __restrict__ ax,
                                              float* __restrict__ ay, float* __restrict__ az,
                                              double* __restrict__ ugrav, unsigned long long* __restrict__ stats,
-                                             int32_t* frontA, int32_t* frontB, int32_t* mlst, int32_t* llst,
-                                             int frontCap, double& upot)
+                                             int32_t* stack, int32_t* mlst, int32_t* llst, int stackCap, double& upot)
 {
     const int lane   = threadIdx.x & 63;
     const int64_t i  = first + g * 64 + lane;
@@ -232,64 +234,56 @@ __device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t l
     float xr = float(xi - tc[0]), yr = float(yi - tc[1]), zr = float(zi - tc[2]);
     float acc[4] = {0, 0, 0, 0};
 
-    int32_t* cur = frontA;
-    int32_t* nxt = frontB;
-    int nf = 1, nm = 0, nl = 0;
+    int sp = 1, nm = 0, nl = 0;
     unsigned long long totM2P = 0, totP2P = 0;
-    if (lane == 0) cur[0] = 0;
+    if (lane == 0) stack[0] = 0;
     gWaveSync<kSpill>();
-    while (nf > 0)
+    while (sp > 0)
     {
-        int nn = 0;
-        for (int base = 0; base < nf; base += 64)
+        const int cnt  = min(sp, 64);
+        const int base = sp - cnt;
+        int32_t nd     = lane < cnt ? gLoad<kSpill>(stack + base + lane) : -1;
+        sp             = base;
+        gWaveSync<kSpill>(); // all lanes read their node before the pushes below overwrite the popped slots
+        bool isM2P = false, isLeaf = false, isInt = false;
+        if (nd >= 0)
         {
-            int idx    = base + lane;
-            int32_t nd = idx < nf ? gLoad<kSpill>(cur + idx) : -1;
-            bool isM2P = false, isLeaf = false, isInt = false;
-            if (nd >= 0)
-            {
-                const double* c = t.centers + 4 * nd;
-                bool violated   = macViolated(c, c[3], tc, ts);
-                isM2P           = !violated && c[3] != 0.0;
-                isLeaf          = violated && t.n2l[nd] >= 0;
-                isInt           = violated && t.n2l[nd] < 0;
-            }
-            uint64_t bm = ballot(isM2P), bl = ballot(isLeaf), bi = ballot(isInt);
-            int cm = __popcll(bm), cl = __popcll(bl), ci = __popcll(bi);
-            // flush the queues if this batch would overflow them
-            if (nm + cm > kGM2P)
-            {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                flushM2P(mlst, nm, t, xi, yi, zi, acc);
-                nm = 0;
-            }
-            if (nl + cl > kGLeaves)
-            {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                totP2P += flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
-                nl = 0;
-            }
-            if (isM2P) mlst[nm + __popcll(bm & lanemaskLt())] = nd;
-            if (isLeaf) llst[nl + __popcll(bl & lanemaskLt())] = nd;
-            if (isInt)
-            {
-                int pos    = nn + 8 * __popcll(bi & lanemaskLt());
-                int32_t co = t.child[nd];
-                if (pos + 8 <= frontCap)
-                    for (int k = 0; k < 8; ++k)
-                        nxt[pos + k] = co + k;
-            }
-            nm += cm;
-            nl += cl;
-            totM2P += cm;
-            nn += 8 * ci;
+            const double* c = t.centers + 4 * nd;
+            bool violated   = macViolated(c, c[3], tc, ts);
+            isM2P           = !violated && c[3] != 0.0;
+            isLeaf          = violated && t.n2l[nd] >= 0;
+            isInt           = violated && t.n2l[nd] < 0;
         }
+        uint64_t bm = ballot(isM2P), bl = ballot(isLeaf), bi = ballot(isInt);
+        int cm = __popcll(bm), cl = __popcll(bl), ci = __popcll(bi);
+        // flush the queues if this batch would overflow them
+        if (nm + cm > kGM2P)
+        {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            flushM2P(mlst, nm, t, xi, yi, zi, acc);
+            nm = 0;
+        }
+        if (nl + cl > kGLeaves)
+        {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            totP2P += flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
+            nl = 0;
+        }
+        if (isM2P) mlst[nm + __popcll(bm & lanemaskLt())] = nd;
+        if (isLeaf) llst[nl + __popcll(bl & lanemaskLt())] = nd;
+        if (sp + 8 * ci > stackCap) return false;
+        if (isInt)
+        {
+            int pos    = sp + 8 * __popcll(bi & lanemaskLt());
+            int32_t co = t.child[nd];
+            for (int k = 0; k < 8; ++k)
+                stack[pos + k] = co + k;
+        }
+        nm += cm;
+        nl += cl;
+        totM2P += cm;
+        sp += 8 * ci;
         gWaveSync<kSpill>();
-        if (nn > frontCap) return false;
-        int32_t* tmp = cur;
-        cur          = nxt;
-        nxt          = tmp;
-        nf           = nn;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     flushM2P(mlst, nm, t, xi, yi, zi, acc);
@@ -307,7 +301,7 @@ __device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t l
     if (lane == 0)
     {
         // stats: [0] sum of P2P per target, [1] failed groups, [2] sum of M2P, [3] max P2P, [4] max M2P,
-        //        [5] spilled groups (queued for the global-frontier kernel)
+        //        [5] spilled groups (queued for the global-stack kernel)
         auto nv = (unsigned long long)(min(int64_t(64), last - (first + g * 64)));
         atomicAdd(&stats[0], totP2P * nv);
         atomicAdd(&stats[2], totM2P * nv);
@@ -340,8 +334,7 @@ __global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last
                                                      unsigned long long* __restrict__ stats,
                                                      int32_t* __restrict__ spillList, int frontCap)
 {
-    __shared__ int32_t frontA[kGWaves][kGFront];
-    __shared__ int32_t frontB[kGWaves][kGFront];
+    __shared__ int32_t stack[kGWaves][kGStack];
     __shared__ int32_t m2pList[kGWaves][kGM2P];
     __shared__ int32_t leafList[kGWaves][kGLeaves];
     __shared__ double red[kGWaves];
@@ -353,15 +346,15 @@ __global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last
     double upot             = 0;
     if (g < numGroups)
     {
-        bool ok = gravityGroup<false>(g, first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, stats, frontA[wave],
-                                      frontB[wave], m2pList[wave], leafList[wave], frontCap, upot);
+        bool ok = gravityGroup<false>(g, first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, stats, stack[wave],
+                                      m2pList[wave], leafList[wave], frontCap, upot);
         if (!ok && (threadIdx.x & 63) == 0) spillList[atomicAdd(&stats[5], 1ull)] = int32_t(g);
     }
     blockEnergy(upot, red, kGWaves, out);
 }
 
 constexpr int kGSpillWaves = 128;
-constexpr int kGSpillFront = 32768;
+constexpr int kGSpillFront = 65536;
 
 __global__ __launch_bounds__(64) void gravitySpillKernel(int64_t first, int64_t last, GravTree t,
                                                          const double* __restrict__ x, const double* __restrict__ y,
@@ -377,14 +370,13 @@ __global__ __launch_bounds__(64) void gravitySpillKernel(int64_t first, int64_t 
     __shared__ int32_t leafList[kGLeaves];
     __shared__ double red[1];
     const int64_t numSpill = int64_t(__hip_atomic_load(&stats[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    int32_t* frontA = scratch + int64_t(blockIdx.x) * 2 * kGSpillFront;
-    int32_t* frontB = frontA + kGSpillFront;
-    double upot     = 0;
+    int32_t* stack = scratch + int64_t(blockIdx.x) * kGSpillFront;
+    double upot    = 0;
     for (int64_t k = blockIdx.x; k < numSpill; k += gridDim.x)
     {
         double u = 0;
         bool ok  = gravityGroup<true>(spillList[k], first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, stats,
-                                      frontA, frontB, m2pList, leafList, kGSpillFront, u);
+                                      stack, m2pList, leafList, kGSpillFront, u);
         upot += u;
         if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
     }
@@ -395,7 +387,7 @@ size_t gravityScratchBytes(int64_t n)
 {
     int64_t groups = (n + 63) / 64;
     return size_t((groups + 63) / 64 * 64) * sizeof(int32_t) +
-           size_t(kGSpillWaves) * 2 * kGSpillFront * sizeof(int32_t);
+           size_t(kGSpillWaves) * kGSpillFront * sizeof(int32_t);
 }
 
 void computeGravity(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
@@ -412,7 +404,7 @@ void computeGravity(int64_t first, int64_t last, const int32_t* child, const int
     int32_t* spillMem  = spillList + (groups + 63) / 64 * 64;
     unsigned grid      = unsigned((groups + kGWaves - 1) / kGWaves);
     gravityKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
-                                               spillList, testFrontCap > 0 ? min(testFrontCap, kGFront) : kGFront);
+                                               spillList, testFrontCap > 0 ? min(testFrontCap, kGStack) : kGStack);
     SPHX_LAUNCH_CHECK();
     gravitySpillKernel<<<kGSpillWaves, 64, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
                                                    spillList, spillMem);

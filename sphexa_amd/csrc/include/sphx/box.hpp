@@ -59,9 +59,18 @@ SPHX_HD double distanceSqPbc(double x1, double y1, double z1, double x2, double 
 template<class T>
 SPHX_HD T foldOne(T v, T r, T L, bool periodic)
 {
+#ifdef SPHX_BRANCHY_FOLD
+    if (periodic)
+    {
+        if (v > r) v -= L;
+        else if (v < -r) v += L;
+    }
+    return v;
+#else
     T lo = v > r ? v - L : v;
     T hi = v < -r ? v + L : lo;
     return periodic ? hi : v;
+#endif
 }
 
 template<class T>

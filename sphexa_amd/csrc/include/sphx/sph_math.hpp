@@ -53,11 +53,17 @@ SPHX_HD T tableLookup(const T* table, T v)
     constexpr T dx     = T(2.0) / nInt;
     constexpr T invDx  = T(1) / dx;
     int idx            = int(v * invDx);
-    bool inside        = idx < nInt;
-    idx                = inside ? idx : nInt - 1;
+#ifdef SPHX_BRANCHY_TABLE
+    if (idx >= nInt) return T(0);
+    T d = (table[idx + 1] - table[idx]) * invDx;
+    return table[idx] + d * (v - T(idx) * dx);
+#else
+    bool inside = idx < nInt;
+    idx         = inside ? idx : nInt - 1;
     T t0 = table[idx], t1 = table[idx + 1];
     T r  = t0 + (t1 - t0) * invDx * (v - T(idx) * dx);
     return inside ? r : T(0);
+#endif
 }
 
 //! @brief smoothing length update targeting ng0 neighbors (reference kernels.hpp updateH)

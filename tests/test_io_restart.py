@@ -86,3 +86,17 @@ def test_profile_and_energy_counters(tmp_path):
     names = set(rd.dataset_names())
     rd.close_step()
     assert {"node", "node_timeStamps"} <= names or {"acc", "acc_timeStamps"} <= names
+
+
+def test_insitu_hook(tmp_path, monkeypatch):
+    import sys
+
+    monkeypatch.syspath_prepend(str(__import__("pathlib").Path(__file__).parent / "helpers"))
+    import insitu_probe
+
+    insitu_probe.CALLS.clear()
+    _run_cli(["--init", "sedov", "-n", "8", "-s", "2", "--insitu", "insitu_probe", "-o", str(tmp_path / "d.h5"),
+              "--device", "cpu", "--quiet"])
+    kinds = [c[0] for c in insitu_probe.CALLS]
+    assert kinds == ["init", "exec", "exec", "fin"]
+    assert insitu_probe.CALLS[1][2] == 8**3
