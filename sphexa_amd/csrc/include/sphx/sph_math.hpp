@@ -53,7 +53,8 @@ SPHX_HD T tableLookup(const T* table, T v)
     constexpr T dx     = T(2.0) / nInt;
     constexpr T invDx  = T(1) / dx;
     int idx            = int(v * invDx);
-#ifdef SPHX_BRANCHY_TABLE
+#ifndef SPHX_SELECT_TABLE
+    // a (wave-uniformly) skipped branch is cheaper than always loading + selecting (measured, profiles/)
     if (idx >= nInt) return T(0);
     T d = (table[idx + 1] - table[idx]) * invDx;
     return table[idx] + d * (v - T(idx) * dx);
