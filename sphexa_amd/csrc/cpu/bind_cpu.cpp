@@ -53,7 +53,7 @@ void conservedQuantities(int64_t, int64_t, const double*, const double*, const d
 namespace
 {
 using BoxArr   = std::array<double, 9>;
-using ConstArr = std::array<double, 13>;
+using ConstArr = std::array<double, 15>;
 using Ptr      = uintptr_t;
 
 template<class T>
@@ -90,6 +90,8 @@ SphConsts toConsts(const ConstArr& a)
     s.ramp          = float(a[10]);
     s.ng0           = unsigned(a[11]);
     s.ngmax         = unsigned(a[12]);
+    s.sincIndex     = float(a[13]);
+    s.kernelChoice  = int(a[14]);
     return s;
 }
 

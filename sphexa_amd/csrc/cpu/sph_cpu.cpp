@@ -93,7 +93,7 @@ void xmass(int64_t first, int64_t last, const SphConsts& sc, const Box& box, con
 #pragma omp parallel for schedule(static)
     for (int64_t i = first; i < last; ++i)
         xm[i] = xmassJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i], ld,
-                           wh);
+                           KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice});
 }
 
 void veDefGradh(int64_t first, int64_t last, const SphConsts& sc, const Box& box, const int32_t* nidx,
@@ -104,7 +104,7 @@ void veDefGradh(int64_t first, int64_t last, const SphConsts& sc, const Box& box
 #pragma omp parallel for schedule(static)
     for (int64_t i = first; i < last; ++i)
         veDefGradhJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i], ld,
-                        wh, whd, kx[i], gradh[i]);
+                        KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice}, kx[i], gradh[i]);
 }
 
 void eosVe(int64_t first, int64_t last, const SphConsts& sc, const double* temp, const float* m, const float* kx,
@@ -147,7 +147,7 @@ void iad(int64_t first, int64_t last, const SphConsts& sc, const Box& box, const
     for (int64_t i = first; i < last; ++i)
     {
         float c[6];
-        iadJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i], ld, wh, c);
+        iadJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i], ld, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c);
         for (int k = 0; k < 6; ++k)
             cij[k][i] = c[k];
     }
@@ -166,7 +166,7 @@ void divvCurlv(int64_t first, int64_t last, const SphConsts& sc, const Box& box,
         float g[6];
         float ci[6] = {cij[0][i], cij[1][i], cij[2][i], cij[3][i], cij[4][i], cij[5][i]};
         divvCurlvJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i], kx[i],
-                       ci, ld, wh, divv[i], curlv[i], doGrad ? g : nullptr);
+                       ci, ld, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, divv[i], curlv[i], doGrad ? g : nullptr);
         if (doGrad)
             for (int k = 0; k < 6; ++k)
                 dV[k][i] = g[k];
@@ -185,7 +185,7 @@ void iadDivvCurlv(int64_t first, int64_t last, const SphConsts& sc, const Box& b
     {
         float c[6], g[6];
         iadDivvCurlvJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), h[i],
-                          kx[i], ld, wh, c, divv[i], curlv[i], doGrad ? g : nullptr);
+                          kx[i], ld, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, divv[i], curlv[i], doGrad ? g : nullptr);
         for (int k = 0; k < 6; ++k)
         {
             cij[k][i] = c[k];
@@ -205,7 +205,7 @@ void avSwitches(int64_t first, int64_t last, const SphConsts& sc, const Box& box
     {
         float ci[6] = {cij[0][i], cij[1][i], cij[2][i], cij[3][i], cij[4][i], cij[5][i]};
         alpha[i]    = avSwitchesJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax),
-                                      h[i], ci, ld, wh, dt, sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
+                                      h[i], ci, ld, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt, sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
     }
 }
 
@@ -224,9 +224,9 @@ double momentumEnergyVe(int64_t first, int64_t last, const SphConsts& sc, const 
         const int32_t* nb = nidx + (i - first) * sc.ngmax;
         unsigned n        = capped(nc, i, sc.ngmax);
         if (avClean)
-            momentumEnergyJLoop<true>(unsigned(i), sc, box, nb, 1, n, ld, ldg, p.wh, ax[i], ay[i], az[i], du[i], mvs);
+            momentumEnergyJLoop<true>(unsigned(i), sc, box, nb, 1, n, ld, ldg, KernelFn{p.wh, nullptr, sc.sincIndex, sc.kernelChoice}, ax[i], ay[i], az[i], du[i], mvs);
         else
-            momentumEnergyJLoop<false>(unsigned(i), sc, box, nb, 1, n, ld, ldg, p.wh, ax[i], ay[i], az[i], du[i], mvs);
+            momentumEnergyJLoop<false>(unsigned(i), sc, box, nb, 1, n, ld, ldg, KernelFn{p.wh, nullptr, sc.sincIndex, sc.kernelChoice}, ax[i], ay[i], az[i], du[i], mvs);
         float dti = tsKCourant(mvs, p.h[i], p.c[i], float(sc.Kcour));
         minDt     = std::min(minDt, double(dti));
     }
@@ -244,7 +244,7 @@ double momentumEnergyStd(int64_t first, int64_t last, const SphConsts& sc, const
     {
         float mvs;
         momentumEnergyStdJLoop(unsigned(i), sc.K, box, nidx + (i - first) * sc.ngmax, 1, capped(nc, i, sc.ngmax), ld,
-                               p.wh, ax[i], ay[i], az[i], du[i], mvs);
+                               KernelFn{p.wh, nullptr, sc.sincIndex, sc.kernelChoice}, ax[i], ay[i], az[i], du[i], mvs);
         float dti = tsKCourant(mvs, p.h[i], p.c[i], float(sc.Kcour));
         minDt     = std::min(minDt, double(dti));
     }

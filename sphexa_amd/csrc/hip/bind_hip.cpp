@@ -15,7 +15,7 @@ using namespace sphx::hip;
 namespace
 {
 using BoxArr   = std::array<double, 9>;
-using ConstArr = std::array<double, 13>;
+using ConstArr = std::array<double, 15>;
 using Ptr      = uintptr_t;
 
 template<class T>
@@ -54,6 +54,8 @@ SphConsts toConsts(const ConstArr& a)
     s.ramp          = float(a[10]);
     s.ng0           = unsigned(a[11]);
     s.ngmax         = unsigned(a[12]);
+    s.sincIndex     = float(a[13]);
+    s.kernelChoice  = int(a[14]);
     return s;
 }
 

@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, B
     const int32_t* nbr;
     unsigned n;
     if (!targetOf(a, i, nbr, n)) return;
-    xm[i] = xmassJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcPos>{rec}, wh);
+    xm[i] = xmassJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcPos>{rec}, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice});
 }
 
 __global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts sc, Box box,
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts 
     unsigned n;
     if (!targetOf(a, i, nbr, n)) return;
     float k, g;
-    veDefGradhJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcPos>{rec}, wh, whd, k, g);
+    veDefGradhJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcPos>{rec}, KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice}, k, g);
     kx[i]    = k;
     gradh[i] = g;
 }
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void iadKernel(NbrArgs a, SphConsts sc, Box
     unsigned n;
     if (!targetOf(a, i, nbr, n)) return;
     float c[6];
-    iadJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcIad>{rec}, wh, c);
+    iadJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcIad>{rec}, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c);
     for (int k = 0; k < 6; ++k)
         cij.p[k][i] = c[k];
 }
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConst
     if (!targetOf(a, i, nbr, n)) return;
     RecLoader<SrcIad> ld{rec};
     float c[6], g[6], dvi, cvi;
-    iadDivvCurlvJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], kx[i], ld, wh, c, dvi, cvi, doGrad ? g : nullptr);
+    iadDivvCurlvJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], kx[i], ld, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, doGrad ? g : nullptr);
     for (int k = 0; k < 6; ++k)
         cij.p[k][i] = c[k];
     divv[i]  = dvi;
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void avSwitchesKernel(NbrArgs a, SphConsts 
     unsigned n;
     if (!targetOf(a, i, nbr, n)) return;
     float ci[6] = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
-    alpha[i]    = avSwitchesJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], ci, RecLoader<SrcIad>{rec}, wh, dt,
+    alpha[i]    = avSwitchesJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], ci, RecLoader<SrcIad>{rec}, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt,
                                   sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
 }
 
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphC
     {
         float mvs, axi, ayi, azi;
         double dui;
-        momentumEnergyJLoop<avClean>(unsigned(i), sc, box, nbr, 64, n, RecLoader<SrcMom>{rec}, GradVLoader{gv}, wh,
+        momentumEnergyJLoop<avClean>(unsigned(i), sc, box, nbr, 64, n, RecLoader<SrcMom>{rec}, GradVLoader{gv}, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice},
                                      axi, ayi, azi, dui, mvs);
         ax[i] = axi;
         ay[i] = ayi;
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyStdKernel(NbrArgs a, Sph
     {
         float mvs, axi, ayi, azi;
         double dui;
-        momentumEnergyStdJLoop(unsigned(i), sc.K, box, nbr, 64, n, RecLoader<SrcStd>{rec}, wh, axi, ayi, azi, dui,
+        momentumEnergyStdJLoop(unsigned(i), sc.K, box, nbr, 64, n, RecLoader<SrcStd>{rec}, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui,
                                mvs);
         ax[i] = axi;
         ay[i] = ayi;

@@ -43,6 +43,8 @@ struct SphConsts
     float ramp;
     unsigned ng0;
     unsigned ngmax;
+    float sincIndex;  // exponent n of the sinc^n kernel
+    int kernelChoice; // 0: sinc^n, 1: 0.9 sinc^4 + 0.1 sinc^9
 };
 
 //! @brief linear interpolation in a table sampled on [0, 2]
@@ -66,6 +68,65 @@ SPHX_HD T tableLookup(const T* table, T v)
     return inside ? r : T(0);
 #endif
 }
+
+/*! @brief SPH kernel W(v) and dW/dv on [0, 2) (reference sph_kernel_tables.hpp: sinc^n of (pi/2) v, or the
+ *         0.9 sinc^4 + 0.1 sinc^9 mix, tabulated at 20000 points and interpolated by lt::lookup).
+ *
+ * The OpenMP path interpolates the same 20000-point tables as the reference. On the GPU the tables (80 kB each)
+ * do not fit the 32 kB vector L1, so every lookup pair became an L2 round trip inside the pair loop; there the
+ * kernel is evaluated analytically from one sin/cos pair instead (the table's interpolation error, ~1e-8
+ * relative, is below fp32 rounding). Build with -DSPHX_TABLE_KERNEL to use the tables on the GPU as well.
+ */
+struct KernelFn
+{
+    const HT* wh;
+    const HT* whd;
+    HT n;
+    int choice;
+
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(SPHX_TABLE_KERNEL)
+    //! sinc(x) and d sinc/dv for x = (pi/2) v
+    SPHX_HD void sinc(HT v, HT& s, HT& ds) const
+    {
+        constexpr HT halfPi = HT(1.5707963267948966);
+        HT x  = halfPi * v;
+        HT sn = __sinf(x), cs = __cosf(x);
+        HT ix = HT(1) / x;
+        s     = v > HT(0) ? sn * ix : HT(1);
+        ds    = v > HT(0) ? halfPi * (cs - s) * ix : HT(0);
+    }
+    SPHX_HD static HT powN(HT s, HT n)
+    {
+        if (n == HT(6))
+        {
+            HT s3 = s * s * s;
+            return s3 * s3;
+        }
+        return s > HT(0) ? exp2(n * log2(s)) : HT(0);
+    }
+    SPHX_HD HT w(HT v) const
+    {
+        if (v >= HT(2)) return HT(0);
+        HT s, ds;
+        sinc(v, s, ds);
+        if (choice == 0) return powN(s, n);
+        HT s2 = s * s, s4 = s2 * s2;
+        return HT(0.9) * s4 + HT(0.1) * s4 * s4 * s;
+    }
+    SPHX_HD HT dw(HT v) const
+    {
+        if (v >= HT(2)) return HT(0);
+        HT s, ds;
+        sinc(v, s, ds);
+        if (choice == 0) return n * powN(s, n - HT(1)) * ds;
+        HT s2 = s * s, s3 = s2 * s, s8 = (s2 * s2) * (s2 * s2);
+        return (HT(0.9) * HT(4) * s3 + HT(0.1) * HT(9) * s8) * ds;
+    }
+#else
+    SPHX_HD HT w(HT v) const { return tableLookup(wh, v); }
+    SPHX_HD HT dw(HT v) const { return tableLookup(whd, v); }
+#endif
+};
 
 //! @brief smoothing length update targeting ng0 neighbors (reference kernels.hpp updateH)
 template<class T>
@@ -250,7 +311,7 @@ SPHX_HD void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const Ld& 
 //! @brief xm_i = m_i / rho0_i, rho0_i = K h^-3 sum_j W_ij m_j including self (reference xmass_kern.hpp)
 template<class Idx, class Ld>
 SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                      const Ld& ld, const HT* wh)
+                      const Ld& ld, const KernelFn& kf)
 {
     SrcPos pi = ld(i);
     HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv;
@@ -259,7 +320,7 @@ SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
-        rho0 += tableLookup(wh, dist * hInv) * pj.m;
+        rho0 += kf.w(dist * hInv) * pj.m;
     });
     return pi.m / (rho0 * HT(K) * h3Inv);
 }
@@ -267,7 +328,7 @@ SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
 //! @brief kx (VE normalization) and grad-h term (reference ve_def_gradh_kern.hpp)
 template<class Idx, class Ld>
 SPHX_HD void veDefGradhJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                             const Ld& ld, const HT* wh, const HT* whd, HT& kxOut, HT& gradhOut)
+                             const Ld& ld, const KernelFn& kf, HT& kxOut, HT& gradhOut)
 {
     SrcPos pi = ld(i);
     HT mi = pi.m, xmi = pi.xm;
@@ -281,8 +342,8 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const Box& box, const Idx* nb
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist  = sqrt(rx * rx + ry * ry + rz * rz);
         HT v     = dist * hInv;
-        HT w     = tableLookup(wh, v);
-        HT dw    = tableLookup(whd, v);
+        HT w     = kf.w(v);
+        HT dw    = kf.dw(v);
         HT dterh = -(HT(3) * w + v * dw);
         HT xmj   = pj.xm;
         kxi += w * xmj;
@@ -323,7 +384,7 @@ SPHX_HD void invertTau(HT tau[6], HT hi, double K, HT c[6])
 //! @brief IAD matrix with volumes vol_j (VE: xm/kx, STD: m/rho) (reference hydro_ve/iad_kern.hpp, hydro_std)
 template<class Idx, class Ld>
 SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                      const Ld& ld, const HT* wh, HT c[6])
+                      const Ld& ld, const KernelFn& kf, HT c[6])
 {
     HT tau[6] = {0, 0, 0, 0, 0, 0};
     SrcIad pi = ld(i);
@@ -332,7 +393,7 @@ SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
-        HT w    = tableLookup(wh, dist * hInv);
+        HT w    = kf.w(dist * hInv);
         HT vw   = pj.vol * w;
         tau[0] += rx * rx * vw;
         tau[1] += rx * ry * vw;
@@ -347,7 +408,7 @@ SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
 //! @brief velocity divergence, |curl|, optional symmetric velocity gradient (reference divv_curlv_kern.hpp)
 template<class Idx, class Ld>
 SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                            HT kxi, const HT ci[6], const Ld& ld, const HT* wh, HT& divvOut, HT& curlvOut, HT* dV)
+                            HT kxi, const HT ci[6], const Ld& ld, const KernelFn& kf, HT& divvOut, HT& curlvOut, HT* dV)
 {
     SrcIad pi = ld(i);
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
@@ -358,7 +419,7 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
         HT vxji = pj.vx - pi.vx, vyji = pj.vy - pi.vy, vzji = pj.vz - pi.vz;
-        HT W    = tableLookup(wh, dist * hInv);
+        HT W    = kf.w(dist * hInv);
         HT tA0  = -(c11 * rx + c12 * ry + c13 * rz) * W;
         HT tA1  = -(c12 * rx + c22 * ry + c23 * rz) * W;
         HT tA2  = -(c13 * rx + c23 * ry + c33 * rz) * W;
@@ -398,7 +459,7 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
  */
 template<class Idx, class Ld>
 SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                               HT kxi, const Ld& ld, const HT* wh, HT c[6], HT& divvOut, HT& curlvOut, HT* dV)
+                               HT kxi, const Ld& ld, const KernelFn& kf, HT c[6], HT& divvOut, HT& curlvOut, HT* dV)
 {
     HT tau[6]  = {0, 0, 0, 0, 0, 0};
     HT M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
@@ -408,7 +469,7 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* 
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrt(rx * rx + ry * ry + rz * rz);
-        HT w    = tableLookup(wh, dist * hInv);
+        HT w    = kf.w(dist * hInv);
         HT vw   = pj.vol * w;
         tau[0] += rx * rx * vw;
         tau[1] += rx * ry * vw;
@@ -455,7 +516,7 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* 
 //! @brief Cullen-Dehnen style AV switch (reference av_switches_kern.hpp)
 template<class Idx, class Ld>
 SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                           const HT ci6[6], const Ld& ld, const HT* wh, double dt, HT alphamin, HT alphamax,
+                           const HT ci6[6], const Ld& ld, const KernelFn& kf, double dt, HT alphamin, HT alphamax,
                            HT decayConstant, HT alpha_i)
 {
     SrcIad pi = ld(i);
@@ -476,7 +537,7 @@ SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const Box& box, const Idx* nbr,
         HT vsij = HT(0);
         if (rv < HT(0)) { vsij = ci + pj.c - HT(3) * rv * invDist; }
         vsig   = smax(vsig, vsij);
-        HT W   = HT(K) * hInv3 * tableLookup(wh, dist * hInv);
+        HT W   = HT(K) * hInv3 * kf.w(dist * hInv);
         HT tA0 = -(c11 * rx + c12 * ry + c13 * rz) * W;
         HT tA1 = -(c12 * rx + c22 * ry + c23 * rz) * W;
         HT tA2 = -(c13 * rx + c23 * ry + c33 * rz) * W;
@@ -529,7 +590,7 @@ SPHX_HD HT avRvCorrection(HT rx, HT ry, HT rz, HT eta_ab, HT eta_crit, const HT 
 //! @brief VE momentum and energy equations (reference hydro_ve/momentum_energy_kern.hpp)
 template<bool avClean, class Idx, class Ld, class LdG>
 SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box, const Idx* nbr, int stride,
-                                 unsigned nc, const Ld& ld, const LdG& ldg, const HT* wh, HT& axOut, HT& ayOut,
+                                 unsigned nc, const Ld& ld, const LdG& ldg, const KernelFn& kf, HT& axOut, HT& ayOut,
                                  HT& azOut, double& duOut, HT& maxvsignalOut)
 {
     SrcMom pi = ld(i);
@@ -557,8 +618,8 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
         HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
         HT hjInv = pj.ih;
         HT v1 = dist * hInv, v2 = dist * hjInv;
-        HT Wi = hInv3 * tableLookup(wh, v1);
-        HT Wj = hjInv * hjInv * hjInv * tableLookup(wh, v2);
+        HT Wi = hInv3 * kf.w(v1);
+        HT Wj = hjInv * hjInv * hjInv * kf.w(v2);
 
         HT tAi0 = -(pi.c11 * rx + pi.c12 * ry + pi.c13 * rz) * Wi;
         HT tAi1 = -(pi.c12 * rx + pi.c22 * ry + pi.c23 * rz) * Wi;
@@ -629,7 +690,7 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
 //! @brief standard SPH momentum and energy, constant alpha=1 AV (reference hydro_std/momentum_energy_kern.hpp)
 template<class Idx, class Ld>
 SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc,
-                                    const Ld& ld, const HT* wh, HT& axOut, HT& ayOut, HT& azOut, double& duOut,
+                                    const Ld& ld, const KernelFn& kf, HT& axOut, HT& ayOut, HT& azOut, double& duOut,
                                     HT& maxvsignalOut)
 {
     SrcStd pi = ld(i);
@@ -647,8 +708,8 @@ SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const 
         HT hjInv = pj.ih;
         HT v1 = dist * hInv, v2 = dist * hjInv;
         HT rv = rx * vxij + ry * vyij + rz * vzij;
-        HT Wi = hInv3 * tableLookup(wh, v1);
-        HT Wj = hjInv * hjInv * hjInv * tableLookup(wh, v2);
+        HT Wi = hInv3 * kf.w(v1);
+        HT Wj = hjInv * hjInv * hjInv * kf.w(v2);
         HT tAi0 = pi.c11 * rx + pi.c12 * ry + pi.c13 * rz;
         HT tAi1 = pi.c12 * rx + pi.c22 * ry + pi.c23 * rz;
         HT tAi2 = pi.c13 * rx + pi.c23 * ry + pi.c33 * rz;

@@ -231,7 +231,8 @@ class ParticlesData:
         """the SphConsts layout expected by the native modules"""
         return [float(self.K), float(self.Kcour), float(self.Krho), float(self.gamma), float(self.muiConst),
                 float(self.alphamin), float(self.alphamax), float(self.decay_constant), float(self.Atmin),
-                float(self.Atmax), float(self.ramp), float(self.ng0), float(self.ngmax)]
+                float(self.Atmax), float(self.ramp), float(self.ng0), float(self.ngmax), float(self.sincIndex),
+                float(self.kernelChoice)]
 
     def set_output_fields(self, names: List[str]) -> List[str]:
         """select output fields; returns names that are not particle fields"""
