@@ -219,10 +219,15 @@ class Domain:
 
         names = list(own.keys())
         sorted_fields = sfc_ops.gather_many(perm, [own[f] for f in names])
-        out = {}
-        for f, t in zip(names, sorted_fields):
-            out[f], _ = self.comm.alltoallv(t, send_counts, recv_counts)
-        new_keys, _ = self.comm.alltoallv(skeys, send_counts, recv_counts)
+        # one packed all-to-all for keys + every conserved field (rows of bytes, like the halo exchange)
+        tensors = [skeys] + sorted_fields
+        packed = _pack_rows(tensors, None)
+        recv, _ = self.comm.alltoallv(packed, send_counts, recv_counts)
+        n_new = recv.shape[0]
+        outs = [torch.empty(n_new, dtype=t.dtype, device=t.device) for t in tensors]
+        _unpack_rows(recv, outs, 0)
+        new_keys = outs[0]
+        out = dict(zip(names, outs[1:]))
         self.stats["migrated_out"] = sum(send_counts) - send_counts[self.rank]
         return new_keys, out
 
