@@ -312,18 +312,28 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("gravity_set_mac", [](int64_t N, Ptr prefixes, const BoxArr& box, int kind, double invTheta, Ptr centers,
                                 Ptr s)
           { gravitySetMac(N, P<KeyT>(prefixes), toBox(box), kind, invTheta, P<double>(centers), St(s)); });
-    m.def("compute_gravity",
+    m.def("gravity_lists",
+          [](int64_t first, int64_t last, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr centers, Ptr mp, Ptr x, Ptr y,
+             Ptr z, Ptr stats, Ptr scratch, int testFrontCap, int capM, int capL, Ptr s)
+          {
+              computeGravityLists(first, last, P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne),
+                                  P<double>(centers), P<void>(mp), P<double>(x), P<double>(y), P<double>(z),
+                                  P<unsigned long long>(stats), P<void>(scratch), testFrontCap, capM, capL, St(s));
+          });
+    m.def("gravity_eval",
           [](int64_t first, int64_t last, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr centers, Ptr mp, Ptr x, Ptr y,
              Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay, Ptr az, Ptr ugrav, Ptr out, Ptr stats, Ptr scratch,
-             int testFrontCap, Ptr s)
+             int capM, int capL, Ptr poff, Ptr pidx, Ptr pacc, Ptr s)
           {
-              computeGravity(first, last, P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne),
-                             P<double>(centers), P<void>(mp), P<double>(x), P<double>(y), P<double>(z), P<float>(h),
-                             P<float>(mm), float(G), P<float>(ax), P<float>(ay), P<float>(az), P<double>(ugrav),
-                             P<double>(out), P<unsigned long long>(stats), P<void>(scratch), testFrontCap,
-                             St(s));
+              computeGravityEval(first, last, P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne),
+                                 P<double>(centers), P<void>(mp), P<double>(x), P<double>(y), P<double>(z),
+                                 P<float>(h), P<float>(mm), float(G), P<float>(ax), P<float>(ay), P<float>(az),
+                                 P<double>(ugrav), P<double>(out), P<unsigned long long>(stats), P<void>(scratch),
+                                 capM, capL, P<int64_t>(poff), P<int32_t>(pidx), P<void>(pacc), St(s));
           });
-    m.def("gravity_scratch_bytes", [](int64_t n) { return gravityScratchBytes(n); });
+    m.def("gravity_scratch_bytes", [](int64_t n, int capM, int capL) { return gravityScratchBytes(n, capM, capL); });
+    m.def("gravity_particle_counts", [](Ptr scratch, int64_t n, int capM, int capL)
+          { return reinterpret_cast<uintptr_t>(gravityParticleCounts(P<void>(scratch), n, capM, capL)); });
     m.def("direct_sum",
           [](int64_t first, int64_t last, int64_t n, Ptr x, Ptr y, Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay,
              Ptr az, Ptr ugrav, Ptr out, Ptr s)

@@ -4,10 +4,12 @@
  * per level), nbody/traversal.cuh:60-526 (traverse: warp per target group, breadth-first with approx (M2P) and
  * body (P2P) queues, potential reduction), nbody/direct.cuh:44-112 (O(N^2) tiled direct sum).
  *
- * Design: one wave = 64 SFC-consecutive targets. The BFS frontier lives in LDS; MAC-accepted nodes are queued in an
- * LDS M2P list, MAC-failing leaves in an LDS P2P list; both are flushed whenever they fill. M2P entries are
- * broadcast as wave-uniform (scalar-cache) loads; P2P source tiles are loaded coalesced, converted to fp32
- * coordinates relative to the group center and broadcast with v_readlane.
+ * Design: one wave = 64 SFC-consecutive targets. The node stack lives in LDS; MAC-accepted nodes are queued in an
+ * LDS M2P list, the particles of MAC-failing leaves in an LDS P2P list; both are flushed whenever they fill. M2P
+ * node data are wave-uniform scalar loads, pipelined one node ahead. P2P sources are staged 64 at a time in LDS
+ * (fp32, relative to the group center) and evaluated as 64x16 target-source tiles on the matrix cores:
+ * v_mfma_f32_16x16x4_f32 forms the squared distances and the softening radii (h_i + h_j)^2, the VALU does the
+ * rsqrt and accumulates the weights (see P2PTarget).
  */
 #include <cfloat>
 
@@ -117,11 +119,30 @@ void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, do
 }
 
 // --------------------------------------------------------------------------------------------- traversal
+//
+// Two phases (interaction lists), so that each runs at its own register/LDS budget and occupancy:
+//   1. gravityListKernel: one wave per 64-target group walks the tree (LIFO node stack in LDS, vector MAC against
+//      the group's bounding box) and writes the MAC-accepted nodes (M2P) and the opened leaves (P2P) of the group
+//      to fixed-capacity slabs in global memory. Light on registers -> many waves per CU hide the dependent node
+//      loads of the walk.
+//   2. gravityM2PKernel / gravityP2PKernel: one wave per group streams its lists: M2P nodes 64 at a time
+//      (coalesced gathers, staged in LDS, evaluated with broadcast LDS reads, next batch in flight), P2P particles
+//      64 at a time as 64x16 target-source tiles on the matrix cores (see P2PTarget). Two kernels so that the
+//      register-light M2P loop runs at twice the occupancy of the MFMA tile loop.
+// Groups whose stack or lists overflow are evaluated by the fused spill kernel (traversal + evaluation with a
+// global-memory stack).
 
-constexpr int kGWaves   = 4;
-constexpr int kGStack   = 2048;
-constexpr int kGM2P     = 256;
-constexpr int kGLeaves  = 128;
+#ifndef SPHX_M2P_WAVES
+#define SPHX_M2P_WAVES 6 // launch bound (waves per SIMD) of the M2P kernel
+#endif
+#ifndef SPHX_M2P_UNROLL
+#define SPHX_M2P_UNROLL 2 // unroll of the per-node M2P loop
+#endif
+
+constexpr int kGWaves = 4;
+constexpr int kGStack = 2048;
+constexpr int kGM2P   = 256;
+constexpr int kGP2P   = 512; // particle indices queued for P2P per wave
 
 struct GravTree
 {
@@ -133,53 +154,256 @@ struct GravTree
     const Quadrupole* mp;
 };
 
-//! @brief apply the queued multipoles to the lane's target (relative fp32 coordinates)
-__device__ inline void flushM2P(const int32_t* list, int n, const GravTree& t, double xi, double yi, double zi,
-                                float acc[4])
+//! @brief per-wave LDS work areas of the evaluation (the M2P staging area aliases the P2P tile)
+struct GravLists
 {
-    for (int k = 0; k < n; ++k)
+    int32_t* mlst; // MAC-accepted nodes (M2P), fused path only
+    int32_t* plst; // particle indices of opened leaves (P2P)
+    float4* spos;  // staged P2P tile: {x, y, z, |x|^2} relative to the group center; M2P: 3 x 64 records
+    float4* smh;   // staged P2P tile: {m, h, h^2, 0}
+};
+
+/*! @brief M2P of a list of nodes, 64 per batch: lane k gathers node k's expansion center (fp32, relative to the
+ *         group center tc) and quadrupole, the batch is staged in LDS as 3 float4 per node and every lane applies
+ *         all of them to its target through wave-uniform (broadcast) LDS reads; the next batch's gathers are in
+ *         flight meanwhile. Relative fp32 centers are exact enough: an accepted node is farther from the group box
+ *         than its MAC radius, so |r| is not small against the rounding of (c - tc) and (x - tc).
+ */
+__device__ inline void evalM2P(const int32_t* list, int n, const GravTree& t, const double tc[3], float xr, float yr,
+                               float zr, float4* stage, float acc[4])
+{
+    n = __builtin_amdgcn_readfirstlane(n);
+    if (n <= 0) return;
+    const int lane = laneId();
+    // raw node data of the batch in flight: loaded unconditionally (clamped index) and converted only when staged,
+    // so no wait on the loads is needed before the arithmetic of the current batch
+    double rc[3];
+    float4 q0, q1;
+    auto gather = [&](int32_t nd)
     {
-        int32_t nd      = __builtin_amdgcn_readfirstlane(list[k]);
         const double* c = t.centers + 4 * nd;
-        Quadrupole q    = t.mp[nd];
-        m2p(float(xi - c[0]), float(yi - c[1]), float(zi - c[2]), q, acc);
+        const float4* q = reinterpret_cast<const float4*>(t.mp + nd);
+        rc[0] = c[0], rc[1] = c[1], rc[2] = c[2];
+        q0 = q[0], q1 = q[1];
+    };
+    // node indices are read two batches ahead, node data one batch ahead of the arithmetic
+    int32_t idxN  = lane < n ? list[lane] : 0;
+    int32_t idxNN = 64 + lane < n ? list[64 + lane] : 0;
+    gather(idxN);
+    for (int b0 = 0; b0 < n; b0 += 64)
+    {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stage[lane] = make_float4(float(rc[0] - tc[0]), float(rc[1] - tc[1]), float(rc[2] - tc[2]), q0.x);
+        stage[64 + lane]  = make_float4(q0.y, q0.z, q0.w, q1.x); // qxx qxy qxz qyy
+        stage[128 + lane] = make_float4(q1.y, q1.z, 0.f, 0.f);   // qyz qzz
+        idxN              = idxNN;
+        idxNN             = b0 + 128 + lane < n ? list[b0 + 128 + lane] : 0;
+        gather(idxN); // unconditional (past the end: clamped index) so the loads land in the loop registers directly
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int cnt = min(64, n - b0);
+#pragma unroll SPHX_M2P_UNROLL
+        for (int k = 0; k < cnt; ++k)
+        {
+            float4 a = stage[k], b = stage[64 + k], c = stage[128 + k];
+            Quadrupole q;
+            q.q[qMass]  = a.w;
+            q.q[qXX]    = b.x;
+            q.q[qXY]    = b.y;
+            q.q[qXZ]    = b.z;
+            q.q[qYY]    = b.w;
+            q.q[qYZ]    = c.x;
+            q.q[qZZ]    = c.y;
+            q.q[qTrace] = 0.f;
+            m2p(xr - a.x, yr - a.y, zr - a.z, q, acc);
+        }
     }
 }
 
-//! @brief P2P of the lane's target with all particles of the queued leaves
-__device__ inline int flushP2P(const int32_t* list, int n, const GravTree& t, const double* x, const double* y,
-                               const double* z, const float* h, const float* m, const double gc[3], float xr,
-                               float yr, float zr, float hi, float acc[4], int lane)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+//! @brief v_max_f32 without the NaN-quieting canonicalization fmaxf adds for MFMA results (inputs are finite)
+__device__ __forceinline__ float maxNoCanon(float a, float b)
 {
-    int numP2P = 0;
-    for (int l = 0; l < n; ++l)
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+/*! @brief target side of the MFMA P2P tile, built once per 64-target group.
+ *
+ * A 64-target x 16-source block is four v_mfma_f32_16x16x4_f32 tiles (targets in blocks tb of 16). With sources on
+ * the MFMA rows and targets on the columns, lane l owns target tb*16 + (l & 15) and sources 4*(l >> 4) + r, r < 4,
+ * of each 16-source block:
+ *     R2[s][t]  = |x_s|^2 + sum_k [x_s, y_s, z_s, 1]_k [-2x_t, -2y_t, -2z_t, |x_t|^2]_k     (C input |x_s|^2)
+ *     H2[s][t]  = sum_k [h_s^2, h_s, 1, 0]_k [1, 2h_t, h_t^2, 0]_k = (h_s + h_t)^2
+ * The VALU then does max / rsqrt / weights and accumulates sum_s w (x_s, y_s, z_s, 1) and the potential per lane;
+ * a = sum_s w x_s - x_t sum_s w is formed once at the end. Coordinates are fp32 relative to the group center.
+ * The expanded R2 carries an absolute rounding error ~eps (|x_s|^2 + |x_t|^2): a tile is evaluated this way only if
+ * that is below ~4e-6 of the smallest softening radius (h_s + h_t)^2 in the tile, otherwise (sparse groups much
+ * larger than h) with the plain VALU pair loop over the same staged sources.
+ */
+struct P2PTarget
+{
+    float bR2[4], bH2[4];
+    float sx[4], sy[4], sz[4], sw[4], phi[4];
+    float xr, yr, zr, hi, v[4]; // VALU path: own target, own accumulators
+    float maxT2, hminT;         // group extent for the accuracy test
+};
+
+constexpr float kMfmaP2PTol = 4e-6f / 6e-8f; // tolerated (|x_s|^2 + |x_t|^2) / (h_s + h_t)^2_min
+
+__device__ __forceinline__ void p2pInit(P2PTarget& T, float xr, float yr, float zr, float hi)
+{
+    const int lane = laneId(), k = lane >> 4;
+    const float r2 = xr * xr + yr * yr + zr * zr;
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
     {
-        int32_t nd = __builtin_amdgcn_readfirstlane(list[l]);
-        int32_t a = t.ns[nd], b = t.ne[nd];
-        numP2P += b - a;
-        for (int32_t c0 = a; c0 < b; c0 += 64)
+        int src = tb * 16 + (lane & 15);
+        float X = __shfl(xr, src), Y = __shfl(yr, src), Z = __shfl(zr, src), R = __shfl(r2, src);
+        float H = __shfl(hi, src);
+        T.bR2[tb] = k == 0 ? -2.f * X : (k == 1 ? -2.f * Y : (k == 2 ? -2.f * Z : R));
+        T.bH2[tb] = k == 0 ? 1.f : (k == 1 ? 2.f * H : (k == 2 ? H * H : 0.f));
+        T.sx[tb] = T.sy[tb] = T.sz[tb] = T.sw[tb] = T.phi[tb] = 0.f;
+    }
+    T.xr = xr, T.yr = yr, T.zr = zr, T.hi = hi;
+    T.v[0] = T.v[1] = T.v[2] = T.v[3] = 0.f;
+    T.maxT2 = waveMax(r2);
+    T.hminT = waveMin(hi);
+}
+
+//! @brief sum the per-lane partials of P2PTarget over the four source lane groups; returns {phi, ax, ay, az} of the
+//!        lane's own target (lane = target index in the group)
+__device__ __forceinline__ void p2pFinish(const P2PTarget& T, float acc[4])
+{
+    const int lane = laneId(), tb = lane >> 4;
+    float v[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+    {
+        float p[5] = {T.phi[b], T.sx[b], T.sy[b], T.sz[b], T.sw[b]};
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
         {
-            int32_t j = c0 + lane;
-            int cnt   = min(64, b - c0);
-            float sx = 0, sy = 0, sz = 0, sm = 0, sh = 0;
-            if (j < b)
-            {
-                sx = float(x[j] - gc[0]);
-                sy = float(y[j] - gc[1]);
-                sz = float(z[j] - gc[2]);
-                sm = m[j];
-                sh = h[j];
-            }
+            float s = p[q];
+            s += __shfl_xor(s, 16);
+            s += __shfl_xor(s, 32);
+            v[q] = (b == tb) ? s : v[q];
+        }
+    }
+    acc[0] += v[0] + T.v[0];
+    acc[1] += v[1] - T.xr * v[4] + T.v[1];
+    acc[2] += v[2] - T.yr * v[4] + T.v[2];
+    acc[3] += v[3] - T.zr * v[4] + T.v[3];
+}
+
+//! @brief all queued P2P particles against the group's 64 targets, 64 sources per staged LDS tile
+__device__ inline void flushP2P(const int32_t* plst, int n, const GravLists& L, const double* x, const double* y,
+                                const double* z, const float* h, const float* m, const double gc[3], P2PTarget& T)
+{
+    n = __builtin_amdgcn_readfirstlane(n);
+    if (n <= 0) return;
+    const int lane = laneId(), kq = lane >> 4;
+    // particle indices are read two chunks ahead, particle data one chunk ahead of the tile arithmetic; the data
+    // of the chunk in flight stay raw (unconditional loads at a clamped index) until they are staged
+    double rx, ry, rz;
+    float rh, rm;
+    auto gather = [&](int32_t j)
+    {
+        rx = x[j], ry = y[j], rz = z[j];
+        rh = h[j], rm = m[j];
+    };
+    int32_t jN  = lane < n ? plst[lane] : plst[0];
+    int32_t jNN = 64 + lane < n ? plst[64 + lane] : plst[0];
+    gather(jN);
+    for (int c0 = 0; c0 < n; c0 += 64)
+    {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // previous tile fully read before it is overwritten
+        const bool valid = c0 + lane < n;
+        float sx = float(rx - gc[0]), sy = float(ry - gc[1]), sz = float(rz - gc[2]);
+        // padding source: m = 0 at the group center with h = 1 (finite weight, zero contribution)
+        const float4 Pn = valid ? make_float4(sx, sy, sz, sx * sx + sy * sy + sz * sz) : make_float4(0, 0, 0, 0);
+        const float4 Qn = valid ? make_float4(rm, rh, rh * rh, 0.f) : make_float4(0.f, 1.f, 1.f, 0.f);
+        L.spos[lane]    = Pn;
+        L.smh[lane]     = Qn;
+        const int cnt   = min(64, n - c0);
+#ifdef SPHX_GRAV_VALU_P2P
+        const bool mfma = false;
+#else
+        const float hs  = waveMin(lane < cnt ? Qn.y : 3.0e38f);
+        const float hh  = hs + T.hminT;
+        const bool mfma = waveMax(Pn.w) + T.maxT2 <= kMfmaP2PTol * hh * hh;
+#endif
+        jN = jNN;
+        jNN = c0 + 128 + lane < n ? plst[c0 + 128 + lane] : plst[0];
+        gather(jN); // unconditional (past the end: clamped index) so the loads land in the loop registers directly
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (!mfma)
+        {
             for (int k = 0; k < cnt; ++k)
             {
-                float dx = readLaneF(sx, k) - xr;
-                float dy = readLaneF(sy, k) - yr;
-                float dz = readLaneF(sz, k) - zr;
-                p2p(dx, dy, dz, readLaneF(sm, k), hi, readLaneF(sh, k), acc);
+                float4 P = L.spos[k], Q = L.smh[k];
+                p2p(P.x - T.xr, P.y - T.yr, P.z - T.zr, Q.x, T.hi, Q.y, T.v);
+            }
+            continue;
+        }
+        const int nsb = (cnt + 15) >> 4;
+        for (int sb = 0; sb < nsb; ++sb)
+        {
+            float4 Pa = L.spos[sb * 16 + (lane & 15)];
+            float4 Qa = L.smh[sb * 16 + (lane & 15)];
+            float aR  = kq == 0 ? Pa.x : (kq == 1 ? Pa.y : (kq == 2 ? Pa.z : 1.f));
+            float aH  = kq == 0 ? Qa.z : (kq == 1 ? Qa.y : (kq == 2 ? 1.f : 0.f));
+            float4 Pr[4];
+            float mr[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                Pr[r] = L.spos[sb * 16 + 4 * kq + r];
+                mr[r] = L.smh[sb * 16 + 4 * kq + r].x;
+            }
+            const f32x4 cR  = {Pr[0].w, Pr[1].w, Pr[2].w, Pr[3].w};
+            const f32x4 c0v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int tb = 0; tb < 4; ++tb)
+            {
+                f32x4 R2 = __builtin_amdgcn_mfma_f32_16x16x4f32(aR, T.bR2[tb], cR, 0, 0, 0);
+                f32x4 H2 = __builtin_amdgcn_mfma_f32_16x16x4f32(aH, T.bH2[tb], c0v, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    float re = maxNoCanon(R2[r], H2[r]);
+                    float ir = __builtin_amdgcn_rsqf(re);
+                    float w  = mr[r] * ir * (ir * ir);
+                    T.phi[tb] -= w * R2[r];
+                    T.sx[tb] += w * Pr[r].x;
+                    T.sy[tb] += w * Pr[r].y;
+                    T.sz[tb] += w * Pr[r].z;
+                    T.sw[tb] += w;
+                }
             }
         }
     }
-    return numP2P;
+}
+
+//! @brief append the particles of leaf (a0, n0) to the P2P list, evaluating the list whenever it is full
+__device__ __forceinline__ void queueLeaf(int a0, int n0, int& np, const GravLists& L, const double* x,
+                                          const double* y, const double* z, const float* h, const float* m,
+                                          const double tc[3], P2PTarget& T)
+{
+    const int lane = laneId();
+    for (int off = 0; off < n0; off += 64)
+    {
+        const int c = min(64, n0 - off);
+        if (np + c > kGP2P)
+        {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            flushP2P(L.plst, np, L, x, y, z, h, m, tc, T);
+            np = 0;
+        }
+        if (lane < c) L.plst[np + lane] = a0 + off + lane;
+        np += c;
+    }
 }
 
 template<bool kSpill>
@@ -196,13 +420,94 @@ __device__ __forceinline__ int32_t gLoad(const int32_t* p)
     else { return *p; }
 }
 
-/*! @brief Barnes-Hut traversal of one 64-target group (one wave): last-in-first-out over chunks of up to 64 nodes
- *         (each lane tests one node against the vector MAC of the group's bounding box); accepted nodes queue in
- *         the LDS M2P list, opened leaves in the LDS leaf list, both flushed in batches; children of opened
- *         internal nodes are pushed on the stack. Popping the most recently pushed nodes first keeps the stack
- *         at O(depth x 8 x 64) entries instead of a whole tree level (breadth-first). Returns false (nothing
- *         written) if the stack overflows @p stackCap — the group is then redone by the spill kernel with a
- *         global-memory stack.
+//! @brief center and half extent of the group's target bounding box (all lanes), fp64
+__device__ __forceinline__ void groupBox(double xi, double yi, double zi, double tc[3], double ts[3])
+{
+    double p[3] = {xi, yi, zi};
+    for (int d = 0; d < 3; ++d)
+    {
+        double a = waveMin(p[d]);
+        double b = waveMax(p[d]);
+        tc[d]    = 0.5 * (a + b);
+        ts[d]    = 0.5 * (b - a);
+    }
+}
+
+/*! @brief one LIFO pop of up to 64 nodes: each lane tests one node against the vector MAC of the group box.
+ *         Children of opened internal nodes are pushed on the stack (most recently pushed popped first, so the stack
+ *         holds O(depth x 8 x 64) entries instead of a whole tree level). Returns false on stack overflow.
+ */
+template<bool kSpill>
+__device__ __forceinline__ bool popAndTest(const GravTree& t, int32_t* stack, int& sp, int stackCap,
+                                           const double tc[3], const double ts[3], int32_t& nd, bool& isM2P,
+                                           bool& isLeaf)
+{
+    const int lane = laneId();
+    const int cnt  = min(sp, 64);
+    const int base = sp - cnt;
+    nd             = lane < cnt ? gLoad<kSpill>(stack + base + lane) : -1;
+    sp             = base;
+    gWaveSync<kSpill>(); // all lanes read their node before the pushes below overwrite the popped slots
+    isM2P = isLeaf = false;
+    bool isInt     = false;
+    if (nd >= 0)
+    {
+        const double* c = t.centers + 4 * nd;
+        bool violated   = macViolated(c, c[3], tc, ts);
+        const bool leaf = t.n2l[nd] >= 0;
+        isM2P           = !violated && c[3] != 0.0;
+        isLeaf          = violated && leaf;
+        isInt           = violated && !leaf;
+    }
+    const uint64_t bi = ballot(isInt);
+    const int ci      = __popcll(bi);
+    if (sp + 8 * ci > stackCap) return false;
+    if (isInt)
+    {
+        int pos    = sp + 8 * __popcll(bi & lanemaskLt());
+        int32_t co = t.child[nd];
+        for (int k = 0; k < 8; ++k)
+            stack[pos + k] = co + k;
+    }
+    sp += 8 * ci;
+    return true;
+}
+
+//! @brief scale by G, write accelerations/potential of the lane's target, accumulate stats
+__device__ __forceinline__ void gravityStore(int64_t g, int64_t first, int64_t last, const float acc[4], float G,
+                                             const float* m, float* ax, float* ay, float* az, double* ugrav,
+                                             unsigned long long* stats, unsigned long long totP2P,
+                                             unsigned long long totM2P, double& upot, float4* pacc = nullptr)
+{
+    const int64_t i = first + g * 64 + laneId();
+    if (i < last)
+    {
+        double u = double(G) * double(m[i]) * double(acc[0]);
+        upot     = u;
+        if (pacc) { pacc[i - first] = make_float4(acc[0], acc[1], acc[2], acc[3]); } // added by gravityCombine
+        else
+        {
+            if (ugrav) ugrav[i] += u;
+            ax[i] += G * acc[1];
+            ay[i] += G * acc[2];
+            az[i] += G * acc[3];
+        }
+    }
+    if (laneId() == 0)
+    {
+        // stats: [0] sum of P2P per target, [1] failed groups, [2] sum of M2P, [3] max P2P, [4] max M2P,
+        //        [5] groups queued for the fused global-stack kernel, [6]/[7] slab demand (leaves / M2P nodes)
+        auto nv = (unsigned long long)(min(int64_t(64), last - (first + g * 64)));
+        atomicAdd(&stats[0], totP2P * nv);
+        atomicAdd(&stats[2], totM2P * nv);
+        atomicMax(&stats[3], totP2P);
+        atomicMax(&stats[4], totM2P);
+    }
+}
+
+/*! @brief fused traversal + evaluation of one group (global-memory stack): the fallback for groups whose LDS stack
+ *         or list slabs overflow in the two-phase path. M2P nodes queue in the LDS list (wave-uniform loads), opened
+ *         leaves go straight to the P2P list.
  */
 template<bool kSpill>
 __device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t last, const GravTree& t,
@@ -211,103 +516,55 @@ __device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t l
                                              const float* __restrict__ m, float G, float* __restrict__ ax,
                                              float* __restrict__ ay, float* __restrict__ az,
                                              double* __restrict__ ugrav, unsigned long long* __restrict__ stats,
-                                             int32_t* stack, int32_t* mlst, int32_t* llst, int stackCap, double& upot)
+                                             int32_t* stack, const GravLists& L, int stackCap, double& upot)
 {
-    const int lane   = threadIdx.x & 63;
-    const int64_t i  = first + g * 64 + lane;
-    const bool valid = i < last;
-    const int64_t ii = valid ? i : (last - 1);
+    const int lane   = laneId();
+    const int64_t ii = min(first + g * 64 + lane, last - 1);
     double xi = x[ii], yi = y[ii], zi = z[ii];
     float hi  = h[ii];
-
     double tc[3], ts[3];
-    {
-        double p[3] = {xi, yi, zi};
-        for (int d = 0; d < 3; ++d)
-        {
-            double a = waveMin(p[d]);
-            double b = waveMax(p[d]);
-            tc[d]    = 0.5 * (a + b);
-            ts[d]    = 0.5 * (b - a);
-        }
-    }
+    groupBox(xi, yi, zi, tc, ts);
     float xr = float(xi - tc[0]), yr = float(yi - tc[1]), zr = float(zi - tc[2]);
     float acc[4] = {0, 0, 0, 0};
+    P2PTarget T;
+    p2pInit(T, xr, yr, zr, hi);
 
-    int sp = 1, nm = 0, nl = 0;
+    int sp = 1, nm = 0, np = 0;
     unsigned long long totM2P = 0, totP2P = 0;
     if (lane == 0) stack[0] = 0;
     gWaveSync<kSpill>();
     while (sp > 0)
     {
-        const int cnt  = min(sp, 64);
-        const int base = sp - cnt;
-        int32_t nd     = lane < cnt ? gLoad<kSpill>(stack + base + lane) : -1;
-        sp             = base;
-        gWaveSync<kSpill>(); // all lanes read their node before the pushes below overwrite the popped slots
-        bool isM2P = false, isLeaf = false, isInt = false;
-        if (nd >= 0)
-        {
-            const double* c = t.centers + 4 * nd;
-            bool violated   = macViolated(c, c[3], tc, ts);
-            isM2P           = !violated && c[3] != 0.0;
-            isLeaf          = violated && t.n2l[nd] >= 0;
-            isInt           = violated && t.n2l[nd] < 0;
-        }
-        uint64_t bm = ballot(isM2P), bl = ballot(isLeaf), bi = ballot(isInt);
-        int cm = __popcll(bm), cl = __popcll(bl), ci = __popcll(bi);
-        // flush the queues if this batch would overflow them
+        int32_t nd;
+        bool isM2P, isLeaf;
+        if (!popAndTest<kSpill>(t, stack, sp, stackCap, tc, ts, nd, isM2P, isLeaf)) return false;
+        int32_t la = isLeaf ? t.ns[nd] : 0, lb = isLeaf ? t.ne[nd] : 0;
+        uint64_t bm = ballot(isM2P), bl = ballot(isLeaf);
+        int cm      = __popcll(bm);
         if (nm + cm > kGM2P)
         {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            flushM2P(mlst, nm, t, xi, yi, zi, acc);
+            evalM2P(L.mlst, nm, t, tc, xr, yr, zr, L.spos, acc);
             nm = 0;
         }
-        if (nl + cl > kGLeaves)
-        {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            totP2P += flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
-            nl = 0;
-        }
-        if (isM2P) mlst[nm + __popcll(bm & lanemaskLt())] = nd;
-        if (isLeaf) llst[nl + __popcll(bl & lanemaskLt())] = nd;
-        if (sp + 8 * ci > stackCap) return false;
-        if (isInt)
-        {
-            int pos    = sp + 8 * __popcll(bi & lanemaskLt());
-            int32_t co = t.child[nd];
-            for (int k = 0; k < 8; ++k)
-                stack[pos + k] = co + k;
-        }
+        if (isM2P) L.mlst[nm + __popcll(bm & lanemaskLt())] = nd;
         nm += cm;
-        nl += cl;
         totM2P += cm;
-        sp += 8 * ci;
+        while (bl)
+        {
+            const int src = __builtin_ctzll(bl);
+            bl &= bl - 1;
+            const int a0 = readLaneI(la, src), n0 = readLaneI(lb, src) - a0;
+            totP2P += n0;
+            queueLeaf(a0, n0, np, L, x, y, z, h, m, tc, T);
+        }
         gWaveSync<kSpill>();
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    flushM2P(mlst, nm, t, xi, yi, zi, acc);
-    totP2P += flushP2P(llst, nl, t, x, y, z, h, m, tc, xr, yr, zr, hi, acc, lane);
-
-    if (valid)
-    {
-        double u = double(G) * double(m[i]) * double(acc[0]);
-        upot     = u;
-        if (ugrav) ugrav[i] += u;
-        ax[i] += G * acc[1];
-        ay[i] += G * acc[2];
-        az[i] += G * acc[3];
-    }
-    if (lane == 0)
-    {
-        // stats: [0] sum of P2P per target, [1] failed groups, [2] sum of M2P, [3] max P2P, [4] max M2P,
-        //        [5] spilled groups (queued for the global-stack kernel)
-        auto nv = (unsigned long long)(min(int64_t(64), last - (first + g * 64)));
-        atomicAdd(&stats[0], totP2P * nv);
-        atomicAdd(&stats[2], totM2P * nv);
-        atomicMax(&stats[3], totP2P);
-        atomicMax(&stats[4], totM2P);
-    }
+    evalM2P(L.mlst, nm, t, tc, xr, yr, zr, L.spos, acc);
+    flushP2P(L.plst, np, L, x, y, z, h, m, tc, T);
+    p2pFinish(T, acc);
+    gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, totP2P, totM2P, upot);
     return true;
 }
 
@@ -325,32 +582,237 @@ __device__ __forceinline__ void blockEnergy(double upot, double* red, int nw, do
     }
 }
 
-__global__ __launch_bounds__(256) void gravityKernel(int64_t first, int64_t last, GravTree t,
-                                                     const double* __restrict__ x, const double* __restrict__ y,
-                                                     const double* __restrict__ z, const float* __restrict__ h,
-                                                     const float* __restrict__ m, float G, float* __restrict__ ax,
-                                                     float* __restrict__ ay, float* __restrict__ az,
-                                                     double* __restrict__ ugrav, double* __restrict__ out,
-                                                     unsigned long long* __restrict__ stats,
-                                                     int32_t* __restrict__ spillList, int frontCap)
+struct GravLds
 {
-    __shared__ int32_t stack[kGWaves][kGStack];
-    __shared__ int32_t m2pList[kGWaves][kGM2P];
-    __shared__ int32_t leafList[kGWaves][kGLeaves];
-    __shared__ double red[kGWaves];
+    int32_t mlst[kGM2P];
+    int32_t plst[kGP2P];
+    float4 stage[3 * 64]; // P2P tile (2 x 64) or M2P batch (3 x 64)
+};
 
+__device__ __forceinline__ GravLists listsOf(GravLds& s)
+{
+    return GravLists{s.mlst, s.plst, s.stage, s.stage + 64};
+}
+
+//! @brief global-memory interaction list slabs: per group capM node ids and capL leaf ids + 2 counts (-1: fallback)
+struct GravSlabs
+{
+    int32_t* mlist;
+    int32_t* llist;
+    int32_t* counts; // per group: M2P nodes, P2P leaves (-1: evaluated by the fused fallback kernel)
+    int32_t* pcount; // per group: P2P particles (sum of the opened leaves' sizes), 0 for fallback groups
+    int capM;
+    int capL;
+};
+
+__global__ __launch_bounds__(256) void gravityListKernel(int64_t first, int64_t last, GravTree t,
+                                                         const double* __restrict__ x, const double* __restrict__ y,
+                                                         const double* __restrict__ z, GravSlabs S,
+                                                         unsigned long long* __restrict__ stats,
+                                                         int32_t* __restrict__ spillList, int stackCap)
+{
+    __shared__ int32_t stackAll[kGWaves][kGStack];
+    const int lane          = laneId();
     const int wave          = threadIdx.x >> 6;
     const int64_t numGroups = (last - first + 63) / 64;
-    const unsigned lb       = xcdRemap(blockIdx.x, gridDim.x);
-    const int64_t g         = int64_t(lb) * kGWaves + wave;
-    double upot             = 0;
-    if (g < numGroups)
+    const int64_t g         = int64_t(xcdRemap(blockIdx.x, gridDim.x)) * kGWaves + wave;
+    if (g >= numGroups) return;
+    int32_t* stack   = stackAll[wave];
+    const int64_t ii = min(first + g * 64 + lane, last - 1);
+    double tc[3], ts[3];
+    groupBox(x[ii], y[ii], z[ii], tc, ts);
+
+    int32_t* ml = S.mlist + g * S.capM;
+    int32_t* ll = S.llist + g * S.capL;
+    int sp = 1, nm = 0, nl = 0, np = 0;
+    bool ok = true;
+    if (lane == 0) stack[0] = 0;
+    gWaveSync<false>();
+    while (sp > 0)
     {
-        bool ok = gravityGroup<false>(g, first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, stats, stack[wave],
-                                      m2pList[wave], leafList[wave], frontCap, upot);
-        if (!ok && (threadIdx.x & 63) == 0) spillList[atomicAdd(&stats[5], 1ull)] = int32_t(g);
+        int32_t nd;
+        bool isM2P, isLeaf;
+        if (!popAndTest<false>(t, stack, sp, stackCap, tc, ts, nd, isM2P, isLeaf))
+        {
+            ok = false;
+            break;
+        }
+        uint64_t bm = ballot(isM2P), bl = ballot(isLeaf);
+        int cm = __popcll(bm), cl = __popcll(bl);
+        if (nm + cm > S.capM || nl + cl > S.capL)
+        {
+            // record the demand seen so far ([6] leaves, [7] M2P nodes) so the host can grow the slabs
+            if (lane == 0)
+            {
+                atomicMax(&stats[6], (unsigned long long)(nl + cl));
+                atomicMax(&stats[7], (unsigned long long)(nm + cm));
+            }
+            ok = false;
+            break;
+        }
+        if (isM2P) ml[nm + __popcll(bm & lanemaskLt())] = nd;
+        if (isLeaf)
+        {
+            ll[nl + __popcll(bl & lanemaskLt())] = nd;
+            np += t.ne[nd] - t.ns[nd];
+        }
+        nm += cm;
+        nl += cl;
+        gWaveSync<false>();
+    }
+    np = waveSum(np);
+    if (lane == 0)
+    {
+        S.counts[2 * g]     = ok ? nm : -1;
+        S.counts[2 * g + 1] = ok ? nl : -1;
+        S.pcount[g]         = ok ? np : 0;
+        if (!ok) spillList[atomicAdd(&stats[5], 1ull)] = int32_t(g);
+    }
+}
+
+/*! @brief expand each group's opened leaves into its contiguous run of P2P particle indices pidx[poff[g] ..) (one
+ *         wave per group; coalesced writes of up to 64 indices per leaf)
+ */
+__global__ __launch_bounds__(256) void gravityExpandKernel(int64_t first, int64_t last, GravTree t, GravSlabs S,
+                                                           const int64_t* __restrict__ poff,
+                                                           int32_t* __restrict__ pidx)
+{
+    const int lane          = laneId();
+    const int64_t numGroups = (last - first + 63) / 64;
+    const int64_t g         = int64_t(blockIdx.x) * kGWaves + (threadIdx.x >> 6);
+    if (g >= numGroups) return;
+    const int nl = __builtin_amdgcn_readfirstlane(S.counts[2 * g + 1]);
+    if (nl <= 0) return;
+    const int32_t* ll = S.llist + g * S.capL;
+    int32_t* out      = pidx + poff[g];
+    int64_t pos       = 0;
+    for (int b0 = 0; b0 < nl; b0 += 64)
+    {
+        int32_t leaf = b0 + lane < nl ? ll[b0 + lane] : -1;
+        int32_t la = leaf >= 0 ? t.ns[leaf] : 0, lb = leaf >= 0 ? t.ne[leaf] : 0;
+        const int cnt = min(64, nl - b0);
+        for (int q = 0; q < cnt; ++q)
+        {
+            const int a0 = readLaneI(la, q), n0 = readLaneI(lb, q) - a0;
+            for (int off = lane; off < n0; off += 64)
+                out[pos + off] = a0 + off;
+            pos += n0;
+        }
+    }
+}
+
+//! @brief shared prologue of the evaluation kernels: the group's targets, fp64 box center, fp32 relative coordinates
+struct EvalTarget
+{
+    double tc[3], ts[3];
+    float xr, yr, zr, hi;
+};
+
+__device__ __forceinline__ EvalTarget evalTarget(int64_t g, int64_t first, int64_t last, const double* x,
+                                                 const double* y, const double* z, const float* h)
+{
+    EvalTarget e;
+    const int64_t ii = min(first + g * 64 + laneId(), last - 1);
+    double xi = x[ii], yi = y[ii], zi = z[ii];
+    groupBox(xi, yi, zi, e.tc, e.ts);
+    e.xr = float(xi - e.tc[0]);
+    e.yr = float(yi - e.tc[1]);
+    e.zr = float(zi - e.tc[2]);
+    e.hi = h[ii];
+    return e;
+}
+
+/*! @brief M2P part of the evaluation (one wave per group): light on registers, so many waves per SIMD hide the
+ *         LDS and transcendental latencies of the multipole loop
+ */
+__global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t first, int64_t last, GravTree t,
+                                                           const double* __restrict__ x,
+                                                           const double* __restrict__ y,
+                                                           const double* __restrict__ z,
+                                                           const float* __restrict__ h, const float* __restrict__ m,
+                                                           float G, float* __restrict__ ax, float* __restrict__ ay,
+                                                           float* __restrict__ az, double* __restrict__ ugrav,
+                                                           double* __restrict__ out,
+                                                           unsigned long long* __restrict__ stats, GravSlabs S)
+{
+    __shared__ float4 stage[kGWaves][3 * 64];
+    __shared__ double red[kGWaves];
+    const int wave          = threadIdx.x >> 6;
+    const int64_t numGroups = (last - first + 63) / 64;
+    const int64_t g         = int64_t(xcdRemap(blockIdx.x, gridDim.x)) * kGWaves + wave;
+    double upot             = 0;
+    const int nm            = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[2 * g]) : -1;
+    if (nm >= 0)
+    {
+        EvalTarget e = evalTarget(g, first, last, x, y, z, h);
+        float acc[4] = {0, 0, 0, 0};
+        evalM2P(S.mlist + g * S.capM, nm, t, e.tc, e.xr, e.yr, e.zr, stage[wave], acc);
+        gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, 0ull, (unsigned long long)nm, upot);
     }
     blockEnergy(upot, red, kGWaves, out);
+}
+
+#ifndef SPHX_P2P_WAVES
+#define SPHX_P2P_WAVES 3 // waves per SIMD of the MFMA P2P kernel (4 spills registers)
+#endif
+
+//! @brief P2P part of the evaluation (one wave per group): leaf list -> particle list -> MFMA tiles
+__global__ __launch_bounds__(256, SPHX_P2P_WAVES) void gravityP2PKernel(int64_t first, int64_t last, GravTree t,
+                                                           const double* __restrict__ x,
+                                                           const double* __restrict__ y,
+                                                           const double* __restrict__ z,
+                                                           const float* __restrict__ h, const float* __restrict__ m,
+                                                           float G, float* __restrict__ ax, float* __restrict__ ay,
+                                                           float* __restrict__ az, double* __restrict__ ugrav,
+                                                           double* __restrict__ out,
+                                                           unsigned long long* __restrict__ stats, GravSlabs S,
+                                                           const int64_t* __restrict__ poff,
+                                                           const int32_t* __restrict__ pidx,
+                                                           float4* __restrict__ pacc)
+{
+    __shared__ GravLds lds[kGWaves];
+    __shared__ double red[kGWaves];
+    const int lane          = laneId();
+    const int wave          = threadIdx.x >> 6;
+    const int64_t numGroups = (last - first + 63) / 64;
+    const int64_t g         = int64_t(xcdRemap(blockIdx.x, gridDim.x)) * kGWaves + wave;
+    double upot             = 0;
+    const int nl            = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[2 * g + 1]) : -1;
+    if (nl >= 0)
+    {
+        GravLists L  = listsOf(lds[wave]);
+        EvalTarget e = evalTarget(g, first, last, x, y, z, h);
+        float acc[4] = {0, 0, 0, 0};
+        P2PTarget T;
+        p2pInit(T, e.xr, e.yr, e.zr, e.hi);
+        const int64_t p0 = poff[g];
+        const int np     = int(poff[g + 1] - p0);
+        flushP2P(pidx + p0, np, L, x, y, z, h, m, e.tc, T);
+        p2pFinish(T, acc);
+        unsigned long long totP2P = (unsigned long long)np;
+        gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, totP2P, 0ull, upot, pacc);
+    }
+    else if (g < numGroups)
+    {
+        // fallback group: its P2P share comes from the fused kernel, which adds to ax directly
+        const int64_t i = first + g * 64 + lane;
+        if (i < last) pacc[i - first] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    blockEnergy(upot, red, kGWaves, out);
+}
+
+//! @brief add the P2P partials (computed concurrently with the M2P kernel on a second stream) to the outputs
+__global__ void gravityCombineKernel(int64_t first, int64_t last, const float4* __restrict__ pacc,
+                                     const float* __restrict__ m, float G, float* __restrict__ ax,
+                                     float* __restrict__ ay, float* __restrict__ az, double* __restrict__ ugrav)
+{
+    int64_t i = first + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= last) return;
+    float4 a = pacc[i - first];
+    ax[i] += G * a.y;
+    ay[i] += G * a.z;
+    az[i] += G * a.w;
+    if (ugrav) ugrav[i] += double(G) * double(m[i]) * double(a.x);
 }
 
 constexpr int kGSpillWaves = 128;
@@ -366,8 +828,7 @@ __global__ __launch_bounds__(64) void gravitySpillKernel(int64_t first, int64_t 
                                                          const int32_t* __restrict__ spillList,
                                                          int32_t* __restrict__ scratch)
 {
-    __shared__ int32_t m2pList[kGM2P];
-    __shared__ int32_t leafList[kGLeaves];
+    __shared__ GravLds lds;
     __shared__ double red[1];
     const int64_t numSpill = int64_t(__hip_atomic_load(&stats[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     int32_t* stack = scratch + int64_t(blockIdx.x) * kGSpillFront;
@@ -376,38 +837,106 @@ __global__ __launch_bounds__(64) void gravitySpillKernel(int64_t first, int64_t 
     {
         double u = 0;
         bool ok  = gravityGroup<true>(spillList[k], first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, stats,
-                                      stack, m2pList, leafList, kGSpillFront, u);
+                                      stack, listsOf(lds), kGSpillFront, u);
         upot += u;
         if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
     }
     blockEnergy(upot, red, 1, out);
 }
 
-size_t gravityScratchBytes(int64_t n)
+static int64_t padTo64(int64_t v) { return (v + 63) / 64 * 64; }
+
+size_t gravityScratchBytes(int64_t n, int capM, int capL)
 {
     int64_t groups = (n + 63) / 64;
-    return size_t((groups + 63) / 64 * 64) * sizeof(int32_t) +
-           size_t(kGSpillWaves) * kGSpillFront * sizeof(int32_t);
+    return size_t(padTo64(groups) + int64_t(kGSpillWaves) * kGSpillFront + padTo64(2 * groups) + padTo64(groups) +
+                  groups * int64_t(capM + capL)) *
+           sizeof(int32_t);
 }
 
-void computeGravity(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
-                    const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
-                    const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
-                    double* ugrav, double* out, unsigned long long* stats, void* scratch, int testFrontCap,
-                    hipStream_t s)
+struct GravScratch
+{
+    int32_t* spillList;
+    int32_t* spillMem;
+    GravSlabs S;
+};
+
+static GravScratch carve(void* scratch, int64_t groups, int capM, int capL)
+{
+    GravScratch c;
+    c.spillList = static_cast<int32_t*>(scratch);
+    c.spillMem  = c.spillList + padTo64(groups);
+    int32_t* counts = c.spillMem + int64_t(kGSpillWaves) * kGSpillFront;
+    int32_t* pcount = counts + padTo64(2 * groups);
+    int32_t* mlist  = pcount + padTo64(groups);
+    int32_t* llist  = mlist + groups * int64_t(capM);
+    c.S             = GravSlabs{mlist, llist, counts, pcount, capM, capL};
+    return c;
+}
+
+int32_t* gravityParticleCounts(void* scratch, int64_t n, int capM, int capL)
+{
+    return carve(scratch, (n + 63) / 64, capM, capL).S.pcount;
+}
+
+void computeGravityLists(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
+                         const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
+                         const double* z, unsigned long long* stats, void* scratch, int testFrontCap, int capM,
+                         int capL, hipStream_t s)
 {
     int64_t n = last - first;
     if (n <= 0) return;
     GravTree t{child, n2l, ns, ne, centers, (const Quadrupole*)mp};
-    int64_t groups     = (n + 63) / 64;
-    int32_t* spillList = static_cast<int32_t*>(scratch);
-    int32_t* spillMem  = spillList + (groups + 63) / 64 * 64;
-    unsigned grid      = unsigned((groups + kGWaves - 1) / kGWaves);
-    gravityKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
-                                               spillList, testFrontCap > 0 ? min(testFrontCap, kGStack) : kGStack);
+    int64_t groups = (n + 63) / 64;
+    GravScratch c  = carve(scratch, groups, capM, capL);
+    unsigned grid  = unsigned((groups + kGWaves - 1) / kGWaves);
+    int cap        = testFrontCap > 0 ? min(testFrontCap, kGStack) : kGStack;
+    gravityListKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, c.S, stats, c.spillList, cap);
+    SPHX_LAUNCH_CHECK();
+}
+
+void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
+                        const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
+                        const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
+                        double* ugrav, double* out, unsigned long long* stats, void* scratch, int capM, int capL,
+                        const int64_t* poff, int32_t* pidx, void* paccBuf, hipStream_t s)
+{
+    float4* pacc = static_cast<float4*>(paccBuf);
+    int64_t n = last - first;
+    if (n <= 0) return;
+    GravTree t{child, n2l, ns, ne, centers, (const Quadrupole*)mp};
+    int64_t groups = (n + 63) / 64;
+    GravScratch c  = carve(scratch, groups, capM, capL);
+    unsigned grid  = unsigned((groups + kGWaves - 1) / kGWaves);
+    gravityExpandKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, c.S, poff, pidx);
+    SPHX_LAUNCH_CHECK();
+    // the M2P kernel (register-light, latency bound) and the MFMA P2P kernel run concurrently: P2P on a side stream
+    // forked from and joined back into s; its partials land in pacc and are added by gravityCombineKernel
+    static thread_local hipStream_t side = nullptr;
+    static thread_local hipEvent_t fork = nullptr, join = nullptr;
+    if (!side)
+    {
+        SPHX_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+        SPHX_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+        SPHX_CHECK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+    }
+#ifdef SPHX_GRAV_SERIAL
+    side = s;
+#endif
+    SPHX_CHECK(hipEventRecord(fork, s));
+    SPHX_CHECK(hipStreamWaitEvent(side, fork, 0));
+    gravityP2PKernel<<<grid, 64 * kGWaves, 0, side>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
+                                                      stats, c.S, poff, pidx, pacc);
+    SPHX_LAUNCH_CHECK();
+    SPHX_CHECK(hipEventRecord(join, side));
+    gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
+                                                   c.S);
+    SPHX_LAUNCH_CHECK();
+    SPHX_CHECK(hipStreamWaitEvent(s, join, 0));
+    gravityCombineKernel<<<gridFor(n, 256), 256, 0, s>>>(first, last, pacc, m, G, ax, ay, az, ugrav);
     SPHX_LAUNCH_CHECK();
     gravitySpillKernel<<<kGSpillWaves, 64, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
-                                                   spillList, spillMem);
+                                                   c.spillList, c.spillMem);
     SPHX_LAUNCH_CHECK();
 }
 

@@ -138,12 +138,19 @@ void gravityUpsweepLevel(int64_t a, int64_t b, const int32_t* n2l, const int32_t
                          hipStream_t s);
 void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, double invTheta, double* centers,
                    hipStream_t s);
-void computeGravity(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
-                    const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
-                    const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
-                    double* ugrav, double* out, unsigned long long* stats, void* scratch, int testFrontCap,
-                    hipStream_t s);
-size_t gravityScratchBytes(int64_t n);
+// Barnes-Hut in two phases: interaction lists (+ per-group P2P particle counts), then evaluation given the
+// exclusive scan poff (groups + 1 entries) of those counts and a pidx buffer of poff[groups] entries
+size_t gravityScratchBytes(int64_t n, int capM, int capL);
+int32_t* gravityParticleCounts(void* scratch, int64_t n, int capM, int capL);
+void computeGravityLists(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
+                         const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
+                         const double* z, unsigned long long* stats, void* scratch, int testFrontCap, int capM,
+                         int capL, hipStream_t s);
+void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
+                        const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
+                        const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
+                        double* ugrav, double* out, unsigned long long* stats, void* scratch, int capM, int capL,
+                        const int64_t* poff, int32_t* pidx, void* pacc, hipStream_t s);
 void directSum(int64_t first, int64_t last, int64_t n, const double* x, const double* y, const double* z,
                const float* h, const float* m, float G, float* ax, float* ay, float* az, double* ugrav, double* out,
                hipStream_t s);

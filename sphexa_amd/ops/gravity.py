@@ -21,6 +21,21 @@ def _stream():
 
 # test hook: >0 shrinks the LDS frontier of the GPU traversal so that groups take the global-memory spill path
 TEST_FRONT_CAP = 0
+# per-group capacities of the GPU interaction-list slabs (M2P nodes, P2P leaves); groups that need more are evaluated
+# by the fused fallback kernel and the capacities grow for the next call (test hook: set TEST_CAPS to force them)
+_CAPS = {"m": 2048, "l": 512}
+TEST_CAPS = None
+
+
+def _round64(v: int) -> int:
+    return (int(v) + 63) // 64 * 64
+
+
+def _int32_view(ptr: int, count: int, base: torch.Tensor) -> torch.Tensor:
+    """int32 tensor aliasing ``count`` elements at device address ``ptr`` inside the byte buffer ``base``"""
+    off = ptr - base.data_ptr()
+    assert off % 4 == 0 and 0 <= off and off + 4 * count <= base.numel() * base.element_size()
+    return base.view(torch.uint8)[off:off + 4 * count].view(torch.int32)
 
 
 def upsweep(tree: Octree, x, y, z, m, box: Box, theta: float, sfc_kind: int = 0):
@@ -57,19 +72,42 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
     if x.is_cuda:
         hp = _lib.hip()
         out = torch.zeros(2, dtype=torch.float64, device=x.device)
-        st_dev = torch.zeros(6, dtype=torch.int64, device=x.device)
+        st_dev = torch.zeros(8, dtype=torch.int64, device=x.device)
         from .neighbors import _scratch
 
-        scratch = _scratch(hp.gravity_scratch_bytes(last - first), x.device)
-        hp.compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
-                           tree.node_start.data_ptr(), tree.node_end.data_ptr(), centers.data_ptr(), mp.data_ptr(),
-                           x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), m.data_ptr(), float(G),
-                           ax.data_ptr(), ay.data_ptr(), az.data_ptr(), 0 if ugrav is None else ugrav.data_ptr(),
-                           out.data_ptr(), st_dev.data_ptr(), scratch.data_ptr(), TEST_FRONT_CAP, _stream())
+        cap_m, cap_l = TEST_CAPS if TEST_CAPS is not None else (_CAPS["m"], _CAPS["l"])
+        n = last - first
+        groups = (n + 63) // 64
+        scratch = _scratch(hp.gravity_scratch_bytes(n, cap_m, cap_l), x.device)
+        tree_args = (tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
+                     tree.node_end.data_ptr(), centers.data_ptr(), mp.data_ptr())
+        s = _stream()
+        # phase 1: interaction lists + per-group P2P particle counts
+        hp.gravity_lists(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), st_dev.data_ptr(),
+                         scratch.data_ptr(), TEST_FRONT_CAP, cap_m, cap_l, s)
+        pcount = _int32_view(hp.gravity_particle_counts(scratch.data_ptr(), n, cap_m, cap_l), groups, scratch)
+        poff = torch.zeros(groups + 1, dtype=torch.int64, device=x.device)
+        torch.cumsum(pcount, 0, out=poff[1:])
+        total = int(poff[-1].item())
+        pidx = torch.empty(max(total, 1), dtype=torch.int32, device=x.device)
+        pacc = torch.empty(4 * n, dtype=torch.float32, device=x.device)  # P2P partials (phi, a) per target
+        # phase 2: expand leaves to particle runs, M2P, MFMA P2P, fused fallback for overflowing groups
+        hp.gravity_eval(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
+                        m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
+                        0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), st_dev.data_ptr(),
+                        scratch.data_ptr(), cap_m, cap_l, poff.data_ptr(), pidx.data_ptr(), pacc.data_ptr(), s)
         st = st_dev.cpu()
+        if TEST_CAPS is None and int(st[5]) > 0:
+            # groups fell back to the (slow, serial) fused kernel: grow the slabs to the observed demand while the
+            # slab memory stays below ~6% of the device (it is 4 B x groups x (capM + capL))
+            budget = torch.cuda.get_device_properties(x.device).total_memory // 16
+            cm = min(max(_CAPS["m"], _round64(1.25 * int(st[7]))), 16384)
+            cl = min(max(_CAPS["l"], _round64(1.25 * int(st[6]))), 8192)
+            if 4 * groups * (cm + cl) <= budget:
+                _CAPS["m"], _CAPS["l"] = cm, cl
         if stats is not None:
             stats.update(p2p=int(st[0]), m2p=int(st[2]), max_p2p=int(st[3]), max_m2p=int(st[4]),
-                         spilled=int(st[5]))
+                         fallback=int(st[5]), caps=(cap_m, cap_l))
         if int(st[1]) > 0:
             raise RuntimeError(f"gravity traversal stack overflow in {int(st[1])} groups")
         return float(out[0].item())

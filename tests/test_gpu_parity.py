@@ -197,7 +197,10 @@ def test_neighbor_spill_path(gpu, monkeypatch):
     assert neighbor_lists_as_sets(nl, dg["nc"]) == sets_ref
 
 
-def test_gravity_spill_path(gpu, monkeypatch):
+@pytest.mark.parametrize("hook", ["front", "caps"])
+def test_gravity_spill_path(gpu, monkeypatch, hook):
+    """groups overflowing the LDS stack (front) or the interaction-list slabs (caps) are evaluated by the fused
+    global-stack kernel: same interactions, results equal to fp32 summation-order differences"""
     from sphexa_amd.ops import gravity as G
     from test_gravity import _setup as gsetup
 
@@ -205,12 +208,17 @@ def test_gravity_spill_path(gpu, monkeypatch):
     box, ot, x, y, z, m, h = gsetup(n, gpu)
     c, mp = G.upsweep(ot, x, y, z, m, box, 0.5)
     acc = [torch.zeros(n, dtype=torch.float32, device=gpu) for _ in range(3)]
-    e_ref = G.compute_gravity(ot, c, mp, 0, n, x, y, z, h, m, 1.0, *acc)
-    monkeypatch.setattr(G, "TEST_FRONT_CAP", 16)
+    st_ref = {}
+    e_ref = G.compute_gravity(ot, c, mp, 0, n, x, y, z, h, m, 1.0, *acc, stats=st_ref)
+    if hook == "front":
+        monkeypatch.setattr(G, "TEST_FRONT_CAP", 16)
+    else:
+        monkeypatch.setattr(G, "TEST_CAPS", (256, 64))
     acc2 = [torch.zeros(n, dtype=torch.float32, device=gpu) for _ in range(3)]
     st = {}
     e2 = G.compute_gravity(ot, c, mp, 0, n, x, y, z, h, m, 1.0, *acc2, stats=st)
-    assert st["spilled"] > 0
+    assert st["fallback"] > st_ref["fallback"]
+    assert st["p2p"] == st_ref["p2p"] and st["m2p"] == st_ref["m2p"]
     for a, b in zip(acc, acc2):
-        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
-    assert abs(e2 - e_ref) < 1e-6 * abs(e_ref)
+        assert float((a - b).abs().max()) < 1e-4 * float(a.abs().max())
+    assert abs(e2 - e_ref) < 1e-5 * abs(e_ref)
