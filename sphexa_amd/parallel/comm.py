@@ -7,7 +7,8 @@ Replaces the reference's MPI layer (domain/include/cstone/primitives/mpi_wrapper
   * MPI_Allreduce(MIN/SUM/MAX) on host scalars    -> ``allreduce`` on device tensors (no host staging)
   * tag/epoch protocol                            -> not needed: collectives are stream ordered and issued in the
                                                      same order on every rank
-World size 1 short-circuits every call.
+World size 1 short-circuits every call. With the gloo backend, device tensors are staged through host memory (gloo has
+no all-to-all for device tensors): this lets several ranks share one GPU in tests of the multi-rank GPU path.
 """
 
 from __future__ import annotations
@@ -32,10 +33,18 @@ class Comm:
         else:
             self.rank, self.size, self.backend = 0, 1, None
 
+    def _staged(self, t: torch.Tensor) -> bool:
+        return self.backend == "gloo" and t.is_cuda
+
     # -------------------------------------------------------------------------------------------- collectives
     def allreduce(self, t: torch.Tensor, op: str = SUM) -> torch.Tensor:
         if self.size > 1:
-            dist.all_reduce(t, op=_OPS[op], group=self.group)
+            if self._staged(t):
+                h = t.cpu()
+                dist.all_reduce(h, op=_OPS[op], group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=_OPS[op], group=self.group)
         return t
 
     def allreduce_scalar(self, v: float, op: str = SUM, device=None, dtype=torch.float64) -> float:
@@ -72,15 +81,19 @@ class Comm:
         if recv_counts is None:
             recv_counts = self.exchange_counts(send_counts)
         shape = (sum(recv_counts),) + tuple(send.shape[1:])
-        recv = torch.empty(shape, dtype=send.dtype, device=send.device)
-        dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=list(recv_counts),
+        staged = self._staged(send)
+        src = send.contiguous().cpu() if staged else send.contiguous()
+        recv = torch.empty(shape, dtype=send.dtype, device=src.device)
+        dist.all_to_all_single(recv, src, output_split_sizes=list(recv_counts),
                                input_split_sizes=list(send_counts), group=self.group)
-        return recv, list(recv_counts)
+        return (recv.to(send.device) if staged else recv), list(recv_counts)
 
     def allgather_var(self, t: torch.Tensor) -> List[torch.Tensor]:
         """gather tensors of different first-dimension sizes from all ranks"""
         if self.size == 1:
             return [t]
+        if self._staged(t):
+            return [o.to(t.device) for o in Comm.allgather_var(self, t.cpu())]
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
         ns = [torch.empty_like(n) for _ in range(self.size)]
         dist.all_gather(ns, n, group=self.group)
