@@ -28,6 +28,7 @@ struct NbrArgs
     const int32_t* nidx;
     const int32_t* nc;
     unsigned ngmax;
+    unsigned ntot = 0; // number of source records (set by the launchers; clamps the cooperative gathers)
 };
 
 struct PosArgs

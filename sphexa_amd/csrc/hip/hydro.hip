@@ -25,17 +25,45 @@ namespace sphx::hip
 
 constexpr int kBlock = 256;
 
+/*! @brief target of this thread and its neighbor list. Threads past the last target stay alive with an empty list
+ *         and a clamped index (the cooperative gathers need all 64 lanes of a wave); they store nothing.
+ */
 __device__ __forceinline__ bool targetOf(const NbrArgs& a, int64_t& i, const int32_t*& nbr, unsigned& n)
 {
     unsigned lb = xcdRemap(blockIdx.x, gridDim.x);
     int64_t t   = int64_t(lb) * kBlock + threadIdx.x;
     i           = a.first + t;
-    if (i >= a.last) return false;
-    int64_t g = t >> 6;
-    nbr       = a.nidx + g * int64_t(a.ngmax) * 64 + (t & 63);
-    int cnt   = a.nc[i] - 1;
-    n         = unsigned(cnt < 0 ? 0 : (unsigned(cnt) < a.ngmax ? cnt : a.ngmax));
+    int64_t g   = t >> 6;
+    nbr         = a.nidx + g * int64_t(a.ngmax) * 64 + (t & 63);
+    if (i >= a.last)
+    {
+        i = a.last - 1;
+        n = 0;
+        return false;
+    }
+    int cnt = a.nc[i] - 1;
+    n       = unsigned(cnt < 0 ? 0 : (unsigned(cnt) < a.ngmax ? cnt : a.ngmax));
     return true;
+}
+
+//! @brief per-wave LDS tile of the cooperative gathers (CoopLoader) for records of type R
+template<class R>
+__device__ __forceinline__ float4* waveTile(float4* blockTile)
+{
+    return blockTile + (threadIdx.x >> 6) * 64 * CoopLoader<R>::S;
+}
+
+template<class R>
+__device__ __forceinline__ CoopLoader<R> coopOf(const R* rec, float4* blockTile, int64_t self, const NbrArgs& a)
+{
+    return CoopLoader<R>{rec, waveTile<R>(blockTile), unsigned(self), a.ntot - 1};
+}
+
+//! @brief the launchers' view of the neighbor arguments with the record count set
+inline NbrArgs withTot(NbrArgs a, int64_t ntot)
+{
+    a.ntot = unsigned(ntot);
+    return a;
 }
 
 inline unsigned gridT(const NbrArgs& a) { return gridFor(a.last - a.first, kBlock); }
@@ -147,11 +175,14 @@ __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, B
                                                       const SrcPos* __restrict__ rec, const float* __restrict__ wh,
                                                       float* __restrict__ xm)
 {
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcPos>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
-    if (!targetOf(a, i, nbr, n)) return;
-    xm[i] = xmassJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcPos>{rec}, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice});
+    const bool valid = targetOf(a, i, nbr, n);
+    float v = xmassJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], coopOf(rec, tile, i, a),
+                         KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice});
+    if (valid) xm[i] = v;
 }
 
 __global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts sc, Box box,
@@ -159,12 +190,15 @@ __global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts 
                                                            const float* __restrict__ wh, const float* __restrict__ whd,
                                                            float* __restrict__ kx, float* __restrict__ gradh)
 {
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcPos>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
-    if (!targetOf(a, i, nbr, n)) return;
+    const bool valid = targetOf(a, i, nbr, n);
     float k, g;
-    veDefGradhJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcPos>{rec}, KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice}, k, g);
+    veDefGradhJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], coopOf(rec, tile, i, a),
+                    KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice}, k, g);
+    if (!valid) return;
     kx[i]    = k;
     gradh[i] = g;
 }
@@ -208,12 +242,15 @@ __global__ __launch_bounds__(kBlock) void iadKernel(NbrArgs a, SphConsts sc, Box
                                                     const SrcIad* __restrict__ rec, const float* __restrict__ wh,
                                                     Six cij)
 {
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcIad>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
-    if (!targetOf(a, i, nbr, n)) return;
+    const bool valid = targetOf(a, i, nbr, n);
     float c[6];
-    iadJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], RecLoader<SrcIad>{rec}, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c);
+    iadJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], coopOf(rec, tile, i, a),
+             KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c);
+    if (!valid) return;
     for (int k = 0; k < 6; ++k)
         cij.p[k][i] = c[k];
 }
@@ -227,13 +264,15 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConst
                                                              float* __restrict__ divv, float* __restrict__ curlv,
                                                              Six dV, int doGrad)
 {
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcIad>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
-    if (!targetOf(a, i, nbr, n)) return;
-    RecLoader<SrcIad> ld{rec};
+    const bool valid = targetOf(a, i, nbr, n);
     float c[6], g[6], dvi, cvi;
-    iadDivvCurlvJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], kx[i], ld, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, doGrad ? g : nullptr);
+    iadDivvCurlvJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], kx[i], coopOf(rec, tile, i, a),
+                      KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, doGrad ? g : nullptr);
+    if (!valid) return;
     for (int k = 0; k < 6; ++k)
         cij.p[k][i] = c[k];
     divv[i]  = dvi;
@@ -249,13 +288,16 @@ __global__ __launch_bounds__(kBlock) void avSwitchesKernel(NbrArgs a, SphConsts 
                                                            const float* __restrict__ wh, double dt,
                                                            float* __restrict__ alpha)
 {
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcIad>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
-    if (!targetOf(a, i, nbr, n)) return;
+    const bool valid = targetOf(a, i, nbr, n);
     float ci[6] = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
-    alpha[i]    = avSwitchesJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], ci, RecLoader<SrcIad>{rec}, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt,
-                                  sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
+    float al    = avSwitchesJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], ci, coopOf(rec, tile, i, a),
+                                  KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt, sc.alphamin, sc.alphamax,
+                                  sc.decayConstant, alpha[i]);
+    if (valid) alpha[i] = al;
 }
 
 //! @brief block min of the Courant time step, then one atomic per block
@@ -295,17 +337,18 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphC
                                                                  float* __restrict__ az, double* __restrict__ du,
                                                                  float* __restrict__ minDt)
 {
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcMom>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
     bool valid = targetOf(a, i, nbr, n);
     float dti  = FLT_MAX;
+    float mvs, axi, ayi, azi;
+    double dui;
+    momentumEnergyJLoop<avClean>(unsigned(i), sc, box, nbr, 64, n, coopOf(rec, tile, i, a), GradVLoader{gv},
+                                 KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui, mvs);
     if (valid)
     {
-        float mvs, axi, ayi, azi;
-        double dui;
-        momentumEnergyJLoop<avClean>(unsigned(i), sc, box, nbr, 64, n, RecLoader<SrcMom>{rec}, GradVLoader{gv}, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice},
-                                     axi, ayi, azi, dui, mvs);
         ax[i] = axi;
         ay[i] = ayi;
         az[i] = azi;
@@ -323,17 +366,18 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyStdKernel(NbrArgs a, Sph
                                                                   float* __restrict__ az, double* __restrict__ du,
                                                                   float* __restrict__ minDt)
 {
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcStd>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
     bool valid = targetOf(a, i, nbr, n);
     float dti  = FLT_MAX;
+    float mvs, axi, ayi, azi;
+    double dui;
+    momentumEnergyStdJLoop(unsigned(i), sc.K, box, nbr, 64, n, coopOf(rec, tile, i, a),
+                           KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui, mvs);
     if (valid)
     {
-        float mvs, axi, ayi, azi;
-        double dui;
-        momentumEnergyStdJLoop(unsigned(i), sc.K, box, nbr, 64, n, RecLoader<SrcStd>{rec}, KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui,
-                               mvs);
         ax[i] = axi;
         ay[i] = ayi;
         az[i] = azi;
@@ -454,7 +498,7 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
 {
     if (a.last <= a.first) return;
     packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, nullptr, (SrcPos*)rec);
-    xmassKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, h, (const SrcPos*)rec, wh, xm);
+    xmassKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcPos*)rec, wh, xm);
     SPHX_LAUNCH_CHECK();
 }
 
@@ -464,7 +508,7 @@ void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
 {
     if (a.last <= a.first) return;
     packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, xm, (SrcPos*)rec);
-    veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, h, (const SrcPos*)rec, wh, whd, kx, gradh);
+    veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcPos*)rec, wh, whd, kx, gradh);
     SPHX_LAUNCH_CHECK();
 }
 
@@ -494,7 +538,7 @@ void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, co
     Six c;
     for (int k = 0; k < 6; ++k)
         c.p[k] = cij[k];
-    iadKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, h, (const SrcIad*)rec, wh, c);
+    iadKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcIad*)rec, wh, c);
     SPHX_LAUNCH_CHECK();
 }
 
@@ -512,7 +556,7 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
         c.p[k] = cij[k];
         g.p[k] = dV[k];
     }
-    iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, h, kx, (const SrcIad*)rec, wh, c, divv, curlv, g,
+    iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, kx, (const SrcIad*)rec, wh, c, divv, curlv, g,
                                                    dV[0] != nullptr);
     SPHX_LAUNCH_CHECK();
 }
@@ -527,7 +571,7 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
     Six cc;
     for (int k = 0; k < 6; ++k)
         cc.p[k] = cij[k];
-    avSwitchesKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, h, cc, (const SrcIad*)rec, wh, dt, alpha);
+    avSwitchesKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, cc, (const SrcIad*)rec, wh, dt, alpha);
     SPHX_LAUNCH_CHECK();
 }
 
@@ -540,10 +584,10 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
     packMomKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, (SrcMom*)rec, gv);
     if (avClean)
         momentumEnergyVeKernel<true>
-            <<<gridT(a), kBlock, 0, s>>>(a, sc, box, (const SrcMom*)rec, gv, wh, ax, ay, az, du, minDt);
+            <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, (const SrcMom*)rec, gv, wh, ax, ay, az, du, minDt);
     else
         momentumEnergyVeKernel<false>
-            <<<gridT(a), kBlock, 0, s>>>(a, sc, box, (const SrcMom*)rec, nullptr, wh, ax, ay, az, du, minDt);
+            <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, (const SrcMom*)rec, nullptr, wh, ax, ay, az, du, minDt);
     SPHX_LAUNCH_CHECK();
 }
 
@@ -553,7 +597,7 @@ void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, in
 {
     if (a.last <= a.first) return;
     packStdKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, (SrcStd*)rec);
-    momentumEnergyStdKernel<<<gridT(a), kBlock, 0, s>>>(a, sc, box, (const SrcStd*)rec, wh, ax, ay, az, du, minDt);
+    momentumEnergyStdKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, (const SrcStd*)rec, wh, ax, ay, az, du, minDt);
     SPHX_LAUNCH_CHECK();
 }
 

@@ -308,6 +308,181 @@ SPHX_HD void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const Ld& 
     }
 }
 
+#ifndef SPHX_COOP_MIN_CHUNKS
+#define SPHX_COOP_MIN_CHUNKS 3 // records of fewer 16-byte chunks use per-lane gathers (A/B measured, profiles/)
+#endif
+
+#if defined(__HIPCC__)
+/*! @brief record loader of the gfx950 pair loops: cooperative, cache-line-coalesced gathers staged through LDS.
+ *
+ * At neighbor step k every lane needs the C x 16-byte record of its own neighbor j. Loading it directly costs C
+ * wave-wide gathers in which all 64 lanes touch different cache lines (64 L1 tag lookups per instruction, the
+ * bottleneck of the pair loops). Here the wave loads the 64 records as 64*C consecutive 16-byte chunks: in
+ * instruction q lane l fetches chunk p of record r, q*64 + l = r*C + p, so a record's chunks come from adjacent lanes
+ * and one instruction touches ~64/C records' lines instead of 64. The chunks are written to a per-wave LDS tile
+ * (record stride C|1 float4: conflict-free 16-lane groups) and every lane reads back its own record. The
+ * neighbor index of record r comes from lane r (ds_bpermute). Indices are read two steps ahead and the gathers of
+ * step k+1 are in flight while step k is evaluated. Lanes past their own neighbor count fetch @p self (valid
+ * address) and skip the evaluation; all 64 lanes must call the loop (uniform trip count = wave max of nc).
+ */
+template<class R>
+struct CoopLoader
+{
+    const R* r;
+    float4* tile; // 64 * (C | 1) float4 of LDS per wave
+    unsigned self;
+    unsigned last; // highest valid record index (clamps the indices of finished lanes' slots)
+    static constexpr int C = int(sizeof(R) / 16);
+    static constexpr int S = C | 1;
+    static_assert(sizeof(R) % 16 == 0, "records are whole float4s");
+
+    __device__ R operator()(unsigned j) const { return r[j]; }
+
+    //! @brief index of the record whose chunk this lane fetches in instruction q of step k: read straight from the
+    //!        lane-interleaved list (the 64 indices of a step are one 256-byte segment), clamped for finished lanes
+    template<class Idx>
+    __device__ __forceinline__ unsigned index(const Idx* nbr, int stride, unsigned k, int q) const
+    {
+        const int lane = threadIdx.x & 63;
+        const int rr   = (q * 64 + lane) / C;
+        return min(unsigned(nbr[int(k) * stride + (rr - lane)]), last);
+    }
+
+    //! @brief index of the record whose chunk this lane fetches in instruction q, from the owning lane's index j
+    __device__ __forceinline__ unsigned spread(unsigned j, int q) const
+    {
+        const int rr = (q * 64 + int(threadIdx.x & 63)) / C;
+        return unsigned(__shfl(int(j), rr));
+    }
+
+    //! @brief chunk q of the cooperative gather: this lane's 16 bytes of record rr = (q*64 + lane) / C
+    __device__ __forceinline__ float4 issue(unsigned jr, int q) const
+    {
+        const int c  = q * 64 + (threadIdx.x & 63);
+        const int rr = c / C;
+        return reinterpret_cast<const float4*>(r)[size_t(jr) * C + (c - rr * C)];
+    }
+
+    __device__ __forceinline__ void stage(float4 v, int q) const
+    {
+        const int c  = q * 64 + (threadIdx.x & 63);
+        const int rr = c / C;
+        tile[rr * S + (c - rr * C)] = v;
+    }
+
+    __device__ __forceinline__ float4 own(int p) const { return tile[(threadIdx.x & 63) * S + p]; }
+};
+
+template<int B, class Idx, class R, class F>
+__device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const CoopLoader<R>& ld, F&& f)
+{
+    constexpr int C = CoopLoader<R>::C;
+#ifdef SPHX_NO_COOP
+    constexpr bool direct = true; // A/B switch: per-lane record gathers everywhere
+#else
+    constexpr bool direct = C < SPHX_COOP_MIN_CHUNKS;
+#endif
+    if constexpr (direct)
+    {
+        // small records: per-lane gathers, B in flight (measured faster than the cooperative path for 32 B)
+        unsigned k = 0;
+        for (; k + B <= nc; k += B)
+        {
+            unsigned j[B];
+            R rr[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                j[u] = unsigned(nbr[(k + u) * stride]);
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                rr[u] = ld(j[u]);
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                f(j[u], rr[u]);
+        }
+        for (; k < nc; ++k)
+        {
+            unsigned j = unsigned(nbr[k * stride]);
+            f(j, ld(j));
+        }
+        return;
+    }
+    unsigned ncMax  = nc;
+    for (int o = 32; o > 0; o >>= 1)
+        ncMax = max(ncMax, unsigned(__shfl_xor(int(ncMax), o)));
+    ncMax = __builtin_amdgcn_readfirstlane(ncMax);
+    if (ncMax == 0) return;
+#ifdef SPHX_COOP_LIST_INDEX
+    // per chunk-instruction record indices read from the list two steps ahead (C index loads per step)
+    unsigned iN[C], iNN[C];
+    float4 rawC[C], rawN[C], o[C];
+#pragma unroll
+    for (int q = 0; q < C; ++q)
+    {
+        rawC[q] = ld.issue(ld.index(nbr, stride, 0, q), q);
+        iN[q]   = ld.index(nbr, stride, 1, q);
+    }
+    unsigned jC = 0 < nc ? unsigned(nbr[0]) : ld.self;
+    for (unsigned k = 0; k < ncMax; ++k)
+    {
+        const unsigned jN = k + 1 < nc ? unsigned(nbr[(k + 1) * stride]) : ld.self;
+#pragma unroll
+        for (int q = 0; q < C; ++q)
+        {
+            iNN[q]  = ld.index(nbr, stride, k + 2, q); // reads stay inside the list allocation (+ 2 rows)
+            rawN[q] = ld.issue(iN[q], q);
+        }
+#else
+    // own neighbor index read three steps ahead (one coalesced load per step), spread to the chunk lanes with
+    // ds_bpermute two steps ahead, chunk data gathered one step ahead of the evaluation
+    unsigned iN[C], iNN[C];
+    float4 rawC[C], rawN[C], o[C];
+    const unsigned j0 = 0 < nc ? unsigned(nbr[0]) : ld.self;
+    const unsigned j1 = 1 < nc ? unsigned(nbr[stride]) : ld.self;
+    unsigned jNN      = 2 < nc ? unsigned(nbr[2 * stride]) : ld.self;
+#pragma unroll
+    for (int q = 0; q < C; ++q)
+    {
+        rawC[q] = ld.issue(ld.spread(j0, q), q);
+        iN[q]   = ld.spread(j1, q);
+    }
+    unsigned jC = j0, jN = j1;
+    for (unsigned k = 0; k < ncMax; ++k)
+    {
+        const unsigned jNNN = k + 3 < nc ? unsigned(nbr[(k + 3) * stride]) : ld.self;
+#pragma unroll
+        for (int q = 0; q < C; ++q)
+        {
+            iNN[q]  = ld.spread(jNN, q);
+            rawN[q] = ld.issue(iN[q], q);
+        }
+#endif
+#pragma unroll
+        for (int q = 0; q < C; ++q)
+            ld.stage(rawC[q], q);
+#pragma unroll
+        for (int p = 0; p < C; ++p)
+            o[p] = ld.own(p);
+        R rec;
+        __builtin_memcpy(&rec, o, sizeof(R));
+        if (k < nc) f(jC, rec);
+#pragma unroll
+        for (int q = 0; q < C; ++q)
+        {
+            rawC[q] = rawN[q];
+            iN[q]   = iNN[q];
+        }
+        jC = jN;
+#ifdef SPHX_COOP_LIST_INDEX
+    }
+#else
+        jN  = jNN;
+        jNN = jNNN;
+    }
+#endif
+}
+#endif
+
 //! @brief xm_i = m_i / rho0_i, rho0_i = K h^-3 sum_j W_ij m_j including self (reference xmass_kern.hpp)
 template<class Idx, class Ld>
 SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,

@@ -71,7 +71,8 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
     if x.is_cuda:
         hp = _lib.hip()
         num_groups = (n + GROUP - 1) // GROUP
-        need = max(num_groups, 1) * GROUP * ngmax
+        # + 2 rows: the cooperative gathers of the pair loops read the index rows two steps ahead
+        need = max(num_groups, 1) * GROUP * ngmax + 2 * GROUP
         if nidx is None or nidx.numel() < need:
             nidx = torch.empty(need, dtype=torch.int32, device=x.device)
         stats = torch.zeros(4, dtype=torch.int64, device=x.device)
