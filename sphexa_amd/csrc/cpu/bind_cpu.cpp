@@ -16,6 +16,8 @@ using namespace sphx;
 
 namespace sphx::cpu
 {
+void bindTreeUtil(py::module& m);
+void bindGravityExtra(py::module& m);
 int64_t findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                       const TreeView& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, uint32_t* nc,
                       bool iterateH);
@@ -122,6 +124,8 @@ std::array<float*, 6> six(const std::array<Ptr, 6>& a)
 PYBIND11_MODULE(_sphx_cpu, m)
 {
     m.doc() = "sphexa_amd OpenMP reference path";
+    cpu::bindTreeUtil(m);
+    cpu::bindGravityExtra(m);
 
     m.def("num_threads", []() { return omp_get_max_threads(); });
 

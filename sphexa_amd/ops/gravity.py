@@ -182,3 +182,47 @@ def m2p_flat(first: int, last: int, x, y, z, m, mcenters: torch.Tensor, mquads: 
     return float(_lib.cpu().m2p_flat(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), m.data_ptr(), M,
                                      mc.data_ptr(), mq.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(),
                                      az.data_ptr(), 0 if ugrav is None else ugrav.data_ptr()))
+
+
+def compute_gravity_ewald(tree: Octree, centers, mp, first: int, last: int, x, y, z, h, m, G: float, box: Box,
+                          ax, ay, az, shells: int = 1, ugrav=None) -> float:
+    """periodic self-gravity (cubic box): Barnes-Hut over the central box and ``shells`` of replicas plus the Ewald
+    lattice sum of the root multipole for all farther images (reference nbody/traversal_ewald_cpu.hpp, CPU-only
+    there as well). Device tensors are evaluated through host copies. Adds G * a to ax, ay, az."""
+    L = box.hi[0] - box.lo[0]
+    if any(abs((box.hi[d] - box.lo[d]) - L) > 1e-12 * L for d in range(3)):
+        raise ValueError("Ewald gravity needs a cubic box")
+    dev = x.device
+    host = [t.cpu() if t is not None else None for t in (x, y, z, h, m, ax, ay, az, ugrav)]
+    hx, hy, hz, hh, hm, hax, hay, haz, hu = host
+    args = [tree.child_offsets.cpu(), tree.node_to_leaf.cpu(), tree.node_start.cpu(), tree.node_end.cpu(),
+            centers.cpu(), mp.cpu()]
+    e = _lib.cpu().compute_gravity_ewald(first, last, *[a.data_ptr() for a in args], hx.data_ptr(), hy.data_ptr(),
+                                         hz.data_ptr(), hh.data_ptr(), hm.data_ptr(), float(G), float(L), int(shells),
+                                         hax.data_ptr(), hay.data_ptr(), haz.data_ptr(),
+                                         0 if hu is None else hu.data_ptr())
+    if dev.type != "cpu":
+        for dst, src in ((ax, hax), (ay, hay), (az, haz), (ugrav, hu)):
+            if dst is not None:
+                dst.copy_(src)
+    return float(e)
+
+
+def direct_ewald(x, y, z, m, G: float, L: float):
+    """O(N^2) Ewald sum (fp64, unsoftened) of all particles: (ax, ay, az) float64 tensors and 0.5 G sum m phi"""
+    x, y, z, m = (t.cpu().contiguous() for t in (x, y, z, m))
+    n = x.numel()
+    out = [torch.zeros(n, dtype=torch.float64) for _ in range(3)]
+    e = _lib.cpu().direct_ewald(n, x.data_ptr(), y.data_ptr(), z.data_ptr(), m.data_ptr(), float(G), float(L),
+                                *[o.data_ptr() for o in out])
+    return out, float(e)
+
+
+def direct_sum_kahan(x, y, z, h, m):
+    """O(N^2) softened accelerations accumulated in fp32 with Kahan compensation (CPU)"""
+    x, y, z, h, m = (t.cpu().contiguous() for t in (x, y, z, h, m))
+    n = x.numel()
+    out = [torch.zeros(n, dtype=torch.float32) for _ in range(3)]
+    _lib.cpu().direct_sum_kahan(n, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), m.data_ptr(),
+                                *[o.data_ptr() for o in out])
+    return out

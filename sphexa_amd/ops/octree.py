@@ -189,3 +189,45 @@ def _build_octree_hip(tree, counts, keys, x, y, z, offset) -> Octree:
     return Octree(tree=tree, counts=counts, num_nodes=N, num_leaves=L, prefixes=codes_s, child_offsets=child,
                   parents=parents, node_to_leaf=vals_s, leaf_to_node=leaf_to_node, level_range=lr, node_start=ns,
                   node_end=ne, center=center, half=half, offset=offset)
+
+
+# ------------------------------------------------------------------------------------------ tree utilities
+# (reference tree/btree.hpp, tree/cs_util.hpp, tree/continuum.hpp, traversal/peers.hpp; native: cpu/tree_util_cpu.cpp)
+
+def _np_keys(tree) -> np.ndarray:
+    if isinstance(tree, torch.Tensor):
+        tree = tree.cpu().numpy()
+    return np.ascontiguousarray(np.asarray(tree).view(np.uint64) if np.asarray(tree).dtype == np.int64
+                                else np.asarray(tree, dtype=np.uint64))
+
+
+def binary_radix_tree(leaf_keys) -> dict:
+    """Karras binary radix tree over sorted unique keys: dict of left/right children (>= 0 internal, < 0 leaf ~idx),
+    first/last leaf of every internal node and its common-prefix length in bits"""
+    return _lib.cpu().binary_radix_tree(_np_keys(leaf_keys))
+
+
+def check_invariants(tree) -> str:
+    """'' if ``tree`` is a valid cornerstone leaf array, else the first violated invariant"""
+    return _lib.cpu().check_invariants(_np_keys(tree))
+
+
+def uniform_tree(level: int) -> np.ndarray:
+    """cornerstone leaf array with all 8^level leaves at ``level`` (reference makeUniformNLevelTree)"""
+    return _lib.cpu().uniform_tree(int(level))
+
+
+def continuum_tree(n: float, bucket: int, lo=(0.0, 0.0, 0.0), hi=(1.0, 1.0, 1.0), gaussian=None,
+                   max_iter: int = 32) -> np.ndarray:
+    """cornerstone tree for ``n`` particles distributed with a continuous density (uniform, or ``gaussian`` =
+    (center[3], sigma)) in the box, leaves holding at most ``bucket`` particles (reference computeContinuumCsarray)"""
+    kind, c, sigma = (0, (0.0, 0.0, 0.0), 1.0) if gaussian is None else (1, tuple(gaussian[0]), float(gaussian[1]))
+    return _lib.cpu().continuum_tree(kind, list(c), sigma, float(n), int(bucket), list(lo) + list(hi), max_iter)
+
+
+def find_peers(global_tree, assignment, rank: int, box, sfc_kind: int, theta: float) -> List[int]:
+    """ranks owning global-tree leaves that fail the mutual minimum-distance MAC against ``rank``'s leaves
+    (``assignment``: leaf-index boundaries per rank, length ranks + 1)"""
+    bc = [int(b) for b in box.bc]
+    return _lib.cpu().find_peers(_np_keys(global_tree), np.asarray(assignment, dtype=np.int64), int(rank),
+                                 list(box.lo) + list(box.hi), bc, int(sfc_kind), float(theta))
