@@ -299,6 +299,21 @@ PYBIND11_MODULE(_sphx_hip, m)
                                 P<float>(ax), P<float>(ay), P<float>(az), P<double>(du), P<float>(minDt), St(s));
           });
     // ---------------------------------------------------------------------------------------------- gravity
+    // ---------------------------------------------------------------------------------------------- cooling
+    m.def("cool_particles", [](int64_t first, int64_t last, double dt, Ptr rho, Ptr u, Ptr du,
+                               const std::array<double, 7>& a, Ptr s)
+          {
+              coolParticles(first, last, dt, P<float>(rho), P<double>(u), P<double>(du),
+                            CoolingParams{a[0], a[1], a[2], a[3], a[4], a[5], a[6]}, St(s));
+          });
+    m.def("cooling_timestep", [](int64_t first, int64_t last, Ptr rho, Ptr u, const std::array<double, 7>& a,
+                                 Ptr out, Ptr s)
+          {
+              coolingTimestep(first, last, P<float>(rho), P<double>(u),
+                              CoolingParams{a[0], a[1], a[2], a[3], a[4], a[5], a[6]}, P<double>(out), St(s));
+          });
+    m.def("cooling_eos", [](int64_t first, int64_t last, double gamma, Ptr rho, Ptr u, Ptr pr, Ptr c, Ptr s)
+          { coolingEos(first, last, gamma, P<float>(rho), P<double>(u), P<float>(pr), P<float>(c), St(s)); });
     m.def("gravity_leaves", [](Ptr n2l, int64_t N, Ptr ns, Ptr ne, Ptr x, Ptr y, Ptr z, Ptr mm, Ptr centers, Ptr mp,
                                Ptr s)
           {

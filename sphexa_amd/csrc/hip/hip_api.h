@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include "sphx/box.hpp"
+#include "sphx/cooling.hpp"
 #include "sphx/sph_math.hpp"
 
 namespace sphx::hip
@@ -131,6 +132,14 @@ void updateH(int64_t first, int64_t last, unsigned ng0, const int32_t* nc, float
 void conservedQuantities(int64_t first, int64_t last, const double* x, const double* y, const double* z,
                          const float* vx, const float* vy, const float* vz, const float* m, const double* temp,
                          const double* u, const int32_t* nc, double cv, double* out, hipStream_t s);
+
+// cooling.hip (physics: sphx/cooling.hpp); coolingTimestep min-reduces into *out (initialize to 1e300)
+void coolParticles(int64_t first, int64_t last, double dt, const float* rho, const double* u, double* du,
+                   const CoolingParams& p, hipStream_t s);
+void coolingTimestep(int64_t first, int64_t last, const float* rho, const double* u, const CoolingParams& p,
+                     double* out, hipStream_t s);
+void coolingEos(int64_t first, int64_t last, double gamma, const float* rho, const double* u, float* pr, float* c,
+                hipStream_t s);
 
 // gravity.hip
 void gravityLeaves(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,

@@ -56,5 +56,7 @@ def initializer_factory(init: str, glass: str | None = None):
 
         return GreshoChan(glass, settings)
     if name == "evrard-cooling":
-        raise RuntimeError("--init evrard-cooling requires the Grackle chemistry library, not available here")
+        from .cases import EvrardGlassSphereCooling
+
+        return EvrardGlassSphereCooling(glass, settings)
     raise ValueError(f"unknown initial condition: {name}")

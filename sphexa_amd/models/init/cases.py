@@ -131,6 +131,24 @@ class EvrardGlassSphere(SimInitializer):
         return Box.cube(-r, r, OPEN)
 
 
+class EvrardGlassSphereCooling(EvrardGlassSphere):
+    """Evrard collapse with radiative cooling (reference evrard_cooling_init.hpp:41-88): u = u0 everywhere and the
+    cooling units / switches as ``cooling::*`` settings (use with ``--prop std-cooling``)"""
+
+    def __init__(self, glass=None, settings_file=None):
+        from ..cooling import cooling_constants
+
+        super().__init__(glass, None)
+        c = dict(evrard_constants())
+        c.update(cooling_constants())
+        self.settings = build_settings(c, settings_file)
+
+    def init(self, rank, num_ranks, n, d):
+        box = super().init(rank, num_ranks, n, d)
+        d.fill_if_allocated("u", self.settings["u0"])
+        return box
+
+
 # ------------------------------------------------------------------------------------------- isobaric cube
 def isobaric_cube_constants():
     return {"r": 0.25, "rDelta": 0.25, "dim": 3, "gamma": 5.0 / 3.0, "rhoExt": 1.0, "rhoInt": 8.0, "pIsobaric": 2.5,

@@ -287,6 +287,7 @@ def propagator_factory(name: str, av_clean: bool, out, rank: int, quiet: bool = 
             raise RuntimeError("--prop turbulence needs the turbulence settings (use --init turbulence)")
         return TurbVeProp(out, rank, av_clean, quiet, settings)
     if name == "std-cooling":
-        raise RuntimeError("--prop std-cooling requires the Grackle chemistry library, which is not available in "
-                           "this build")
+        from .cooling import HydroCoolingProp
+
+        return HydroCoolingProp(out, rank, quiet, settings)
     raise ValueError(f"Unknown propagator choice: {name}")
