@@ -19,6 +19,7 @@ namespace sphx::cpu
 void bindTreeUtil(py::module& m);
 void bindGravityExtra(py::module& m);
 void bindCooling(py::module& m);
+void bindMultipole(py::module& m);
 int64_t findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                       const TreeView& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, uint32_t* nc,
                       bool iterateH);
@@ -128,6 +129,7 @@ PYBIND11_MODULE(_sphx_cpu, m)
     cpu::bindTreeUtil(m);
     cpu::bindGravityExtra(m);
     cpu::bindCooling(m);
+    cpu::bindMultipole(m);
 
     m.def("num_threads", []() { return omp_get_max_threads(); });
 

@@ -299,6 +299,23 @@ PYBIND11_MODULE(_sphx_hip, m)
                                 P<float>(ax), P<float>(ay), P<float>(az), P<double>(du), P<float>(minDt), St(s));
           });
     // ---------------------------------------------------------------------------------------------- gravity
+    // ---------------------------------------------------------------------------------------- order-P multipoles
+    m.def("multipole_upsweep", [](int order, int64_t N, Ptr n2l, Ptr child, std::vector<int64_t> levelRange, Ptr ns,
+                                  Ptr ne, Ptr x, Ptr y, Ptr z, Ptr mm, Ptr centers, Ptr Q, Ptr s)
+          {
+              multipoleUpsweep(order, N, P<int32_t>(n2l), P<int32_t>(child), levelRange.data(), P<int32_t>(ns),
+                               P<int32_t>(ne), P<double>(x), P<double>(y), P<double>(z), P<float>(mm),
+                               P<double>(centers), P<float>(Q), St(s));
+          });
+    m.def("compute_gravity_multipole",
+          [](int order, int64_t first, int64_t last, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr centers, Ptr Q, Ptr x,
+             Ptr y, Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay, Ptr az, Ptr ugrav, Ptr esum, Ptr overflow, Ptr s)
+          {
+              computeGravityMultipole(order, first, last, P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns),
+                                      P<int32_t>(ne), P<double>(centers), P<float>(Q), P<double>(x), P<double>(y),
+                                      P<double>(z), P<float>(h), P<float>(mm), G, P<float>(ax), P<float>(ay),
+                                      P<float>(az), P<double>(ugrav), P<double>(esum), P<int>(overflow), St(s));
+          });
     // ---------------------------------------------------------------------------------------------- cooling
     m.def("cool_particles", [](int64_t first, int64_t last, double dt, Ptr rho, Ptr u, Ptr du,
                                const std::array<double, 7>& a, Ptr s)

@@ -141,6 +141,16 @@ void coolingTimestep(int64_t first, int64_t last, const float* rho, const double
 void coolingEos(int64_t first, int64_t last, double gamma, const float* rho, const double* u, float* pr, float* c,
                 hipStream_t s);
 
+// multipole.hip (order-P Cartesian multipoles, P in [1, 6]; math: sphx/multipole.hpp)
+void multipoleUpsweep(int order, int64_t N, const int32_t* n2l, const int32_t* child, const int64_t* levelRange,
+                      const int32_t* ns, const int32_t* ne, const double* x, const double* y, const double* z,
+                      const float* m, const double* centers, float* Q, hipStream_t s);
+void computeGravityMultipole(int order, int64_t first, int64_t last, const int32_t* child, const int32_t* n2l,
+                             const int32_t* ns, const int32_t* ne, const double* centers, const float* Q,
+                             const double* x, const double* y, const double* z, const float* h, const float* m,
+                             double G, float* ax, float* ay, float* az, double* ugrav, double* esum, int* overflow,
+                             hipStream_t s);
+
 // gravity.hip
 void gravityLeaves(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
                    const double* y, const double* z, const float* m, double* centers, void* mp, hipStream_t s);

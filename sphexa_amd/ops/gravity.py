@@ -226,3 +226,48 @@ def direct_sum_kahan(x, y, z, h, m):
     _lib.cpu().direct_sum_kahan(n, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), m.data_ptr(),
                                 *[o.data_ptr() for o in out])
     return out
+
+
+# ------------------------------------------------------------------------------------- order-P multipoles (G3)
+def multipole_size(order: int) -> int:
+    """moments of degree < order: order (order+1) (order+2) / 6 (reference SphericalMultipole TermSize)"""
+    return order * (order + 1) * (order + 2) // 6
+
+
+def multipole_upsweep(tree: Octree, centers, x, y, z, m, order: int):
+    """order-P Cartesian moments of every node about the expansion centers of ``upsweep`` (mass centers); fp64 on
+    the host, fp32 on the GPU (accumulated in fp64)"""
+    N = tree.num_nodes
+    ts = multipole_size(order)
+    if x.is_cuda:
+        Q = torch.zeros(ts * N, dtype=torch.float32, device=x.device)
+        _lib.hip().multipole_upsweep(order, N, tree.node_to_leaf.data_ptr(), tree.child_offsets.data_ptr(),
+                                     tree.level_range, tree.node_start.data_ptr(), tree.node_end.data_ptr(),
+                                     x.data_ptr(), y.data_ptr(), z.data_ptr(), m.data_ptr(), centers.data_ptr(),
+                                     Q.data_ptr(), _stream())
+    else:
+        Q = torch.zeros(ts * N, dtype=torch.float64)
+        _lib.cpu().multipole_upsweep(order, N, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
+                                     tree.level_range, tree.node_start.data_ptr(), tree.node_end.data_ptr(),
+                                     x.data_ptr(), y.data_ptr(), z.data_ptr(), m.data_ptr(), centers.data_ptr(),
+                                     Q.data_ptr())
+    return Q
+
+
+def compute_gravity_multipole(tree: Octree, centers, Q, order: int, first: int, last: int, x, y, z, h, m, G: float,
+                              ax, ay, az, ugrav=None) -> float:
+    """Barnes-Hut with order-P far field (same MAC and near field as ``compute_gravity``); returns 0.5 sum G m phi"""
+    if last <= first:
+        return 0.0
+    args = (tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
+            tree.node_end.data_ptr(), centers.data_ptr(), Q.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(),
+            h.data_ptr(), m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
+            0 if ugrav is None else ugrav.data_ptr())
+    if x.is_cuda:
+        out = torch.zeros(1, dtype=torch.float64, device=x.device)
+        ovf = torch.zeros(1, dtype=torch.int32, device=x.device)
+        _lib.hip().compute_gravity_multipole(order, first, last, *args, out.data_ptr(), ovf.data_ptr(), _stream())
+        if int(ovf.item()) != 0:
+            raise RuntimeError("multipole traversal stack overflow")
+        return float(out.item())
+    return _lib.cpu().compute_gravity_multipole(order, first, last, *args)
