@@ -53,6 +53,7 @@ Where possible options are:
     -o PATH             Location of generated output files
     --device DEV        cuda (default when a GPU is present) or cpu (OpenMP reference path)
     --insitu MOD[:FN]   In-situ adaptor module called every iteration with the local particle fields
+    --no-watchdog       Do not abort on non-finite energies or time steps
 """
 
 
@@ -81,6 +82,7 @@ def main(argv=None) -> int:
     quiet = parser.exists("--quiet")
     av_clean = parser.exists("--avclean")
     duration = float(parser.get("--duration", 2 ** 31 - 1))
+    watchdog = not parser.exists("--no-watchdog")
     write_freq = str(parser.get("-w", "0"))
     write_enabled = write_freq != "0" or bool(write_extra)
     prof_enabled = parser.exists("--profile")
@@ -145,6 +147,8 @@ def main(argv=None) -> int:
         propagator.step(domain, d)
         box = domain.box
         observables.compute_and_write(d, domain, comm)
+        if watchdog:
+            check_finite(d)
         propagator.print_iteration_timings(domain, d)
         viz.execute(d, domain)
 
@@ -171,6 +175,17 @@ def main(argv=None) -> int:
     observables.close()
     viz.finalize()
     return 0
+
+
+def check_finite(d):
+    """NaN/Inf watchdog on the globally reduced observables (SURVEY 5.3 detect-and-abort): a non-finite energy or
+    time step aborts the run on every rank at the same iteration instead of propagating garbage into outputs"""
+    import math
+
+    vals = {"etot": d.etot, "ecin": d.ecin, "eint": d.eint, "minDt": d.minDt}
+    bad = [k for k, v in vals.items() if not math.isfinite(float(v))]
+    if bad:
+        raise FloatingPointError(f"non-finite {', '.join(bad)} at iteration {d.iteration} (t = {d.ttot})")
 
 
 def write_step(writer, path, d, domain, propagator):
