@@ -7,8 +7,8 @@
  *   * every neighbor loop first packs the source fields it needs into a 16-byte aligned array of records (one
  *     streaming pass), so a neighbor costs 2-8 dwordx4 loads of one contiguous 32-128 B record instead of up to 21
  *     scattered 4/8-byte gathers;
- *   * neighbor lists come from the wave64 search, lane-interleaved, so the index load of step k is one coalesced
- *     256-byte access per wave;
+ *   * neighbor lists come from the wave64 search in 4-entry blocks per lane (kBlockedList), so the indices of four
+ *     steps are one coalesced 1 KiB load per wave;
  *   * blocks are remapped so each XCD walks a contiguous SFC range of target groups (shared neighbors stay in that
  *     XCD's L2);
  *   * IAD and the velocity divergence/curl run in one kernel (c_ij of the target is all divv needs).
@@ -34,7 +34,7 @@ __device__ __forceinline__ bool targetOf(const NbrArgs& a, int64_t& i, const int
     int64_t t   = int64_t(lb) * kBlock + threadIdx.x;
     i           = a.first + t;
     int64_t g   = t >> 6;
-    nbr         = a.nidx + g * int64_t(a.ngmax) * 64 + (t & 63);
+    nbr         = a.nidx + g * int64_t((a.ngmax + 3) & ~3u) * 64 + (t & 63) * 4; // kBlockedList layout
     if (i >= a.last)
     {
         i = a.last - 1;
@@ -102,8 +102,8 @@ __global__ void packIadKernel(int64_t n, const double* __restrict__ x, const dou
     r.vx   = vx ? vx[i] : 0.f;
     r.vy   = vy ? vy[i] : 0.f;
     r.vz   = vz ? vz[i] : 0.f;
-    r.xm   = xm ? xm[i] : 0.f;
-    r.c    = c ? c[i] : 0.f;
+    if (c) r.c = c[i];
+    else r.xm = xm ? xm[i] : 0.f;
     r.divv = divv ? divv[i] : 0.f;
     out[i] = r;
 }
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, B
     const int32_t* nbr;
     unsigned n;
     const bool valid = targetOf(a, i, nbr, n);
-    float v = xmassJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], coopOf(rec, tile, i, a),
+    float v = xmassJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], coopOf(rec, tile, i, a),
                          KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice});
     if (valid) xm[i] = v;
 }
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts 
     unsigned n;
     const bool valid = targetOf(a, i, nbr, n);
     float k, g;
-    veDefGradhJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], coopOf(rec, tile, i, a),
+    veDefGradhJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], coopOf(rec, tile, i, a),
                     KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice}, k, g);
     if (!valid) return;
     kx[i]    = k;
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(kBlock) void iadKernel(NbrArgs a, SphConsts sc, Box
     unsigned n;
     const bool valid = targetOf(a, i, nbr, n);
     float c[6];
-    iadJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], coopOf(rec, tile, i, a),
+    iadJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], coopOf(rec, tile, i, a),
              KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c);
     if (!valid) return;
     for (int k = 0; k < 6; ++k)
@@ -270,8 +270,8 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConst
     unsigned n;
     const bool valid = targetOf(a, i, nbr, n);
     float c[6], g[6], dvi, cvi;
-    iadDivvCurlvJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], kx[i], coopOf(rec, tile, i, a),
-                      KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, doGrad ? g : nullptr);
+    iadDivvCurlvJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], kx[i], coopOf(rec, tile, i, a),
+                      KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, g);
     if (!valid) return;
     for (int k = 0; k < 6; ++k)
         cij.p[k][i] = c[k];
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(kBlock) void avSwitchesKernel(NbrArgs a, SphConsts 
     unsigned n;
     const bool valid = targetOf(a, i, nbr, n);
     float ci[6] = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
-    float al    = avSwitchesJLoop(unsigned(i), sc.K, box, nbr, 64, n, h[i], ci, coopOf(rec, tile, i, a),
+    float al    = avSwitchesJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], ci, coopOf(rec, tile, i, a),
                                   KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt, sc.alphamin, sc.alphamax,
                                   sc.decayConstant, alpha[i]);
     if (valid) alpha[i] = al;
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphC
     float dti  = FLT_MAX;
     float mvs, axi, ayi, azi;
     double dui;
-    momentumEnergyJLoop<avClean>(unsigned(i), sc, box, nbr, 64, n, coopOf(rec, tile, i, a), GradVLoader{gv},
+    momentumEnergyJLoop<avClean>(unsigned(i), sc, box, nbr, kBlockedList, n, coopOf(rec, tile, i, a), GradVLoader{gv},
                                  KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui, mvs);
     if (valid)
     {
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyStdKernel(NbrArgs a, Sph
     float dti  = FLT_MAX;
     float mvs, axi, ayi, azi;
     double dui;
-    momentumEnergyStdJLoop(unsigned(i), sc.K, box, nbr, 64, n, coopOf(rec, tile, i, a),
+    momentumEnergyStdJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, coopOf(rec, tile, i, a),
                            KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui, mvs);
     if (valid)
     {

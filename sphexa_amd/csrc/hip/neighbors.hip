@@ -15,6 +15,12 @@
  *      tests |x_i - x_j|^2 < 4h_i^2 in fp32; candidates inside a rounding band around the radius are re-tested in
  *      fp64 with the reference's minimum-image formula, so the neighbor sets equal the fp64 CPU search exactly
  *   4. lanes whose count is out of [ng0/4, ngmax+1] update h and the wave repeats
+ *
+ * List storage (sphx::kBlockedList): a lane's entries 4b..4b+3 form one int4 at nidx + g*ngmax4*64 + 256 b + 4 lane,
+ * so step k of a pair loop reads one coalesced 1 KiB block per four steps. Hits go to a per-lane ring of 8 slots in
+ * LDS; whenever some lane's ring is full, every lane holding >= 4 pending entries writes one block (dwordx4): the
+ * wave issues a few dozen list stores per group instead of one partially masked store per candidate source (the
+ * search was bound by those stores in the texture data path).
  */
 #include "common.h"
 #include "hip_api.h"
@@ -26,12 +32,22 @@ namespace sphx::hip
 
 constexpr int kWavesPerBlock = 4;
 constexpr int kFrontCap      = 512;
-constexpr int kLeafCap       = 1024;
+constexpr int kLeafCap       = 512;
+constexpr int kRing          = 8; // hit ring slots per lane (two list blocks)
+constexpr int kRingStride    = 9; // LDS words per lane (odd: the 32 lanes of a ds_write_b32 group hit distinct banks)
 
 //! @brief fold a coordinate difference into [-L/2, L/2] in periodic dimensions
 __device__ __forceinline__ double foldMin(double dx, const Box& b, int d)
 {
     return b.bc[d] == kPeriodic ? dx - b.len(d) * rint(dx * b.ilen(d)) : dx;
+}
+
+//! @brief load through the scalar cache: the tree is read-only during the search, and a wave-uniform address in the
+//!        constant address space selects s_load (a divergent one still compiles to a vector load)
+template<class T>
+__device__ __forceinline__ T ldConst(const T* p)
+{
+    return *(const __attribute__((address_space(4))) T*)(p);
 }
 
 //! @brief ordering point between lanes of one wave exchanging data through the frontier/leaf storage
@@ -50,17 +66,30 @@ __device__ __forceinline__ int32_t ldList(const int32_t* p)
     else { return *p; }
 }
 
+struct TreeView
+{
+    const int32_t* __restrict__ child;
+    const int32_t* __restrict__ n2l;
+    const int32_t* __restrict__ ns;
+    const int32_t* __restrict__ ne;
+    const double* __restrict__ center;
+    const double* __restrict__ half;
+};
+
 /*! @brief search of one target group (one wave). Returns false if the frontier or the leaf list overflowed the
  *         given capacities (nothing is written then, the group is retried by the spill kernel).
  */
 template<bool kSpill>
 __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t last, const double* __restrict__ x,
                                             const double* __restrict__ y, const double* __restrict__ z,
-                                            float* __restrict__ h, const NsTree& t, const Box& box, unsigned ng0,
+                                            float* __restrict__ h, const NsTree& tree, const Box& box, unsigned ng0,
                                             unsigned ngmax, int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
                                             int iterateH, unsigned long long* __restrict__ stats, int32_t* frontA,
-                                            int32_t* frontB, int32_t* leaves, int frontCap, int leafCap)
+                                            int32_t* frontB, int32_t* leaves, int frontCap, int leafCap,
+                                            int32_t* ring)
 {
+    // the tree is read-only here: restrict-qualified views let the uniform leaf loads go through the scalar cache
+    const TreeView t{tree.child, tree.n2l, tree.ns, tree.ne, tree.center, tree.half};
     const int lane   = threadIdx.x & 63;
     const int64_t i  = first + g * 64 + lane;
     const bool valid = i < last;
@@ -73,7 +102,9 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         zi = z[i];
         hi = h[i];
     }
-    int32_t* nlist = nidx + g * int64_t(ngmax) * 64 + lane;
+    const unsigned ngmax4 = (ngmax + 3) & ~3u;
+    int4* nlist           = reinterpret_cast<int4*>(nidx + g * int64_t(ngmax4) * 64) + lane;
+    int32_t* myRing       = ring + lane * kRingStride;
     const unsigned ngmin = ng0 / 4;
 
     unsigned ncSph = 1;
@@ -160,14 +191,30 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         const float gsf[3] = {float(gs[0]) + 2.0f * delta, float(gs[1]) + 2.0f * delta, float(gs[2]) + 2.0f * delta};
 
         unsigned cnt = 0;
+        unsigned fb  = 0; // list blocks of this lane already written
+        // write the next block (4 ring entries) of every lane in `who`
+        auto flushBlock = [&](bool who)
+        {
+            if (who)
+            {
+                const int s0 = int(4 * fb) & (kRing - 1);
+                int4 v       = make_int4(myRing[s0], myRing[s0 + 1], myRing[s0 + 2], myRing[s0 + 3]);
+                nlist[int64_t(fb) * 64] = v;
+                fb++;
+            }
+        };
         for (int l = 0; l < nLeaves; ++l)
         {
             int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + l));
+            // leaf data is wave-uniform: scalar loads (constant address space), no texture-path traffic
+            const double lc[3] = {ldConst(t.center + 3 * nd), ldConst(t.center + 3 * nd + 1),
+                                  ldConst(t.center + 3 * nd + 2)};
+            const double lh[3] = {ldConst(t.half + 3 * nd), ldConst(t.half + 3 * nd + 1), ldConst(t.half + 3 * nd + 2)};
             // skip leaves outside every lane's sphere (same strict test as the CPU traversal)
-            bool touch = valid && pointBoxDistSq(ip, t.center + 3 * nd, t.half + 3 * nd, box) < radiusSq;
+            bool touch = valid && pointBoxDistSq(ip, lc, lh, box) < radiusSq;
             if (!ballot(touch)) continue;
-            int32_t a = t.ns[nd];
-            int32_t b = t.ne[nd];
+            int32_t a = ldConst(t.ns + nd);
+            int32_t b = ldConst(t.ne + nd);
             for (int32_t c0 = a; c0 < b; c0 += 64)
             {
                 int32_t j = c0 + lane;
@@ -192,17 +239,28 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     bool hit   = d2 < r2f - band;
                     if (!hit && d2 <= r2f + band)
                     {
-                        hit = distanceSqPbc(x[jj], y[jj], z[jj], xi, yi, zi, box) < radiusSq;
+                        hit = distanceSqPbc(ldConst(x + jj), ldConst(y + jj), ldConst(z + jj), xi, yi, zi, box) <
+                              radiusSq;
                     }
-                    if (valid && hit && jj != i)
+                    const bool mine = valid && hit && jj != i;
+                    if (mine)
                     {
-                        if (cnt < ngmax) nlist[int64_t(cnt) * 64] = int32_t(jj);
+                        if (cnt < ngmax) myRing[cnt & (kRing - 1)] = int32_t(jj);
                         cnt++;
                     }
+                    // a full ring (8 pending) forces a flush of every lane holding a whole block
+                    const unsigned pend = min(cnt, ngmax) - 4 * fb;
+                    if (ballot(pend >= unsigned(kRing))) flushBlock(pend >= 4);
                 }
             }
         }
         ncSph = 1 + cnt;
+        // remaining entries (at most 7 per lane; block tails beyond the count are never read)
+        {
+            unsigned pend = min(cnt, ngmax) - 4 * fb;
+            flushBlock(pend > 0);
+            flushBlock(pend > 4);
+        }
 
         // 4. smoothing length iteration
         bool repeat = iterateH && valid && (ncSph < ngmin || (ncSph - 1) > ngmax);
@@ -231,6 +289,7 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
     __shared__ int32_t frontA[kWavesPerBlock][kFrontCap];
     __shared__ int32_t frontB[kWavesPerBlock][kFrontCap];
     __shared__ int32_t leaves[kWavesPerBlock][kLeafCap];
+    __shared__ int32_t ring[kWavesPerBlock][64 * kRingStride];
 
     const int wave          = threadIdx.x >> 6;
     const int64_t numGroups = (last - first + 63) / 64;
@@ -239,7 +298,7 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
     if (g >= numGroups) return;
 
     bool ok = searchGroup<false>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
-                                 frontA[wave], frontB[wave], leaves[wave], frontCap, kLeafCap);
+                                 frontA[wave], frontB[wave], leaves[wave], frontCap, kLeafCap, ring[wave]);
     if (!ok && (threadIdx.x & 63) == 0)
     {
         unsigned long long slot = atomicAdd(&stats[2], 1ull);
@@ -264,6 +323,7 @@ __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, in
                                                                const int32_t* __restrict__ spillList,
                                                                int32_t* __restrict__ scratch)
 {
+    __shared__ int32_t ring[64 * kRingStride];
     const int64_t numSpill = int64_t(__hip_atomic_load(&stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     int32_t* frontA = scratch + int64_t(blockIdx.x) * (2 * kSpillFront + kSpillLeaves);
     int32_t* frontB = frontA + kSpillFront;
@@ -272,7 +332,7 @@ __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, in
     {
         int64_t g = spillList[k];
         bool ok   = searchGroup<true>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
-                                      frontA, frontB, leaves, kSpillFront, kSpillLeaves);
+                                      frontA, frontB, leaves, kSpillFront, kSpillLeaves, ring);
         if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
     }
 }

@@ -46,4 +46,24 @@ SPHX_HD float rsqrtF(float x)
 
 SPHX_HD double rsqrtF(double x) { return 1.0 / std::sqrt(x); }
 
+//! @brief sqrt(x) of a pair distance: bare v_sqrt_f32 on the GPU (1 ulp, no denormal rescaling sequence)
+SPHX_HD float sqrtF(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sqrtf(x);
+#else
+    return std::sqrt(x);
+#endif
+}
+
+//! @brief 1/x: v_rcp_f32 on the GPU (1 ulp) instead of the IEEE division sequence, division on the host
+SPHX_HD float rcpF(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+
 } // namespace sphx

@@ -13,9 +13,12 @@
  * 16-byte aligned array-of-records buffers packed once per loop, so one neighbor costs 2-8 dwordx4 loads from one
  * or two cache lines instead of up to 21 scattered 4-byte gathers. Fields that the reference derives per pair
  * (xm/kx, kx*m/xm) are packed already derived — bit-identical because the same fp32 operations are applied.
- * The neighbor list accessor is (nbr, stride): neighbor k is nbr[k*stride]; stride 1 on the CPU, 64 on the GPU.
+ * The neighbor list accessor is (nbr, stride): neighbor k is nbr[k*stride] with stride 1 on the CPU; on the GPU
+ * (stride == kBlockedList) a lane's entries 4b..4b+3 are one int4 at nbr + 256 b (listAt).
  */
 #pragma once
+
+#include <cstddef>
 
 #include "annotation.hpp"
 #include "box.hpp"
@@ -91,7 +94,7 @@ struct KernelFn
         constexpr HT halfPi = HT(1.5707963267948966);
         HT x  = halfPi * v;
         HT sn = __sinf(x), cs = __cosf(x);
-        HT ix = HT(1) / x;
+        HT ix = rcpF(x);
         s     = v > HT(0) ? sn * ix : HT(1);
         ds    = v > HT(0) ? halfPi * (cs - s) * ix : HT(0);
     }
@@ -201,16 +204,22 @@ struct alignas(16) SrcPos
     HT xm;
 };
 
-//! @brief IAD + divv/curlv + AV switches: 48 B; vol = xm/kx (VE) or m/rho (STD)
+//! @brief IAD + divv/curlv + AV switches: 48 B (three 16-B chunks); vol = xm/kx (VE) or m/rho (STD). The IAD and
+//!        divv/curlv loops read xm, the AV-switch loop reads c (and divv): they share one slot, filled by the pack
+//!        for the loop that follows.
 struct alignas(16) SrcIad
 {
     CT x, y, z;
     HT vol;
     HT vx, vy, vz;
-    HT xm;
-    HT c;
+    union
+    {
+        HT xm;
+        HT c;
+    };
     HT divv;
 };
+static_assert(sizeof(SrcIad) == 48, "SrcIad is three 16-byte chunks");
 
 //! @brief VE momentum/energy: 96 B (+ velocity gradient for AV cleaning: 128 B). Per-particle factors of the pair
 //!        terms are precomputed at pack time (1/h, m/rho) so the pair loop has no divisions.
@@ -278,6 +287,16 @@ constexpr bool kDeviceBatching = false;
  *         are latency bound otherwise: one dependent index->record->math chain per iteration). The OpenMP build
  *         evaluates one neighbor at a time. Evaluation order (and hence the floating-point sums) is unchanged.
  */
+//! @brief list stride value of the GPU layout: 4-entry blocks per lane, blocks of one group 256 entries apart
+constexpr int kBlockedList = -4;
+
+//! @brief neighbor k of a list (see the file comment for the two layouts)
+template<class Idx>
+SPHX_HD Idx listAt(const Idx* nbr, int stride, unsigned k)
+{
+    return stride == kBlockedList ? nbr[size_t(k >> 2) * 256 + (k & 3)] : nbr[size_t(k) * size_t(stride)];
+}
+
 template<int B, class Idx, class Ld, class F>
 SPHX_HD void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const Ld& ld, F&& f)
 {
@@ -291,7 +310,7 @@ SPHX_HD void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const Ld& 
             Rec r[B];
 #pragma unroll
             for (int u = 0; u < B; ++u)
-                j[u] = unsigned(nbr[(k + u) * stride]);
+                j[u] = unsigned(listAt(nbr, stride, k + u));
 #pragma unroll
             for (int u = 0; u < B; ++u)
                 r[u] = ld(j[u]);
@@ -303,7 +322,7 @@ SPHX_HD void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const Ld& 
 #pragma nounroll
     for (; k < nc; ++k)
     {
-        unsigned j = unsigned(nbr[k * stride]);
+        unsigned j = unsigned(listAt(nbr, stride, k));
         f(j, ld(j));
     }
 }
@@ -313,6 +332,106 @@ SPHX_HD void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const Ld& 
 #endif
 
 #if defined(__HIPCC__)
+//! @brief double from the two 32-bit halves of a staged chunk
+__device__ __forceinline__ double chunkDouble(float lo, float hi)
+{
+    return __hiloint2double(__float_as_int(hi), __float_as_int(lo));
+}
+
+/*! @brief record from its staged 16-byte chunks, field by field in registers. A memcpy/bit-cast of the chunk array
+ *         into the record would leave a private array that the compiler promotes to LDS (per-lane ds_write_b64 /
+ *         ds_read_b32..b128 round trips with 2-4 way bank conflicts on every neighbor).
+ */
+template<class R>
+__device__ R coopUnpack(const float4* o);
+
+template<>
+__device__ __forceinline__ SrcPos coopUnpack<SrcPos>(const float4* o)
+{
+    static_assert(offsetof(SrcPos, m) == 24 && sizeof(SrcPos) == 32, "SrcPos layout");
+    SrcPos r;
+    r.x  = chunkDouble(o[0].x, o[0].y);
+    r.y  = chunkDouble(o[0].z, o[0].w);
+    r.z  = chunkDouble(o[1].x, o[1].y);
+    r.m  = o[1].z;
+    r.xm = o[1].w;
+    return r;
+}
+
+template<>
+__device__ __forceinline__ SrcIad coopUnpack<SrcIad>(const float4* o)
+{
+    static_assert(offsetof(SrcIad, vol) == 24 && offsetof(SrcIad, divv) == 44, "SrcIad layout");
+    SrcIad r;
+    r.x    = chunkDouble(o[0].x, o[0].y);
+    r.y    = chunkDouble(o[0].z, o[0].w);
+    r.z    = chunkDouble(o[1].x, o[1].y);
+    r.vol  = o[1].z;
+    r.vx   = o[1].w;
+    r.vy   = o[2].x;
+    r.vz   = o[2].y;
+    r.xm   = o[2].z;
+    r.divv = o[2].w;
+    return r;
+}
+
+template<>
+__device__ __forceinline__ SrcMom coopUnpack<SrcMom>(const float4* o)
+{
+    static_assert(offsetof(SrcMom, vx) == 24 && offsetof(SrcMom, c11) == 40 && offsetof(SrcMom, m) == 64 &&
+                      offsetof(SrcMom, mrho) == 88 && sizeof(SrcMom) == 96,
+                  "SrcMom layout");
+    SrcMom r;
+    r.x     = chunkDouble(o[0].x, o[0].y);
+    r.y     = chunkDouble(o[0].z, o[0].w);
+    r.z     = chunkDouble(o[1].x, o[1].y);
+    r.vx    = o[1].z;
+    r.vy    = o[1].w;
+    r.vz    = o[2].x;
+    r.ih    = o[2].y;
+    r.c11   = o[2].z;
+    r.c12   = o[2].w;
+    r.c13   = o[3].x;
+    r.c22   = o[3].y;
+    r.c23   = o[3].z;
+    r.c33   = o[3].w;
+    r.m     = o[4].x;
+    r.c     = o[4].y;
+    r.xm    = o[4].z;
+    r.rho   = o[4].w;
+    r.prho  = o[5].x;
+    r.alpha = o[5].y;
+    r.mrho  = o[5].z;
+    return r;
+}
+
+template<>
+__device__ __forceinline__ SrcStd coopUnpack<SrcStd>(const float4* o)
+{
+    static_assert(offsetof(SrcStd, vx) == 24 && offsetof(SrcStd, c11) == 40 && offsetof(SrcStd, m) == 64 &&
+                      sizeof(SrcStd) == 80,
+                  "SrcStd layout");
+    SrcStd r;
+    r.x   = chunkDouble(o[0].x, o[0].y);
+    r.y   = chunkDouble(o[0].z, o[0].w);
+    r.z   = chunkDouble(o[1].x, o[1].y);
+    r.vx  = o[1].z;
+    r.vy  = o[1].w;
+    r.vz  = o[2].x;
+    r.ih  = o[2].y;
+    r.c11 = o[2].z;
+    r.c12 = o[2].w;
+    r.c13 = o[3].x;
+    r.c22 = o[3].y;
+    r.c23 = o[3].z;
+    r.c33 = o[3].w;
+    r.m   = o[4].x;
+    r.rho = o[4].y;
+    r.p   = o[4].z;
+    r.c   = o[4].w;
+    return r;
+}
+
 /*! @brief record loader of the gfx950 pair loops: cooperative, cache-line-coalesced gathers staged through LDS.
  *
  * At neighbor step k every lane needs the C x 16-byte record of its own neighbor j. Loading it directly costs C
@@ -385,24 +504,27 @@ __device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const C
     if constexpr (direct)
     {
         // small records: per-lane gathers, B in flight (measured faster than the cooperative path for 32 B)
+        // small records: per-lane gathers, one list block (4 indices) and its 4 records in flight
+        static_assert(B == 4, "the direct path consumes one 4-entry list block per batch");
         unsigned k = 0;
-        for (; k + B <= nc; k += B)
+        const int4* blk = reinterpret_cast<const int4*>(nbr);
+        int4 v          = blk[0]; // next block prefetched while the current one is evaluated
+        for (; k + 4 <= nc; k += 4)
         {
-            unsigned j[B];
-            R rr[B];
+            const int4 vn       = blk[size_t((k >> 2) + 1) * 64];
+            const unsigned j[4] = {unsigned(v.x), unsigned(v.y), unsigned(v.z), unsigned(v.w)};
+            v                   = vn;
+            R rr[4];
 #pragma unroll
-            for (int u = 0; u < B; ++u)
-                j[u] = unsigned(nbr[(k + u) * stride]);
-#pragma unroll
-            for (int u = 0; u < B; ++u)
+            for (int u = 0; u < 4; ++u)
                 rr[u] = ld(j[u]);
 #pragma unroll
-            for (int u = 0; u < B; ++u)
+            for (int u = 0; u < 4; ++u)
                 f(j[u], rr[u]);
         }
         for (; k < nc; ++k)
         {
-            unsigned j = unsigned(nbr[k * stride]);
+            unsigned j = unsigned(listAt(nbr, stride, k));
             f(j, ld(j));
         }
         return;
@@ -412,74 +534,77 @@ __device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const C
         ncMax = max(ncMax, unsigned(__shfl_xor(int(ncMax), o)));
     ncMax = __builtin_amdgcn_readfirstlane(ncMax);
     if (ncMax == 0) return;
-#ifdef SPHX_COOP_LIST_INDEX
-    // per chunk-instruction record indices read from the list two steps ahead (C index loads per step)
-    unsigned iN[C], iNN[C];
-    float4 rawC[C], rawN[C], o[C];
-#pragma unroll
-    for (int q = 0; q < C; ++q)
+    // Neighbor indices come in 4-entry list blocks (one coalesced 1 KiB load per four steps, two blocks ahead), are
+    // spread to the chunk lanes with ds_bpermute two steps ahead, and the chunk data is gathered one step ahead of
+    // the evaluation. Unrolled by four with ping-pong buffers (A/B data, I1/I2 indices): no register rotation.
+    auto consume = [&](const float4 (&raw)[C], unsigned j, unsigned k)
     {
-        rawC[q] = ld.issue(ld.index(nbr, stride, 0, q), q);
-        iN[q]   = ld.index(nbr, stride, 1, q);
-    }
-    unsigned jC = 0 < nc ? unsigned(nbr[0]) : ld.self;
-    for (unsigned k = 0; k < ncMax; ++k)
-    {
-        const unsigned jN = k + 1 < nc ? unsigned(nbr[(k + 1) * stride]) : ld.self;
+        float4 o[C];
 #pragma unroll
         for (int q = 0; q < C; ++q)
-        {
-            iNN[q]  = ld.index(nbr, stride, k + 2, q); // reads stay inside the list allocation (+ 2 rows)
-            rawN[q] = ld.issue(iN[q], q);
-        }
-#else
-    // own neighbor index read three steps ahead (one coalesced load per step), spread to the chunk lanes with
-    // ds_bpermute two steps ahead, chunk data gathered one step ahead of the evaluation
-    unsigned iN[C], iNN[C];
-    float4 rawC[C], rawN[C], o[C];
-    const unsigned j0 = 0 < nc ? unsigned(nbr[0]) : ld.self;
-    const unsigned j1 = 1 < nc ? unsigned(nbr[stride]) : ld.self;
-    unsigned jNN      = 2 < nc ? unsigned(nbr[2 * stride]) : ld.self;
-#pragma unroll
-    for (int q = 0; q < C; ++q)
-    {
-        rawC[q] = ld.issue(ld.spread(j0, q), q);
-        iN[q]   = ld.spread(j1, q);
-    }
-    unsigned jC = j0, jN = j1;
-    for (unsigned k = 0; k < ncMax; ++k)
-    {
-        const unsigned jNNN = k + 3 < nc ? unsigned(nbr[(k + 3) * stride]) : ld.self;
-#pragma unroll
-        for (int q = 0; q < C; ++q)
-        {
-            iNN[q]  = ld.spread(jNN, q);
-            rawN[q] = ld.issue(iN[q], q);
-        }
-#endif
-#pragma unroll
-        for (int q = 0; q < C; ++q)
-            ld.stage(rawC[q], q);
+            ld.stage(raw[q], q);
 #pragma unroll
         for (int p = 0; p < C; ++p)
             o[p] = ld.own(p);
-        R rec;
-        __builtin_memcpy(&rec, o, sizeof(R));
-        if (k < nc) f(jC, rec);
+#ifndef SPHX_COOP_NARROW
+        // keep every chunk live as a whole: otherwise the fields a loop leaves unused split the 16-byte LDS reads
+        // into ds_read_b32/b64/read2 pieces whose bank groups conflict 2-4 ways at the odd record strides
+#pragma unroll
+        for (int p = 0; p < C; ++p)
+            asm volatile("" : "+v"(o[p].x), "+v"(o[p].y), "+v"(o[p].z), "+v"(o[p].w));
+#endif
+        const R rec = coopUnpack<R>(o);
+        if (k < nc) f(j, rec);
+    };
+    const int4* blk = reinterpret_cast<const int4*>(nbr); // block b at blk[64 b]
+    // entry e of a block for step k; entries past the lane's count are garbage: use the lane's own record
+    auto pick = [&](unsigned v, unsigned k) { return k < nc ? v : ld.self; };
+    int4 B0 = blk[0], B1 = blk[64];
+    unsigned I1[C], I2[C];
+    float4 A[C], Bf[C];
+    {
+        const unsigned j0 = pick(unsigned(B0.x), 0), j1 = pick(unsigned(B0.y), 1);
 #pragma unroll
         for (int q = 0; q < C; ++q)
         {
-            rawC[q] = rawN[q];
-            iN[q]   = iNN[q];
+            A[q]  = ld.issue(ld.spread(j0, q), q);
+            I1[q] = ld.spread(j1, q);
         }
-        jC = jN;
-#ifdef SPHX_COOP_LIST_INDEX
     }
-#else
-        jN  = jNN;
-        jNN = jNNN;
+    for (unsigned k = 0; k < ncMax; k += 4)
+    {
+        const int4 B2 = blk[size_t((k >> 2) + 2) * 64]; // list allocation carries two spare block rows
+#pragma unroll
+        for (int q = 0; q < C; ++q)
+        {
+            I2[q] = ld.spread(pick(unsigned(B0.z), k + 2), q);
+            Bf[q] = ld.issue(I1[q], q);
+        }
+        consume(A, pick(unsigned(B0.x), k), k);
+#pragma unroll
+        for (int q = 0; q < C; ++q)
+        {
+            I1[q] = ld.spread(pick(unsigned(B0.w), k + 3), q);
+            A[q]  = ld.issue(I2[q], q);
+        }
+        consume(Bf, pick(unsigned(B0.y), k + 1), k + 1);
+#pragma unroll
+        for (int q = 0; q < C; ++q)
+        {
+            I2[q] = ld.spread(pick(unsigned(B1.x), k + 4), q);
+            Bf[q] = ld.issue(I1[q], q);
+        }
+        consume(A, pick(unsigned(B0.z), k + 2), k + 2);
+#pragma unroll
+        for (int q = 0; q < C; ++q)
+        {
+            I1[q] = ld.spread(pick(unsigned(B1.y), k + 5), q);
+            A[q]  = ld.issue(I2[q], q);
+        }
+        consume(Bf, pick(unsigned(B0.w), k + 3), k + 3);
+        B0 = B1;
+        B1 = B2;
     }
-#endif
 }
 #endif
 
@@ -494,7 +619,7 @@ SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
     forEachNeighbor<SPHX_BATCH_POS>(nbr, stride, nc, ld, [&](unsigned j, const SrcPos& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
-        HT dist = sqrt(rx * rx + ry * ry + rz * rz);
+        HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
         rho0 += kf.w(dist * hInv) * pj.m;
     });
     return pi.m / (rho0 * HT(K) * h3Inv);
@@ -515,7 +640,7 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const Box& box, const Idx* nb
     forEachNeighbor<SPHX_BATCH_POS>(nbr, stride, nc, ld, [&](unsigned j, const SrcPos& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
-        HT dist  = sqrt(rx * rx + ry * ry + rz * rz);
+        HT dist  = sqrtF(rx * rx + ry * ry + rz * rz);
         HT v     = dist * hInv;
         HT w     = kf.w(v);
         HT dw    = kf.dw(v);
@@ -567,7 +692,7 @@ SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
-        HT dist = sqrt(rx * rx + ry * ry + rz * rz);
+        HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
         HT w    = kf.w(dist * hInv);
         HT vw   = pj.vol * w;
         tau[0] += rx * rx * vw;
@@ -592,7 +717,7 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
-        HT dist = sqrt(rx * rx + ry * ry + rz * rz);
+        HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
         HT vxji = pj.vx - pi.vx, vyji = pj.vy - pi.vy, vzji = pj.vz - pi.vz;
         HT W    = kf.w(dist * hInv);
         HT tA0  = -(c11 * rx + c12 * ry + c13 * rz) * W;
@@ -643,7 +768,7 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* 
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
-        HT dist = sqrt(rx * rx + ry * ry + rz * rz);
+        HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
         HT w    = kf.w(dist * hInv);
         HT vw   = pj.vol * w;
         tau[0] += rx * rx * vw;
@@ -832,10 +957,10 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
         else
         {
             // xmi^(2-s) xmj^s = xmi^2 (xmj/xmi)^s and xmj^(2-s) xmi^s = xmj^2 (xmj/xmi)^-s
-            HT sigma = ramp * (dRho / sRho - Atmin);
-            HT q     = exp2(sigma * (log2(xmj) - log2xmi));
-            a_mom    = xmi * xmi * q;
-            b_mom    = xmj * xmj / q;
+            HT sigma = ramp * (dRho * rcpF(sRho) - Atmin);
+            HT e     = sigma * (log2(xmj) - log2xmi);
+            a_mom    = xmi * xmi * exp2(e);
+            b_mom    = xmj * xmj * exp2(-e);
         }
 
         HT av  = mj * invRhoi * visc;
@@ -954,8 +1079,8 @@ struct SoaIad
         r.vx   = vx ? vx[j] : HT(0);
         r.vy   = vy ? vy[j] : HT(0);
         r.vz   = vz ? vz[j] : HT(0);
-        r.xm   = xm ? xm[j] : HT(0);
-        r.c    = c ? c[j] : HT(0);
+        if (c) r.c = c[j];
+        else r.xm = xm ? xm[j] : HT(0);
         r.divv = divv ? divv[j] : HT(0);
         return r;
     }

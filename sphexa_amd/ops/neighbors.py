@@ -7,8 +7,9 @@ loop (the reference GPU path re-traverses the tree in each of its five kernels).
 
 Storage layouts
   * CPU:  ``nidx[(i - first) * ngmax + k]``
-  * HIP:  target groups of 64 consecutive particles (one wave64 per group);
-          ``nidx[(g * ngmax + k) * 64 + lane]`` so that step k of the j-loop is one coalesced 256-B load per wave.
+  * HIP:  target groups of 64 consecutive particles (one wave64 per group), entries in 4-entry blocks per lane:
+          ``nidx[g * ngmax4 * 64 + (k // 4) * 256 + lane * 4 + k % 4]`` (ngmax4 = ngmax rounded up to 4), so that
+          four steps of a pair loop are one coalesced 1 KiB load per wave and the search writes whole blocks.
 ``nc`` (a particle field) counts neighbors *including* self, as in the reference.
 """
 
@@ -23,6 +24,10 @@ from .octree import Octree
 from ..utils.box import Box
 
 GROUP = 64
+
+
+def _round4(v: int) -> int:
+    return (v + 3) // 4 * 4
 
 
 def _stream():
@@ -71,8 +76,8 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
     if x.is_cuda:
         hp = _lib.hip()
         num_groups = (n + GROUP - 1) // GROUP
-        # + 2 rows: the cooperative gathers of the pair loops read the index rows two steps ahead
-        need = max(num_groups, 1) * GROUP * ngmax + 2 * GROUP
+        # + 2 block rows: the pair loops prefetch list blocks two ahead
+        need = max(num_groups, 1) * GROUP * _round4(ngmax) + 2 * 4 * GROUP
         if nidx is None or nidx.numel() < need:
             nidx = torch.empty(need, dtype=torch.int32, device=x.device)
         stats = torch.zeros(4, dtype=torch.int64, device=x.device)
@@ -110,8 +115,8 @@ def neighbor_lists_as_sets(nl: NeighborList, nc: torch.Tensor):
         cnt = min(int(ncc[i]) - 1, nl.ngmax)
         if nl.grouped:
             g, lane = divmod(i - nl.first, GROUP)
-            base = g * nl.ngmax * GROUP
-            s = {int(nidx[base + k * GROUP + lane]) for k in range(cnt)}
+            base = g * _round4(nl.ngmax) * GROUP + lane * 4
+            s = {int(nidx[base + (k // 4) * 4 * GROUP + k % 4]) for k in range(cnt)}
         else:
             base = (i - nl.first) * nl.ngmax
             s = set(int(v) for v in nidx[base:base + cnt].tolist())
