@@ -503,8 +503,8 @@ __device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const C
 #endif
     if constexpr (direct)
     {
-        // small records: per-lane gathers, B in flight (measured faster than the cooperative path for 32 B)
-        // small records: per-lane gathers, one list block (4 indices) and its 4 records in flight
+        // small records (cooperative path measured slower for 32 B): per-lane gathers, one list block (4 indices) and its records in flight (a deeper
+        // software pipeline measured slower: more VGPRs, same texture-path work)
         static_assert(B == 4, "the direct path consumes one 4-entry list block per batch");
         unsigned k = 0;
         const int4* blk = reinterpret_cast<const int4*>(nbr);
