@@ -100,6 +100,9 @@ def main():
             nsteps = max(prop.timer.num_accum, 1)
             for k, v in prop.timer.accum.items():
                 print(f"# substep {k:28s} {1000.0 * v / nsteps:10.3f} ms/step", file=sys.stderr)
+            if hasattr(d, "nc_rounds") and d.nc_rounds > 0:
+                print(f"# neighbor search: {d.nc_rounds:.2f} rounds and {d.nc_leaves:.1f} candidate leaves per "
+                      f"64-particle group (last step), {getattr(d, 'nc_spilled', 0)} spilled groups", file=sys.stderr)
             if prop.gravity is not None and prop.gravity.stats:
                 print(f"# gravity stats {prop.gravity.stats}", file=sys.stderr)
             if device.type == "cuda":

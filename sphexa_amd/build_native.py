@@ -101,9 +101,11 @@ def build_hip(verbose=False, variant=None, defines=()):
     srcs = sorted(glob.glob(os.path.join(CSRC, "hip", "*.hip")) + glob.glob(os.path.join(CSRC, "hip", "*.cpp")))
     target = os.path.join(out_dir, "_sphx_hip" + EXT)
     # fp32 division/sqrt as the hardware rcp/sqrt (<= 1 ulp) instead of the IEEE correctly-rounded expansions
-    # (~10 VALU each): the SPH pair loops are VALU-bound on MI355X (profiles/), the results stay fp32-accurate
+    # (~10 VALU each): the SPH pair loops are VALU-bound on MI355X (profiles/), the results stay fp32-accurate.
+    # No SLP vectorization: its v_pk_*_f32 pairs cost operand-packing moves and registers in the pair loops
+    # (A/B: Sedov -n 400 192 -> 183 ms/step, momentum/energy 45 -> 40 ms; Evrard -n 200 41.6 -> 40.2 ms)
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-             "-fno-hip-fp32-correctly-rounded-divide-sqrt",
+             "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
              f"-I{os.path.join(CSRC, 'include')}", f"-I{os.path.join(CSRC, 'hip')}"] + list(defines) + _py_includes()
     hdrs = _headers() + glob.glob(os.path.join(CSRC, "hip", "*.h"))
     jobs, objs = [], []

@@ -109,6 +109,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
 
     unsigned ncSph = 1;
     int round      = 0;
+    unsigned leavesTouched = 0; // candidate leaves of the last round (statistics)
     for (;; ++round)
     {
         // 1. group search box
@@ -192,6 +193,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
 
         unsigned cnt = 0;
         unsigned fb  = 0; // list blocks of this lane already written
+        leavesTouched = 0;
         // write the next block (4 ring entries) of every lane in `who`
         auto flushBlock = [&](bool who)
         {
@@ -213,6 +215,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
             // skip leaves outside every lane's sphere (same strict test as the CPU traversal)
             bool touch = valid && pointBoxDistSq(ip, lc, lh, box) < radiusSq;
             if (!ballot(touch)) continue;
+            leavesTouched++;
             int32_t a = ldConst(t.ns + nd);
             int32_t b = ldConst(t.ne + nd);
             for (int32_t c0 = a; c0 < b; c0 += 64)
@@ -263,12 +266,17 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         }
 
         // 4. smoothing length iteration
-        bool repeat = iterateH && valid && (ncSph < ngmin || (ncSph - 1) > ngmax);
+        bool repeat = (iterateH & 1) && valid && (ncSph < ngmin || (ncSph - 1) > ngmax);
         if (!ballot(repeat) || round >= 10) break;
         if (repeat) hi = sphx::updateH<float>(ng0, ncSph, hi);
     }
 
     if (lane == 0 && round >= 10) atomicAdd(&stats[0], 1ull);
+    if (lane == 0 && (iterateH & 2)) // statistics (opt-in): search rounds and candidate leaves, summed over groups
+    {
+        atomicAdd(&stats[3], (unsigned long long)(round + 1));
+        atomicAdd(&stats[4], (unsigned long long)leavesTouched);
+    }
     if (valid)
     {
         nc[i] = int32_t(ncSph);

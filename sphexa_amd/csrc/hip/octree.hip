@@ -181,17 +181,21 @@ __device__ inline void storeBox(double* center, double* half, int64_t i, const d
     }
 }
 
-//! @brief tight boxes of leaf particles, optionally expanded per particle by factor*h
-__global__ void leafBoxesKernel(const int32_t* __restrict__ n2l, int64_t N, const int32_t* __restrict__ ns,
-                                const int32_t* __restrict__ ne, const double* __restrict__ x,
-                                const double* __restrict__ y, const double* __restrict__ z,
-                                const float* __restrict__ h, double factor, double* __restrict__ center,
-                                double* __restrict__ half)
+//! @brief tight boxes of leaf particles, optionally expanded per particle by factor*h. One wave per node: the
+//!        lanes read the leaf's particles coalesced and reduce min/max across the wave (a thread per leaf looping
+//!        over its particles touched 64 cache lines per load instruction).
+__global__ __launch_bounds__(256) void leafBoxesKernel(const int32_t* __restrict__ n2l, int64_t N,
+                                                       const int32_t* __restrict__ ns, const int32_t* __restrict__ ne,
+                                                       const double* __restrict__ x, const double* __restrict__ y,
+                                                       const double* __restrict__ z, const float* __restrict__ h,
+                                                       double factor, double* __restrict__ center,
+                                                       double* __restrict__ half)
 {
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= N || n2l[i] < 0) return;
+    const int64_t i = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (i >= N || n2l[i] < 0) return; // wave-uniform
+    const int lane = threadIdx.x & 63;
     double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
-    for (int32_t p = ns[i]; p < ne[i]; ++p)
+    for (int32_t p = ns[i] + lane; p < ne[i]; p += 64)
     {
         double r    = h ? factor * double(h[p]) : 0.0;
         double v[3] = {x[p], y[p], z[p]};
@@ -201,14 +205,20 @@ __global__ void leafBoxesKernel(const int32_t* __restrict__ n2l, int64_t N, cons
             mx[d] = fmax(mx[d], v[d] + r);
         }
     }
-    storeBox(center, half, i, mn, mx);
+    for (int d = 0; d < 3; ++d)
+    {
+        mn[d] = waveMin(mn[d]);
+        mx[d] = waveMax(mx[d]);
+    }
+    if (lane == 0) storeBox(center, half, i, mn, mx);
 }
 
 void leafBoxes(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
                const double* y, const double* z, const float* h, double factor, double* center, double* half,
                hipStream_t s)
 {
-    leafBoxesKernel<<<gridFor(N, 128), 128, 0, s>>>(n2l, N, ns, ne, x, y, z, h, factor, center, half);
+    if (N <= 0) return;
+    leafBoxesKernel<<<unsigned((N + 3) / 4), 256, 0, s>>>(n2l, N, ns, ne, x, y, z, h, factor, center, half);
     SPHX_LAUNCH_CHECK();
 }
 

@@ -15,6 +15,7 @@ Storage layouts
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -54,6 +55,8 @@ class NeighborSearchError(RuntimeError):
 _SCRATCH: dict = {}
 # test hook: >0 shrinks the LDS frontier of the GPU search so that groups take the global-memory spill path
 TEST_FRONT_CAP = 0
+# collect per-step search statistics on the GPU (rounds, candidate leaves; a few atomics per group)
+COLLECT_STATS = os.environ.get("SPHX_SEARCH_STATS") == "1"
 
 
 def _scratch(nbytes: int, device) -> torch.Tensor:
@@ -80,18 +83,21 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         need = max(num_groups, 1) * GROUP * _round4(ngmax) + 2 * 4 * GROUP
         if nidx is None or nidx.numel() < need:
             nidx = torch.empty(need, dtype=torch.int32, device=x.device)
-        stats = torch.zeros(4, dtype=torch.int64, device=x.device)
+        stats = torch.zeros(8, dtype=torch.int64, device=x.device)
         scratch = _scratch(hp.neighbor_scratch_bytes(n), x.device)
         hp.find_neighbors(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), tree.num_nodes,
                           tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
                           tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
-                          d.ng0, ngmax, nidx.data_ptr(), nc.data_ptr(), int(iterate_h), stats.data_ptr(),
+                          d.ng0, ngmax, nidx.data_ptr(), nc.data_ptr(), int(iterate_h) | (2 if COLLECT_STATS else 0),
+                          stats.data_ptr(),
                           scratch.data_ptr(), TEST_FRONT_CAP, _stream())
         st = stats.cpu()
         if int(st[1]) > 0:
             raise NeighborSearchError(f"GPU traversal stack overflow in {int(st[1])} groups")
         d.nc_fail = int(st[0])
         d.nc_spilled = int(st[2])
+        d.nc_rounds = int(st[3]) / max(num_groups, 1)  # mean search rounds per group (h iteration)
+        d.nc_leaves = int(st[4]) / max(num_groups, 1)  # mean candidate leaves per group and step
         return NeighborList(nidx, first, last, ngmax, True)
 
     need = max(n, 1) * ngmax
