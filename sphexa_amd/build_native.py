@@ -45,6 +45,18 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _flags_changed(obj_dir, tag, flags):
+    """True (and records the new set) if the compile flags of ``tag`` differ from the last build's"""
+    stamp = os.path.join(obj_dir, f".{tag}.flags")
+    cur = " ".join(flags)
+    old = open(stamp).read() if os.path.exists(stamp) else None
+    if old != cur:
+        with open(stamp, "w") as f:
+            f.write(cur)
+        return True
+    return False
+
+
 def _run(cmd):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -108,11 +120,12 @@ def build_hip(verbose=False, variant=None, defines=()):
              "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
              f"-I{os.path.join(CSRC, 'include')}", f"-I{os.path.join(CSRC, 'hip')}"] + list(defines) + _py_includes()
     hdrs = _headers() + glob.glob(os.path.join(CSRC, "hip", "*.h"))
+    force = _flags_changed(obj_dir, "hip", flags)
     jobs, objs = [], []
     for s in srcs:
         o = os.path.join(obj_dir, "hip_" + os.path.basename(s) + ".o")
         objs.append(o)
-        if _newer(o, [s] + hdrs):
+        if force or _newer(o, [s] + hdrs):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
             jobs.append(([hipcc, *flags, *lang, "-c", s, "-o", o], o))
     _compile_all(jobs, verbose)
