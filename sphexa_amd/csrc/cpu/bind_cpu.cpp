@@ -28,6 +28,7 @@ void xmass(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const
 void veDefGradh(int64_t, int64_t, const SphConsts&, const Box&, const int32_t*, const uint32_t*, const double*,
                 const double*, const double*, const float*, const float*, const float*, const float*, const float*,
                 float*, float*);
+void eosPolytropic(int64_t first, int64_t last, const float* kx, const float* xm, const float* m, float* p, float* c);
 void eosVe(int64_t, int64_t, const SphConsts&, const double*, const float*, const float*, const float*, const float*,
            float*, float*, float*, float*);
 void eosStd(int64_t, int64_t, const SphConsts&, const double*, const float*, float*, float*, float*);
@@ -268,6 +269,8 @@ PYBIND11_MODULE(_sphx_cpu, m)
                          P<float>(gradh), P<float>(prho), P<float>(c), P<float>(rho), P<float>(p));
           });
 
+    m.def("eos_polytropic", [](int64_t first, int64_t last, Ptr kx, Ptr xm, Ptr mm, Ptr p, Ptr c)
+          { cpu::eosPolytropic(first, last, P<float>(kx), P<float>(xm), P<float>(mm), P<float>(p), P<float>(c)); });
     m.def("eos_std", [](int64_t first, int64_t last, const ConstArr& sc, Ptr temp, Ptr mm, Ptr rho, Ptr p, Ptr c)
           {
               cpu::eosStd(first, last, toConsts(sc), P<double>(temp), P<float>(mm), P<float>(rho), P<float>(p),

@@ -123,6 +123,19 @@ void eosVe(int64_t first, int64_t last, const SphConsts& sc, const double* temp,
     }
 }
 
+//! @brief polytropic EOS with rho = kx m / xm (reference computeEOS_Polytropic)
+void eosPolytropic(int64_t first, int64_t last, const float* kx, const float* xm, const float* m, float* p, float* c)
+{
+#pragma omp parallel for schedule(static)
+    for (int64_t i = first; i < last; ++i)
+    {
+        double rho = double(kx[i]) * m[i] / xm[i], pi, ci;
+        polytropicEOS(rho, pi, ci);
+        p[i] = float(pi);
+        c[i] = float(ci);
+    }
+}
+
 void eosStd(int64_t first, int64_t last, const SphConsts& sc, const double* temp, const float* m, float* rho,
             float* p, float* c)
 {

@@ -205,6 +205,8 @@ PYBIND11_MODULE(_sphx_hip, m)
               eosVe(first, last, toConsts(c), P<double>(temp), P<float>(mm), P<float>(kx), P<float>(xm),
                     P<float>(gradh), P<float>(prho), P<float>(cc), P<float>(rho), P<float>(p), St(s));
           });
+    m.def("eos_polytropic", [](int64_t first, int64_t last, Ptr kx, Ptr xm, Ptr mm, Ptr p, Ptr c, Ptr s)
+          { eosPolytropic(first, last, P<float>(kx), P<float>(xm), P<float>(mm), P<float>(p), P<float>(c), St(s)); });
     m.def("eos_std", [](int64_t first, int64_t last, const ConstArr& c, Ptr temp, Ptr mm, Ptr rho, Ptr p, Ptr cc,
                         Ptr s)
           {

@@ -219,6 +219,26 @@ __global__ void eosVeKernel(int64_t first, int64_t last, SphConsts sc, const dou
     if (p) p[i] = float(pi);
 }
 
+__global__ void eosPolytropicKernel(int64_t first, int64_t last, const float* __restrict__ kx,
+                                    const float* __restrict__ xm, const float* __restrict__ m, float* __restrict__ p,
+                                    float* __restrict__ c)
+{
+    int64_t i = first + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= last) return;
+    double rho = double(kx[i]) * m[i] / xm[i], pi, ci;
+    polytropicEOS(rho, pi, ci);
+    p[i] = float(pi);
+    c[i] = float(ci);
+}
+
+void eosPolytropic(int64_t first, int64_t last, const float* kx, const float* xm, const float* m, float* p, float* c,
+                   hipStream_t s)
+{
+    if (last <= first) return;
+    eosPolytropicKernel<<<gridFor(last - first, 256), 256, 0, s>>>(first, last, kx, xm, m, p, c);
+    SPHX_LAUNCH_CHECK();
+}
+
 __global__ void eosStdKernel(int64_t first, int64_t last, SphConsts sc, const double* __restrict__ temp,
                              const float* __restrict__ m, float* __restrict__ rho, float* __restrict__ p,
                              float* __restrict__ c)

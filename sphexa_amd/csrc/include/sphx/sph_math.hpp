@@ -161,6 +161,16 @@ SPHX_HD void idealGasEOS(double temp, double rho, double mui, double gamma, doub
     c          = sqrt(tmp);
 }
 
+/*! @brief polytropic EOS p = K rho^gamma (gamma = 3) of a 1.4 M_sun, 12.8 km neutron star (K fixed for that star,
+ *         reference sph/include/sph/eos.hpp:50-85 polytropicEOS / computeEOS_Polytropic); returns p, c
+ */
+SPHX_HD void polytropicEOS(double rho, double& p, double& c)
+{
+    constexpr double Kpol = 2.246341237993810232e-10, gammaPol = 3.0;
+    p                     = Kpol * rho * rho * rho;
+    c                     = sqrt(gammaPol * p / rho);
+}
+
 //! @brief ideal gas EOS from internal energy: returns p, c
 SPHX_HD void idealGasEOSu(double u, double rho, double gamma, double& p, double& c)
 {

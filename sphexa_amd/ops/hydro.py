@@ -95,6 +95,16 @@ def compute_eos_ve(d, first: int, last: int):
         _lib.cpu().eos_ve(*args)
 
 
+def compute_eos_polytropic(d, first: int, last: int):
+    """p, c from the polytropic neutron-star EOS with rho = kx m / xm (reference sph/eos.hpp:50-85)"""
+    args = (first, last, d["kx"].data_ptr(), d["xm"].data_ptr(), d["m"].data_ptr(), d["p"].data_ptr(),
+            d["c"].data_ptr())
+    if _is_gpu(d):
+        _lib.hip().eos_polytropic(*args, _stream())
+    else:
+        _lib.cpu().eos_polytropic(*args)
+
+
 def compute_eos_std(d, first: int, last: int):
     args = (first, last, d.consts_array(), d["temp"].data_ptr(), d["m"].data_ptr(), d["rho"].data_ptr(),
             d["p"].data_ptr(), d["c"].data_ptr())

@@ -1,4 +1,4 @@
-"""Radiative cooling (reference physics/cooling + propagator std_hydro_grackle.hpp + init evrard_cooling_init.hpp):
+"""Radiative cooling and the polytropic EOS (reference physics/cooling + propagator std_hydro_grackle.hpp + init evrard_cooling_init.hpp):
 equilibrium cooling function, implicit particle cooling, the std-cooling propagator on the evrard-cooling case, and
 HIP vs OpenMP parity of the cooling kernels."""
 
@@ -86,3 +86,21 @@ def test_cooling_kernels_gpu_match_cpu(gpu):
     assert torch.allclose(out[0][0], out[1][0], rtol=1e-9, atol=1e-12)
     assert torch.allclose(out[0][1], out[1][1]) and torch.allclose(out[0][2], out[1][2])
     assert abs(out[0][3] - out[1][3]) <= 1e-9 * out[0][3]
+
+
+def test_polytropic_eos():
+    """reference sph/eos.hpp:50-85: p = K rho^3 (K = 2.2463e-10), c = sqrt(3 p / rho), rho = kx m / xm"""
+    from sphexa_amd.ops import hydro as H
+
+    class D(dict):
+        device = torch.device("cpu")
+
+    n = 100
+    g = torch.Generator().manual_seed(0)
+    d = D({k: torch.rand(n, generator=g) + 0.5 for k in ("kx", "xm", "m")})
+    d.update(p=torch.zeros(n), c=torch.zeros(n))
+    H.compute_eos_polytropic(d, 0, n)
+    rho = d["kx"].double() * d["m"].double() / d["xm"].double()
+    p = 2.246341237993810232e-10 * rho ** 3
+    assert torch.allclose(d["p"].double(), p, rtol=1e-6)
+    assert torch.allclose(d["c"].double(), torch.sqrt(3 * p / rho), rtol=1e-6)
