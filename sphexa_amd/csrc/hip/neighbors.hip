@@ -32,7 +32,7 @@ namespace sphx::hip
 
 constexpr int kWavesPerBlock = 4;
 constexpr int kFrontCap      = 512;
-constexpr int kLeafCap       = 512;
+constexpr int kLeafCap       = 512; // LDS candidate-leaf list per wave (A/B: 1024 costs occupancy, 512 spills few groups)
 constexpr int kRing          = 8; // hit ring slots per lane (two list blocks)
 constexpr int kRingStride    = 9; // LDS words per lane (odd: the 32 lanes of a ds_write_b32 group hit distinct banks)
 
