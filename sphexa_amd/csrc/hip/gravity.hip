@@ -20,26 +20,57 @@
 namespace sphx::hip
 {
 
-__global__ void gravityLeavesKernel(const int32_t* __restrict__ n2l, int64_t N, const int32_t* __restrict__ ns,
-                                    const int32_t* __restrict__ ne, const double* __restrict__ x,
-                                    const double* __restrict__ y, const double* __restrict__ z,
-                                    const float* __restrict__ m, double* __restrict__ centers,
-                                    Quadrupole* __restrict__ mp)
+//! @brief leaf mass centers and traceless quadrupoles (p2m), one wave per node: the lanes read the leaf's particles
+//!        coalesced and the moments are wave reductions (a thread per leaf looping over its particles touched 64
+//!        cache lines per load instruction)
+__global__ __launch_bounds__(256) void gravityLeavesKernel(const int32_t* __restrict__ n2l, int64_t N,
+                                                           const int32_t* __restrict__ ns,
+                                                           const int32_t* __restrict__ ne,
+                                                           const double* __restrict__ x, const double* __restrict__ y,
+                                                           const double* __restrict__ z, const float* __restrict__ m,
+                                                           double* __restrict__ centers, Quadrupole* __restrict__ mp)
 {
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= N || n2l[i] < 0) return;
+    const int64_t i = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (i >= N || n2l[i] < 0) return; // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int32_t a = ns[i], b = ne[i];
     double c[4] = {0, 0, 0, 0};
-    for (int32_t p = ns[i]; p < ne[i]; ++p)
+    for (int32_t p = a + lane; p < b; p += 64)
     {
-        c[0] += m[p] * x[p];
-        c[1] += m[p] * y[p];
-        c[2] += m[p] * z[p];
-        c[3] += m[p];
+        double mi = m[p];
+        c[0] += mi * x[p];
+        c[1] += mi * y[p];
+        c[2] += mi * z[p];
+        c[3] += mi;
     }
-    double inv    = c[3] != 0 ? 1.0 / c[3] : 0.0;
-    double com[3] = {c[0] * inv, c[1] * inv, c[2] * inv};
+    for (int k = 0; k < 4; ++k)
+        c[k] = waveSum(c[k]);
+    const double inv    = c[3] != 0 ? 1.0 / c[3] : 0.0;
+    const double com[3] = {c[0] * inv, c[1] * inv, c[2] * inv};
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int32_t p = a + lane; p < b; p += 64)
+    {
+        double rx = x[p] - com[0], ry = y[p] - com[1], rz = z[p] - com[2], mi = m[p];
+        acc[0] += rx * rx * mi;
+        acc[1] += rx * ry * mi;
+        acc[2] += rx * rz * mi;
+        acc[3] += ry * ry * mi;
+        acc[4] += ry * rz * mi;
+        acc[5] += rz * rz * mi;
+    }
+    for (int k = 0; k < 6; ++k)
+        acc[k] = waveSum(acc[k]);
+    if (lane != 0) return;
+    const double tr = acc[0] + acc[3] + acc[5];
     Quadrupole q;
-    p2m(x, y, z, m, ns[i], ne[i], com, q);
+    q.q[qMass]         = MT(c[3]);
+    q.q[qXX]           = MT(3 * acc[0] - tr);
+    q.q[qYY]           = MT(3 * acc[3] - tr);
+    q.q[qZZ]           = MT(3 * acc[5] - tr);
+    q.q[qXY]           = MT(3 * acc[1]);
+    q.q[qXZ]           = MT(3 * acc[2]);
+    q.q[qYZ]           = MT(3 * acc[4]);
+    q.q[qTrace]        = MT(tr);
     mp[i]              = q;
     centers[4 * i + 0] = com[0];
     centers[4 * i + 1] = com[1];
@@ -99,7 +130,8 @@ __global__ void gravitySetMacKernel(int64_t N, const KeyT* __restrict__ prefixes
 void gravityLeaves(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
                    const double* y, const double* z, const float* m, double* centers, void* mp, hipStream_t s)
 {
-    gravityLeavesKernel<<<gridFor(N, 128), 128, 0, s>>>(n2l, N, ns, ne, x, y, z, m, centers, (Quadrupole*)mp);
+    if (N <= 0) return;
+    gravityLeavesKernel<<<unsigned((N + 3) / 4), 256, 0, s>>>(n2l, N, ns, ne, x, y, z, m, centers, (Quadrupole*)mp);
     SPHX_LAUNCH_CHECK();
 }
 

@@ -56,7 +56,7 @@ __device__ __forceinline__ float4* waveTile(float4* blockTile)
 template<class R>
 __device__ __forceinline__ CoopLoader<R> coopOf(const R* rec, float4* blockTile, int64_t self, const NbrArgs& a)
 {
-    return CoopLoader<R>{rec, waveTile<R>(blockTile), unsigned(self), a.ntot - 1};
+    return CoopLoader<R>{rec, waveTile<R>(blockTile), unsigned(self)};
 }
 
 //! @brief the launchers' view of the neighbor arguments with the record count set

@@ -459,23 +459,12 @@ struct CoopLoader
 {
     const R* r;
     float4* tile; // 64 * (C | 1) float4 of LDS per wave
-    unsigned self;
-    unsigned last; // highest valid record index (clamps the indices of finished lanes' slots)
+    unsigned self; // the target's own record: stands in for list entries past the lane's count
     static constexpr int C = int(sizeof(R) / 16);
     static constexpr int S = C | 1;
     static_assert(sizeof(R) % 16 == 0, "records are whole float4s");
 
     __device__ R operator()(unsigned j) const { return r[j]; }
-
-    //! @brief index of the record whose chunk this lane fetches in instruction q of step k: read straight from the
-    //!        lane-interleaved list (the 64 indices of a step are one 256-byte segment), clamped for finished lanes
-    template<class Idx>
-    __device__ __forceinline__ unsigned index(const Idx* nbr, int stride, unsigned k, int q) const
-    {
-        const int lane = threadIdx.x & 63;
-        const int rr   = (q * 64 + lane) / C;
-        return min(unsigned(nbr[int(k) * stride + (rr - lane)]), last);
-    }
 
     //! @brief index of the record whose chunk this lane fetches in instruction q, from the owning lane's index j
     __device__ __forceinline__ unsigned spread(unsigned j, int q) const
@@ -506,11 +495,7 @@ template<int B, class Idx, class R, class F>
 __device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const CoopLoader<R>& ld, F&& f)
 {
     constexpr int C = CoopLoader<R>::C;
-#ifdef SPHX_NO_COOP
-    constexpr bool direct = true; // A/B switch: per-lane record gathers everywhere
-#else
     constexpr bool direct = C < SPHX_COOP_MIN_CHUNKS;
-#endif
     if constexpr (direct)
     {
         // small records (cooperative path measured slower for 32 B): per-lane gathers, one list block (4 indices) and its records in flight (a deeper
