@@ -22,7 +22,22 @@ def main():
         for i, l in enumerate(body):
             m = re.match(r"^\.(LBB\w+):.*Loop Header: Depth=(\d)", l)
             if not m:
-                continue
+                # nested headers carry the label on the previous line
+                m2 = re.match(r"^\s*; =>.*Loop Header: Depth=(\d)", l)
+                if not m2 or i == 0:
+                    continue
+                ml = re.match(r"^\.(LBB\w+):", body[i - 1])
+                if not ml:
+                    continue
+
+                class _M:
+                    def __init__(self, a, b):
+                        self.g = (a, b)
+
+                    def group(self, k):
+                        return self.g[k - 1]
+
+                m = _M(ml.group(1), m2.group(1))
             tag = "Header=" + m.group(1)[1:] if m.group(1).startswith("L") else m.group(1)
             tag = "Header=" + m.group(1).replace("LBB", "BB")
             # every block of the loop carries "in Loop: Header=BBx_y" (or is the header): gather their instructions

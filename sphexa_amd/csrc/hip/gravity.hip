@@ -193,6 +193,7 @@ struct GravLists
     int32_t* plst; // particle indices of opened leaves (P2P)
     float4* spos;  // staged P2P tile: {x, y, z, |x|^2} relative to the group center; M2P: 3 x 64 records
     float4* smh;   // staged P2P tile: {m, h, h^2, 0}
+    float4* sxm;   // staged P2P tile for the VALU path: {x, y, z, m}, then the 64 h values as 16 float4
 };
 
 /*! @brief M2P of a list of nodes, 64 per batch: lane k gathers node k's expansion center (fp32, relative to the
@@ -356,8 +357,6 @@ __device__ inline void flushP2P(const int32_t* plst, int n, const GravLists& L, 
         // padding source: m = 0 at the group center with h = 1 (finite weight, zero contribution)
         const float4 Pn = valid ? make_float4(sx, sy, sz, sx * sx + sy * sy + sz * sz) : make_float4(0, 0, 0, 0);
         const float4 Qn = valid ? make_float4(rm, rh, rh * rh, 0.f) : make_float4(0.f, 1.f, 1.f, 0.f);
-        L.spos[lane]    = Pn;
-        L.smh[lane]     = Qn;
         const int cnt   = min(64, n - c0);
 #ifdef SPHX_GRAV_VALU_P2P
         const bool mfma = false;
@@ -366,16 +365,46 @@ __device__ inline void flushP2P(const int32_t* plst, int n, const GravLists& L, 
         const float hh  = hs + T.hminT;
         const bool mfma = waveMax(Pn.w) + T.maxT2 <= kMfmaP2PTol * hh * hh;
 #endif
+        if (mfma)
+        {
+            L.spos[lane] = Pn;
+            L.smh[lane]  = Qn;
+        }
+        else
+        {
+            // VALU tile: one broadcast ds_read_b128 per source plus one per four h values (a float4 {x,y,z,|x|^2}
+            // + {m,h,h^2,0} pair is read as b96 + half a read2_b64: 8-cycle instructions on a shared LDS)
+            L.sxm[lane]                            = make_float4(Pn.x, Pn.y, Pn.z, Qn.x);
+            reinterpret_cast<float*>(L.sxm + 64)[lane] = Qn.y;
+        }
         jN = jNN;
         jNN = c0 + 128 + lane < n ? plst[c0 + 128 + lane] : plst[0];
         gather(jN); // unconditional (past the end: clamped index) so the loads land in the loop registers directly
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (!mfma)
         {
-            for (int k = 0; k < cnt; ++k)
+            int k = 0;
+            for (; k + 4 <= cnt; k += 4)
             {
-                float4 P = L.spos[k], Q = L.smh[k];
-                p2p(P.x - T.xr, P.y - T.yr, P.z - T.zr, Q.x, T.hi, Q.y, T.v);
+                float4 H = L.sxm[64 + (k >> 2)];
+                float4 P[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    P[u] = L.sxm[k + u];
+                // whole-register uses keep the broadcast reads at full width (b128: 4 LDS cycles per wave)
+                asm volatile("" : "+v"(H.x), "+v"(H.y), "+v"(H.z), "+v"(H.w));
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    asm volatile("" : "+v"(P[u].x), "+v"(P[u].y), "+v"(P[u].z), "+v"(P[u].w));
+                const float hu[4] = {H.x, H.y, H.z, H.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    p2p(P[u].x - T.xr, P[u].y - T.yr, P[u].z - T.zr, P[u].w, T.hi, hu[u], T.v);
+            }
+            for (; k < cnt; ++k)
+            {
+                float4 P = L.sxm[k];
+                p2p(P.x - T.xr, P.y - T.yr, P.z - T.zr, P.w, T.hi, reinterpret_cast<const float*>(L.sxm + 64)[k], T.v);
             }
             continue;
         }
@@ -623,7 +652,7 @@ struct GravLds
 
 __device__ __forceinline__ GravLists listsOf(GravLds& s)
 {
-    return GravLists{s.mlst, s.plst, s.stage, s.stage + 64};
+    return GravLists{s.mlst, s.plst, s.stage, s.stage + 64, s.stage}; // VALU tile aliases the MFMA tile
 }
 
 //! @brief global-memory interaction list slabs: per group capM node ids and capL leaf ids + 2 counts (-1: fallback)
