@@ -33,8 +33,13 @@ namespace sphx::hip
 constexpr int kWavesPerBlock = 4;
 constexpr int kFrontCap      = 512;
 constexpr int kLeafCap       = 512; // LDS candidate-leaf list per wave (A/B: 1024 costs occupancy, 512 spills few groups)
-constexpr int kRing          = 8; // hit ring slots per lane (two list blocks)
-constexpr int kRingStride    = 9; // LDS words per lane (odd: the 32 lanes of a ds_write_b32 group hit distinct banks)
+constexpr int kRing          = 16; // hit ring slots per lane (four list blocks)
+constexpr int kRingStride    = 17; // LDS words per lane (odd: the 32 lanes of a ds_write_b32 group hit distinct banks)
+constexpr int kStage         = 128; // staged candidate sources per wave (float4 {x, y, z, j}, group-relative fp32)
+constexpr int kRingWords     = 64 * kRingStride;
+//! per-wave LDS work area: the traversal frontiers, then (candidate phase) the hit ring + the staging ring
+constexpr int kWorkWords = 2 * kFrontCap > kRingWords + 4 * kStage ? 2 * kFrontCap : kRingWords + 4 * kStage;
+static_assert((kRingWords * 4) % 16 == 0, "staging ring must be 16-B aligned");
 
 //! @brief fold a coordinate difference into [-L/2, L/2] in periodic dimensions
 __device__ __forceinline__ double foldMin(double dx, const Box& b, int d)
@@ -86,7 +91,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                                             unsigned ngmax, int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
                                             int iterateH, unsigned long long* __restrict__ stats, int32_t* frontA,
                                             int32_t* frontB, int32_t* leaves, int frontCap, int leafCap,
-                                            int32_t* ring)
+                                            int32_t* work)
 {
     // the tree is read-only here: restrict-qualified views let the uniform leaf loads go through the scalar cache
     const TreeView t{tree.child, tree.n2l, tree.ns, tree.ne, tree.center, tree.half};
@@ -104,7 +109,9 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     }
     const unsigned ngmax4 = (ngmax + 3) & ~3u;
     int4* nlist           = reinterpret_cast<int4*>(nidx + g * int64_t(ngmax4) * 64) + lane;
-    int32_t* myRing       = ring + lane * kRingStride;
+    // hit ring and staging ring alias the frontiers (fast path): they are only live in the candidate phase
+    int32_t* myRing       = work + lane * kRingStride;
+    float4* stage         = reinterpret_cast<float4*>(work + kRingWords);
     const unsigned ngmin = ng0 / 4;
 
     unsigned ncSph = 1;
@@ -205,6 +212,42 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                 fb++;
             }
         };
+        // test `count` (a multiple of 4) staged sources against every lane; one flush check per four sources
+        // (pending <= 11 after a check, <= 15 before the next: fits the 16-slot ring)
+        unsigned sHead = 0, sTail = 0; // wave-uniform positions in the staging ring
+        auto testStaged = [&](unsigned count)
+        {
+            for (unsigned k = 0; k < count; k += 4)
+            {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                {
+                    const float4 s   = stage[(sHead + k + u) & (kStage - 1)]; // broadcast ds_read_b128
+                    const float dx   = s.x - xir;
+                    const float dy   = s.y - yir;
+                    const float dz   = s.z - zir;
+                    const float d2   = dx * dx + dy * dy + dz * dz;
+                    const int32_t jj = __float_as_int(s.w);
+                    bool hit         = d2 < r2f - band;
+                    const bool maybe = !hit && d2 <= r2f + band;
+                    if (ballot(maybe)) // rare: fp64 re-test of candidates in the rounding band
+                    {
+                        const int32_t ju = __builtin_amdgcn_readfirstlane(jj);
+                        const bool h64   = distanceSqPbc(ldConst(x + ju), ldConst(y + ju), ldConst(z + ju), xi, yi,
+                                                         zi, box) < radiusSq;
+                        hit = hit || (maybe && h64);
+                    }
+                    if (valid && hit && jj != int32_t(i))
+                    {
+                        if (cnt < ngmax) myRing[cnt & (kRing - 1)] = jj;
+                        cnt++;
+                    }
+                }
+                const unsigned pend = min(cnt, ngmax) - 4 * fb;
+                if (ballot(pend >= 12u)) flushBlock(pend >= 4);
+            }
+            sHead += count;
+        };
         for (int l = 0; l < nLeaves; ++l)
         {
             int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + l));
@@ -231,38 +274,35 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     // only sources inside the group search box can be a neighbor of any lane
                     inBox = !relOk || (fabsf(xr) <= gsf[0] && fabsf(yr) <= gsf[1] && fabsf(zr) <= gsf[2]);
                 }
-                for (uint64_t mask = ballot(inBox); mask; mask &= mask - 1)
+                // compact the in-box sources into the staging ring (source order kept: deterministic lists)
+                const uint64_t m = ballot(inBox);
+                if (inBox)
+                    stage[(sTail + unsigned(__popcll(m & lanemaskLt()))) & (kStage - 1)] =
+                        make_float4(xr, yr, zr, __int_as_float(j));
+                sTail += unsigned(__popcll(m));
+                if (sTail - sHead >= 64)
                 {
-                    const int k = __builtin_ctzll(mask);
-                    float dx = readLaneF(xr, k) - xir;
-                    float dy = readLaneF(yr, k) - yir;
-                    float dz = readLaneF(zr, k) - zir;
-                    float d2 = dx * dx + dy * dy + dz * dz;
-                    const int64_t jj = int64_t(c0) + k;
-                    bool hit   = d2 < r2f - band;
-                    if (!hit && d2 <= r2f + band)
-                    {
-                        hit = distanceSqPbc(ldConst(x + jj), ldConst(y + jj), ldConst(z + jj), xi, yi, zi, box) <
-                              radiusSq;
-                    }
-                    const bool mine = valid && hit && jj != i;
-                    if (mine)
-                    {
-                        if (cnt < ngmax) myRing[cnt & (kRing - 1)] = int32_t(jj);
-                        cnt++;
-                    }
-                    // a full ring (8 pending) forces a flush of every lane holding a whole block
-                    const unsigned pend = min(cnt, ngmax) - 4 * fb;
-                    if (ballot(pend >= unsigned(kRing))) flushBlock(pend >= 4);
+                    waveSync<false>();
+                    testStaged(64);
                 }
             }
         }
+        {
+            // pad the tail to a multiple of 4 with far-away sentinels (d2 = inf: never a hit, never in the band)
+            const unsigned rem = sTail - sHead;
+            const unsigned pad = (4 - (rem & 3)) & 3;
+            if (unsigned(lane) < pad)
+                stage[(sTail + lane) & (kStage - 1)] = make_float4(1e30f, 1e30f, 1e30f, __int_as_float(-1));
+            waveSync<false>();
+            testStaged(rem + pad);
+        }
         ncSph = 1 + cnt;
-        // remaining entries (at most 7 per lane; block tails beyond the count are never read)
+        // remaining entries (at most 11 per lane; block tails beyond the count are never read)
         {
             unsigned pend = min(cnt, ngmax) - 4 * fb;
             flushBlock(pend > 0);
             flushBlock(pend > 4);
+            flushBlock(pend > 8);
         }
 
         // 4. smoothing length iteration
@@ -294,10 +334,8 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
                                                            int iterateH, unsigned long long* __restrict__ stats,
                                                            int32_t* __restrict__ spillList, int frontCap)
 {
-    __shared__ int32_t frontA[kWavesPerBlock][kFrontCap];
-    __shared__ int32_t frontB[kWavesPerBlock][kFrontCap];
+    __shared__ __attribute__((aligned(16))) int32_t work[kWavesPerBlock][kWorkWords];
     __shared__ int32_t leaves[kWavesPerBlock][kLeafCap];
-    __shared__ int32_t ring[kWavesPerBlock][64 * kRingStride];
 
     const int wave          = threadIdx.x >> 6;
     const int64_t numGroups = (last - first + 63) / 64;
@@ -306,7 +344,7 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
     if (g >= numGroups) return;
 
     bool ok = searchGroup<false>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
-                                 frontA[wave], frontB[wave], leaves[wave], frontCap, kLeafCap, ring[wave]);
+                                 work[wave], work[wave] + kFrontCap, leaves[wave], frontCap, kLeafCap, work[wave]);
     if (!ok && (threadIdx.x & 63) == 0)
     {
         unsigned long long slot = atomicAdd(&stats[2], 1ull);
@@ -331,7 +369,7 @@ __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, in
                                                                const int32_t* __restrict__ spillList,
                                                                int32_t* __restrict__ scratch)
 {
-    __shared__ int32_t ring[64 * kRingStride];
+    __shared__ __attribute__((aligned(16))) int32_t work[kRingWords + 4 * kStage];
     const int64_t numSpill = int64_t(__hip_atomic_load(&stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     int32_t* frontA = scratch + int64_t(blockIdx.x) * (2 * kSpillFront + kSpillLeaves);
     int32_t* frontB = frontA + kSpillFront;
@@ -340,7 +378,7 @@ __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, in
     {
         int64_t g = spillList[k];
         bool ok   = searchGroup<true>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
-                                      frontA, frontB, leaves, kSpillFront, kSpillLeaves, ring);
+                                      frontA, frontB, leaves, kSpillFront, kSpillLeaves, work);
         if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
     }
 }
