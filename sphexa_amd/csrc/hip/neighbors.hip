@@ -40,6 +40,7 @@ constexpr int kRingWords     = 64 * kRingStride;
 //! per-wave LDS work area: the traversal frontiers, then (candidate phase) the hit ring + the staging ring
 constexpr int kWorkWords = 2 * kFrontCap > kRingWords + 4 * kStage ? 2 * kFrontCap : kRingWords + 4 * kStage;
 static_assert((kRingWords * 4) % 16 == 0, "staging ring must be 16-B aligned");
+static_assert(kRingStride > kRing, "the padding word of a lane absorbs entries past ngmax");
 
 //! @brief fold a coordinate difference into [-L/2, L/2] in periodic dimensions
 __device__ __forceinline__ double foldMin(double dx, const Box& b, int d)
@@ -217,12 +218,26 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         unsigned sHead = 0, sTail = 0; // wave-uniform positions in the staging ring
         auto testStaged = [&](unsigned count)
         {
+            // four broadcast ds_read_b128 per batch, the next batch's issued before this batch's tests (software
+            // pipelined: one LDS latency per four sources instead of one per source). Reads past `count` stay
+            // inside the ring and are discarded.
+            float4 S[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                S[u] = stage[(sHead + u) & (kStage - 1)];
             for (unsigned k = 0; k < count; k += 4)
             {
+                float4 C[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                 {
-                    const float4 s   = stage[(sHead + k + u) & (kStage - 1)]; // broadcast ds_read_b128
+                    C[u] = S[u];
+                    S[u] = stage[(sHead + k + 4 + u) & (kStage - 1)];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                {
+                    const float4 s   = C[u];
                     const float dx   = s.x - xir;
                     const float dy   = s.y - yir;
                     const float dz   = s.z - zir;
@@ -239,7 +254,8 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     }
                     if (valid && hit && jj != int32_t(i))
                     {
-                        if (cnt < ngmax) myRing[cnt & (kRing - 1)] = jj;
+                        // entries past ngmax go to the lane's padding word (slot 16) instead of a guarded store
+                        myRing[cnt < ngmax ? int(cnt & (kRing - 1)) : kRing] = jj;
                         cnt++;
                     }
                 }
