@@ -169,6 +169,56 @@ __global__ void packStdKernel(int64_t n, StdFields f, SrcStd* __restrict__ out)
     out[i] = r;
 }
 
+/*! @brief XMass source record: coordinates as 32-bit fixed-point offsets in the box (16 B: one dwordx4 gather per
+ *         neighbor instead of two for the 32-B SrcPos). Periodic dimensions span the full 2^32 range, so the wrapping
+ *         int32 difference of two offsets IS the minimum image; open dimensions use 2^30 per box length (|dx| < 2L
+ *         stays in range). The pair separation is exact in the integers and rounds once when converted to fp32
+ *         (quantum <= 1e-9 L), i.e. to the same fp32 accuracy as the fp64 difference of the SrcPos path.
+ */
+struct alignas(16) SrcPosQ
+{
+    uint32_t x, y, z;
+    float m;
+};
+
+struct QFrame
+{
+    double lo[3], s[3]; // offset = rint((x - lo) * s) mod 2^32
+    float inv[3];       // separation = int32(offset_i - offset_j) * inv
+};
+
+inline QFrame qframeOf(const Box& b)
+{
+    QFrame q;
+    for (int d = 0; d < 3; ++d)
+    {
+        const double L = b.len(d) > 0 ? b.len(d) : 1.0;
+        q.lo[d]        = b.lo[d];
+        q.s[d]         = (b.periodic(d) ? 4294967296.0 : 1073741824.0) / L;
+        q.inv[d]       = float(1.0 / q.s[d]);
+    }
+    return q;
+}
+
+__device__ __forceinline__ uint32_t quantize(double v, double lo, double s)
+{
+    return uint32_t((unsigned long long)(long long)rint((v - lo) * s));
+}
+
+__global__ void packPosQKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                               const double* __restrict__ z, const float* __restrict__ m, QFrame q,
+                               SrcPosQ* __restrict__ out)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcPosQ r;
+    r.x    = quantize(x[i], q.lo[0], q.s[0]);
+    r.y    = quantize(y[i], q.lo[1], q.s[1]);
+    r.z    = quantize(z[i], q.lo[2], q.s[2]);
+    r.m    = m[i];
+    out[i] = r;
+}
+
 // ------------------------------------------------------------------------------------------------ VE loops
 
 __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, Box box, const float* __restrict__ h,
@@ -183,6 +233,31 @@ __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, B
     float v = xmassJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], coopOf(rec, tile, i, a),
                          KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice});
     if (valid) xm[i] = v;
+}
+
+//! @brief XMass on fixed-point records (see SrcPosQ): same sum as xmassJLoop (sph_math.hpp), half the gathers
+__global__ __launch_bounds__(kBlock) void xmassQKernel(NbrArgs a, SphConsts sc, QFrame q, const float* __restrict__ h,
+                                                       const SrcPosQ* __restrict__ rec, const float* __restrict__ wh,
+                                                       float* __restrict__ xm)
+{
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcPosQ>::S];
+    int64_t i;
+    const int32_t* nbr;
+    unsigned n;
+    const bool valid = targetOf(a, i, nbr, n);
+    const auto ld    = coopOf(rec, tile, i, a);
+    const KernelFn kf{wh, nullptr, sc.sincIndex, sc.kernelChoice};
+    const SrcPosQ pi = ld(unsigned(i));
+    const float hi = h[i], hInv = 1.f / hi, h3Inv = hInv * hInv * hInv;
+    float rho0 = pi.m;
+    forEachNeighbor<SPHX_BATCH_POS>(nbr, kBlockedList, n, ld, [&](unsigned, const SrcPosQ& pj) {
+        const float rx   = float(int32_t(pi.x - pj.x)) * q.inv[0];
+        const float ry   = float(int32_t(pi.y - pj.y)) * q.inv[1];
+        const float rz   = float(int32_t(pi.z - pj.z)) * q.inv[2];
+        const float dist = sqrtF(rx * rx + ry * ry + rz * rz);
+        rho0 += kf.w(dist * hInv) * pj.m;
+    });
+    if (valid) xm[i] = pi.m / (rho0 * float(sc.K) * h3Inv);
 }
 
 __global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts sc, Box box,
@@ -517,8 +592,14 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
            const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s)
 {
     if (a.last <= a.first) return;
+#ifdef SPHX_XMASS_FP64_RECORDS
     packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, nullptr, (SrcPos*)rec);
     xmassKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcPos*)rec, wh, xm);
+#else
+    const QFrame q = qframeOf(box);
+    packPosQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, q, (SrcPosQ*)rec);
+    xmassQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec, wh, xm);
+#endif
     SPHX_LAUNCH_CHECK();
 }
 
