@@ -192,12 +192,12 @@ PYBIND11_MODULE(_sphx_hip, m)
           });
     m.def("ve_def_gradh", [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc,
                              Ptr x, Ptr y, Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr whd, Ptr xm, Ptr kx, Ptr gradh,
-                             int64_t ntot, Ptr rec, Ptr s)
+                             int64_t ntot, Ptr rec, Ptr s, double mUniform)
           {
               auto sc = toConsts(c);
               veDefGradh(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
                          P<double>(z), P<float>(h), P<float>(mm), P<float>(wh), P<float>(whd), P<float>(xm),
-                         P<void>(rec), P<float>(kx), P<float>(gradh), St(s));
+                         P<void>(rec), P<float>(kx), P<float>(gradh), float(mUniform), St(s));
           });
     m.def("eos_ve", [](int64_t first, int64_t last, const ConstArr& c, Ptr temp, Ptr mm, Ptr kx, Ptr xm, Ptr gradh,
                        Ptr prho, Ptr cc, Ptr rho, Ptr p, Ptr s)

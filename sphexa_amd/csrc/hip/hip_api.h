@@ -104,7 +104,7 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
            const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s);
 void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                 const double* y, const double* z, const float* h, const float* m, const float* wh, const float* whd,
-                const float* xm, void* rec, float* kx, float* gradh, hipStream_t s);
+                const float* xm, void* rec, float* kx, float* gradh, float mUniform, hipStream_t s);
 void eosPolytropic(int64_t first, int64_t last, const float* kx, const float* xm, const float* m, float* p, float* c,
                    hipStream_t s);
 void eosVe(int64_t first, int64_t last, const SphConsts& sc, const double* temp, const float* m, const float* kx,

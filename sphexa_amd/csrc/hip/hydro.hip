@@ -169,42 +169,7 @@ __global__ void packStdKernel(int64_t n, StdFields f, SrcStd* __restrict__ out)
     out[i] = r;
 }
 
-/*! @brief XMass source record: coordinates as 32-bit fixed-point offsets in the box (16 B: one dwordx4 gather per
- *         neighbor instead of two for the 32-B SrcPos). Periodic dimensions span the full 2^32 range, so the wrapping
- *         int32 difference of two offsets IS the minimum image; open dimensions use 2^30 per box length (|dx| < 2L
- *         stays in range). The pair separation is exact in the integers and rounds once when converted to fp32
- *         (quantum <= 1e-9 L), i.e. to the same fp32 accuracy as the fp64 difference of the SrcPos path.
- */
-struct alignas(16) SrcPosQ
-{
-    uint32_t x, y, z;
-    float m;
-};
-
-struct QFrame
-{
-    double lo[3], s[3]; // offset = rint((x - lo) * s) mod 2^32
-    float inv[3];       // separation = int32(offset_i - offset_j) * inv
-};
-
-inline QFrame qframeOf(const Box& b)
-{
-    QFrame q;
-    for (int d = 0; d < 3; ++d)
-    {
-        const double L = b.len(d) > 0 ? b.len(d) : 1.0;
-        q.lo[d]        = b.lo[d];
-        q.s[d]         = (b.periodic(d) ? 4294967296.0 : 1073741824.0) / L;
-        q.inv[d]       = float(1.0 / q.s[d]);
-    }
-    return q;
-}
-
-__device__ __forceinline__ uint32_t quantize(double v, double lo, double s)
-{
-    return uint32_t((unsigned long long)(long long)rint((v - lo) * s));
-}
-
+//! @brief XMass source records on the fixed-point frame (QFrame, sph_math.hpp): one dwordx4 gather per neighbor
 __global__ void packPosQKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
                                const double* __restrict__ z, const float* __restrict__ m, QFrame q,
                                SrcPosQ* __restrict__ out)
@@ -217,6 +182,77 @@ __global__ void packPosQKernel(int64_t n, const double* __restrict__ x, const do
     r.z    = quantize(z[i], q.lo[2], q.s[2]);
     r.m    = m[i];
     out[i] = r;
+}
+
+__global__ void packXmQKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                              const double* __restrict__ z, const float* __restrict__ xm, QFrame q,
+                              SrcXmQ* __restrict__ out)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcXmQ r;
+    r.x    = quantize(x[i], q.lo[0], q.s[0]);
+    r.y    = quantize(y[i], q.lo[1], q.s[1]);
+    r.z    = quantize(z[i], q.lo[2], q.s[2]);
+    r.xm   = xm[i];
+    out[i] = r;
+}
+
+__global__ void packIadQKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                               const double* __restrict__ z, const float* __restrict__ kx,
+                               const float* __restrict__ vx, const float* __restrict__ vy,
+                               const float* __restrict__ vz, const float* __restrict__ xm, QFrame q,
+                               SrcIadQ* __restrict__ out)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcIadQ r;
+    r.x    = quantize(x[i], q.lo[0], q.s[0]);
+    r.y    = quantize(y[i], q.lo[1], q.s[1]);
+    r.z    = quantize(z[i], q.lo[2], q.s[2]);
+    r.vol  = xm[i] / kx[i];
+    r.vx   = vx[i];
+    r.vy   = vy[i];
+    r.vz   = vz[i];
+    r.xm   = xm[i];
+    out[i] = r;
+}
+
+__global__ void packMomQKernel(int64_t n, MomFields f, QFrame q, SrcMomQ* __restrict__ out,
+                               SrcGradV* __restrict__ gv)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcMomQ r;
+    r.x     = quantize(f.x[i], q.lo[0], q.s[0]);
+    r.y     = quantize(f.y[i], q.lo[1], q.s[1]);
+    r.z     = quantize(f.z[i], q.lo[2], q.s[2]);
+    r.vx    = f.vx[i];
+    r.vy    = f.vy[i];
+    r.vz    = f.vz[i];
+    r.ih    = 1.0f / f.h[i];
+    r.c11   = f.cij[0][i];
+    r.c12   = f.cij[1][i];
+    r.c13   = f.cij[2][i];
+    r.c22   = f.cij[3][i];
+    r.c23   = f.cij[4][i];
+    r.c33   = f.cij[5][i];
+    r.m     = f.m[i];
+    r.c     = f.c[i];
+    r.xm    = f.xm[i];
+    r.rho   = f.kx[i] * f.m[i] / f.xm[i];
+    r.prho  = f.prho[i];
+    r.alpha = f.alpha[i];
+    r.mrho  = f.m[i] / r.rho;
+    out[i]  = r;
+    if (gv)
+    {
+        SrcGradV g;
+        for (int k = 0; k < 6; ++k)
+            g.dV[k] = f.dV[k][i];
+        g.pad[0] = g.pad[1] = 0.f;
+        gv[i]                = g;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------ VE loops
@@ -260,19 +296,21 @@ __global__ __launch_bounds__(kBlock) void xmassQKernel(NbrArgs a, SphConsts sc, 
     if (valid) xm[i] = pi.m / (rho0 * float(sc.K) * h3Inv);
 }
 
-__global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts sc, Box box,
-                                                           const float* __restrict__ h, const SrcPos* __restrict__ rec,
+template<class R, class G>
+__global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts sc, G box,
+                                                           const float* __restrict__ h, const R* __restrict__ rec,
                                                            const float* __restrict__ wh, const float* __restrict__ whd,
-                                                           float* __restrict__ kx, float* __restrict__ gradh)
+                                                           float* __restrict__ kx, float* __restrict__ gradh,
+                                                           float mUniform)
 {
-    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcPos>::S];
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
     const bool valid = targetOf(a, i, nbr, n);
     float k, g;
     veDefGradhJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], coopOf(rec, tile, i, a),
-                    KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice}, k, g);
+                    KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice}, k, g, mUniform);
     if (!valid) return;
     kx[i]    = k;
     gradh[i] = g;
@@ -351,15 +389,16 @@ __global__ __launch_bounds__(kBlock) void iadKernel(NbrArgs a, SphConsts sc, Box
 }
 
 //! @brief IAD matrix, then divv/curlv (+ velocity gradient) in the same kernel over the same neighbor list
-__global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConsts sc, Box box,
+template<class R, class G>
+__global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConsts sc, G box,
                                                              const float* __restrict__ h,
                                                              const float* __restrict__ kx,
-                                                             const SrcIad* __restrict__ rec,
+                                                             const R* __restrict__ rec,
                                                              const float* __restrict__ wh, Six cij,
                                                              float* __restrict__ divv, float* __restrict__ curlv,
                                                              Six dV, int doGrad)
 {
-    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcIad>::S];
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
@@ -423,16 +462,16 @@ struct GradVLoader
     }
 };
 
-template<bool avClean>
-__global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphConsts sc, Box box,
-                                                                 const SrcMom* __restrict__ rec,
+template<bool avClean, class R, class G>
+__global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphConsts sc, G box,
+                                                                 const R* __restrict__ rec,
                                                                  const SrcGradV* __restrict__ gv,
                                                                  const float* __restrict__ wh,
                                                                  float* __restrict__ ax, float* __restrict__ ay,
                                                                  float* __restrict__ az, double* __restrict__ du,
                                                                  float* __restrict__ minDt)
 {
-    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcMom>::S];
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
@@ -448,7 +487,7 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphC
         ay[i] = ayi;
         az[i] = azi;
         du[i] = dui;
-        SrcMom ri = rec[i];
+        const R ri = rec[i];
         dti       = tsKCourant(mvs, 1.0f / ri.ih, ri.c, float(sc.Kcour));
     }
     reduceMinDt(dti, minDt);
@@ -592,7 +631,7 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
            const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s)
 {
     if (a.last <= a.first) return;
-#ifdef SPHX_XMASS_FP64_RECORDS
+#ifdef SPHX_FP64_RECORDS
     packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, nullptr, (SrcPos*)rec);
     xmassKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcPos*)rec, wh, xm);
 #else
@@ -605,11 +644,22 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
 
 void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                 const double* y, const double* z, const float* h, const float* m, const float* wh, const float* whd,
-                const float* xm, void* rec, float* kx, float* gradh, hipStream_t s)
+                const float* xm, void* rec, float* kx, float* gradh, float mUniform, hipStream_t s)
 {
     if (a.last <= a.first) return;
-    packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, xm, (SrcPos*)rec);
-    veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcPos*)rec, wh, whd, kx, gradh);
+    if (mUniform > 0.f)
+    {
+        const QFrame q = qframeOf(box);
+        packXmQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, q, (SrcXmQ*)rec);
+        veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcXmQ*)rec, wh, whd, kx,
+                                                     gradh, mUniform);
+    }
+    else
+    {
+        packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, xm, (SrcPos*)rec);
+        veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcPos*)rec, wh, whd, kx,
+                                                     gradh, 0.f);
+    }
     SPHX_LAUNCH_CHECK();
 }
 
@@ -649,16 +699,23 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
                   float* curlv, float* const dV[6], hipStream_t s)
 {
     if (a.last <= a.first) return;
-    packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, nullptr, nullptr,
-                                                     (SrcIad*)rec);
     Six c, g;
     for (int k = 0; k < 6; ++k)
     {
         c.p[k] = cij[k];
         g.p[k] = dV[k];
     }
-    iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, kx, (const SrcIad*)rec, wh, c, divv, curlv, g,
-                                                   dV[0] != nullptr);
+#ifdef SPHX_FP64_RECORDS
+    packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, nullptr, nullptr,
+                                                     (SrcIad*)rec);
+    iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, kx, (const SrcIad*)rec, wh, c, divv,
+                                                   curlv, g, dV[0] != nullptr);
+#else
+    const QFrame q = qframeOf(box);
+    packIadQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, q, (SrcIadQ*)rec);
+    iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv,
+                                                   curlv, g, dV[0] != nullptr);
+#endif
     SPHX_LAUNCH_CHECK();
 }
 
@@ -682,6 +739,7 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
 {
     if (a.last <= a.first) return;
     SrcGradV* gv = avClean ? (SrcGradV*)recGradV : nullptr;
+#ifdef SPHX_FP64_RECORDS
     packMomKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, (SrcMom*)rec, gv);
     if (avClean)
         momentumEnergyVeKernel<true>
@@ -689,6 +747,16 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
     else
         momentumEnergyVeKernel<false>
             <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, (const SrcMom*)rec, nullptr, wh, ax, ay, az, du, minDt);
+#else
+    const QFrame q = qframeOf(box);
+    packMomQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, q, (SrcMomQ*)rec, gv);
+    if (avClean)
+        momentumEnergyVeKernel<true>
+            <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, (const SrcMomQ*)rec, gv, wh, ax, ay, az, du, minDt);
+    else
+        momentumEnergyVeKernel<false>
+            <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, (const SrcMomQ*)rec, nullptr, wh, ax, ay, az, du, minDt);
+#endif
     SPHX_LAUNCH_CHECK();
 }
 

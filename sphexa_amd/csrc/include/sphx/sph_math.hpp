@@ -19,6 +19,7 @@
 #pragma once
 
 #include <cstddef>
+#include <cstdint>
 
 #include "annotation.hpp"
 #include "box.hpp"
@@ -258,6 +259,44 @@ struct alignas(16) SrcStd
     HT m, rho, p, c;
 };
 
+//! @brief fixed-point (QFrame) variants of the gfx950 records: XMass 16 B, Gradh with uniform mass 16 B (the mass
+//!        comes from the launch), IAD + divv/curlv 32 B, VE momentum 80 B
+struct alignas(16) SrcPosQ
+{
+    uint32_t x, y, z;
+    HT m;
+};
+
+struct alignas(16) SrcXmQ
+{
+    uint32_t x, y, z;
+    HT xm;
+};
+
+struct alignas(16) SrcIadQ
+{
+    uint32_t x, y, z;
+    HT vol;
+    HT vx, vy, vz;
+    HT xm;
+};
+static_assert(sizeof(SrcIadQ) == 32, "SrcIadQ is two 16-byte chunks");
+
+struct alignas(16) SrcMomQ
+{
+    uint32_t x, y, z;
+    HT vx, vy, vz;
+    HT ih;
+    HT c11, c12, c13, c22, c23, c33;
+    HT m, c, xm, rho;
+    HT prho, alpha, mrho;
+};
+static_assert(sizeof(SrcMomQ) == 80, "SrcMomQ is five 16-byte chunks");
+
+//! @brief source mass of a Gradh record: stored, or the uniform mass of the launch (SrcXmQ)
+SPHX_HD HT massOf(const SrcPos& p, HT) { return p.m; }
+SPHX_HD HT massOf(const SrcXmQ&, HT mUniform) { return mUniform; }
+
 //! @brief pair separation (i - j) in hydro precision with the j-loop periodic fold at 2h_i
 SPHX_HD void pairDelta(CT xi, CT yi, CT zi, CT xj, CT yj, CT zj, HT hi, const Box& box, HT& rx, HT& ry, HT& rz)
 {
@@ -265,6 +304,53 @@ SPHX_HD void pairDelta(CT xi, CT yi, CT zi, CT xj, CT yj, CT zj, HT hi, const Bo
     ry = HT(yi - yj);
     rz = HT(zi - zj);
     foldPbc(box, HT(2) * hi, rx, ry, rz);
+}
+
+/*! @brief fixed-point coordinate frame of the gfx950 source records: coordinates become 32-bit offsets in the box.
+ *         Periodic dimensions span the full 2^32 range, so the wrapping int32 difference of two offsets IS the
+ *         minimum image (no fold); open dimensions use 2^30 per box length (|dx| < 2L stays in range). The pair
+ *         separation is exact in the integers and rounds once when converted to fp32 (quantum <= 1e-9 L), i.e. to
+ *         the accuracy of the fp64 difference rounded to fp32. Records shrink by 12 B, which is what lets XMass,
+ *         Gradh (uniform mass), IAD and momentum drop one 16-B gather chunk per neighbor.
+ */
+struct QFrame
+{
+    double lo[3], s[3]; // offset = rint((x - lo) * s) mod 2^32
+    float inv[3];       // separation = int32(offset_i - offset_j) * inv
+};
+
+inline QFrame qframeOf(const Box& b)
+{
+    QFrame q;
+    for (int d = 0; d < 3; ++d)
+    {
+        const double L = b.len(d) > 0 ? b.len(d) : 1.0;
+        q.lo[d]        = b.lo[d];
+        q.s[d]         = (b.periodic(d) ? 4294967296.0 : 1073741824.0) / L;
+        q.inv[d]       = float(1.0 / q.s[d]);
+    }
+    return q;
+}
+
+SPHX_HD uint32_t quantize(double v, double lo, double s)
+{
+    return uint32_t((unsigned long long)(long long)rint((v - lo) * s));
+}
+
+//! @brief pair separation of two records with fp64 coordinates (minimum image folded at 2h_i)
+template<class R>
+SPHX_HD void pairSep(const Box& box, const R& pi, const R& pj, HT hi, HT& rx, HT& ry, HT& rz)
+{
+    pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
+}
+
+//! @brief pair separation of two fixed-point records (QFrame): wrapping integer difference, one rounding
+template<class R>
+SPHX_HD void pairSep(const QFrame& q, const R& pi, const R& pj, HT, HT& rx, HT& ry, HT& rz)
+{
+    rx = HT(int32_t(pi.x - pj.x)) * q.inv[0];
+    ry = HT(int32_t(pi.y - pj.y)) * q.inv[1];
+    rz = HT(int32_t(pi.z - pj.z)) * q.inv[2];
 }
 
 //! @brief 1/sqrt(x) in hydro precision (annotation.hpp rsqrtF)
@@ -416,6 +502,51 @@ __device__ __forceinline__ SrcMom coopUnpack<SrcMom>(const float4* o)
 }
 
 template<>
+__device__ __forceinline__ SrcMomQ coopUnpack<SrcMomQ>(const float4* o)
+{
+    static_assert(offsetof(SrcMomQ, vx) == 12 && offsetof(SrcMomQ, c11) == 28 && offsetof(SrcMomQ, m) == 52 &&
+                      offsetof(SrcMomQ, mrho) == 76,
+                  "SrcMomQ layout");
+    SrcMomQ r;
+    r.x     = __float_as_uint(o[0].x);
+    r.y     = __float_as_uint(o[0].y);
+    r.z     = __float_as_uint(o[0].z);
+    r.vx    = o[0].w;
+    r.vy    = o[1].x;
+    r.vz    = o[1].y;
+    r.ih    = o[1].z;
+    r.c11   = o[1].w;
+    r.c12   = o[2].x;
+    r.c13   = o[2].y;
+    r.c22   = o[2].z;
+    r.c23   = o[2].w;
+    r.c33   = o[3].x;
+    r.m     = o[3].y;
+    r.c     = o[3].z;
+    r.xm    = o[3].w;
+    r.rho   = o[4].x;
+    r.prho  = o[4].y;
+    r.alpha = o[4].z;
+    r.mrho  = o[4].w;
+    return r;
+}
+
+template<>
+__device__ __forceinline__ SrcIadQ coopUnpack<SrcIadQ>(const float4* o)
+{
+    SrcIadQ r;
+    r.x   = __float_as_uint(o[0].x);
+    r.y   = __float_as_uint(o[0].y);
+    r.z   = __float_as_uint(o[0].z);
+    r.vol = o[0].w;
+    r.vx  = o[1].x;
+    r.vy  = o[1].y;
+    r.vz  = o[1].z;
+    r.xm  = o[1].w;
+    return r;
+}
+
+template<>
 __device__ __forceinline__ SrcStd coopUnpack<SrcStd>(const float4* o)
 {
     static_assert(offsetof(SrcStd, vx) == 24 && offsetof(SrcStd, c11) == 40 && offsetof(SrcStd, m) == 64 &&
@@ -500,7 +631,7 @@ __device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const C
     {
         // small records (cooperative path measured slower for 32 B): per-lane gathers, one list block (4 indices)
         // and its records in flight (a deeper software pipeline measured slower: more VGPRs, same texture work)
-        static_assert(B == 4, "the direct path consumes one 4-entry list block per batch");
+        // (B is ignored: the direct path always consumes one 4-entry list block per batch)
         unsigned k = 0;
         const int4* blk = reinterpret_cast<const int4*>(nbr);
         int4 v = blk[0]; // next block prefetched while the current one is evaluated (A/B: beats per-step block
@@ -622,20 +753,21 @@ SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
 }
 
 //! @brief kx (VE normalization) and grad-h term (reference ve_def_gradh_kern.hpp)
-template<class Idx, class Ld>
-SPHX_HD void veDefGradhJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                             const Ld& ld, const KernelFn& kf, HT& kxOut, HT& gradhOut)
+template<class G, class Idx, class Ld>
+SPHX_HD void veDefGradhJLoop(unsigned i, double K, const G& box, const Idx* nbr, int stride, unsigned nc, HT hi,
+                             const Ld& ld, const KernelFn& kf, HT& kxOut, HT& gradhOut,
+                             HT mUniform = HT(0))
 {
-    SrcPos pi = ld(i);
-    HT mi = pi.m, xmi = pi.xm;
+    const auto pi = ld(i);
+    HT mi = massOf(pi, mUniform), xmi = pi.xm;
     HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv;
 
     HT kxi      = xmi;
     HT whomegai = -HT(3) * xmi;
     HT wrho0i   = -HT(3) * mi;
-    forEachNeighbor<SPHX_BATCH_POS>(nbr, stride, nc, ld, [&](unsigned j, const SrcPos& pj) {
+    forEachNeighbor<SPHX_BATCH_POS>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
-        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
+        pairSep(box, pi, pj, hi, rx, ry, rz);
         HT dist  = sqrtF(rx * rx + ry * ry + rz * rz);
         HT v     = dist * hInv;
         HT w     = kf.w(v);
@@ -644,7 +776,7 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const Box& box, const Idx* nb
         HT xmj   = pj.xm;
         kxi += w * xmj;
         whomegai += dterh * xmj;
-        wrho0i += dterh * pj.m;
+        wrho0i += dterh * massOf(pj, mUniform);
     });
     HT Kf = HT(K);
     kxi *= Kf * h3Inv;
@@ -753,17 +885,17 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
  * M[a][b] = sum_j v_ji[a] xm_j W_ij r_ij[b], so M is accumulated together with tau and the neighbor data is read
  * once. Mathematically identical; rounding differs from the two-pass form at the 1e-7 relative level.
  */
-template<class Idx, class Ld>
-SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
+template<class G, class Idx, class Ld>
+SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nbr, int stride, unsigned nc, HT hi,
                                HT kxi, const Ld& ld, const KernelFn& kf, HT c[6], HT& divvOut, HT& curlvOut, HT* dV)
 {
     HT tau[6]  = {0, 0, 0, 0, 0, 0};
     HT M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-    SrcIad pi  = ld(i);
+    const auto pi = ld(i);
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
-    forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
+    forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
-        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
+        pairSep(box, pi, pj, hi, rx, ry, rz);
         HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
         HT w    = kf.w(dist * hInv);
         HT vw   = pj.vol * w;
@@ -884,12 +1016,12 @@ SPHX_HD HT avRvCorrection(HT rx, HT ry, HT rz, HT eta_ab, HT eta_crit, const HT 
 }
 
 //! @brief VE momentum and energy equations (reference hydro_ve/momentum_energy_kern.hpp)
-template<bool avClean, class Idx, class Ld, class LdG>
-SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box, const Idx* nbr, int stride,
+template<bool avClean, class G, class Idx, class Ld, class LdG>
+SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, const Idx* nbr, int stride,
                                  unsigned nc, const Ld& ld, const LdG& ldg, const KernelFn& kf, HT& axOut, HT& ayOut,
                                  HT& azOut, double& duOut, HT& maxvsignalOut)
 {
-    SrcMom pi = ld(i);
+    const auto pi = ld(i);
     HT hInv = pi.ih, hi = HT(1) / hInv, ci = pi.c, alphai = pi.alpha, xmi = pi.xm;
     HT rhoi = pi.rho, prhoi = pi.prho, invRhoi = HT(1) / rhoi, log2xmi = log2(xmi);
     HT hInv3 = hInv * hInv * hInv;
@@ -905,9 +1037,9 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const Box& box
     HT maxvs = 0, mx = 0, my = 0, mz = 0, energy = 0, aviscE = 0;
     const HT Atmin = sc.Atmin, Atmax = sc.Atmax, ramp = sc.ramp;
 
-    forEachNeighbor<SPHX_BATCH_MOM>(nbr, stride, nc, ld, [&](unsigned j, const SrcMom& pj) {
+    forEachNeighbor<SPHX_BATCH_MOM>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
-        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
+        pairSep(box, pi, pj, hi, rx, ry, rz);
         HT r2      = rx * rx + ry * ry + rz * rz;
         HT invDist = rsqrtH(r2);
         HT dist    = r2 * invDist;

@@ -73,13 +73,30 @@ def compute_density(d, nl: NeighborList, box: Box):
     compute_xmass(d, nl, box, out_field="rho")
 
 
+def uniform_mass(d) -> float:
+    """The common particle mass when every particle (halos included) has the same one, else 0. The GPU Gradh loop
+    then reads 16-B fixed-point records without the mass (one gather chunk per neighbor instead of two). Cached on
+    the identity and version of the mass tensor, so only steps that replaced or modified it pay the min/max."""
+    m = d["m"][: d.size]
+    key = (m.data_ptr(), m.numel(), m._version)
+    hit = getattr(d, "_m_uniform", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    if m.numel() == 0:
+        return 0.0
+    lo, hi = torch.stack(torch.aminmax(m)).tolist()
+    val = float(lo) if (lo == hi and lo > 0) else 0.0
+    d._m_uniform = (key, val)
+    return val
+
+
 def compute_ve_def_gradh(d, nl: NeighborList, box: Box):
     nidx, nc = _nl_args(nl, d)
     args = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d.whd.data_ptr(),
             d["xm"].data_ptr(), d["kx"].data_ptr(), d["gradh"].data_ptr())
     if _is_gpu(d):
-        _lib.hip().ve_def_gradh(*args, *_gpu_tail(d))
+        _lib.hip().ve_def_gradh(*args, *_gpu_tail(d), uniform_mass(d))
     else:
         _lib.cpu().ve_def_gradh(*args)
 
