@@ -255,6 +255,26 @@ __global__ void packMomQKernel(int64_t n, MomFields f, QFrame q, SrcMomQ* __rest
     }
 }
 
+__global__ void packAvQKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                              const double* __restrict__ z, const float* __restrict__ kx,
+                              const float* __restrict__ vx, const float* __restrict__ vy,
+                              const float* __restrict__ vz, const float* __restrict__ xm,
+                              const float* __restrict__ c, QFrame q, SrcAvQ* __restrict__ out)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcAvQ r;
+    r.x    = quantize(x[i], q.lo[0], q.s[0]);
+    r.y    = quantize(y[i], q.lo[1], q.s[1]);
+    r.z    = quantize(z[i], q.lo[2], q.s[2]);
+    r.vol  = xm[i] / kx[i];
+    r.vx   = vx[i];
+    r.vy   = vy[i];
+    r.vz   = vz[i];
+    r.c    = c[i];
+    out[i] = r;
+}
+
 // ------------------------------------------------------------------------------------------------ VE loops
 
 __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, Box box, const float* __restrict__ h,
@@ -429,6 +449,25 @@ __global__ __launch_bounds__(kBlock) void avSwitchesKernel(NbrArgs a, SphConsts 
     const bool valid = targetOf(a, i, nbr, n);
     float ci[6] = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
     float al    = avSwitchesJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], ci, coopOf(rec, tile, i, a),
+                                  KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt, sc.alphamin, sc.alphamax,
+                                  sc.decayConstant, alpha[i]);
+    if (valid) alpha[i] = al;
+}
+
+//! @brief AV switches on fixed-point records (SrcAvQ + divv field): same loop as avSwitchesKernel
+__global__ __launch_bounds__(kBlock) void avSwitchesQKernel(NbrArgs a, SphConsts sc, QFrame q,
+                                                            const float* __restrict__ h, Six cij,
+                                                            const SrcAvQ* __restrict__ rec,
+                                                            const float* __restrict__ divv,
+                                                            const float* __restrict__ wh, double dt,
+                                                            float* __restrict__ alpha)
+{
+    int64_t i;
+    const int32_t* nbr;
+    unsigned n;
+    const bool valid = targetOf(a, i, nbr, n);
+    float ci[6] = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
+    float al    = avSwitchesJLoop(unsigned(i), sc.K, q, nbr, kBlockedList, n, h[i], ci, AvQLoader{rec, divv},
                                   KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt, sc.alphamin, sc.alphamax,
                                   sc.decayConstant, alpha[i]);
     if (valid) alpha[i] = al;
@@ -725,11 +764,18 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                 const float* divv, double dt, void* rec, float* alpha, hipStream_t s)
 {
     if (a.last <= a.first) return;
-    packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, c, divv, (SrcIad*)rec);
     Six cc;
     for (int k = 0; k < 6; ++k)
         cc.p[k] = cij[k];
+#ifdef SPHX_FP64_RECORDS
+    packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, c, divv, (SrcIad*)rec);
     avSwitchesKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, cc, (const SrcIad*)rec, wh, dt, alpha);
+#else
+    const QFrame q = qframeOf(box);
+    packAvQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, c, q, (SrcAvQ*)rec);
+    avSwitchesQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, cc, (const SrcAvQ*)rec, divv, wh, dt,
+                                                  alpha);
+#endif
     SPHX_LAUNCH_CHECK();
 }
 

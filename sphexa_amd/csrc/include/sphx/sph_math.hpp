@@ -622,6 +622,72 @@ struct CoopLoader
     __device__ __forceinline__ float4 own(int p) const { return tile[(threadIdx.x & 63) * S + p]; }
 };
 
+/*! @brief per-lane gather loop of the small records (any loader returning a record by value): one list block
+ *         (4 indices) and its records in flight per step */
+template<class Idx, class Ld, class F>
+__device__ void forEachNeighborDirect(const Idx* nbr, int stride, unsigned nc, const Ld& ld, F&& f)
+{
+    // small records (cooperative path measured slower for 32 B): per-lane gathers, one list block (4 indices)
+    // and its records in flight (a deeper software pipeline measured slower: more VGPRs, same texture work)
+    // (B is ignored: the direct path always consumes one 4-entry list block per batch)
+    unsigned k = 0;
+    const int4* blk = reinterpret_cast<const int4*>(nbr);
+    int4 v = blk[0]; // next block prefetched while the current one is evaluated (A/B: beats per-step block
+                     // loads and per-entry index loads by 5 %)
+    for (; k + 4 <= nc; k += 4)
+    {
+        const int4 vn       = blk[size_t((k >> 2) + 1) * 64];
+        const unsigned j[4] = {unsigned(v.x), unsigned(v.y), unsigned(v.z), unsigned(v.w)};
+        v                   = vn;
+        decltype(ld(0u)) rr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            rr[u] = ld(j[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            f(j[u], rr[u]);
+    }
+    for (; k < nc; ++k)
+    {
+        unsigned j = unsigned(listAt(nbr, stride, k));
+        f(j, ld(j));
+    }
+}
+
+/*! @brief AV-switch source records on the fixed-point frame: 32 B stored (coordinates, vol, v, c) + divv read from
+ *         its own field, i.e. two dwordx4 gathers and one dword gather per neighbor instead of three chunks of the
+ *         48-B SrcIad (the six fields of the AV loop do not fit the 20 B left next to the coordinates) */
+struct alignas(16) SrcAvQ
+{
+    uint32_t x, y, z;
+    HT vol;
+    HT vx, vy, vz;
+    HT c;
+};
+
+struct SrcAvQd
+{
+    uint32_t x, y, z;
+    HT vol, vx, vy, vz, c, divv;
+};
+
+struct AvQLoader
+{
+    const SrcAvQ* r;
+    const HT* divv;
+    __device__ SrcAvQd operator()(unsigned j) const
+    {
+        const SrcAvQ a = r[j];
+        return SrcAvQd{a.x, a.y, a.z, a.vol, a.vx, a.vy, a.vz, a.c, divv[j]};
+    }
+};
+
+template<int B, class Idx, class F>
+__device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const AvQLoader& ld, F&& f)
+{
+    forEachNeighborDirect(nbr, stride, nc, ld, f);
+}
+
 template<int B, class Idx, class R, class F>
 __device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const CoopLoader<R>& ld, F&& f)
 {
@@ -629,31 +695,7 @@ __device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const C
     constexpr bool direct = C < SPHX_COOP_MIN_CHUNKS;
     if constexpr (direct)
     {
-        // small records (cooperative path measured slower for 32 B): per-lane gathers, one list block (4 indices)
-        // and its records in flight (a deeper software pipeline measured slower: more VGPRs, same texture work)
-        // (B is ignored: the direct path always consumes one 4-entry list block per batch)
-        unsigned k = 0;
-        const int4* blk = reinterpret_cast<const int4*>(nbr);
-        int4 v = blk[0]; // next block prefetched while the current one is evaluated (A/B: beats per-step block
-                         // loads and per-entry index loads by 5 %)
-        for (; k + 4 <= nc; k += 4)
-        {
-            const int4 vn       = blk[size_t((k >> 2) + 1) * 64];
-            const unsigned j[4] = {unsigned(v.x), unsigned(v.y), unsigned(v.z), unsigned(v.w)};
-            v                   = vn;
-            R rr[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                rr[u] = ld(j[u]);
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                f(j[u], rr[u]);
-        }
-        for (; k < nc; ++k)
-        {
-            unsigned j = unsigned(listAt(nbr, stride, k));
-            f(j, ld(j));
-        }
+        forEachNeighborDirect(nbr, stride, nc, ld, f);
         return;
     }
     unsigned ncMax  = nc;
@@ -942,21 +984,21 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nb
 }
 
 //! @brief Cullen-Dehnen style AV switch (reference av_switches_kern.hpp)
-template<class Idx, class Ld>
-SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
+template<class G, class Idx, class Ld>
+SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const G& box, const Idx* nbr, int stride, unsigned nc, HT hi,
                            const HT ci6[6], const Ld& ld, const KernelFn& kf, double dt, HT alphamin, HT alphamax,
                            HT decayConstant, HT alpha_i)
 {
-    SrcIad pi = ld(i);
+    const auto pi = ld(i);
     HT ci     = pi.c;
     HT c11 = ci6[0], c12 = ci6[1], c13 = ci6[2], c22 = ci6[3], c23 = ci6[4], c33 = ci6[5];
     HT vsig  = HT(1.e-40) * ci;
     HT hInv  = HT(1) / hi, hInv3 = hInv * hInv * hInv;
     HT divvi = pi.divv;
     HT gx = 0, gy = 0, gz = 0;
-    forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
+    forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
-        pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
+        pairSep(box, pi, pj, hi, rx, ry, rz);
         HT r2      = rx * rx + ry * ry + rz * rz;
         HT invDist = rsqrtH(r2);
         HT dist    = r2 * invDist;
