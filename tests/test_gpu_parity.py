@@ -222,3 +222,35 @@ def test_gravity_spill_path(gpu, monkeypatch, hook):
     for a, b in zip(acc, acc2):
         assert float((a - b).abs().max()) < 1e-4 * float(a.abs().max())
     assert abs(e2 - e_ref) < 1e-5 * abs(e_ref)
+
+
+def test_ve_step_nonuniform_mass_matches_cpu(gpu):
+    """Masses with a 10 % spread: the GPU Gradh loop takes the stored-mass record path (SrcPos) instead of the
+    uniform-mass fixed-point one (SrcXmQ); every other loop runs on fixed-point records either way."""
+    results = {}
+    for dev in ("cpu", gpu):
+        d = P.ParticlesData(dev)
+        prop = HydroVeProp(None, 0)
+        prop.activate_fields(d)
+        box = SedovGrid().init(0, 1, 14, d)
+        g = torch.Generator().manual_seed(3)
+        d["m"] = (d["m"].cpu() * (1 + 0.1 * torch.rand(d.size, generator=g))).to(d["m"].dtype).to(dev)
+        if str(dev) != "cpu":
+            assert H.uniform_mass(d) == 0.0
+        dom = Domain(Comm(), box)
+        prop.sync(dom, d)
+        prop.step(dom, d)
+        results[str(dev)] = {f: d[f].clone().cpu() for f in ("kx", "xm", "c11", "alpha", "ax", "du")}
+    c, g = results["cpu"], results[str(gpu)]
+    for f in ("kx", "xm", "c11", "alpha"):
+        assert _rel(g[f], c[f]) < 2e-5, f
+    for f in ("ax", "du"):
+        assert _rel(g[f], c[f]) < 2e-3, f
+
+
+def test_uniform_mass_detection(gpu):
+    d, prop, dom = _setup(gpu, n=8)
+    m0 = float(d["m"][0])
+    assert H.uniform_mass(d) == pytest.approx(m0)
+    d["m"][3] *= 2  # in-place change bumps the tensor version: the cached value is not reused
+    assert H.uniform_mass(d) == 0.0
