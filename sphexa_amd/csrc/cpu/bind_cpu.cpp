@@ -58,7 +58,7 @@ void conservedQuantities(int64_t, int64_t, const double*, const double*, const d
 namespace
 {
 using BoxArr   = std::array<double, 9>;
-using ConstArr = std::array<double, 15>;
+using ConstArr = std::array<double, 16>;
 using Ptr      = uintptr_t;
 
 template<class T>
@@ -97,6 +97,7 @@ SphConsts toConsts(const ConstArr& a)
     s.ngmax         = unsigned(a[12]);
     s.sincIndex     = float(a[13]);
     s.kernelChoice  = int(a[14]);
+    s.fixedPoint    = int(a[15]);
     return s;
 }
 

@@ -670,14 +670,17 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
            const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s)
 {
     if (a.last <= a.first) return;
-#ifdef SPHX_FP64_RECORDS
-    packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, nullptr, (SrcPos*)rec);
-    xmassKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcPos*)rec, wh, xm);
-#else
-    const QFrame q = qframeOf(box);
-    packPosQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, q, (SrcPosQ*)rec);
-    xmassQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec, wh, xm);
-#endif
+    if (!sc.fixedPoint)
+    {
+        packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, nullptr, (SrcPos*)rec);
+        xmassKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcPos*)rec, wh, xm);
+    }
+    else
+    {
+        const QFrame q = qframeOf(box);
+        packPosQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, q, (SrcPosQ*)rec);
+        xmassQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec, wh, xm);
+    }
     SPHX_LAUNCH_CHECK();
 }
 
@@ -686,7 +689,7 @@ void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                 const float* xm, void* rec, float* kx, float* gradh, float mUniform, hipStream_t s)
 {
     if (a.last <= a.first) return;
-    if (mUniform > 0.f)
+    if (mUniform > 0.f && sc.fixedPoint)
     {
         const QFrame q = qframeOf(box);
         packXmQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, q, (SrcXmQ*)rec);
@@ -744,17 +747,20 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
         c.p[k] = cij[k];
         g.p[k] = dV[k];
     }
-#ifdef SPHX_FP64_RECORDS
-    packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, nullptr, nullptr,
-                                                     (SrcIad*)rec);
-    iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, kx, (const SrcIad*)rec, wh, c, divv,
-                                                   curlv, g, dV[0] != nullptr);
-#else
-    const QFrame q = qframeOf(box);
-    packIadQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, q, (SrcIadQ*)rec);
-    iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv,
-                                                   curlv, g, dV[0] != nullptr);
-#endif
+    if (!sc.fixedPoint)
+    {
+        packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, nullptr, nullptr,
+                                                         (SrcIad*)rec);
+        iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, kx, (const SrcIad*)rec, wh, c, divv,
+                                                       curlv, g, dV[0] != nullptr);
+    }
+    else
+    {
+        const QFrame q = qframeOf(box);
+        packIadQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, q, (SrcIadQ*)rec);
+        iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv,
+                                                       curlv, g, dV[0] != nullptr);
+    }
     SPHX_LAUNCH_CHECK();
 }
 
@@ -767,15 +773,18 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
     Six cc;
     for (int k = 0; k < 6; ++k)
         cc.p[k] = cij[k];
-#ifdef SPHX_FP64_RECORDS
-    packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, c, divv, (SrcIad*)rec);
-    avSwitchesKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, cc, (const SrcIad*)rec, wh, dt, alpha);
-#else
-    const QFrame q = qframeOf(box);
-    packAvQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, c, q, (SrcAvQ*)rec);
-    avSwitchesQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, cc, (const SrcAvQ*)rec, divv, wh, dt,
-                                                  alpha);
-#endif
+    if (!sc.fixedPoint)
+    {
+        packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, c, divv, (SrcIad*)rec);
+        avSwitchesKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, cc, (const SrcIad*)rec, wh, dt, alpha);
+    }
+    else
+    {
+        const QFrame q = qframeOf(box);
+        packAvQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, c, q, (SrcAvQ*)rec);
+        avSwitchesQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, cc, (const SrcAvQ*)rec, divv, wh, dt,
+                                                      alpha);
+    }
     SPHX_LAUNCH_CHECK();
 }
 
@@ -785,24 +794,27 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
 {
     if (a.last <= a.first) return;
     SrcGradV* gv = avClean ? (SrcGradV*)recGradV : nullptr;
-#ifdef SPHX_FP64_RECORDS
-    packMomKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, (SrcMom*)rec, gv);
-    if (avClean)
-        momentumEnergyVeKernel<true>
-            <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, (const SrcMom*)rec, gv, wh, ax, ay, az, du, minDt);
+    if (!sc.fixedPoint)
+    {
+        packMomKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, (SrcMom*)rec, gv);
+        if (avClean)
+            momentumEnergyVeKernel<true>
+                <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, (const SrcMom*)rec, gv, wh, ax, ay, az, du, minDt);
+        else
+            momentumEnergyVeKernel<false>
+                <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, (const SrcMom*)rec, nullptr, wh, ax, ay, az, du, minDt);
+    }
     else
-        momentumEnergyVeKernel<false>
-            <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, (const SrcMom*)rec, nullptr, wh, ax, ay, az, du, minDt);
-#else
-    const QFrame q = qframeOf(box);
-    packMomQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, q, (SrcMomQ*)rec, gv);
-    if (avClean)
-        momentumEnergyVeKernel<true>
-            <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, (const SrcMomQ*)rec, gv, wh, ax, ay, az, du, minDt);
-    else
-        momentumEnergyVeKernel<false>
-            <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, (const SrcMomQ*)rec, nullptr, wh, ax, ay, az, du, minDt);
-#endif
+    {
+        const QFrame q = qframeOf(box);
+        packMomQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, q, (SrcMomQ*)rec, gv);
+        if (avClean)
+            momentumEnergyVeKernel<true>
+                <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, (const SrcMomQ*)rec, gv, wh, ax, ay, az, du, minDt);
+        else
+            momentumEnergyVeKernel<false>
+                <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, (const SrcMomQ*)rec, nullptr, wh, ax, ay, az, du, minDt);
+    }
     SPHX_LAUNCH_CHECK();
 }
 

@@ -49,6 +49,8 @@ struct SphConsts
     unsigned ngmax;
     float sincIndex;  // exponent n of the sinc^n kernel
     int kernelChoice; // 0: sinc^n, 1: 0.9 sinc^4 + 0.1 sinc^9
+    int fixedPoint;   // GPU pair loops may read fixed-point (QFrame) records: set when the coordinate quantum is
+                      // <= 2^-18 of the smallest h (ops/hydro.py: fixed_point_ok), else fp64-coordinate records
 };
 
 //! @brief linear interpolation in a table sampled on [0, 2]

@@ -86,6 +86,7 @@ class ParticlesData:
         self.maxDtIncrease = 1.1
         self.sincIndex = 6.0
         self.kernelChoice = 0
+        self.fixedPoint = 1  # GPU pair loops on fixed-point records (ops/hydro.py: fixed_point_ok)
         self.totalNeighbors = 0
 
         self.size = 0
@@ -232,7 +233,7 @@ class ParticlesData:
         return [float(self.K), float(self.Kcour), float(self.Krho), float(self.gamma), float(self.muiConst),
                 float(self.alphamin), float(self.alphamax), float(self.decay_constant), float(self.Atmin),
                 float(self.Atmax), float(self.ramp), float(self.ng0), float(self.ngmax), float(self.sincIndex),
-                float(self.kernelChoice)]
+                float(self.kernelChoice), float(self.fixedPoint)]
 
     def set_output_fields(self, names: List[str]) -> List[str]:
         """select output fields; returns names that are not particle fields"""

@@ -18,7 +18,7 @@ import torch
 
 from . import _lib
 from .neighbors import NeighborList
-from ..utils.box import Box
+from ..utils.box import Box, PERIODIC
 
 CIJ = ("c11", "c12", "c13", "c22", "c23", "c33")
 DV = ("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")
@@ -60,7 +60,7 @@ def _gpu_tail(d, which=(0,)):
 def compute_xmass(d, nl: NeighborList, box: Box, out_field: str = "xm"):
     first, last = nl.first, nl.last
     nidx, nc = _nl_args(nl, d)
-    args = (first, last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+    args = (first, last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d[out_field].data_ptr())
     if _is_gpu(d):
         _lib.hip().xmass(*args, *_gpu_tail(d))
@@ -71,6 +71,36 @@ def compute_xmass(d, nl: NeighborList, box: Box, out_field: str = "xm"):
 def compute_density(d, nl: NeighborList, box: Box):
     """STD density: the XMass loop written into rho (volume element m/rho0), see hydro_std/density.hpp"""
     compute_xmass(d, nl, box, out_field="rho")
+
+
+# fixed-point records: the coordinate quantum (box length / 2^32 periodic, / 2^30 open) must stay below this
+# fraction of the SMALLEST h, i.e. the separation error of the densest particle below ~4e-6 h (~16 fp32 ulp at
+# r = h; a median particle is typically 10x better: Evrard -n 200 hmin/hmed = 0.087, Sedov lattice: 1)
+FIXED_POINT_REL_QUANTUM = 2.0 ** -18
+
+
+def fixed_point_ok(d, box: Box) -> bool:
+    """Whether the GPU pair loops may read fixed-point coordinate records (QFrame, sph_math.hpp) for this box and
+    these smoothing lengths; otherwise they read fp64-coordinate records. Cached on the identity and version of h."""
+    h = d["h"][: d.size]
+    key = (h.data_ptr(), h.numel(), h._version)
+    hit = getattr(d, "_h_min", None)
+    if hit is None or hit[0] != key:
+        hit = (key, float(h.min()) if h.numel() else 0.0)
+        d._h_min = hit
+    hmin = hit[1]
+    quantum = 0.0
+    for L, bc in zip(box.lengths(), box.bc):
+        L = L if L > 0 else 1.0
+        quantum = max(quantum, L / (2.0 ** 32 if bc == PERIODIC else 2.0 ** 30))
+    return hmin > 0 and quantum <= FIXED_POINT_REL_QUANTUM * hmin
+
+
+def _consts(d, box: Box):
+    """SphConsts array of a pair loop, with the fixed-point switch of the GPU path decided for this box"""
+    if _is_gpu(d):
+        d.fixedPoint = 1 if fixed_point_ok(d, box) else 0
+    return d.consts_array()
 
 
 def uniform_mass(d) -> float:
@@ -92,7 +122,7 @@ def uniform_mass(d) -> float:
 
 def compute_ve_def_gradh(d, nl: NeighborList, box: Box):
     nidx, nc = _nl_args(nl, d)
-    args = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+    args = (nl.first, nl.last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d.whd.data_ptr(),
             d["xm"].data_ptr(), d["kx"].data_ptr(), d["gradh"].data_ptr())
     if _is_gpu(d):
@@ -134,7 +164,7 @@ def compute_eos_std(d, first: int, last: int):
 def compute_iad(d, nl: NeighborList, box: Box, numer: str, denom: str):
     """IAD matrices; VE uses volumes xm/kx, STD uses m/rho"""
     nidx, nc = _nl_args(nl, d)
-    args = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+    args = (nl.first, nl.last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["h"].data_ptr(), d.wh.data_ptr(), d[numer].data_ptr(), d[denom].data_ptr(),
             [d[c].data_ptr() for c in CIJ])
     if _is_gpu(d):
@@ -147,7 +177,7 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
     """VE IAD matrices, velocity divergence and curl (+ velocity gradient for AV cleaning), fused"""
     nidx, nc = _nl_args(nl, d)
     dv = [d[n].data_ptr() for n in DV] if av_clean else [0] * 6
-    args = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+    args = (nl.first, nl.last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(), d["h"].data_ptr(),
             [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["kx"].data_ptr(), d["xm"].data_ptr(),
             d["divv"].data_ptr(), d["curlv"].data_ptr(), dv)
@@ -159,7 +189,7 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
 
 def compute_av_switches(d, nl: NeighborList, box: Box):
     nidx, nc = _nl_args(nl, d)
-    args = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+    args = (nl.first, nl.last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(), d["h"].data_ptr(),
             d["c"].data_ptr(), [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["kx"].data_ptr(),
             d["xm"].data_ptr(), d["divv"].data_ptr(), float(d.minDt), d["alpha"].data_ptr())
@@ -173,7 +203,7 @@ def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = F
     """accelerations (-grad P / rho + AV), du/dt and the per-particle Courant time-step minimum"""
     nidx, nc = _nl_args(nl, d)
     dv = [d[n].data_ptr() for n in DV] if av_clean else [d["c11"].data_ptr()] * 6
-    common = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+    common = (nl.first, nl.last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
               d["z"].data_ptr(), d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(), d["h"].data_ptr(),
               d["m"].data_ptr(), d["prho"].data_ptr(), d["c"].data_ptr(), [d[c].data_ptr() for c in CIJ],
               d["kx"].data_ptr(), d["xm"].data_ptr(), d["alpha"].data_ptr(), dv, d.wh.data_ptr(), bool(av_clean),
@@ -189,7 +219,7 @@ def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = F
 
 def compute_momentum_energy_std(d, nl: NeighborList, box: Box):
     nidx, nc = _nl_args(nl, d)
-    common = (nl.first, nl.last, d.consts_array(), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
+    common = (nl.first, nl.last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
               d["z"].data_ptr(), d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(), d["h"].data_ptr(),
               d["m"].data_ptr(), d["rho"].data_ptr(), d["p"].data_ptr(), d["c"].data_ptr(),
               [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["ax"].data_ptr(), d["ay"].data_ptr(),

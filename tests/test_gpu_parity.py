@@ -254,3 +254,27 @@ def test_uniform_mass_detection(gpu):
     assert H.uniform_mass(d) == pytest.approx(m0)
     d["m"][3] *= 2  # in-place change bumps the tensor version: the cached value is not reused
     assert H.uniform_mass(d) == 0.0
+
+
+def test_ve_step_fp64_records_matches_cpu(gpu, monkeypatch):
+    """fp64-coordinate record path of the GPU pair loops (taken when the fixed-point quantum is too coarse for the
+    smallest h, ops/hydro.py: fixed_point_ok)"""
+    monkeypatch.setattr(H, "fixed_point_ok", lambda d, box: False)
+    results = {}
+    for dev in ("cpu", gpu):
+        d = P.ParticlesData(dev)
+        prop = HydroVeProp(None, 0)
+        prop.activate_fields(d)
+        box = SedovGrid().init(0, 1, 14, d)
+        dom = Domain(Comm(), box)
+        prop.sync(dom, d)
+        prop.step(dom, d)
+        if str(dev) != "cpu":
+            assert d.fixedPoint == 0
+        results[str(dev)] = {f: d[f].clone().cpu() for f in ("kx", "xm", "c11", "alpha", "ax", "du")}
+    c, g = results["cpu"], results[str(gpu)]
+    for f in ("kx", "xm", "c11", "alpha"):
+        assert _rel(g[f], c[f]) < 2e-5, f
+    for f in ("ax", "du"):
+        assert _rel(g[f], c[f]) < 2e-3, f
+
