@@ -11,6 +11,12 @@ sort, octree, migration, halo discovery + LET), neighbor search with h iteration
 exchanges, gravity (upsweep, traversal, remote multipoles), global dt reduction and the position/energy/h update.
 
 Scaling: the problem size is fixed as N grows -> strong scaling.
+
+Launch: ``--gpus N`` with N > 1 and no torchrun environment (WORLD_SIZE unset) re-launches this script under
+``torch.distributed.run`` with N local ranks as a *child process* before anything touches the GPU, and exits with the
+child's exit code. Each rank binds cuda:LOCAL_RANK and joins one RCCL communicator; the JSON line reports the world
+size and backend the communicator actually has, and the run aborts if that differs from ``--gpus``.
+``--device cpu`` runs the same path on CPU ranks over gloo (plumbing checks without a GPU).
 """
 
 from __future__ import annotations
@@ -18,6 +24,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,6 +37,24 @@ METRIC = "particle-updates/sec (whole node), Sedov -n 400 and Evrard+gravity -n 
 BASELINE_VALUE = None  # the reference publishes no throughput numbers
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _self_launch(nproc: int) -> int:
+    """run this script under torch.distributed.run with ``nproc`` local ranks (child process, no exec)"""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -37,16 +63,22 @@ def main():
     ap.add_argument("--init", default="sedov", help="test case (sedov, evrard, noh, ...)")
     ap.add_argument("-n", type=int, default=None, help="particles per dimension (default 400 sedov, 200 evrard)")
     ap.add_argument("--prop", default="ve")
+    ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args.gpus))
     n = args.n if args.n is not None else (200 if args.init == "evrard" else 400)
 
     from sphexa_amd.app.simulation import Simulation
     from sphexa_amd.parallel.comm import init_distributed
 
-    comm = init_distributed("nccl" if torch.cuda.is_available() else "gloo")
+    use_cuda = args.device == "cuda" or (args.device == "auto" and torch.cuda.is_available())
+    comm = init_distributed("nccl" if use_cuda else "gloo")
     rank, size = comm.rank, comm.size
-    if torch.cuda.is_available():
+    if size != args.gpus:
+        raise SystemExit(f"bench: communicator has {size} ranks but --gpus {args.gpus} was requested")
+    if use_cuda:
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
@@ -93,7 +125,8 @@ def main():
             "data": f"synthetic (built-in {args.init} {ic} initial conditions)",
             "config": {"model": f"{args.init} -n {n} --prop {args.prop}{grav} ({int(d.numParticlesGlobal)} particles)",
                        "global_batch": int(d.numParticlesGlobal), "seq_len": 1,
-                       "parallelism": f"sfc-domain-decomposition x{size}"},
+                       "parallelism": f"sfc-domain-decomposition x{size}", "ranks": size,
+                       "backend": comm.backend or "none"},
         }
         print(json.dumps(out), flush=True)
         if args.verbose:

@@ -9,11 +9,19 @@ Replaces the reference's MPI layer (domain/include/cstone/primitives/mpi_wrapper
                                                      same order on every rank
 World size 1 short-circuits every call. With the gloo backend, device tensors are staged through host memory (gloo has
 no all-to-all for device tensors): this lets several ranks share one GPU in tests of the multi-rank GPU path.
+
+RCCL audit mode (``SPHX_COMM_CHECK=1`` or ``Comm(check=True)``): RCCL refuses two ranks on one GPU, so the RCCL path
+cannot run on a 1-GPU box. Instead, every collective issued over gloo is checked against the constraints RCCL puts on
+it — contiguous tensors of an RCCL dtype, integer split sizes that sum to the tensor extents, send/receive tensors on
+one device — and appended to a per-rank signature log (op, dtype, trailing shape). ``verify_sequence()`` all-gathers a
+hash of that log and raises if any two ranks issued a different sequence of collectives (the condition that deadlocks
+or corrupts an RCCL communicator).
 """
 
 from __future__ import annotations
 
 import os
+import zlib
 from typing import List, Sequence, Tuple
 
 import torch
@@ -21,10 +29,17 @@ import torch.distributed as dist
 
 SUM, MIN, MAX = "sum", "min", "max"
 _OPS = {SUM: dist.ReduceOp.SUM, MIN: dist.ReduceOp.MIN, MAX: dist.ReduceOp.MAX}
+# element types RCCL can reduce / move (ncclDataType_t)
+RCCL_DTYPES = {torch.uint8, torch.int8, torch.int32, torch.int64, torch.float16, torch.bfloat16, torch.float32,
+               torch.float64}
+
+
+class CommCheckError(RuntimeError):
+    pass
 
 
 class Comm:
-    def __init__(self, group=None):
+    def __init__(self, group=None, check: bool | None = None):
         self.group = group
         if dist.is_available() and dist.is_initialized():
             self.rank = dist.get_rank(group)
@@ -32,13 +47,49 @@ class Comm:
             self.backend = dist.get_backend(group)
         else:
             self.rank, self.size, self.backend = 0, 1, None
+        self.check = os.environ.get("SPHX_COMM_CHECK") == "1" if check is None else check
+        self.log: List[str] = []
 
     def _staged(self, t: torch.Tensor) -> bool:
         return self.backend == "gloo" and t.is_cuda
 
+    # ----------------------------------------------------------------------------------------- RCCL audit
+    def _audit(self, op: str, *tensors: torch.Tensor, splits: Sequence[Sequence[int]] = ()):
+        if not self.check or self.size == 1:
+            return
+        dev = tensors[0].device
+        for t in tensors:
+            if not t.is_contiguous():
+                raise CommCheckError(f"{op}: non-contiguous tensor {tuple(t.shape)}")
+            if t.dtype not in RCCL_DTYPES:
+                raise CommCheckError(f"{op}: dtype {t.dtype} is not an RCCL type")
+            if t.device != dev:
+                raise CommCheckError(f"{op}: tensors on {dev} and {t.device}")
+        for sp, t in zip(splits, tensors):
+            if any((not isinstance(v, int)) or v < 0 for v in sp) or len(sp) != self.size:
+                raise CommCheckError(f"{op}: bad split sizes {list(sp)[:8]}")
+            if sum(sp) != (t.shape[0] if t.dim() else 1):
+                raise CommCheckError(f"{op}: splits sum {sum(sp)} != extent {t.shape[0]}")
+        t = tensors[0]
+        self.log.append(f"{op}:{str(t.dtype)}:{tuple(t.shape[1:])}")
+
+    def verify_sequence(self) -> int:
+        """all ranks must have issued the same collectives in the same order; returns the number checked"""
+        if self.size == 1:
+            return len(self.log)
+        sig = zlib.crc32("|".join(self.log).encode()) & 0x7FFFFFFF
+        t = torch.tensor([sig, len(self.log)], dtype=torch.int64, device=self._dev())
+        outs = [torch.empty_like(t) for _ in range(self.size)]
+        dist.all_gather(outs, t, group=self.group)
+        vals = [tuple(int(v) for v in o.cpu().tolist()) for o in outs]
+        if len(set(vals)) != 1:
+            raise CommCheckError(f"ranks issued different collective sequences: {vals}")
+        return len(self.log)
+
     # -------------------------------------------------------------------------------------------- collectives
     def allreduce(self, t: torch.Tensor, op: str = SUM) -> torch.Tensor:
         if self.size > 1:
+            self._audit("allreduce_" + op, t)
             if self._staged(t):
                 h = t.cpu()
                 dist.all_reduce(h, op=_OPS[op], group=self.group)
@@ -56,6 +107,8 @@ class Comm:
 
     def barrier(self):
         if self.size > 1:
+            if self.check:
+                self.log.append("barrier")
             if self.backend == "nccl":
                 dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
             else:
@@ -68,8 +121,9 @@ class Comm:
         """all-to-all of one integer per peer (replaces MPI_Probe + MPI_Get_count)"""
         if self.size == 1:
             return list(send_counts)
-        s = torch.tensor(list(send_counts), dtype=torch.int64, device=self._dev())
+        s = torch.tensor([int(v) for v in send_counts], dtype=torch.int64, device=self._dev())
         r = torch.empty_like(s)
+        self._audit("exchange_counts", s, r)
         dist.all_to_all_single(r, s, group=self.group)
         return [int(v) for v in r.cpu().tolist()]
 
@@ -80,10 +134,13 @@ class Comm:
             return send[: send_counts[0]].clone(), list(send_counts)
         if recv_counts is None:
             recv_counts = self.exchange_counts(send_counts)
+        send_counts = [int(v) for v in send_counts]
+        recv_counts = [int(v) for v in recv_counts]
         shape = (sum(recv_counts),) + tuple(send.shape[1:])
         staged = self._staged(send)
         src = send.contiguous().cpu() if staged else send.contiguous()
         recv = torch.empty(shape, dtype=send.dtype, device=src.device)
+        self._audit("alltoallv", src, recv, splits=(send_counts, recv_counts))
         dist.all_to_all_single(recv, src, output_split_sizes=list(recv_counts),
                                input_split_sizes=list(send_counts), group=self.group)
         return (recv.to(send.device) if staged else recv), list(recv_counts)
@@ -95,12 +152,14 @@ class Comm:
         if self._staged(t):
             return [o.to(t.device) for o in Comm.allgather_var(self, t.cpu())]
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+        self._audit("allgather_count", n)
         ns = [torch.empty_like(n) for _ in range(self.size)]
         dist.all_gather(ns, n, group=self.group)
         sizes = [int(v.item()) for v in ns]
         mx = max(sizes)
         pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
+        self._audit("allgather", pad)
         outs = [torch.empty_like(pad) for _ in range(self.size)]
         dist.all_gather(outs, pad, group=self.group)
         return [o[:s] for o, s in zip(outs, sizes)]
