@@ -1,20 +1,14 @@
 #!/bin/bash
-# One gpurun pass: GPU tests, smoke, then the two headline benches (Sedov -n 400, Evrard -n 200) with substep
-# timings. Every GPU step has its own time limit; the chain stops at the first failure.
-# usage: bash scripts/gpu_check.sh [tests|bench|all]
+# GPU tests + short Sedov/Evrard benches (used after each change that touches the GPU path)
 set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-what=${1:-all}
-if [ "$what" = tests ] || [ "$what" = all ]; then
-    timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-        > gpurun_out/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
-    tail -3 gpurun_out/gpu_tests.log
-    timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
-fi
-if [ "$what" = bench ] || [ "$what" = all ]; then
-    timeout -k 10 300 python bench.py --steps 5 --warmup 2 --verbose > gpurun_out/bench_sedov400.log 2>&1 || exit 1
-    head -1 gpurun_out/bench_sedov400.log
-    timeout -k 10 300 python bench.py --init evrard -n 200 --steps 5 --warmup 2 --verbose \
-        > gpurun_out/bench_evrard200.log 2>&1 || exit 1
-    head -1 gpurun_out/bench_evrard200.log
-fi
+export TMPDIR=/tmp
+TAG=${1:-check}
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -s --timeout 120 --timeout-method thread > gpurun_out/${TAG}_gputests.log 2>&1 || { echo "gpu tests failed"; tail -40 gpurun_out/${TAG}_gputests.log; exit 1; }
+tail -3 gpurun_out/${TAG}_gputests.log
+grep "fixed-point vs fp64" gpurun_out/${TAG}_gputests.log
+timeout -k 10 240 python -u bench.py --steps 10 --warmup 3 > gpurun_out/${TAG}_sedov.log 2>&1 || { tail -20 gpurun_out/${TAG}_sedov.log; exit 1; }
+grep metric gpurun_out/${TAG}_sedov.log | cut -c1-400
+timeout -k 10 240 python -u bench.py --init evrard -n 200 --steps 10 --warmup 3 --verbose > gpurun_out/${TAG}_evrard.log 2>&1 || { tail -20 gpurun_out/${TAG}_evrard.log; exit 1; }
+grep "metric\|substep\|stats" gpurun_out/${TAG}_evrard.log | cut -c1-400

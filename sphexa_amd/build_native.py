@@ -84,22 +84,31 @@ def _cpu_march():
     return []
 
 
-def build_cpu(verbose=False):
-    os.makedirs(OBJ, exist_ok=True)
+SANITIZE_FLAGS = ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"]
+
+
+def build_cpu(verbose=False, sanitize=False):
+    """``sanitize``: AddressSanitizer + UBSan build of the OpenMP module into _native/sanitize/ (loaded when
+    SPHX_CPU_VARIANT=sanitize; the process needs libasan preloaded, see tests/test_sanitize.py)"""
+    out_dir = os.path.join(OUT, "sanitize") if sanitize else OUT
+    obj_dir = os.path.join(out_dir, "obj") if sanitize else OBJ
+    os.makedirs(obj_dir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "cpu", "*.cpp")))
-    target = os.path.join(OUT, "_sphx_cpu" + EXT)
-    flags = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", f"-I{os.path.join(CSRC, 'include')}",
-             f"-I{os.path.join(CSRC, 'cpu')}"] + _cpu_march() + _py_includes()
+    target = os.path.join(out_dir, "_sphx_cpu" + EXT)
+    opt = ["-O1", "-g"] + SANITIZE_FLAGS if sanitize else ["-O3"] + _cpu_march()
+    flags = opt + ["-std=c++17", "-fPIC", "-fopenmp", f"-I{os.path.join(CSRC, 'include')}",
+                   f"-I{os.path.join(CSRC, 'cpu')}"] + _py_includes()
     hdrs = _headers()
+    force = _flags_changed(obj_dir, "cpu", flags)
     jobs, objs = [], []
     for s in srcs:
-        o = os.path.join(OBJ, "cpu_" + os.path.basename(s) + ".o")
+        o = os.path.join(obj_dir, "cpu_" + os.path.basename(s) + ".o")
         objs.append(o)
-        if _newer(o, [s] + hdrs):
+        if force or _newer(o, [s] + hdrs):
             jobs.append((["g++", *flags, "-c", s, "-o", o], o))
     _compile_all(jobs, verbose)
     if jobs or _newer(target, objs):
-        _run(["g++", "-shared", "-fopenmp", *objs, "-o", target])
+        _run(["g++", "-shared", "-fopenmp", *(SANITIZE_FLAGS if sanitize else []), *objs, "-o", target])
     return target
 
 
@@ -171,6 +180,9 @@ if __name__ == "__main__":
         tag = sys.argv[i + 1]
         defs = [a for a in sys.argv[i + 2:] if a.startswith(("-D", "-f", "-m"))]
         print("ok", build_hip(verbose=True, variant=tag, defines=defs))
+        sys.exit(0)
+    if "--sanitize" in sys.argv:
+        print("ok", build_cpu(verbose=True, sanitize=True))
         sys.exit(0)
     skip_hip = "--no-hip" in sys.argv
     for t in build_all(verbose=True, hip=not skip_hip):

@@ -68,6 +68,8 @@ class Propagator:
         first, last = domain.start_index(), domain.end_index()
         self.nl = find_neighbors(d, domain.octree, domain.box, first, last,
                                  nidx=self.nl.nidx if self.nl is not None else None)
+        if d.device.type == "cuda":
+            H.set_global_h_min(d, domain.comm)
         return first, last
 
     def _gravity(self, domain, d):
@@ -119,6 +121,9 @@ class Propagator:
         print(f"### Check ### Total time: {d.ttot}, current time-step: {d.minDt}", file=o)
         print(f"### Check ### Total energy: {d.etot}, (internal: {d.eint}, kinetic: {d.ecin}, gravitational: "
               f"{d.egrav})", file=o)
+        if getattr(d, "fixedPointPath", None) is not None:
+            print(f"### Check ### pair-loop coordinates: {'fixed-point' if d.fixedPointPath else 'fp64'} records "
+                  f"({getattr(d, 'fixedPointSwitches', 0)} switches)", file=o)
         ot = domain.octree
         print(f"### Check ### Focus Tree Nodes: {ot.num_leaves if ot else 0}, maxDepth {ot.max_depth() if ot else 0}",
               file=o)

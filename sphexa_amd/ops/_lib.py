@@ -21,7 +21,12 @@ def _load(name: str):
         return _cache[name]
     path = os.path.join(_NATIVE_DIR, name + _EXT)
     variant = os.environ.get("SPHX_HIP_VARIANT") if name == "_sphx_hip" else None
-    if variant:
+    if name == "_sphx_cpu" and os.environ.get("SPHX_CPU_VARIANT") == "sanitize":
+        # ASan/UBSan build of the OpenMP module (build_native --sanitize)
+        path = os.path.join(_NATIVE_DIR, "sanitize", name + _EXT)
+        if not os.path.exists(path):
+            raise ImportError(f"sanitizer build not found: {path} (python -m sphexa_amd.build_native --sanitize)")
+    elif variant:
         # tuning builds: sphexa_amd/_native/variants/<tag>/_sphx_hip*.so (build_native --variant tag -DNAME=V ...)
         path = os.path.join(_NATIVE_DIR, "variants", variant, name + _EXT)
         if not os.path.exists(path):

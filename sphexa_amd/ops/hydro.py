@@ -74,26 +74,57 @@ def compute_density(d, nl: NeighborList, box: Box):
 
 
 # fixed-point records: the coordinate quantum (box length / 2^32 periodic, / 2^30 open) must stay below this
-# fraction of the SMALLEST h, i.e. the separation error of the densest particle below ~4e-6 h (~16 fp32 ulp at
-# r = h; a median particle is typically 10x better: Evrard -n 200 hmin/hmed = 0.087, Sedov lattice: 1)
-FIXED_POINT_REL_QUANTUM = 2.0 ** -18
+# fraction of the SMALLEST h. The wrapping int32 difference of two records is exact up to one quantum per component,
+# then rounded once to fp32, so a separation carries <= 2^-22 h_min of error: within 2-4x of the reference's fp32
+# rounding of its fp64 difference at the kernel support of the smallest particle (2^-24 |dx|, |dx| < 2h) and below
+# it for every particle with h >= 4 h_min (sph_math.hpp QFrame). Boxes/h that fail the bound switch the loops to
+# fp64-coordinate records: Evrard's open, collapsing cloud does; periodic lattices down to h ~ 1e-3 L do not.
+FIXED_POINT_REL_QUANTUM = 2.0 ** -22
+
+
+def invalidate_h_cache(d):
+    """h was rewritten by a native kernel (h iteration, h update) or replaced by the domain sync"""
+    d._h_min = None
+    d._h_min_global = None
+
+
+def set_global_h_min(d, comm):
+    """smallest h over all ranks (own + halo particles), so every rank takes the same record path in a step"""
+    h = d["h"][: d.size]
+    loc = h.min().to(torch.float64).reshape(1) if h.numel() else torch.full((1,), math.inf, dtype=torch.float64,
+                                                                              device=h.device)
+    if comm is not None and comm.size > 1:
+        comm.allreduce(loc, "min")
+    d._h_min_global = float(loc.item())
+
+
+def quantum(box: Box) -> float:
+    q = 0.0
+    for L, bc in zip(box.lengths(), box.bc):
+        L = L if L > 0 else 1.0
+        q = max(q, L / (2.0 ** 32 if bc == PERIODIC else 2.0 ** 30))
+    return q
 
 
 def fixed_point_ok(d, box: Box) -> bool:
     """Whether the GPU pair loops may read fixed-point coordinate records (QFrame, sph_math.hpp) for this box and
-    these smoothing lengths; otherwise they read fp64-coordinate records. Cached on the identity and version of h."""
-    h = d["h"][: d.size]
-    key = (h.data_ptr(), h.numel(), h._version)
-    hit = getattr(d, "_h_min", None)
-    if hit is None or hit[0] != key:
-        hit = (key, float(h.min()) if h.numel() else 0.0)
-        d._h_min = hit
-    hmin = hit[1]
-    quantum = 0.0
-    for L, bc in zip(box.lengths(), box.bc):
-        L = L if L > 0 else 1.0
-        quantum = max(quantum, L / (2.0 ** 32 if bc == PERIODIC else 2.0 ** 30))
-    return hmin > 0 and quantum <= FIXED_POINT_REL_QUANTUM * hmin
+    these smoothing lengths; otherwise they read fp64-coordinate records. Uses the per-step global minimum of h when
+    the propagator has set one (set_global_h_min), else the local minimum cached on the identity and version of h."""
+    hmin = getattr(d, "_h_min_global", None)
+    if hmin is None:
+        h = d["h"][: d.size]
+        key = (h.data_ptr(), h.numel(), h._version)
+        hit = getattr(d, "_h_min", None)
+        if hit is None or hit[0] != key:
+            hit = (key, float(h.min()) if h.numel() else 0.0)
+            d._h_min = hit
+        hmin = hit[1]
+    ok = hmin > 0 and quantum(box) <= FIXED_POINT_REL_QUANTUM * hmin
+    prev = getattr(d, "fixedPointPath", None)
+    if prev is not None and prev != ok:
+        d.fixedPointSwitches = getattr(d, "fixedPointSwitches", 0) + 1
+    d.fixedPointPath = ok
+    return ok
 
 
 def _consts(d, box: Box):
@@ -256,3 +287,4 @@ def update_smoothing_length(d, first: int, last: int):
         _lib.hip().update_h(*args, _stream())
     else:
         _lib.cpu().update_h(*args)
+    invalidate_h_cache(d)

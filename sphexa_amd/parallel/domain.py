@@ -45,13 +45,18 @@ from .comm import Comm, MAX, MIN, SUM
 HALO_FIELDS = ("x", "y", "z", "h", "m")
 
 
+class HaloOwnershipError(RuntimeError):
+    """a received halo does not lie in its sender's SFC range (reference halos/halos.hpp:73-105 aborts with 35)"""
+
+
 def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
 class Domain:
     def __init__(self, comm: Comm, box: Box, bucket_size_focus: int = 64, bucket_size: Optional[int] = None,
-                 theta: float = 1.0, sfc_kind: int = sfc_ops.HILBERT, halo_cut_boxes: int = 4096):
+                 theta: float = 1.0, sfc_kind: int = sfc_ops.HILBERT, halo_cut_boxes: int = 4096,
+                 check_halos: bool = True):
         self.comm = comm
         self.rank, self.size = comm.rank, comm.size
         self.box = box.copy()
@@ -60,6 +65,7 @@ class Domain:
         self.theta = theta
         self.sfc_kind = sfc_kind
         self.halo_cut_boxes = halo_cut_boxes
+        self.check_halos = check_halos
 
         self.start = 0
         self.end = 0
@@ -160,6 +166,13 @@ class Domain:
                 if sl.stop > sl.start:
                     sfc_ops.compute_keys(d["x"][sl], d["y"][sl], d["z"][sl], self.box, self.sfc_kind,
                                          out=d["keys"][sl])
+            if self.check_halos:
+                self._check_halo_ownership(d["keys"])
+        # native kernels write h in place (h iteration, h update) without bumping the tensor version: drop the
+        # cached per-step reductions of h and m so the pair loops re-derive them for the new particle set
+        d._h_min = None
+        d._h_min_global = None
+        d._m_uniform = None
 
         all_keys = d["keys"]
         self.local_tree, counts = octree_ops.update_tree(self.local_tree, all_keys, self.bucket_size_focus)
@@ -269,6 +282,24 @@ class Domain:
         self.n_hi = sum(self.halo_recv_counts[self.rank + 1:])
         self._halo_send_rel = send_idx  # relative to own block, converted to absolute below
         self.halo_send_idx = [t + self.n_lo for t in send_idx]
+
+    def _check_halo_ownership(self, keys: torch.Tensor):
+        """every halo received from rank q must carry an SFC key inside q's assigned range, and no halo may fall into
+        this rank's own range (the push-based analog of the reference's checkHalos, halos/halos.hpp:73-105)"""
+        if self.n_lo + self.n_hi == 0:
+            return
+        dev = keys.device
+        bounds = torch.tensor([k if k < 2 ** 63 else 2 ** 63 - 1 for k in self.assignment_keys[1:-1]],
+                              dtype=torch.int64, device=dev)
+        halo_keys = torch.cat([keys[: self.start], keys[self.end:]])
+        senders = [q for q in range(self.size) if q != self.rank]
+        counts = torch.tensor([self.halo_recv_counts[q] for q in senders], dtype=torch.int64)
+        expected = torch.repeat_interleave(torch.tensor(senders, dtype=torch.int64), counts).to(dev)
+        owner = torch.searchsorted(bounds, halo_keys, right=True)
+        bad = int((owner != expected).sum().item())
+        if bad:
+            raise HaloOwnershipError(f"rank {self.rank}: {bad} halo particles are not owned by the rank that sent "
+                                     f"them (assignment {self.assignment_keys})")
 
     def _exchange_multipoles(self, mp_send, gcenters, gquads):
         """one alltoallv of (center xyz f64, quadrupole 8 x f32) rows for the LET far field"""

@@ -17,19 +17,40 @@ class _D:
 
 
 def test_fixed_point_guard():
-    d = _D(torch.full((4,), 1e-3, dtype=torch.float32))
+    d = _D(torch.full((4,), 4e-3, dtype=torch.float32))
+    assert H.FIXED_POINT_REL_QUANTUM <= 2.0 ** -22
     assert H.fixed_point_ok(d, Box([0.0] * 3, [1.0] * 3, [PERIODIC] * 3))
+    # open dimensions use 2^30 steps: 1 / 2^30 = 9.3e-10 <= 2^-22 * 4e-3 = 9.5e-10
     assert H.fixed_point_ok(d, Box([0.0] * 3, [1.0] * 3, [OPEN] * 3))
-    # open box 1000x larger: quantum 1e3 / 2^30 ~ 9e-7 > 2^-18 * 1e-3
-    assert not H.fixed_point_ok(d, Box([0.0] * 3, [1e3] * 3, [OPEN] * 3))
+    assert not H.fixed_point_ok(d, Box([0.0] * 3, [1.1] * 3, [OPEN] * 3))
     # periodic dimensions use the full 2^32 range
-    assert H.fixed_point_ok(d, Box([0.0] * 3, [2.0] * 3, [PERIODIC] * 3))
+    assert H.fixed_point_ok(d, Box([0.0] * 3, [4.0] * 3, [PERIODIC] * 3))
+    assert not H.fixed_point_ok(d, Box([0.0] * 3, [4.2] * 3, [PERIODIC] * 3))
 
 
 def test_fixed_point_guard_tracks_h_updates():
-    h = torch.full((4,), 1e-3, dtype=torch.float32)
+    h = torch.full((4,), 4e-3, dtype=torch.float32)
     d = _D(h)
     box = Box([0.0] * 3, [1.0] * 3, [OPEN] * 3)
     assert H.fixed_point_ok(d, box)
     h[2] = 1e-9  # in-place update bumps the version: the cached minimum is recomputed
     assert not H.fixed_point_ok(d, box)
+
+
+def test_native_h_writers_invalidate_the_cache():
+    """update_smoothing_length writes h through its data pointer (no version bump): the cached minimum must go"""
+    from sphexa_amd.models import particles as P
+
+    d = P.ParticlesData("cpu")
+    d.set_conserved("x", "y", "z", "h", "m")
+    d.set_dependent("nc")
+    d.resize(64)
+    d["h"] = 4e-3
+    d["nc"] = 1  # far too few neighbors: update_h grows h
+    box = Box([0.0] * 3, [1.0] * 3, [OPEN] * 3)
+    assert H.fixed_point_ok(d, box)
+    d._h_min_global = 1e-9  # a stale per-step value
+    H.update_smoothing_length(d, 0, 64)
+    assert getattr(d, "_h_min_global", None) is None
+    assert H.fixed_point_ok(d, box)
+    assert H.fixed_point_ok(d, box) and d._h_min[1] > 4e-3

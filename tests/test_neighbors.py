@@ -76,3 +76,19 @@ def test_ngmax_capping():
     assert nc.max() - 1 > 20  # counts are not capped
     sets = neighbor_lists_as_sets(nl, d["nc"])
     assert max(len(s) for s in sets) == 20
+
+
+def test_h_iteration_failure_raises(monkeypatch):
+    """reference sph/hydro_ve/xmass_gpu.cu:82-92,131 throws when the coupled nc/h iteration does not converge in 10
+    rounds. 30 particles can never give ng0/4 = 50 neighbors, so every particle fails."""
+    from sphexa_amd.ops import neighbors as N
+
+    box = Box.cube(0.0, 1.0, PERIODIC)
+    d, ot, X = _dataset(30, 0.05, box, seed=4)
+    d.ng0, d.ngmax = 200, 250
+    with pytest.raises(N.NeighborSearchError, match="failed to converge"):
+        find_neighbors(d, ot, box, 0, d.size, iterate_h=True)
+    monkeypatch.setattr(N, "ALLOW_NC_FAIL", True)
+    d["h"] = 0.05
+    find_neighbors(d, ot, box, 0, d.size, iterate_h=True)
+    assert d.nc_fail == 30
