@@ -167,8 +167,22 @@ def build_io(verbose=False):
     return target
 
 
+def build_golden(verbose=False):
+    """fp64 instantiation of the SPH j-loops (golden-value tests, csrc/golden/golden.cpp)"""
+    os.makedirs(OBJ, exist_ok=True)
+    src = os.path.join(CSRC, "golden", "golden.cpp")
+    target = os.path.join(OUT, "_sphx_golden" + EXT)
+    flags = ["-O2", "-std=c++17", "-fPIC", "-DSPHX_HYDRO_TYPE=double", f"-I{os.path.join(CSRC, 'include')}"] + \
+        _py_includes()
+    if _newer(target, [src] + _headers()) or _flags_changed(OBJ, "golden", flags):
+        _run(["g++", *flags, "-shared", src, "-o", target])
+        if verbose:
+            print("  built _sphx_golden", flush=True)
+    return target
+
+
 def build_all(verbose=False, hip=True):
-    out = [build_cpu(verbose), build_io(verbose)]
+    out = [build_cpu(verbose), build_io(verbose), build_golden(verbose)]
     if hip:
         out.append(build_hip(verbose))
     return [o for o in out if o]

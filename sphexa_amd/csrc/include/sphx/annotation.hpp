@@ -66,4 +66,8 @@ SPHX_HD float rcpF(float x)
 #endif
 }
 
+// fp64 instantiations of the hydro math (golden-value tests) keep full precision
+SPHX_HD double sqrtF(double x) { return std::sqrt(x); }
+SPHX_HD double rcpF(double x) { return 1.0 / x; }
+
 } // namespace sphx

@@ -27,7 +27,13 @@
 namespace sphx
 {
 
-using HT = float;   // hydro precision (reference sph/types.hpp:39-46)
+#ifndef SPHX_HYDRO_TYPE
+#define SPHX_HYDRO_TYPE float
+#endif
+// hydro precision (reference sph/types.hpp:39-46). Production builds use float; the golden-value module
+// (csrc/golden, tests/test_golden.py) instantiates the same j-loops with double, as the reference's sph/test does.
+using HT = SPHX_HYDRO_TYPE;
+constexpr bool kHydroF32 = sizeof(HT) == 4;
 using CT = double;  // coordinate precision
 
 constexpr int kTableSize = 20000;
@@ -232,7 +238,7 @@ struct alignas(16) SrcIad
     };
     HT divv;
 };
-static_assert(sizeof(SrcIad) == 48, "SrcIad is three 16-byte chunks");
+static_assert(!kHydroF32 || sizeof(SrcIad) == 48, "SrcIad is three 16-byte chunks");
 
 //! @brief VE momentum/energy: 96 B (+ velocity gradient for AV cleaning: 128 B). Per-particle factors of the pair
 //!        terms are precomputed at pack time (1/h, m/rho) so the pair loop has no divisions.
@@ -282,7 +288,7 @@ struct alignas(16) SrcIadQ
     HT vx, vy, vz;
     HT xm;
 };
-static_assert(sizeof(SrcIadQ) == 32, "SrcIadQ is two 16-byte chunks");
+static_assert(!kHydroF32 || sizeof(SrcIadQ) == 32, "SrcIadQ is two 16-byte chunks");
 
 struct alignas(16) SrcMomQ
 {
@@ -293,7 +299,7 @@ struct alignas(16) SrcMomQ
     HT m, c, xm, rho;
     HT prho, alpha, mrho;
 };
-static_assert(sizeof(SrcMomQ) == 80, "SrcMomQ is five 16-byte chunks");
+static_assert(!kHydroF32 || sizeof(SrcMomQ) == 80, "SrcMomQ is five 16-byte chunks");
 
 //! @brief source mass of a Gradh record: stored, or the uniform mass of the launch (SrcXmQ)
 SPHX_HD HT massOf(const SrcPos& p, HT) { return p.m; }

@@ -41,6 +41,8 @@ def _load(name: str):
             build_native.build_hip()
         elif name == "_sphx_io":
             build_native.build_io()
+        elif name == "_sphx_golden":
+            build_native.build_golden()
     if not os.path.exists(path):
         raise ImportError(f"native module {name} not found at {path}")
     spec = importlib.util.spec_from_file_location(name, path)
@@ -61,6 +63,10 @@ def hip():
 
 def io():
     return _load("_sphx_io")
+
+
+def golden():
+    return _load("_sphx_golden")
 
 
 def native_paths():
