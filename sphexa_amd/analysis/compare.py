@@ -1,9 +1,12 @@
 """Compare an SPH snapshot with the analytical solution of its test case and print L1 errors.
 
     python -m sphexa_amd.analysis.compare dump_sedov.h5 [--step N | --time T] [--case sedov|noh|gresho-chan]
+    python -m sphexa_amd.analysis.compare dump_evrard.h5 --case evrard --tstar 0.77
 
 Parity: reference main/src/analytical_solutions/compare_solutions.py:85-126 (Sedov), compare_noh.py (Noh),
-compare_gresho_chan.py (tangential velocity). The reference Sedov script compares pressure and velocity against
+compare_gresho_chan.py (tangential velocity), compare_evrard.py:380-440 (Evrard collapse: the snapshot closest to
+t/t* in {0.77, 1.29, 2.58}, density/pressure/radial velocity normalized and compared with the tabulated profiles,
+L1 = mean |interp(solution, r_i) - value_i|). The reference Sedov script compares pressure and velocity against
 the *density* column of the solution (compare_solutions.py:107,115); its CI thresholds (.jenkins/reframe_ci.py:
 350-353) were recorded with that comparison, so ``reference_quirk=True`` reproduces it for parity checks while the
 default compares like with like.
@@ -96,6 +99,19 @@ def l1_errors(data, attrs, settings, case="sedov", reference_quirk=False):
             out["Pressure"] = S.l1_error(r, data["p"], y_exact=ex["p"])
         if vr is not None:
             out["Velocity"] = S.l1_error(r, vr, y_exact=ex["vel"])
+    elif case == "evrard":
+        norms = S.evrard_norms(settings.get("gravConstant", settings.get("G", 1.0)), settings.get("r", 1.0),
+                               settings.get("mTotal", 1.0))
+        tstar = min(S.EVRARD_TIMES, key=lambda ts: abs(ts * norms["t"] - t))
+        prof = S.evrard_profiles()[tstar]
+        out["t/t*"] = t / norms["t"]
+        if "rho" in data:
+            out["Density"] = S.l1_error(r, data["rho"] / norms["rho"], prof["rho"][:, 0], prof["rho"][:, 1])
+        if "p" in data:
+            out["Pressure"] = S.l1_error(r, data["p"] / norms["p"], prof["p"][:, 0], prof["p"][:, 1])
+        if "vx" in data:
+            vr = (data["vx"] * x + data["vy"] * y + data["vz"] * z) / np.maximum(r, 1e-300)
+            out["Velocity"] = S.l1_error(r, vr / norms["vel"], prof["vel"][:, 0], prof["vel"][:, 1])
     elif case == "gresho-chan":
         r2 = np.sqrt(x * x + y * y)
         vt = (-y * data["vx"] + x * data["vy"]) / np.maximum(r2, 1e-300)
@@ -112,12 +128,21 @@ def main(argv=None):
     g = ap.add_mutually_exclusive_group()
     g.add_argument("-s", "--step", type=int)
     g.add_argument("-t", "--time", type=float)
-    ap.add_argument("--case", default=None, help="sedov | noh | gresho-chan (default: from file attributes)")
+    ap.add_argument("--case", default=None, help="sedov | noh | gresho-chan | evrard (default: from file attributes)")
+    ap.add_argument("--tstar", type=float, default=None, choices=list(S.EVRARD_TIMES),
+                    help="Evrard: compare the snapshot closest to this t/t*")
     ap.add_argument("--reference-quirk", action="store_true",
                     help="compare p and |v| against the density solution like the reference script")
     a = ap.parse_args(argv)
-    data, attrs, settings = load_snapshot(a.simFile, a.step, a.time)
+    time = a.time
+    if a.tstar is not None:
+        a.case = a.case or "evrard"
+        s0 = load_snapshot(a.simFile, None, None)[2]
+        time = a.tstar * S.evrard_norms(s0.get("gravConstant", 1.0), s0.get("r", 1.0), s0.get("mTotal", 1.0))["t"]
+    data, attrs, settings = load_snapshot(a.simFile, a.step, time)
     case = a.case
+    if case is None and "mTotal" in settings and settings.get("gravConstant", 0) != 0:
+        case = "evrard"
     if case is None:
         case = "noh" if "vr0" in settings and settings.get("vr0", 0) < 0 else (
             "gresho-chan" if "gresho-chan" in settings else "sedov")

@@ -134,3 +134,31 @@ def l1_error(r_sim, y_sim, r_sol=None, y_sol=None, y_exact=None):
         order = np.argsort(r_sol)
         y_exact = np.interp(r_sim, np.asarray(r_sol)[order], np.asarray(y_sol)[order])
     return float(np.abs(np.asarray(y_exact) - np.asarray(y_sim)).sum() / len(y_sim))
+
+
+# ------------------------------------------------------------------------------------------------- Evrard
+EVRARD_TIMES = (0.77, 1.29, 2.58)
+
+
+def evrard_profiles():
+    """Tabulated Evrard collapse profiles (density, pressure, radial velocity vs radius, normalized units) at
+    t/t* = 0.77, 1.29, 2.58 — the curves of Evrard (1988) / Steinmetz & Mueller (1993) as tabulated by the reference
+    (main/src/analytical_solutions/compare_evrard.py:86-419; data in analysis/data/evrard_profiles.json)."""
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "evrard_profiles.json")) as f:
+        raw = json.load(f)["profiles"]
+    out = {}
+    for k, t in enumerate(EVRARD_TIMES, start=1):
+        out[t] = {q: np.asarray(raw[f"Evrard_{name}_t{k}"], dtype=np.float64)
+                  for q, name in (("rho", "Density"), ("p", "Pressure"), ("vel", "Velocity"))}
+    return out
+
+
+def evrard_norms(G=1.0, R=1.0, M=1.0):
+    """normalization of the tabulated profiles: time sqrt(R^3 / (G M)), density 3M / (4 pi R^3), internal energy
+    G M / R, velocity sqrt(G M / R), pressure rho_norm u_norm (compare_evrard.py:391-396)"""
+    rho = 3.0 * M / (4.0 * np.pi * R ** 3)
+    u = G * M / R
+    return dict(t=float(np.sqrt(R ** 3 / (G * M))), rho=rho, u=u, vel=float(np.sqrt(u)), p=rho * u)

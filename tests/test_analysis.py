@@ -49,3 +49,29 @@ def test_compare_tool(tmp_path, capsys):
     assert compare_main([out]) == 0
     txt = capsys.readouterr().out
     assert "Density L1 error" in txt and "Pressure L1 error" in txt and "Velocity L1 error" in txt
+
+
+def test_evrard_profiles_table():
+    prof = S.evrard_profiles()
+    assert sorted(prof) == [0.77, 1.29, 2.58]
+    for t, q in prof.items():
+        for name in ("rho", "p", "vel"):
+            r = q[name][:, 0]
+            # radii increase except at the digitized shock jump of the t/t* = 1.29 density curve
+            assert q[name].shape[1] == 2 and (np.diff(r) > -1e-3).all() and r[0] < 0.01 < 0.8 < r[-1]
+        # the collapse: density and pressure fall with radius
+        assert q["rho"][0, 1] > 1e3 > q["rho"][-1, 1]
+    n = S.evrard_norms(1.0, 1.0, 1.0)
+    assert n["t"] == 1.0 and n["rho"] == pytest.approx(3 / (4 * math.pi))
+
+
+def test_compare_tool_evrard(tmp_path, capsys):
+    from sphexa_amd.analysis.compare import main as compare_main
+    from sphexa_amd.app import sphexa
+
+    out = str(tmp_path / "dump_evrard.h5")
+    assert sphexa.main(["--init", "evrard", "-n", "12", "-s", "2", "-w", "2", "-f", "x,y,z,rho,p,vx,vy,vz", "-o", out,
+                        "--device", "cpu", "--quiet"]) == 0
+    assert compare_main([out, "--case", "evrard"]) == 0
+    txt = capsys.readouterr().out
+    assert "Density L1 error" in txt and "Pressure L1 error" in txt and "Velocity L1 error" in txt
