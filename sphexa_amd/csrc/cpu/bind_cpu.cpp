@@ -20,6 +20,7 @@ void bindTreeUtil(py::module& m);
 void bindGravityExtra(py::module& m);
 void bindCooling(py::module& m);
 void bindMultipole(py::module& m);
+void bindLetTree(py::module& m);
 int64_t findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                       const TreeView& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, uint32_t* nc,
                       bool iterateH);
@@ -132,6 +133,7 @@ PYBIND11_MODULE(_sphx_cpu, m)
     cpu::bindGravityExtra(m);
     cpu::bindCooling(m);
     cpu::bindMultipole(m);
+    cpu::bindLetTree(m);
 
     m.def("num_threads", []() { return omp_get_max_threads(); });
 
@@ -407,22 +409,29 @@ PYBIND11_MODULE(_sphx_cpu, m)
 
     m.def("gravity_upsweep",
           [](int64_t N, Ptr child, Ptr n2l, std::vector<int64_t> levelRange, Ptr prefixes, Ptr ns, Ptr ne, Ptr x,
-             Ptr y, Ptr z, Ptr mm, const BoxArr& box, int kind, double invTheta, Ptr centers, Ptr mp)
+             Ptr y, Ptr z, Ptr mm, const BoxArr& box, int kind, double invTheta, Ptr centers, Ptr mp,
+             bool leavesGiven)
           {
               cpu::gravityUpsweep(N, P<int32_t>(child), P<int32_t>(n2l), levelRange.data(), P<KeyT>(prefixes),
                                   P<int32_t>(ns), P<int32_t>(ne), P<double>(x), P<double>(y), P<double>(z),
                                   P<float>(mm), toBox(box), kind, invTheta, P<double>(centers),
-                                  P<Quadrupole>(mp));
-          });
+                                  P<Quadrupole>(mp), leavesGiven);
+          },
+          py::arg("N"), py::arg("child"), py::arg("n2l"), py::arg("levelRange"), py::arg("prefixes"), py::arg("ns"),
+          py::arg("ne"), py::arg("x"), py::arg("y"), py::arg("z"), py::arg("mm"), py::arg("box"), py::arg("kind"),
+          py::arg("invTheta"), py::arg("centers"), py::arg("mp"), py::arg("leavesGiven") = false);
     m.def("compute_gravity",
           [](int64_t first, int64_t last, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr centers, Ptr mp, Ptr x, Ptr y,
-             Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay, Ptr az, Ptr ugrav)
+             Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay, Ptr az, Ptr ugrav, Ptr stats)
           {
               return cpu::computeGravity(first, last, P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns),
                                          P<int32_t>(ne), P<double>(centers), P<Quadrupole>(mp), P<double>(x),
                                          P<double>(y), P<double>(z), P<float>(h), P<float>(mm), G, P<float>(ax),
-                                         P<float>(ay), P<float>(az), P<double>(ugrav));
-          });
+                                         P<float>(ay), P<float>(az), P<double>(ugrav), P<int64_t>(stats));
+          },
+          py::arg("first"), py::arg("last"), py::arg("child"), py::arg("n2l"), py::arg("ns"), py::arg("ne"),
+          py::arg("centers"), py::arg("mp"), py::arg("x"), py::arg("y"), py::arg("z"), py::arg("h"), py::arg("mm"),
+          py::arg("G"), py::arg("ax"), py::arg("ay"), py::arg("az"), py::arg("ugrav"), py::arg("stats") = 0);
     m.def("direct_sum",
           [](int64_t first, int64_t last, int64_t n, Ptr x, Ptr y, Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay,
              Ptr az, Ptr ugrav)

@@ -83,11 +83,11 @@ namespace sphx::cpu
 void gravityUpsweep(int64_t N, const int32_t* child, const int32_t* n2l, const int64_t* levelRange,
                     const KeyT* prefixes, const int32_t* ns, const int32_t* ne, const double* x, const double* y,
                     const double* z, const float* m, const Box& box, int kind, double invTheta, double* centers,
-                    Quadrupole* mp);
+                    Quadrupole* mp, bool leavesGiven = false);
 double computeGravity(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
                       const int32_t* ne, const double* centers, const Quadrupole* mp, const double* x,
                       const double* y, const double* z, const float* h, const float* m, double G, float* ax,
-                      float* ay, float* az, double* ugrav);
+                      float* ay, float* az, double* ugrav, int64_t* stats = nullptr);
 double directSum(int64_t first, int64_t last, int64_t n, const double* x, const double* y, const double* z,
                  const float* h, const float* m, double G, float* ax, float* ay, float* az, double* ugrav);
 void markLet(int64_t nb, const double* bc, const double* bh, const int32_t* child, const int32_t* n2l,

@@ -19,12 +19,13 @@ namespace sphx::cpu
 void gravityUpsweep(int64_t N, const int32_t* child, const int32_t* n2l, const int64_t* levelRange,
                     const KeyT* prefixes, const int32_t* ns, const int32_t* ne, const double* x, const double* y,
                     const double* z, const float* m, const Box& box, int kind, double invTheta, double* centers,
-                    Quadrupole* mp)
+                    Quadrupole* mp, bool leavesGiven)
 {
+    // leavesGiven: leaf centers (mass in slot 3) and quadrupoles are already set (remote LET tree)
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t i = 0; i < N; ++i)
     {
-        if (n2l[i] < 0) continue;
+        if (n2l[i] < 0 || leavesGiven) continue;
         double c[4] = {0, 0, 0, 0};
         for (int32_t p = ns[i]; p < ne[i]; ++p)
         {
@@ -94,11 +95,12 @@ void gravityUpsweep(int64_t N, const int32_t* child, const int32_t* n2l, const i
 double computeGravity(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
                       const int32_t* ne, const double* centers, const Quadrupole* mp, const double* x,
                       const double* y, const double* z, const float* h, const float* m, double G, float* ax,
-                      float* ay, float* az, double* ugrav)
+                      float* ay, float* az, double* ugrav, int64_t* stats)
 {
     constexpr int64_t groupSize = 16;
     double ugravTot             = 0;
-#pragma omp parallel for schedule(dynamic, 4) reduction(+ : ugravTot)
+    int64_t nM2P = 0, nP2P = 0; // interactions summed over targets (stats[0] M2P, stats[1] P2P)
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : ugravTot, nM2P, nP2P)
     for (int64_t g0 = first; g0 < last; g0 += groupSize)
     {
         int64_t nt = std::min(groupSize, last - g0);
@@ -130,11 +132,13 @@ double computeGravity(int64_t first, int64_t last, const int32_t* child, const i
             if (!violated)
             {
                 if (c[3] == 0) continue; // empty
+                nM2P += nt;
                 for (int64_t k = 0; k < nt; ++k)
                     m2p(x[g0 + k] - c[0], y[g0 + k] - c[1], z[g0 + k] - c[2], mp[node], acc[k]);
             }
             else if (n2l[node] >= 0)
             {
+                nP2P += nt * int64_t(ne[node] - ns[node]);
                 for (int64_t k = 0; k < nt; ++k)
                 {
                     int64_t i = g0 + k;
@@ -159,6 +163,11 @@ double computeGravity(int64_t first, int64_t last, const int32_t* child, const i
             ay[i] += float(G * acc[k][2]);
             az[i] += float(G * acc[k][3]);
         }
+    }
+    if (stats)
+    {
+        stats[0] += nM2P;
+        stats[1] += nP2P;
     }
     return 0.5 * ugravTot;
 }

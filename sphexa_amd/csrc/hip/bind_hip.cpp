@@ -413,6 +413,8 @@ PYBIND11_MODULE(_sphx_hip, m)
               markLet(nb, P<double>(bc), P<double>(bh), P<int32_t>(child), P<int32_t>(n2l), P<double>(tc),
                       P<double>(th), P<double>(gc), toBox(box), P<uint8_t>(failed), St(s));
           });
+    m.def("mark_outside_range", [](int64_t N, Ptr prefixes, uint64_t lo, uint64_t hi, Ptr failed, Ptr s)
+          { markOutsideRange(N, P<KeyT>(prefixes), lo, hi, P<uint8_t>(failed), St(s)); });
     m.def("m2p_flat",
           [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr mm, int64_t M, Ptr mc, Ptr mp, double G, Ptr ax,
              Ptr ay, Ptr az, Ptr ugrav, Ptr out, Ptr s)

@@ -1095,6 +1095,26 @@ void markLet(int64_t nb, const double* bc, const double* bh, const int32_t* chil
     SPHX_LAUNCH_CHECK();
 }
 
+//! @brief open every node whose key range is not inside the sender's assigned range [lo, hi): remote LET nodes of
+//!        different senders are then disjoint (cpu/let_tree_cpu.cpp)
+__global__ void markOutsideRangeKernel(int64_t N, const KeyT* __restrict__ prefixes, KeyT lo, KeyT hi,
+                                       uint8_t* __restrict__ failed)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const int l    = placeholderLevel(prefixes[i]);
+    const KeyT k   = placeholderKey(prefixes[i]);
+    const KeyT end = k + nodeRange(l);
+    if (k < lo || end > hi) failed[i] = 1;
+}
+
+void markOutsideRange(int64_t N, const KeyT* prefixes, KeyT lo, KeyT hi, uint8_t* failed, hipStream_t s)
+{
+    if (N <= 0) return;
+    markOutsideRangeKernel<<<gridFor(N, 256), 256, 0, s>>>(N, prefixes, lo, hi, failed);
+    SPHX_LAUNCH_CHECK();
+}
+
 constexpr int kFlatBlock = 256;
 
 /*! @brief every target against every remote multipole (all of them pass the MAC by construction of the LET);

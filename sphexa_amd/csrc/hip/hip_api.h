@@ -179,6 +179,7 @@ void directSum(int64_t first, int64_t last, int64_t n, const double* x, const do
 
 void markLet(int64_t nb, const double* bc, const double* bh, const int32_t* child, const int32_t* n2l,
              const double* tc, const double* th, const double* gc, const Box& box, uint8_t* failed, hipStream_t s);
+void markOutsideRange(int64_t N, const KeyT* prefixes, KeyT lo, KeyT hi, uint8_t* failed, hipStream_t s);
 void m2pFlat(int64_t first, int64_t last, const double* x, const double* y, const double* z, const float* m,
              int64_t M, const double* mc, const void* mp, float G, float* ax, float* ay, float* az, double* ugrav,
              double* out, hipStream_t s);

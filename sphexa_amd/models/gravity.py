@@ -5,8 +5,10 @@ egrav = 0.5 G sum m phi, accelerations added to ax, ay, az) and ryoanji/interfac
 
 Multi-rank: the local octree covers own particles and the halos; remote far-field contributions come through the
 locally-essential tree exchange done in Domain.sync(gravity=True) (parallel/domain.py): every rank pushes to every
-other rank the multipoles of its nodes that satisfy the vector MAC with respect to the receiver's boxes, and the
-particles of leaves that do not (they arrive as halos). Received multipoles are applied as a flat M2P list.
+other rank the multipoles of its nodes that satisfy the vector MAC with respect to the receiver's boxes (and lie in
+the sender's SFC range), and the particles of leaves that do not (they arrive as halos). The received multipoles are
+the leaves of a remote LET tree (ops.gravity.remote_let_tree) that is traversed like the local one: far groups of
+remote nodes are taken as one combined multipole, so the far-field cost grows with log(M), not M.
 """
 
 from __future__ import annotations
@@ -33,8 +35,12 @@ class MultipoleHolder:
         ot = domain.octree
         egrav = G.compute_gravity(ot, self.centers, self.multipoles, first, last, d["x"], d["y"], d["z"], d["h"],
                                   d["m"], d.g, d["ax"], d["ay"], d["az"], stats=self.stats)
-        if domain.size > 1 and domain.remote_centers is not None:
-            egrav += G.m2p_flat(first, last, d["x"], d["y"], d["z"], d["m"], domain.remote_centers,
-                                domain.remote_quads, d.g, d["ax"], d["ay"], d["az"])
+        if domain.size > 1 and getattr(domain, "remote_tree", None) is not None:
+            rt, rc, rmp = domain.remote_tree
+            rstats = {}
+            egrav += G.compute_gravity(rt, rc, rmp, first, last, d["x"], d["y"], d["z"], d["h"], d["m"], d.g,
+                                       d["ax"], d["ay"], d["az"], stats=rstats)
+            self.stats["remote_m2p"] = rstats.get("m2p", 0)
+            self.stats["remote_p2p"] = rstats.get("p2p", 0)
         # rank-local share; the observables reduction sums it over ranks (as the reference's MPI_Reduce does)
         d.egrav = egrav

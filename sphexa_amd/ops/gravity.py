@@ -11,7 +11,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from .octree import MAX_LEVEL, Octree
+from .octree import KEY_END, MAX_LEVEL, Octree
 from ..utils.box import Box
 
 
@@ -111,11 +111,15 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         if int(st[1]) > 0:
             raise RuntimeError(f"gravity traversal stack overflow in {int(st[1])} groups")
         return float(out[0].item())
-    return float(_lib.cpu().compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
-                                            tree.node_start.data_ptr(), tree.node_end.data_ptr(), centers.data_ptr(),
-                                            mp.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
-                                            m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
-                                            0 if ugrav is None else ugrav.data_ptr()))
+    st = torch.zeros(2, dtype=torch.int64)
+    e = float(_lib.cpu().compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
+                                         tree.node_start.data_ptr(), tree.node_end.data_ptr(), centers.data_ptr(),
+                                         mp.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
+                                         m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
+                                         0 if ugrav is None else ugrav.data_ptr(), st.data_ptr()))
+    if stats is not None:
+        stats.update(m2p=int(st[0]), p2p=int(st[1]))
+    return e
 
 
 def direct_sum(first: int, last: int, x, y, z, h, m, G: float, ax, ay, az, ugrav=None) -> float:
@@ -163,6 +167,68 @@ def let_selection(tree: Octree, failed: torch.Tensor, mp: torch.Tensor):
         parent = tree.parents.long()[torch.div(torch.arange(1, N, device=f.device) - 1, 8, rounding_mode="floor")]
         send[1:] &= f[parent]
     return pflags, torch.nonzero(send, as_tuple=False).flatten()
+
+
+def mark_outside_range(tree: Octree, lo: int, hi: int, failed: torch.Tensor):
+    """failed[node] = 1 for every node whose SFC key range is not inside [lo, hi) (the sender's assignment): the
+    remote LET nodes that different ranks send are then disjoint"""
+    hi = min(int(hi), KEY_END)
+    if failed.is_cuda:
+        _lib.hip().mark_outside_range(tree.num_nodes, tree.prefixes.data_ptr(), int(lo), hi, failed.data_ptr(),
+                                      _stream())
+    else:
+        _lib.cpu().mark_outside_range(tree.num_nodes, tree.prefixes.data_ptr(), int(lo), hi, failed.data_ptr())
+    return failed
+
+
+# squared MAC radius of a received remote node: tiny but non-zero (zero marks an empty node), so the traversal
+# always applies it as one multipole. It passed the sender's vector MAC against every box of this rank's domain.
+FORCE_ACCEPT_MAC2 = 1e-300
+
+
+def remote_let_tree(codes: torch.Tensor, rcenters: torch.Tensor, rquads: torch.Tensor, box: Box, theta: float,
+                    sfc_kind: int = 0):
+    """Octree over the remote multipoles received from the other ranks (one leaf per received node, placeholder
+    ``codes`` (M) int64, centers (M, 3) f64, quadrupoles (M, 8) f32), upswept so internal nodes carry the combined
+    multipoles and vector-MAC radii. Returns (octree, centers N x 4, quadrupoles N x 8) for ``compute_gravity``: a
+    hierarchical far field instead of applying all M multipoles to every target."""
+    import numpy as np
+
+    from .octree import build_octree
+
+    dev = rcenters.device
+    leaves, leaf_of = _lib.cpu().remote_leaf_array(codes.cpu().numpy().view(np.uint64))
+    tree = torch.from_numpy(leaves.view(np.int64).copy()).to(dev)
+    L = tree.numel() - 1
+    counts = torch.zeros(L, dtype=torch.int32, device=dev)
+    nokeys = torch.empty(0, dtype=torch.int64, device=dev)
+    nox = torch.empty(0, dtype=torch.float64, device=dev)
+    ot = build_octree(tree, counts, nokeys, nox, nox, nox, 0)
+    N = ot.num_nodes
+    nodes = ot.leaf_to_node.long()[torch.from_numpy(leaf_of).to(dev)]
+    centers = torch.zeros(N, 4, dtype=torch.float64, device=dev)
+    mp = torch.zeros(N, 8, dtype=torch.float32, device=dev)
+    centers[nodes, :3] = rcenters
+    centers[nodes, 3] = rquads[:, 0].double()
+    mp[nodes] = rquads
+    centers, mp = centers.view(-1), mp.view(-1)
+    inv_theta = 1.0 / theta
+    if dev.type == "cuda":
+        h = _lib.hip()
+        s = _stream()
+        for l in range(MAX_LEVEL, -1, -1):
+            a, b = ot.level_range[l], ot.level_range[l + 1]
+            if b > a:
+                h.gravity_upsweep_level(a, b, ot.node_to_leaf.data_ptr(), ot.child_offsets.data_ptr(),
+                                        centers.data_ptr(), mp.data_ptr(), s)
+        h.gravity_set_mac(N, ot.prefixes.data_ptr(), box.to_array(), sfc_kind, inv_theta, centers.data_ptr(), s)
+    else:
+        _lib.cpu().gravity_upsweep(N, ot.child_offsets.data_ptr(), ot.node_to_leaf.data_ptr(), ot.level_range,
+                                   ot.prefixes.data_ptr(), ot.node_start.data_ptr(), ot.node_end.data_ptr(), 0, 0, 0, 0,
+                                   box.to_array(), sfc_kind, inv_theta, centers.data_ptr(), mp.data_ptr(),
+                                   leavesGiven=True)
+    centers.view(-1, 4)[nodes, 3] = FORCE_ACCEPT_MAC2
+    return ot, centers, mp
 
 
 def m2p_flat(first: int, last: int, x, y, z, m, mcenters: torch.Tensor, mquads: torch.Tensor, G: float, ax, ay, az,

@@ -83,6 +83,8 @@ class Domain:
         self.n_hi = 0
         self.remote_centers: Optional[torch.Tensor] = None  # (M, 3) f64 remote multipole expansion centers
         self.remote_quads: Optional[torch.Tensor] = None    # (M, 8) f32 remote quadrupoles
+        self.remote_codes: Optional[torch.Tensor] = None    # (M) int64 placeholder codes of the remote nodes
+        self.remote_tree = None                             # (Octree, centers, quadrupoles) over the remote nodes
         self.stats: Dict[str, float] = {}
 
     # ------------------------------------------------------------------------------------------------ queries
@@ -259,6 +261,11 @@ class Domain:
             from ..ops import gravity as grav_ops
 
             gcenters, gquads = grav_ops.upsweep(ot, x, y, z, own["m"], self.box, self.theta, self.sfc_kind)
+            # only nodes inside this rank's SFC range may leave as multipoles: the remote LET trees then consist of
+            # disjoint nodes (ops.gravity.remote_let_tree)
+            outside = torch.zeros(ot.num_nodes, dtype=torch.uint8, device=x.device)
+            grav_ops.mark_outside_range(ot, self.assignment_keys[self.rank], self.assignment_keys[self.rank + 1],
+                                        outside)
         send_idx: List[torch.Tensor] = []
         mp_send: List[torch.Tensor] = []
         for q in range(self.size):
@@ -268,6 +275,7 @@ class Domain:
                 continue
             if gravity:
                 failed = grav_ops.mark_let(ot, all_boxes[q], gcenters, self.box)
+                failed |= outside
                 pflags, nodes = grav_ops.let_selection(ot, failed, gquads)
                 send_idx.append(torch.nonzero(pflags, as_tuple=False).flatten())
                 mp_send.append(nodes)
@@ -275,7 +283,7 @@ class Domain:
                 flags = _mark_in_boxes(ot, all_boxes[q], x, y, z, self.box)
                 send_idx.append(torch.nonzero(flags, as_tuple=False).flatten())
         if gravity:
-            self._exchange_multipoles(mp_send, gcenters, gquads)
+            self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes)
         self.halo_send_counts = [int(t.numel()) for t in send_idx]
         self.halo_recv_counts = self.comm.exchange_counts(self.halo_send_counts)
         self.n_lo = sum(self.halo_recv_counts[: self.rank])
@@ -301,16 +309,25 @@ class Domain:
             raise HaloOwnershipError(f"rank {self.rank}: {bad} halo particles are not owned by the rank that sent "
                                      f"them (assignment {self.assignment_keys})")
 
-    def _exchange_multipoles(self, mp_send, gcenters, gquads):
-        """one alltoallv of (center xyz f64, quadrupole 8 x f32) rows for the LET far field"""
+    def _exchange_multipoles(self, mp_send, gcenters, gquads, prefixes):
+        """one alltoallv of (center xyz f64, quadrupole 8 x f32, placeholder code) rows for the LET far field; the
+        received nodes become the leaves of this rank's remote LET tree (ops.gravity.remote_let_tree)"""
+        from ..ops import gravity as grav_ops
+
         idx = torch.cat(mp_send)
-        rows = torch.cat([gcenters.view(-1, 4)[idx, :3], gquads.view(-1, 8)[idx].contiguous().view(torch.float64)],
-                         dim=1)
+        rows = torch.cat([gcenters.view(-1, 4)[idx, :3], gquads.view(-1, 8)[idx].contiguous().view(torch.float64),
+                          prefixes[idx].view(torch.float64).view(-1, 1)], dim=1)
         counts = [int(t.numel()) for t in mp_send]
         recv, _ = self.comm.alltoallv(rows, counts)
         self.remote_centers = recv[:, :3].contiguous()
-        self.remote_quads = recv[:, 3:].contiguous().view(torch.float32).view(-1, 8)
+        self.remote_quads = recv[:, 3:7].contiguous().view(torch.float32).view(-1, 8)
+        self.remote_codes = recv[:, 7].contiguous().view(torch.int64)
         self.stats["remote_multipoles"] = recv.shape[0]
+        if recv.shape[0] > 0:
+            self.remote_tree = grav_ops.remote_let_tree(self.remote_codes, self.remote_centers, self.remote_quads,
+                                                        self.box, self.theta, self.sfc_kind)
+        else:
+            self.remote_tree = None
 
     def exchange_halos(self, d, fields: Sequence[str]):
         """fill halo slots of ``fields`` from their owners. One packed all_to_all per call (all fields fused)."""
