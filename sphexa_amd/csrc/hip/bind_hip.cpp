@@ -172,15 +172,29 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("find_neighbors",
           [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr h, int64_t numNodes, Ptr child, Ptr n2l, Ptr ns,
              Ptr ne, Ptr center, Ptr half, const BoxArr& box, unsigned ng0, unsigned ngmax, Ptr nidx, Ptr nc,
-             int iterateH, Ptr stats, Ptr scratch, int testFrontCap, Ptr s)
+             int iterateH, Ptr stats, Ptr scratch, int testFrontCap, Ptr s, Ptr xm, Ptr mm, double mUniform,
+             Ptr wh, const ConstArr& c)
           {
               (void)numNodes;
               NsTree t{P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne), P<double>(center),
                        P<double>(half)};
+              XmFuse xf{};
+              if (xm)
+              {
+                  auto sc = toConsts(c);
+                  xf      = XmFuse{P<float>(xm), P<float>(mm), float(mUniform), float(sc.K),
+                              KernelFn{P<float>(wh), nullptr, sc.sincIndex, sc.kernelChoice}};
+              }
               findNeighbors(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(h), t, toBox(box), ng0,
                             ngmax, P<int32_t>(nidx), P<int32_t>(nc), iterateH, P<unsigned long long>(stats), P<void>(scratch),
-                            testFrontCap, St(s));
-          });
+                            testFrontCap, xf, St(s));
+          },
+          py::arg("first"), py::arg("last"), py::arg("x"), py::arg("y"), py::arg("z"), py::arg("h"),
+          py::arg("numNodes"), py::arg("child"), py::arg("n2l"), py::arg("ns"), py::arg("ne"), py::arg("center"),
+          py::arg("half"), py::arg("box"), py::arg("ng0"), py::arg("ngmax"), py::arg("nidx"), py::arg("nc"),
+          py::arg("iterateH"), py::arg("stats"), py::arg("scratch"), py::arg("testFrontCap"), py::arg("s"),
+          py::arg("xm") = 0, py::arg("m") = 0, py::arg("m_uniform") = 0.0, py::arg("wh") = 0,
+          py::arg("consts") = ConstArr{});
 
     // ---------------------------------------------------------------------------------------------- hydro
     // same argument lists as the OpenMP module, plus (ntot, record workspace(s), stream)
@@ -226,7 +240,7 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("iad_divv_curlv",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
-             Ptr curlv, const std::array<Ptr, 6>& dV, int64_t ntot, Ptr rec, Ptr s)
+             Ptr curlv, const std::array<Ptr, 6>& dV, int64_t ntot, Ptr rec, Ptr s, Ptr avS)
           {
               auto sc = toConsts(c);
               auto cp = six(cij);
@@ -234,20 +248,28 @@ PYBIND11_MODULE(_sphx_hip, m)
               iadDivvCurlv(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
                            P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(wh),
                            P<float>(kx), P<float>(xm), P<void>(rec), cp.data(), P<float>(divv), P<float>(curlv),
-                           g.data(), St(s));
-          });
+                           g.data(), P<void>(avS), St(s));
+          },
+          py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
+          py::arg("x"), py::arg("y"), py::arg("z"), py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("h"),
+          py::arg("cij"), py::arg("wh"), py::arg("kx"), py::arg("xm"), py::arg("divv"), py::arg("curlv"),
+          py::arg("dV"), py::arg("ntot"), py::arg("rec"), py::arg("s"), py::arg("avS") = 0);
     m.def("av_switches",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr cs, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
-             double dt, Ptr alpha, int64_t ntot, Ptr rec, Ptr s)
+             double dt, Ptr alpha, int64_t ntot, Ptr rec, Ptr s, Ptr avS)
           {
               auto sc = toConsts(c);
               auto cp = six(cij);
               avSwitches(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
                          P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(cs), cp.data(),
-                         P<float>(wh), P<float>(kx), P<float>(xm), P<float>(divv), dt, P<void>(rec), P<float>(alpha),
-                         St(s));
-          });
+                         P<float>(wh), P<float>(kx), P<float>(xm), P<float>(divv), dt, P<void>(rec), P<void>(avS),
+                         P<float>(alpha), St(s));
+          },
+          py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
+          py::arg("x"), py::arg("y"), py::arg("z"), py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("h"),
+          py::arg("cs"), py::arg("cij"), py::arg("wh"), py::arg("kx"), py::arg("xm"), py::arg("divv"), py::arg("dt"),
+          py::arg("alpha"), py::arg("ntot"), py::arg("rec"), py::arg("s"), py::arg("avS") = 0);
     m.def("momentum_energy_ve",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr prho, Ptr cs, const std::array<Ptr, 6>& cij, Ptr kx, Ptr xm,

@@ -77,11 +77,22 @@ void markInBoxes(int64_t nb, const double* bc, const double* bh, const int32_t* 
                  const double* y, const double* z, const Box& box, uint8_t* flags, hipStream_t s);
 
 // neighbors.hip
+//! XMass fused into the search (xm == nullptr: lists only): xm_i = m_i / (K h_i^-3 (m_i + sum_j m_j w_ij)) over the
+//! stored neighbors of the final h-iteration round, from the distances the search already computed
+struct XmFuse
+{
+    float* xm;
+    const float* m;  // masses: m_i always, m_j when mUniform == 0
+    float mUniform;  // common particle mass, or 0
+    float K;
+    KernelFn kf;
+};
 // stats: [0] h-iteration failures, [1] groups overflowing even the spill storage, [2] spilled groups
 size_t neighborScratchBytes(int64_t n);
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int32_t* nc,
-                   int iterateH, unsigned long long* stats, void* scratch, int testFrontCap, hipStream_t s);
+                   int iterateH, unsigned long long* stats, void* scratch, int testFrontCap, const XmFuse& xf,
+                   hipStream_t s);
 
 // hydro.hip
 struct MomFields
@@ -117,11 +128,11 @@ void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, co
 void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                   const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                   const float* wh, const float* kx, const float* xm, void* rec, float* const cij[6], float* divv,
-                  float* curlv, float* const dV[6], hipStream_t s);
+                  float* curlv, float* const dV[6], void* avS, hipStream_t s);
 void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                 const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                 const float* c, float* const cij[6], const float* wh, const float* kx, const float* xm,
-                const float* divv, double dt, void* rec, float* alpha, hipStream_t s);
+                const float* divv, double dt, void* rec, const void* avS, float* alpha, hipStream_t s);
 void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const MomFields& f,
                       bool avClean, const float* wh, void* rec, void* recGradV, float* ax, float* ay, float* az,
                       double* du, float* minDt, hipStream_t s);

@@ -255,6 +255,27 @@ __global__ void packMomQKernel(int64_t n, MomFields f, QFrame q, SrcMomQ* __rest
     }
 }
 
+__global__ void packAvVKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                              const double* __restrict__ z, const float* __restrict__ kx,
+                              const float* __restrict__ vx, const float* __restrict__ vy,
+                              const float* __restrict__ vz, const float* __restrict__ xm,
+                              const float* __restrict__ c, const float* __restrict__ divv, QFrame q,
+                              SrcAvV* __restrict__ out)
+{
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcAvV r;
+    r.x    = quantize(x[i], q.lo[0], q.s[0]);
+    r.y    = quantize(y[i], q.lo[1], q.s[1]);
+    r.z    = quantize(z[i], q.lo[2], q.s[2]);
+    r.vd   = xm[i] / kx[i] * divv[i];
+    r.vx   = vx[i];
+    r.vy   = vy[i];
+    r.vz   = vz[i];
+    r.c    = c[i];
+    out[i] = r;
+}
+
 __global__ void packAvQKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
                               const double* __restrict__ z, const float* __restrict__ kx,
                               const float* __restrict__ vx, const float* __restrict__ vy,
@@ -409,28 +430,29 @@ __global__ __launch_bounds__(kBlock) void iadKernel(NbrArgs a, SphConsts sc, Box
 }
 
 //! @brief IAD matrix, then divv/curlv (+ velocity gradient) in the same kernel over the same neighbor list
-template<class R, class G>
+template<bool kAvS, class R, class G>
 __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConsts sc, G box,
                                                              const float* __restrict__ h,
                                                              const float* __restrict__ kx,
                                                              const R* __restrict__ rec,
                                                              const float* __restrict__ wh, Six cij,
                                                              float* __restrict__ divv, float* __restrict__ curlv,
-                                                             Six dV, int doGrad)
+                                                             Six dV, int doGrad, float4* __restrict__ avS)
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
     const int32_t* nbr;
     unsigned n;
     const bool valid = targetOf(a, i, nbr, n);
-    float c[6], g[6], dvi, cvi;
-    iadDivvCurlvJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], kx[i], coopOf(rec, tile, i, a),
-                      KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, g);
+    float c[6], g[6], dvi, cvi, S[3];
+    iadDivvCurlvJLoop<kAvS>(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], kx[i], coopOf(rec, tile, i, a),
+                            KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, g, S);
     if (!valid) return;
     for (int k = 0; k < 6; ++k)
         cij.p[k][i] = c[k];
     divv[i]  = dvi;
     curlv[i] = cvi;
+    if constexpr (kAvS) avS[i - a.first] = make_float4(S[0], S[1], S[2], 0.f);
     if (doGrad)
         for (int k = 0; k < 6; ++k)
             dV.p[k][i] = g[k];
@@ -470,6 +492,29 @@ __global__ __launch_bounds__(kBlock) void avSwitchesQKernel(NbrArgs a, SphConsts
     float al    = avSwitchesJLoop(unsigned(i), sc.K, q, nbr, kBlockedList, n, h[i], ci, AvQLoader{rec, divv},
                                   KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt, sc.alphamin, sc.alphamax,
                                   sc.decayConstant, alpha[i]);
+    if (valid) alpha[i] = al;
+}
+
+//! @brief AV switches on SrcAvV records (vd = vol divv) with the IAD loop's S_i (avSwitchesVJLoop, sph_math.hpp)
+__global__ __launch_bounds__(kBlock) void avSwitchesVKernel(NbrArgs a, SphConsts sc, QFrame q,
+                                                            const float* __restrict__ h, Six cij,
+                                                            const SrcAvV* __restrict__ rec,
+                                                            const float* __restrict__ divv,
+                                                            const float4* __restrict__ avS,
+                                                            const float* __restrict__ wh, double dt,
+                                                            float* __restrict__ alpha)
+{
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcAvV>::S];
+    int64_t i;
+    const int32_t* nbr;
+    unsigned n;
+    const bool valid = targetOf(a, i, nbr, n);
+    float ci[6]    = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
+    const float4 s = avS[i - a.first];
+    const float S[3] = {s.x, s.y, s.z};
+    float al = avSwitchesVJLoop(unsigned(i), sc.K, q, nbr, kBlockedList, n, h[i], ci, divv[i], S,
+                                coopOf(rec, tile, i, a), KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt,
+                                sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
     if (valid) alpha[i] = al;
 }
 
@@ -738,7 +783,7 @@ void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, co
 void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                   const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                   const float* wh, const float* kx, const float* xm, void* rec, float* const cij[6], float* divv,
-                  float* curlv, float* const dV[6], hipStream_t s)
+                  float* curlv, float* const dV[6], void* avS, hipStream_t s)
 {
     if (a.last <= a.first) return;
     Six c, g;
@@ -751,15 +796,20 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
     {
         packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, nullptr, nullptr,
                                                          (SrcIad*)rec);
-        iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, kx, (const SrcIad*)rec, wh, c, divv,
-                                                       curlv, g, dV[0] != nullptr);
+        iadDivvCurlvKernel<false><<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, kx, (const SrcIad*)rec, wh,
+                                                              c, divv, curlv, g, dV[0] != nullptr, nullptr);
     }
     else
     {
         const QFrame q = qframeOf(box);
         packIadQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, q, (SrcIadQ*)rec);
-        iadDivvCurlvKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv,
-                                                       curlv, g, dV[0] != nullptr);
+        // fixed-point path: also the S_i of the AV loop (avSwitchesVJLoop) when a workspace is given
+        if (avS)
+            iadDivvCurlvKernel<true><<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh,
+                                                                 c, divv, curlv, g, dV[0] != nullptr, (float4*)avS);
+        else
+            iadDivvCurlvKernel<false><<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec,
+                                                                  wh, c, divv, curlv, g, dV[0] != nullptr, nullptr);
     }
     SPHX_LAUNCH_CHECK();
 }
@@ -767,7 +817,7 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
 void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                 const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                 const float* c, float* const cij[6], const float* wh, const float* kx, const float* xm,
-                const float* divv, double dt, void* rec, float* alpha, hipStream_t s)
+                const float* divv, double dt, void* rec, const void* avS, float* alpha, hipStream_t s)
 {
     if (a.last <= a.first) return;
     Six cc;
@@ -777,6 +827,13 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
     {
         packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, c, divv, (SrcIad*)rec);
         avSwitchesKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, cc, (const SrcIad*)rec, wh, dt, alpha);
+    }
+    else if (avS)
+    {
+        const QFrame q = qframeOf(box);
+        packAvVKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, c, divv, q, (SrcAvV*)rec);
+        avSwitchesVKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, cc, (const SrcAvV*)rec, divv,
+                                                      (const float4*)avS, wh, dt, alpha);
     }
     else
     {

@@ -21,6 +21,13 @@
  * LDS; whenever some lane's ring is full, every lane holding >= 4 pending entries writes one block (dwordx4): the
  * wave issues a few dozen list stores per group instead of one partially masked store per candidate source (the
  * search was bound by those stores in the texture data path).
+ *
+ * Optional fused XMass (XmFuse, the reference computes rho0 inside its traversal, xmass_gpu.cu:54-101): the ring also
+ * keeps each hit's squared distance and the flushing lanes sum m_j w(r_ij/h_i) over their block. Measured on MI355X
+ * (Sedov -n 400) it costs more than the XMass pass it replaces (search 38 -> 65 ms vs XMass 11 ms): in this
+ * broadcast-test search a wave executes the kernel evaluation whenever ANY lane flushes; a queue that evaluates 64
+ * hits per pass with every lane busy was slower still (84 ms: +12k VALU, +5k SALU, +2.8k LDS instructions per wave
+ * for the appends, profiles/r2_perf_log.md). Kept opt-in (SPHX_FUSE_XMASS=1) with a GPU test.
  */
 #include "common.h"
 #include "hip_api.h"
@@ -33,14 +40,28 @@ namespace sphx::hip
 constexpr int kWavesPerBlock = 4;
 constexpr int kFrontCap      = 512;
 constexpr int kLeafCap       = 512; // LDS candidate-leaf list per wave (A/B: 1024 costs occupancy, 512 spills few groups)
-constexpr int kRing          = 16; // hit ring slots per lane (four list blocks)
-constexpr int kRingStride    = 17; // LDS words per lane (odd: the 32 lanes of a ds_write_b32 group hit distinct banks)
-constexpr int kStage         = 128; // staged candidate sources per wave (float4 {x, y, z, j}, group-relative fp32)
-constexpr int kRingWords     = 64 * kRingStride;
-//! per-wave LDS work area: the traversal frontiers, then (candidate phase) the hit ring + the staging ring
-constexpr int kWorkWords = 2 * kFrontCap > kRingWords + 4 * kStage ? 2 * kFrontCap : kRingWords + 4 * kStage;
-static_assert((kRingWords * 4) % 16 == 0, "staging ring must be 16-B aligned");
-static_assert(kRingStride > kRing, "the padding word of a lane absorbs entries past ngmax");
+#ifndef SPHX_NS_RING
+#define SPHX_NS_RING 16
+#endif
+constexpr int kStage = 128; // staged candidate sources per wave (float4 {x, y, z, j}, group-relative fp32)
+//! hit ring slots per lane (list blocks of 4); the fused-XMass search keeps 2 blocks + their squared distances
+template<bool kXm>
+constexpr int ringSlots() { return kXm ? 8 : SPHX_NS_RING; }
+//! LDS words per lane of the hit ring: indices (+ squared distances) + one padding word that absorbs entries past
+//! ngmax; odd, so the 32 lanes of a ds_write_b32 group hit distinct banks
+template<bool kXm>
+constexpr int ringStride() { return (kXm ? 2 : 1) * ringSlots<kXm>() + 1; }
+template<bool kXm>
+constexpr int ringWords() { return 64 * ringStride<kXm>(); }
+//! candidate-phase LDS of a wave: hit ring + staging ring
+template<bool kXm>
+constexpr int candWords() { return ringWords<kXm>() + 4 * kStage; }
+//! per-wave LDS work area: the traversal frontiers, then (candidate phase) the candidate-phase storage
+template<bool kXm>
+constexpr int workWords() { return 2 * kFrontCap > candWords<kXm>() ? 2 * kFrontCap : candWords<kXm>(); }
+static_assert(ringSlots<false>() == 8 || ringSlots<false>() == 16, "ring of 2 or 4 list blocks");
+static_assert((ringWords<false>() * 4) % 16 == 0 && (ringWords<true>() * 4) % 16 == 0,
+              "staging ring must be 16-B aligned");
 
 //! @brief fold a coordinate difference into [-L/2, L/2] in periodic dimensions
 __device__ __forceinline__ double foldMin(double dx, const Box& b, int d)
@@ -85,14 +106,14 @@ struct TreeView
 /*! @brief search of one target group (one wave). Returns false if the frontier or the leaf list overflowed the
  *         given capacities (nothing is written then, the group is retried by the spill kernel).
  */
-template<bool kSpill>
+template<bool kSpill, bool kXm>
 __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t last, const double* __restrict__ x,
                                             const double* __restrict__ y, const double* __restrict__ z,
                                             float* __restrict__ h, const NsTree& tree, const Box& box, unsigned ng0,
                                             unsigned ngmax, int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
                                             int iterateH, unsigned long long* __restrict__ stats, int32_t* frontA,
                                             int32_t* frontB, int32_t* leaves, int frontCap, int leafCap,
-                                            int32_t* work)
+                                            int32_t* work, const XmFuse& xf)
 {
     // the tree is read-only here: restrict-qualified views let the uniform leaf loads go through the scalar cache
     const TreeView t{tree.child, tree.n2l, tree.ns, tree.ne, tree.center, tree.half};
@@ -111,13 +132,16 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     const unsigned ngmax4 = (ngmax + 3) & ~3u;
     int4* nlist           = reinterpret_cast<int4*>(nidx + g * int64_t(ngmax4) * 64) + lane;
     // hit ring and staging ring alias the frontiers (fast path): they are only live in the candidate phase
-    int32_t* myRing       = work + lane * kRingStride;
-    float4* stage         = reinterpret_cast<float4*>(work + kRingWords);
+    constexpr int kRing    = ringSlots<kXm>();
+    constexpr int kRingPad = ringStride<kXm>() - 1;
+    int32_t* myRing       = work + lane * ringStride<kXm>();
+    float4* stage         = reinterpret_cast<float4*>(work + ringWords<kXm>());
     const unsigned ngmin = ng0 / 4;
 
     unsigned ncSph = 1;
     int round      = 0;
     unsigned leavesTouched = 0; // candidate leaves of the last round (statistics)
+    float rho0             = 0.f; // fused XMass: sum_j m_j w(r_ij / h_i) over the stored entries of the last round
     for (;; ++round)
     {
         // 1. group search box
@@ -202,7 +226,10 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         unsigned cnt = 0;
         unsigned fb  = 0; // list blocks of this lane already written
         leavesTouched = 0;
-        // write the next block (4 ring entries) of every lane in `who`
+        const float hInv = 1.0f / hi;
+        rho0             = 0.f;
+        // write the next block (4 ring entries) of every lane in `who`; with the fused XMass the block's squared
+        // distances (ring slots kRing..2 kRing-1) are turned into kernel sums by the flushing lanes
         auto flushBlock = [&](bool who)
         {
             if (who)
@@ -210,11 +237,26 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                 const int s0 = int(4 * fb) & (kRing - 1);
                 int4 v       = make_int4(myRing[s0], myRing[s0 + 1], myRing[s0 + 2], myRing[s0 + 3]);
                 nlist[int64_t(fb) * 64] = v;
+                if constexpr (kXm)
+                {
+                    const unsigned nv = min(4u, min(cnt, ngmax) - 4 * fb);
+                    const int jj[4]   = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                    {
+                        if (unsigned(u) < nv)
+                        {
+                            const float d2 = __int_as_float(myRing[kRing + s0 + u]);
+                            const float mj = xf.mUniform > 0.f ? xf.mUniform : xf.m[jj[u]];
+                            rho0 += xf.kf.w(sqrtF(d2) * hInv) * mj;
+                        }
+                    }
+                }
                 fb++;
             }
         };
         // test `count` (a multiple of 4) staged sources against every lane; one flush check per four sources
-        // (pending <= 11 after a check, <= 15 before the next: fits the 16-slot ring)
+        // (pending <= kRing - 5 after a check, <= kRing - 1 before the next: fits the ring)
         unsigned sHead = 0, sTail = 0; // wave-uniform positions in the staging ring
         auto testStaged = [&](unsigned count)
         {
@@ -245,22 +287,26 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     const int32_t jj = __float_as_int(s.w);
                     bool hit         = d2 < r2f - band;
                     const bool maybe = !hit && d2 <= r2f + band;
+                    float d2s        = d2;
                     if (ballot(maybe)) // rare: fp64 re-test of candidates in the rounding band
                     {
                         const int32_t ju = __builtin_amdgcn_readfirstlane(jj);
-                        const bool h64   = distanceSqPbc(ldConst(x + ju), ldConst(y + ju), ldConst(z + ju), xi, yi,
-                                                         zi, box) < radiusSq;
-                        hit = hit || (maybe && h64);
+                        const double d64 =
+                            distanceSqPbc(ldConst(x + ju), ldConst(y + ju), ldConst(z + ju), xi, yi, zi, box);
+                        hit = hit || (maybe && d64 < radiusSq);
+                        if (maybe) d2s = float(d64);
                     }
                     if (valid && hit && jj != int32_t(i))
                     {
-                        // entries past ngmax go to the lane's padding word (slot 16) instead of a guarded store
-                        myRing[cnt < ngmax ? int(cnt & (kRing - 1)) : kRing] = jj;
+                        // entries past ngmax go to the lane's padding word instead of a guarded store
+                        const int slot = cnt < ngmax ? int(cnt & (kRing - 1)) : kRingPad;
+                        myRing[slot]   = jj;
+                        if constexpr (kXm) myRing[slot == kRingPad ? kRingPad : slot + kRing] = __float_as_int(d2s);
                         cnt++;
                     }
                 }
                 const unsigned pend = min(cnt, ngmax) - 4 * fb;
-                if (ballot(pend >= 12u)) flushBlock(pend >= 4);
+                if (ballot(pend >= unsigned(kRing - 4))) flushBlock(pend >= 4);
             }
             sHead += count;
         };
@@ -313,13 +359,14 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
             testStaged(rem + pad);
         }
         ncSph = 1 + cnt;
-        // remaining entries (at most 11 per lane; block tails beyond the count are never read)
+        // remaining entries (at most kRing - 5 per lane; block tails beyond the count are never read)
         {
             unsigned pend = min(cnt, ngmax) - 4 * fb;
-            flushBlock(pend > 0);
-            flushBlock(pend > 4);
-            flushBlock(pend > 8);
+#pragma unroll
+            for (int q = 0; q < kRing - 4; q += 4)
+                flushBlock(pend > unsigned(q));
         }
+
 
         // 4. smoothing length iteration
         bool repeat = (iterateH & 1) && valid && (ncSph < ngmin || (ncSph - 1) > ngmax);
@@ -337,20 +384,28 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     {
         nc[i] = int32_t(ncSph);
         h[i]  = hi;
+        if constexpr (kXm)
+        {
+            // rho0 of the final round (the h used for its search radius is the stored h)
+            const float mi   = xf.m[i];
+            const float hInv = 1.0f / hi;
+            xf.xm[i]         = mi / ((mi + rho0) * xf.K * hInv * hInv * hInv);
+        }
     }
     return true;
 }
 
 //! fast path: frontier and leaf list in LDS; overflowing groups are queued for the spill kernel
+template<bool kXm>
 __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_t last, const double* __restrict__ x,
                                                            const double* __restrict__ y,
                                                            const double* __restrict__ z, float* __restrict__ h,
                                                            NsTree t, Box box, unsigned ng0, unsigned ngmax,
                                                            int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
                                                            int iterateH, unsigned long long* __restrict__ stats,
-                                                           int32_t* __restrict__ spillList, int frontCap)
+                                                           int32_t* __restrict__ spillList, int frontCap, XmFuse xf)
 {
-    __shared__ __attribute__((aligned(16))) int32_t work[kWavesPerBlock][kWorkWords];
+    __shared__ __attribute__((aligned(16))) int32_t work[kWavesPerBlock][workWords<kXm>()];
     __shared__ int32_t leaves[kWavesPerBlock][kLeafCap];
 
     const int wave          = threadIdx.x >> 6;
@@ -359,8 +414,9 @@ __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_
     const int64_t g         = int64_t(lb) * kWavesPerBlock + wave;
     if (g >= numGroups) return;
 
-    bool ok = searchGroup<false>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
-                                 work[wave], work[wave] + kFrontCap, leaves[wave], frontCap, kLeafCap, work[wave]);
+    bool ok = searchGroup<false, kXm>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
+                                      work[wave], work[wave] + kFrontCap, leaves[wave], frontCap, kLeafCap, work[wave],
+                                      xf);
     if (!ok && (threadIdx.x & 63) == 0)
     {
         unsigned long long slot = atomicAdd(&stats[2], 1ull);
@@ -375,6 +431,7 @@ constexpr int kSpillWaves  = 128;
 constexpr int kSpillFront  = 16384;
 constexpr int kSpillLeaves = 65536;
 
+template<bool kXm>
 __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, int64_t last,
                                                                const double* __restrict__ x,
                                                                const double* __restrict__ y,
@@ -383,9 +440,9 @@ __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, in
                                                                int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
                                                                int iterateH, unsigned long long* __restrict__ stats,
                                                                const int32_t* __restrict__ spillList,
-                                                               int32_t* __restrict__ scratch)
+                                                               int32_t* __restrict__ scratch, XmFuse xf)
 {
-    __shared__ __attribute__((aligned(16))) int32_t work[kRingWords + 4 * kStage];
+    __shared__ __attribute__((aligned(16))) int32_t work[candWords<kXm>()];
     const int64_t numSpill = int64_t(__hip_atomic_load(&stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     int32_t* frontA = scratch + int64_t(blockIdx.x) * (2 * kSpillFront + kSpillLeaves);
     int32_t* frontB = frontA + kSpillFront;
@@ -393,8 +450,8 @@ __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, in
     for (int64_t k = blockIdx.x; k < numSpill; k += gridDim.x)
     {
         int64_t g = spillList[k];
-        bool ok   = searchGroup<true>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
-                                      frontA, frontB, leaves, kSpillFront, kSpillLeaves, work);
+        bool ok   = searchGroup<true, kXm>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
+                                           frontA, frontB, leaves, kSpillFront, kSpillLeaves, work, xf);
         if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
     }
 }
@@ -407,7 +464,8 @@ size_t neighborScratchBytes(int64_t n)
 
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int32_t* nc,
-                   int iterateH, unsigned long long* stats, void* scratch, int testFrontCap, hipStream_t s)
+                   int iterateH, unsigned long long* stats, void* scratch, int testFrontCap, const XmFuse& xf,
+                   hipStream_t s)
 {
     int64_t n = last - first;
     if (n <= 0) return;
@@ -415,12 +473,23 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
     int32_t* spillList = static_cast<int32_t*>(scratch);
     int32_t* spillMem  = spillList + ((groups + 63) / 64) * 64;
     unsigned grid      = unsigned((groups + kWavesPerBlock - 1) / kWavesPerBlock);
-    findNeighborsKernel<<<grid, 64 * kWavesPerBlock, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc,
-                                                             iterateH, stats, spillList,
-                                                             testFrontCap > 0 ? min(testFrontCap, kFrontCap) : kFrontCap);
-    SPHX_LAUNCH_CHECK();
-    findNeighborsSpillKernel<<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc,
-                                                        iterateH, stats, spillList, spillMem);
+    const int fc       = testFrontCap > 0 ? min(testFrontCap, kFrontCap) : kFrontCap;
+    if (xf.xm)
+    {
+        findNeighborsKernel<true><<<grid, 64 * kWavesPerBlock, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax,
+                                                                       nidx, nc, iterateH, stats, spillList, fc, xf);
+        SPHX_LAUNCH_CHECK();
+        findNeighborsSpillKernel<true><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax, nidx,
+                                                                  nc, iterateH, stats, spillList, spillMem, xf);
+    }
+    else
+    {
+        findNeighborsKernel<false><<<grid, 64 * kWavesPerBlock, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax,
+                                                                        nidx, nc, iterateH, stats, spillList, fc, xf);
+        SPHX_LAUNCH_CHECK();
+        findNeighborsSpillKernel<false><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax,
+                                                                   nidx, nc, iterateH, stats, spillList, spillMem, xf);
+    }
     SPHX_LAUNCH_CHECK();
 }
 

@@ -935,12 +935,14 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
  * M[a][b] = sum_j v_ji[a] xm_j W_ij r_ij[b], so M is accumulated together with tau and the neighbor data is read
  * once. Mathematically identical; rounding differs from the two-pass form at the 1e-7 relative level.
  */
-template<class G, class Idx, class Ld>
+template<bool kAvS = false, class G, class Idx, class Ld>
 SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                               HT kxi, const Ld& ld, const KernelFn& kf, HT c[6], HT& divvOut, HT& curlvOut, HT* dV)
+                               HT kxi, const Ld& ld, const KernelFn& kf, HT c[6], HT& divvOut, HT& curlvOut, HT* dV,
+                               HT* avS = nullptr)
 {
     HT tau[6]  = {0, 0, 0, 0, 0, 0};
     HT M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    HT S[3]    = {0, 0, 0};
     const auto pi = ld(i);
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
@@ -955,6 +957,12 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nb
         tau[3] += ry * ry * vw;
         tau[4] += ry * rz * vw;
         tau[5] += rz * rz * vw;
+        if constexpr (kAvS)
+        {
+            S[0] += vw * rx;
+            S[1] += vw * ry;
+            S[2] += vw * rz;
+        }
         HT xw = pj.xm * w;
         HT ax = (pj.vx - pi.vx) * xw, ay = (pj.vy - pi.vy) * xw, az = (pj.vz - pi.vz) * xw;
         M[0][0] += ax * rx;
@@ -968,6 +976,12 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nb
         M[2][2] += az * rz;
     });
     invertTau(tau, hi, K, c);
+    if constexpr (kAvS)
+    {
+        avS[0] = S[0];
+        avS[1] = S[1];
+        avS[2] = S[2];
+    }
     // dV_a[k] = -sum_b c[k][b] M[a][b], c symmetric (c11 c12 c13 c22 c23 c33)
     HT dVv[3][3];
     for (int a = 0; a < 3; ++a)
@@ -1024,6 +1038,71 @@ SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const G& box, const Idx* nbr, i
         gy += f * tA1;
         gz += f * tA2;
     });
+    HT graddivv = sqrt(gx * gx + gy * gy + gz * gz);
+    HT alphaloc = 0;
+    if (divvi < HT(0))
+    {
+        HT a     = hi * hi * graddivv;
+        alphaloc = alphamax * a / (a + hi * fabs(divvi) + HT(0.05) * ci);
+    }
+    if (alphaloc >= alpha_i) { alpha_i = alphaloc; }
+    else
+    {
+        HT decay    = hi / (decayConstant * vsig);
+        HT alphadot = (alphaloc >= alphamin) ? (alphaloc - alpha_i) / decay : (alphamin - alpha_i) / decay;
+        alpha_i += alphadot * HT(dt);
+    }
+    return alpha_i;
+}
+
+/*! @brief AV-switch source record with the volume-weighted divergence vd = vol divv: 32 B on the fixed-point frame,
+ *         i.e. two dwordx4 gathers per neighbor and no separate divv gather.
+ *
+ * The AV loop's gradient sum  g_i = sum_j vol_j (divv_i - divv_j) tA_ij,  tA_ij = -C_i r_ij K h_i^-3 w_ij,
+ * is linear in the j terms, so  g_i = -K h_i^-3 C_i (divv_i S_i - T_i)  with  S_i = sum_j vol_j w_ij r_ij  (the IAD
+ * loop accumulates it next to tau: same neighbors, same w_ij) and  T_i = sum_j vd_j w_ij r_ij. vol_j and divv_j then
+ * only enter as their product. Mathematically identical to avSwitchesJLoop; rounding differs at the fp32 level.
+ */
+struct alignas(16) SrcAvV
+{
+    uint32_t x, y, z;
+    HT vd;
+    HT vx, vy, vz;
+    HT c;
+};
+static_assert(!kHydroF32 || sizeof(SrcAvV) == 32, "SrcAvV is two 16-byte chunks");
+
+template<class G, class Idx, class Ld>
+SPHX_HD HT avSwitchesVJLoop(unsigned i, double K, const G& box, const Idx* nbr, int stride, unsigned nc, HT hi,
+                            const HT ci6[6], HT divvi, const HT Si[3], const Ld& ld, const KernelFn& kf, double dt,
+                            HT alphamin, HT alphamax, HT decayConstant, HT alpha_i)
+{
+    const auto pi = ld(i);
+    HT ci    = pi.c;
+    HT vsig  = HT(1.e-40) * ci;
+    HT hInv  = HT(1) / hi, hInv3 = hInv * hInv * hInv;
+    HT T[3]  = {0, 0, 0};
+    forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
+        HT rx, ry, rz;
+        pairSep(box, pi, pj, hi, rx, ry, rz);
+        HT r2      = rx * rx + ry * ry + rz * rz;
+        HT invDist = rsqrtH(r2);
+        HT dist    = r2 * invDist;
+        HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
+        HT rv   = rx * vxij + ry * vyij + rz * vzij;
+        HT vsij = HT(0);
+        if (rv < HT(0)) { vsij = ci + pj.c - HT(3) * rv * invDist; }
+        vsig  = smax(vsig, vsij);
+        HT wd = kf.w(dist * hInv) * pj.vd;
+        T[0] += wd * rx;
+        T[1] += wd * ry;
+        T[2] += wd * rz;
+    });
+    const HT D[3] = {divvi * Si[0] - T[0], divvi * Si[1] - T[1], divvi * Si[2] - T[2]};
+    const HT s    = -HT(K) * hInv3;
+    HT gx = s * (ci6[0] * D[0] + ci6[1] * D[1] + ci6[2] * D[2]);
+    HT gy = s * (ci6[1] * D[0] + ci6[3] * D[1] + ci6[4] * D[2]);
+    HT gz = s * (ci6[2] * D[0] + ci6[4] * D[1] + ci6[5] * D[2]);
     HT graddivv = sqrt(gx * gx + gy * gy + gz * gz);
     HT alphaloc = 0;
     if (divvi < HT(0))

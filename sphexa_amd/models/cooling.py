@@ -110,10 +110,12 @@ class HydroCoolingProp(HydroProp):
     def compute_forces(self, domain, d):
         t = self.timer
         box = domain.box
-        first, last = self._neighbors(domain, d)
+        first, last = domain.start_index(), domain.end_index()
+        fused = self._neighbors(domain, d, "rho")
         t.step("FindNeighbors")
         nl = self.nl
-        H.compute_density(d, nl, box)
+        if not fused:
+            H.compute_density(d, nl, box)
         t.step("Density")
         self.cooler.gamma = d.gamma
         self.cooler.eos(d, first, last)

@@ -13,6 +13,7 @@ Parity (reference main/src/propagator/):
 from __future__ import annotations
 
 import math
+import os
 import sys
 from typing import List
 
@@ -22,6 +23,11 @@ from ..ops import hydro as H
 from ..ops.neighbors import find_neighbors
 from ..parallel.comm import MIN
 from ..utils.timer import Timer
+
+# XMass (STD: density) computed inside the GPU neighbor search instead of a separate pass over the lists. Off by
+# default: measured on Sedov -n 400 the search grows by 26 ms (flush-time kernel evaluations are divergent: a wave
+# evaluates whenever any lane flushes a block) while the XMass pass it replaces costs 11 ms (csrc/hip/neighbors.hip).
+FUSE_XMASS = os.environ.get("SPHX_FUSE_XMASS", "0") == "1"
 
 
 class Propagator:
@@ -64,13 +70,18 @@ class Propagator:
         pass
 
     # ---------------------------------------------------------------------------------------------- shared
-    def _neighbors(self, domain, d):
+    def _neighbors(self, domain, d, xmass_field: str | None = None):
+        """neighbor search + h iteration; on the GPU ``xmass_field`` is filled by the search itself (XMass fused
+        into its final round, ops/neighbors.py), and the return value says whether that happened"""
         first, last = domain.start_index(), domain.end_index()
+        fuse = xmass_field is not None and d.device.type == "cuda" and FUSE_XMASS
         self.nl = find_neighbors(d, domain.octree, domain.box, first, last,
-                                 nidx=self.nl.nidx if self.nl is not None else None)
+                                 nidx=self.nl.nidx if self.nl is not None else None,
+                                 xmass_out=d[xmass_field] if fuse else None,
+                                 m_uniform=H.uniform_mass(d) if fuse else 0.0)
         if d.device.type == "cuda":
             H.set_global_h_min(d, domain.comm)
-        return first, last
+        return fuse
 
     def _gravity(self, domain, d):
         if d.g != 0.0:
@@ -151,11 +162,13 @@ class HydroVeProp(Propagator):
         self.sync(domain, d)
         t.step("domain::sync")
         box = domain.box
-        first, last = self._neighbors(domain, d)
+        first, last = domain.start_index(), domain.end_index()
+        fused = self._neighbors(domain, d, "xm")
         t.step("FindNeighbors")
         nl = self.nl
 
-        H.compute_xmass(d, nl, box)
+        if not fused:
+            H.compute_xmass(d, nl, box)
         t.step("XMass")
         domain.exchange_halos(d, ["xm"])
         t.step("mpi::synchronizeHalos")
@@ -245,10 +258,12 @@ class HydroProp(Propagator):
     def compute_forces(self, domain, d):
         t = self.timer
         box = domain.box
-        first, last = self._neighbors(domain, d)
+        first, last = domain.start_index(), domain.end_index()
+        fused = self._neighbors(domain, d, "rho")
         t.step("FindNeighbors")
         nl = self.nl
-        H.compute_density(d, nl, box)
+        if not fused:
+            H.compute_density(d, nl, box)
         t.step("Density")
         H.compute_eos_std(d, first, last)
         t.step("EquationOfState")

@@ -213,7 +213,10 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
             [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["kx"].data_ptr(), d["xm"].data_ptr(),
             d["divv"].data_ptr(), d["curlv"].data_ptr(), dv)
     if _is_gpu(d):
-        _lib.hip().iad_divv_curlv(*args, *_gpu_tail(d))
+        # the AV loop's S_i = sum_j vol_j w_ij r_ij goes to the second record workspace (dead until momentum), so the
+        # AV switches read 32-B records with vd = vol divv (sph_math.hpp SrcAvV)
+        _lib.hip().iad_divv_curlv(*args, *_gpu_tail(d), _rec(d, 1).data_ptr())
+        d._av_s_valid = bool(d.fixedPoint)
     else:
         _lib.cpu().iad_divv_curlv(*args)
 
@@ -225,7 +228,9 @@ def compute_av_switches(d, nl: NeighborList, box: Box):
             d["c"].data_ptr(), [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["kx"].data_ptr(),
             d["xm"].data_ptr(), d["divv"].data_ptr(), float(d.minDt), d["alpha"].data_ptr())
     if _is_gpu(d):
-        _lib.hip().av_switches(*args, *_gpu_tail(d))
+        avs = _rec(d, 1).data_ptr() if (getattr(d, "_av_s_valid", False) and d.fixedPoint) else 0
+        _lib.hip().av_switches(*args, *_gpu_tail(d), avs)
+        d._av_s_valid = False
     else:
         _lib.cpu().av_switches(*args)
 

@@ -82,8 +82,14 @@ def _scratch(nbytes: int, device) -> torch.Tensor:
 
 
 def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
-                   nidx: torch.Tensor | None = None) -> NeighborList:
-    """search neighbors of particles [first, last) within 2h, adjusting h towards ng0 neighbors"""
+                   nidx: torch.Tensor | None = None, xmass_out: torch.Tensor | None = None,
+                   m_uniform: float = 0.0) -> NeighborList:
+    """search neighbors of particles [first, last) within 2h, adjusting h towards ng0 neighbors.
+
+    ``xmass_out`` (GPU only): also compute the VE XMass loop's xm = m / rho0 (reference xmass_kern.hpp) inside the
+    search from the distances of the stored entries (``m_uniform`` > 0: common mass, else per-particle masses), so
+    the separate XMass pass over the lists is skipped.
+    """
     x, y, z, h, nc = d["x"], d["y"], d["z"], d["h"], d["nc"]
     n = last - first
     ngmax = d.ngmax
@@ -103,7 +109,9 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                           tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
                           d.ng0, ngmax, nidx.data_ptr(), nc.data_ptr(), int(iterate_h) | (2 if COLLECT_STATS else 0),
                           stats.data_ptr(),
-                          scratch.data_ptr(), TEST_FRONT_CAP, _stream())
+                          scratch.data_ptr(), TEST_FRONT_CAP, _stream(),
+                          xm=xmass_out.data_ptr() if xmass_out is not None else 0, m=d["m"].data_ptr(),
+                          m_uniform=float(m_uniform), wh=d.wh.data_ptr(), consts=d.consts_array())
         st = stats.cpu()
         if int(st[1]) > 0:
             raise NeighborSearchError(f"GPU traversal stack overflow in {int(st[1])} groups")
