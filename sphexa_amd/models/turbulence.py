@@ -10,7 +10,8 @@ Parity (reference sph/include/sph/hydro_turb/):
   driver.hpp:40-90            updateNoise (OU update) + computeStirring
   main/src/propagator/turb_ve.hpp:52-103  TurbVeProp
 The per-particle stirring sum runs in ``_sphx_hip.compute_stirring`` (mode table staged in LDS) on the GPU.
-The RNG is numpy's MT19937 (reference: std::mt19937 + std::normal_distribution; sequences differ, parity unpinned).
+The RNG reproduces std::mt19937 with libstdc++'s uniform/normal distributions bit for bit (utils/std_random.py), and
+"rngEngineState" is the engine's text serialization stored as a char array, as in the reference.
 """
 
 from __future__ import annotations
@@ -22,6 +23,7 @@ import numpy as np
 import torch
 
 from ..ops import _lib
+from ..utils.std_random import StdMt19937
 from .propagators import HydroVeProp
 
 
@@ -56,9 +58,9 @@ def create_stirring_modes(L, st_max_modes, stir_max, stir_min, spect_form, power
         for ik in range(ikmin, ikmax + 1):
             nang = int(2 ** ndim * math.ceil(ik ** angles_exp))
             for _ in range(nang):
-                phi = twopi * rng.random()
-                theta = math.acos(1.0 - 2.0 * rng.random())
-                rand = ik + rng.random() - 0.5
+                phi = twopi * rng.uniform()
+                theta = math.acos(1.0 - 2.0 * rng.uniform())
+                rand = ik + rng.uniform() - 0.5
                 kx = twopi * round(rand * math.sin(theta) * math.cos(phi)) / L
                 ky = twopi * round(rand * math.sin(theta) * math.sin(phi)) / L
                 kz = twopi * round(rand * math.cos(theta)) / L
@@ -93,7 +95,7 @@ class TurbulenceData:
 
     def __init__(self, constants, verbose=False):
         self.sol_weight = float(constants["solWeight"])
-        self.rng = np.random.Generator(np.random.MT19937(int(constants["rngSeed"])))
+        self.rng = StdMt19937(int(constants["rngSeed"]))
         eps = float(constants["epsilon"])
         L = float(constants["Lbox"])
         vel = float(constants["stMachVelocity"])
@@ -109,7 +111,7 @@ class TurbulenceData:
             int(constants["stSpectForm"]), float(constants["powerLawExp"]), float(constants["anglesExp"]), self.rng)
         if verbose:
             print(f"Total Number of Stirring Modes: {self.num_modes}")
-        self.phases = self.rng.normal(0.0, self.variance, size=6 * self.num_modes)
+        self.phases = self.rng.normal(6 * self.num_modes, 0.0, self.variance)
         self._dev_table = None
 
     @property
@@ -119,7 +121,7 @@ class TurbulenceData:
     def update_noise(self, dt):
         a = math.exp(-dt / self.decay_time)
         b = math.sqrt(1.0 - a * a)
-        self.phases = self.phases * a + self.variance * b * self.rng.standard_normal(self.phases.size)
+        self.phases = self.phases * a + self.variance * b * self.rng.normal(self.phases.size)
 
     def mode_table(self):
         """[M, 10] float32 table {kx, ky, kz, 0, amp*Re(3), amp*Im(3)} for the GPU kernel"""
@@ -158,9 +160,7 @@ class TurbulenceData:
         writer.step_attribute(p + "modes", self.modes.reshape(-1))
         writer.step_attribute(p + "amplitudes", self.amplitudes)
         writer.step_attribute(p + "phases", self.phases)
-        st = self.rng.bit_generator.state["state"]
-        writer.step_attribute("rngEngineState", np.concatenate([np.asarray(st["key"], dtype=np.float64),
-                                                                [float(st["pos"])]]))
+        writer.step_attribute("rngEngineState", np.frombuffer(self.rng.state_text().encode(), dtype=np.int8))
 
     def load(self, attrs):
         p = self.PREFIX
@@ -174,10 +174,8 @@ class TurbulenceData:
         self.amplitudes = g("amplitudes")
         self.phases = g("phases")
         if "rngEngineState" in attrs:
-            s = np.asarray(attrs["rngEngineState"], dtype=np.float64).ravel()
-            st = self.rng.bit_generator.state
-            st["state"] = {"key": s[:-1].astype(np.uint32), "pos": int(s[-1])}
-            self.rng.bit_generator.state = st
+            raw = np.asarray(attrs["rngEngineState"]).ravel().astype(np.int8).tobytes()
+            self.rng.set_state_text(raw.split(b"\0")[0].decode())
 
 
 class TurbVeProp(HydroVeProp):
