@@ -158,7 +158,11 @@ def main(argv=None) -> int:
                 or (wall_reached and write_enabled)):
             write_step(writer, out_file, d, domain, propagator)
         if prof_enabled and (is_output_step(d.iteration, prof_freq) or wall_reached):
-            write_profile(propagator, comm, os.path.join(os.path.dirname(out_file) or ".", "profile"))
+            prof_path = os.path.join(os.path.dirname(out_file) or ".", "profile")
+            if ascii:
+                write_profile(propagator, comm, prof_path)
+            else:
+                propagator.timer.write_timings(sio.file_writer_factory(False, comm), prof_path, comm.size)
             if propagator.timer.pm is not None and not ascii:
                 propagator.timer.pm.write_timings(sio.file_writer_factory(False, comm),
                                                   os.path.join(os.path.dirname(out_file) or ".", "energy"),
@@ -201,7 +205,8 @@ def write_step(writer, path, d, domain, propagator):
 
 
 def write_profile(propagator, comm, path):
-    """substep timings of this rank (rank 0 writes numRanks/numIterations + its timings), reference timer.hpp"""
+    """--ascii variant of the profile: accumulated substep timings as text (rank 0); the HDF5 default is
+    Timer.write_timings (the reference's "timings" field, timer.hpp:61-73)"""
     import numpy as np
 
     t = propagator.timer

@@ -43,6 +43,8 @@ class Timer:
         self.steps: "OrderedDict[str, float]" = OrderedDict()
         self.accum: Dict[str, float] = OrderedDict()
         self.num_accum = 0
+        self.num_start = 0         # start() calls since the last write_timings (the reference's numStartCalled)
+        self.step_times: List[float] = []  # every step() duration since the last write_timings, in call order
         self.pm = None  # optional utils.pm_reader.PmReader sampled at every boundary
 
     def _now(self):
@@ -51,6 +53,7 @@ class Timer:
         return time.perf_counter()
 
     def start(self):
+        self.num_start += 1
         self.steps.clear()
         self.t0 = self.last = self._now()
         if self.pm is not None:
@@ -66,6 +69,7 @@ class Timer:
         dt = now - self.last
         self.last = now
         self.steps[name] = self.steps.get(name, 0.0) + dt
+        self.step_times.append(dt)
         self.accum[name] = self.accum.get(name, 0.0) + dt
         if self.active and self.out is not None:
             print(f"# {name}: {dt:.6f}s", file=self.out)
@@ -88,3 +92,18 @@ class Timer:
 
     def names(self) -> List[str]:
         return list(self.accum.keys())
+
+    def write_timings(self, writer, out_file: str, num_ranks: int):
+        """the reference's Timer::writeTimings (timer.hpp:61-73): one output step holding this rank's step() durations
+        since the last call as the float field "timings" (ranks concatenated by the parallel writer), with
+        numRanks/numIterations step attributes; then the buffers restart"""
+        import numpy as np
+
+        v = np.asarray(self.step_times, dtype=np.float32)
+        writer.add_step(0, v.size, out_file + writer.suffix)
+        writer.step_attribute("numRanks", np.int32(num_ranks))
+        writer.step_attribute("numIterations", np.int32(self.num_start))
+        writer.write_field("timings", v)
+        writer.close_step()
+        self.num_start = 0
+        self.step_times.clear()

@@ -79,8 +79,14 @@ def test_profile_and_energy_counters(tmp_path):
     out = str(tmp_path / "dump.h5")
     _run_cli(["--init", "sedov", "-n", "8", "-s", "2", "--profile", "1", "--pmroot", str(pm), "-o", out,
               "--device", "cpu", "--quiet"])
-    prof = (tmp_path / "profile").read_text().split("\n")
-    assert prof[0].startswith("numRanks 1") and "MomentumAndEnergy" in prof[1]
+    # the reference's Timer::writeTimings layout: one step per write, "timings" = every substep duration in order
+    rd = H5PartReader()
+    rd.set_step(str(tmp_path / "profile.h5"), -1, collective=False)
+    t = rd.read_field("timings", "f")
+    at = rd.step_attributes()
+    rd.close_step()
+    assert int(np.asarray(at["numRanks"]).ravel()[0]) == 1 and int(np.asarray(at["numIterations"]).ravel()[0]) == 1
+    assert t.size >= 10 and (t >= 0).all()
     rd = H5PartReader()
     rd.set_step(str(tmp_path / "energy.h5"), -1, collective=False)
     names = set(rd.dataset_names())
