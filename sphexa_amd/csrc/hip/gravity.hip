@@ -165,7 +165,11 @@ void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, do
 // global-memory stack).
 
 #ifndef SPHX_M2P_WAVES
+#ifdef SPHX_GRAV_VALU_M2P
 #define SPHX_M2P_WAVES 6 // launch bound (waves per SIMD) of the M2P kernel
+#else
+#define SPHX_M2P_WAVES 4 // the MFMA M2P holds 16 accumulators + the 4 targets' data per lane (6 waves spill)
+#endif
 #endif
 #ifndef SPHX_M2P_UNROLL
 #define SPHX_M2P_UNROLL 2 // unroll of the per-node M2P loop
@@ -253,6 +257,132 @@ __device__ inline void evalM2P(const int32_t* list, int n, const GravTree& t, co
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+/*! @brief M2P with the quadrupole-vector products on the matrix cores (v_mfma_f32_16x16x4_f32).
+ *
+ * Per pair (target t, node n, r = t - c_n) the quadrupole term needs Q_n r, a 3x4 by 4-vector product that is
+ * bilinear in node and target data: (Q r)_a = sum_k A_a[n][k] T[k][t] with A_a = [Q_ax, Q_ay, Q_az, -(Q c)_a] per node
+ * and T = [x_t, y_t, z_t, 1]. With nodes on the MFMA rows and targets on the columns, a 16-node x 16-target block of
+ * one component is one v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation); lane l then holds the three
+ * components for nodes 4 (l >> 4) + r, r < 4, and target 16 tb + (l & 15). The VALU finishes the pair (separation,
+ * rsqrt, r.Qr, monopole, accumulation): 25 instead of 34 VALU per pair, the 9 multiply-adds of Q r move to the
+ * matrix pipe (8 issue cycles per 1024 products). Node batches of 64 are staged in LDS as the MFMA A operands
+ * (per node and k one float4 {A_x[k], A_y[k], A_z[k], 0}) plus {c, M}; the next batch's gathers are in flight meanwhile.
+ * No precision guard is needed (unlike the P2P tile): Q t - Q c carries rounding ~eps |Q| |c| against |Q r| with
+ * |c| <= |r| + R_group, and R2 is formed on the VALU from r.
+ */
+__device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t, const double tc[3], float xr,
+                                   float yr, float zr, float4* stage, float acc[4])
+{
+    n = __builtin_amdgcn_readfirstlane(n);
+    if (n <= 0) return;
+    const int lane = laneId(), kq = lane >> 4, col = lane & 15;
+    float4* sC = stage;      // 64 x {cx, cy, cz, M}
+    float4* sA = stage + 64; // 64 x 4 (k) x {A_x[k], A_y[k], A_z[k], 0}
+    // target side: B operand [x, y, z, 1]_k of target 16 tb + col, and the four targets' coordinates
+    float bT[4], tx[4], ty[4], tz[4];
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+    {
+        const int src = tb * 16 + col;
+        tx[tb] = __shfl(xr, src), ty[tb] = __shfl(yr, src), tz[tb] = __shfl(zr, src);
+        bT[tb] = kq == 0 ? tx[tb] : (kq == 1 ? ty[tb] : (kq == 2 ? tz[tb] : 1.f));
+    }
+    float ph[4] = {0, 0, 0, 0}, ax[4] = {0, 0, 0, 0}, ay[4] = {0, 0, 0, 0}, az[4] = {0, 0, 0, 0};
+
+    double rc[3];
+    float4 q0, q1;
+    auto gather = [&](int32_t nd)
+    {
+        const double* c = t.centers + 4 * nd;
+        const float4* q = reinterpret_cast<const float4*>(t.mp + nd);
+        rc[0] = c[0], rc[1] = c[1], rc[2] = c[2];
+        q0 = q[0], q1 = q[1];
+    };
+    int32_t idxN  = lane < n ? list[lane] : 0;
+    int32_t idxNN = 64 + lane < n ? list[64 + lane] : 0;
+    gather(idxN);
+    for (int b0 = 0; b0 < n; b0 += 64)
+    {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // previous batch fully read before it is overwritten
+        {
+            // node b0 + lane: padding nodes (past n) are massless, quadrupole-free and far away (zero contribution)
+            const bool live = b0 + lane < n;
+            const float cx = live ? float(rc[0] - tc[0]) : 1e10f, cy = live ? float(rc[1] - tc[1]) : 1e10f,
+                        cz = live ? float(rc[2] - tc[2]) : 1e10f;
+            const float M   = live ? q0.x : 0.f;
+            const float Qxx = live ? q0.y : 0.f, Qxy = live ? q0.z : 0.f, Qxz = live ? q0.w : 0.f;
+            const float Qyy = live ? q1.x : 0.f, Qyz = live ? q1.y : 0.f, Qzz = live ? q1.z : 0.f;
+            const float Qcx = Qxx * cx + Qxy * cy + Qxz * cz;
+            const float Qcy = Qxy * cx + Qyy * cy + Qyz * cz;
+            const float Qcz = Qxz * cx + Qyz * cy + Qzz * cz;
+            sC[lane]             = make_float4(cx, cy, cz, M);
+            sA[4 * lane + 0]     = make_float4(Qxx, Qxy, Qxz, 0.f);
+            sA[4 * lane + 1]     = make_float4(Qxy, Qyy, Qyz, 0.f);
+            sA[4 * lane + 2]     = make_float4(Qxz, Qyz, Qzz, 0.f);
+            sA[4 * lane + 3]     = make_float4(-Qcx, -Qcy, -Qcz, 0.f);
+        }
+        idxN  = idxNN;
+        idxNN = b0 + 128 + lane < n ? list[b0 + 128 + lane] : 0;
+        gather(idxN);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int ntile = (min(64, n - b0) + 15) >> 4;
+        for (int tile = 0; tile < ntile; ++tile)
+        {
+            const float4 A = sA[4 * (16 * tile + col) + kq];
+            float4 C[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                C[r] = sC[16 * tile + 4 * kq + r];
+            const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int tb = 0; tb < 4; ++tb)
+            {
+                const f32x4 Qx = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[tb], zero, 0, 0, 0);
+                const f32x4 Qy = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[tb], zero, 0, 0, 0);
+                const f32x4 Qz = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[tb], zero, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    const float rx  = tx[tb] - C[r].x, ry = ty[tb] - C[r].y, rz = tz[tb] - C[r].z;
+                    const float r2  = rx * rx + ry * ry + rz * rz;
+                    const float ir  = __builtin_amdgcn_rsqf(r2);
+                    const float ir2 = ir * ir;
+                    const float ir5 = ir2 * ir2 * ir;
+                    const float rQr = rx * Qx[r] + ry * Qy[r] + rz * Qz[r];
+                    const float Mir = C[r].w * ir;
+                    const float t1  = rQr * ir5;
+                    const float cmb = (-2.5f * t1 - Mir) * ir2;
+                    ph[tb] -= Mir + 0.5f * t1;
+                    ax[tb] += ir5 * Qx[r] + cmb * rx;
+                    ay[tb] += ir5 * Qy[r] + cmb * ry;
+                    az[tb] += ir5 * Qz[r] + cmb * rz;
+                }
+            }
+        }
+    }
+    // the partials of target 16 tb + col sit in the four lane groups kq: sum them, lane L keeps target L
+    const int myTb = lane >> 4;
+    float v[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+    {
+        float p[4] = {ph[tb], ax[tb], ay[tb], az[tb]};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            float s = p[q];
+            s += __shfl_xor(s, 16);
+            s += __shfl_xor(s, 32);
+            v[q] = (tb == myTb) ? s : v[q];
+        }
+    }
+    acc[0] += v[0];
+    acc[1] += v[1];
+    acc[2] += v[2];
+    acc[3] += v[3];
+}
+
 
 //! @brief v_max_f32 without the NaN-quieting canonicalization fmaxf adds for MFMA results (inputs are finite)
 __device__ __forceinline__ float maxNoCanon(float a, float b)
@@ -796,7 +926,7 @@ __global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t 
                                                            double* __restrict__ out,
                                                            unsigned long long* __restrict__ stats, GravSlabs S)
 {
-    __shared__ float4 stage[kGWaves][3 * 64];
+    __shared__ float4 stage[kGWaves][5 * 64];
     __shared__ double red[kGWaves];
     const int wave          = threadIdx.x >> 6;
     const int64_t numGroups = (last - first + 63) / 64;
@@ -807,7 +937,11 @@ __global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t 
     {
         EvalTarget e = evalTarget(g, first, last, x, y, z, h);
         float acc[4] = {0, 0, 0, 0};
+#ifdef SPHX_GRAV_VALU_M2P
         evalM2P(S.mlist + g * S.capM, nm, t, e.tc, e.xr, e.yr, e.zr, stage[wave], acc);
+#else
+        evalM2PMfma(S.mlist + g * S.capM, nm, t, e.tc, e.xr, e.yr, e.zr, stage[wave], acc);
+#endif
         gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, 0ull, (unsigned long long)nm, upot);
     }
     blockEnergy(upot, red, kGWaves, out);
