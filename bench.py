@@ -139,7 +139,9 @@ def main():
             if prop.gravity is not None and prop.gravity.stats:
                 print(f"# gravity stats {prop.gravity.stats}", file=sys.stderr)
             if device.type == "cuda":
-                print(f"# max memory allocated {torch.cuda.max_memory_allocated() / 2**30:.2f} GiB", file=sys.stderr)
+                print(f"# max memory allocated {torch.cuda.max_memory_allocated() / 2**30:.2f} GiB "
+                      f"({torch.cuda.max_memory_allocated() / max(d.numParticlesGlobal / size, 1):.0f} B/particle), "
+                      f"held between steps {torch.cuda.memory_allocated() / 2**30:.2f} GiB", file=sys.stderr)
 
 
 if __name__ == "__main__":

@@ -23,7 +23,11 @@ from ..utils.box import Box, PERIODIC
 CIJ = ("c11", "c12", "c13", "c22", "c23", "c33")
 DV = ("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")
 
-REC_BYTES = 128  # largest source record (SrcMom 96 B, SrcGradV 32 B in a second buffer)
+# bytes per particle of the largest source record each GPU loop may pack (sph_math.hpp), for fp64-coordinate / fixed-point
+# runs: the fixed-point loops fall back to fp64-frame records in some cases (stored-mass Gradh: SrcPos 32 B; AV without
+# the IAD loop's S_i and STD IAD: SrcIad 48 B). The workspace is grow-only, so it settles at the momentum record:
+# SrcMom 96 B (fp64) or SrcMomQ 80 B (fixed point); SrcGradV (32 B) and the AV S_i (16 B) use the second buffer
+REC_BYTES = {"xmass": (32, 32), "gradh": (32, 32), "iad": (48, 48), "av": (48, 48), "mom": (96, 80), "std": (80, 80)}
 
 
 def _stream():
@@ -42,19 +46,21 @@ def _is_gpu(d):
     return d.device.type == "cuda"
 
 
-def _rec(d, which: int = 0):
-    """per-dataset record workspace on the GPU (grown with the particle count incl. halos)"""
+def _rec(d, which: int = 0, loop: str = "mom"):
+    """per-dataset record workspace on the GPU (grow-only; particle count incl. halos times the record size)"""
     name = "_rec%d" % which
-    need = d.size * (REC_BYTES if which == 0 else 32)
+    per = REC_BYTES[loop][1 if getattr(d, "fixedPoint", 1) else 0] if which == 0 else 32
+    need = d.size * per
     buf = getattr(d, name, None)
     if buf is None or buf.numel() < need:
+        setattr(d, name, None)  # release before the larger allocation
         buf = torch.empty(int(need * 1.05) + 4096, dtype=torch.uint8, device=d.device)
         setattr(d, name, buf)
     return buf
 
 
-def _gpu_tail(d, which=(0,)):
-    return (d.size,) + tuple(_rec(d, w).data_ptr() for w in which) + (_stream(),)
+def _gpu_tail(d, loop: str, which=(0,)):
+    return (d.size,) + tuple(_rec(d, w, loop).data_ptr() for w in which) + (_stream(),)
 
 
 def compute_xmass(d, nl: NeighborList, box: Box, out_field: str = "xm"):
@@ -63,7 +69,7 @@ def compute_xmass(d, nl: NeighborList, box: Box, out_field: str = "xm"):
     args = (first, last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d[out_field].data_ptr())
     if _is_gpu(d):
-        _lib.hip().xmass(*args, *_gpu_tail(d))
+        _lib.hip().xmass(*args, *_gpu_tail(d, "xmass"))
     else:
         _lib.cpu().xmass(*args)
 
@@ -157,7 +163,7 @@ def compute_ve_def_gradh(d, nl: NeighborList, box: Box):
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d.whd.data_ptr(),
             d["xm"].data_ptr(), d["kx"].data_ptr(), d["gradh"].data_ptr())
     if _is_gpu(d):
-        _lib.hip().ve_def_gradh(*args, *_gpu_tail(d), uniform_mass(d))
+        _lib.hip().ve_def_gradh(*args, *_gpu_tail(d, "gradh"), uniform_mass(d))
     else:
         _lib.cpu().ve_def_gradh(*args)
 
@@ -199,7 +205,7 @@ def compute_iad(d, nl: NeighborList, box: Box, numer: str, denom: str):
             d["z"].data_ptr(), d["h"].data_ptr(), d.wh.data_ptr(), d[numer].data_ptr(), d[denom].data_ptr(),
             [d[c].data_ptr() for c in CIJ])
     if _is_gpu(d):
-        _lib.hip().iad(*args, *_gpu_tail(d))
+        _lib.hip().iad(*args, *_gpu_tail(d, "iad"))
     else:
         _lib.cpu().iad(*args)
 
@@ -215,7 +221,7 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
     if _is_gpu(d):
         # the AV loop's S_i = sum_j vol_j w_ij r_ij goes to the second record workspace (dead until momentum), so the
         # AV switches read 32-B records with vd = vol divv (sph_math.hpp SrcAvV)
-        _lib.hip().iad_divv_curlv(*args, *_gpu_tail(d), _rec(d, 1).data_ptr())
+        _lib.hip().iad_divv_curlv(*args, *_gpu_tail(d, "iad"), _rec(d, 1, "av").data_ptr())
         d._av_s_valid = bool(d.fixedPoint)
     else:
         _lib.cpu().iad_divv_curlv(*args)
@@ -228,8 +234,8 @@ def compute_av_switches(d, nl: NeighborList, box: Box):
             d["c"].data_ptr(), [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["kx"].data_ptr(),
             d["xm"].data_ptr(), d["divv"].data_ptr(), float(d.minDt), d["alpha"].data_ptr())
     if _is_gpu(d):
-        avs = _rec(d, 1).data_ptr() if (getattr(d, "_av_s_valid", False) and d.fixedPoint) else 0
-        _lib.hip().av_switches(*args, *_gpu_tail(d), avs)
+        avs = _rec(d, 1, "av").data_ptr() if (getattr(d, "_av_s_valid", False) and d.fixedPoint) else 0
+        _lib.hip().av_switches(*args, *_gpu_tail(d, "av"), avs)
         d._av_s_valid = False
     else:
         _lib.cpu().av_switches(*args)
@@ -246,7 +252,7 @@ def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = F
               d["ax"].data_ptr(), d["ay"].data_ptr(), d["az"].data_ptr(), d["du"].data_ptr())
     if _is_gpu(d):
         dt = torch.full((1,), math.inf, dtype=torch.float32, device=d.device)
-        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), *_gpu_tail(d, (0, 1)))
+        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), *_gpu_tail(d, "mom", (0, 1)))
         d.minDtCourant_dev = dt
         d.minDtCourant = None
     else:
@@ -262,7 +268,7 @@ def compute_momentum_energy_std(d, nl: NeighborList, box: Box):
               d["az"].data_ptr(), d["du"].data_ptr())
     if _is_gpu(d):
         dt = torch.full((1,), math.inf, dtype=torch.float32, device=d.device)
-        _lib.hip().momentum_energy_std(*common, dt.data_ptr(), *_gpu_tail(d))
+        _lib.hip().momentum_energy_std(*common, dt.data_ptr(), *_gpu_tail(d, "std"))
         d.minDtCourant_dev = dt
         d.minDtCourant = None
     else:

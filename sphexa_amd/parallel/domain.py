@@ -43,6 +43,7 @@ from ..utils.box import Box, PERIODIC
 from .comm import Comm, MAX, MIN, SUM
 
 HALO_FIELDS = ("x", "y", "z", "h", "m")
+REORDER_BATCH = 3  # conserved fields reordered per gather launch in sync (bounds the transient memory)
 
 
 class HaloOwnershipError(RuntimeError):
@@ -144,21 +145,34 @@ class Domain:
 
         skeys, perm = sfc_ops.sort_keys(keys)
         names = list(own.keys())
-        reordered = sfc_ops.gather_many(perm, [own[f] for f in names])
-        own = dict(zip(names, reordered))
         n_own = skeys.numel()
 
         if self.size > 1:
+            # halo discovery reads the sorted own coordinates (+ h, m)
+            disc = [f for f in HALO_FIELDS if f in own]
+            for f, t in zip(disc, sfc_ops.gather_many(perm, [own[f] for f in disc])):
+                own[f] = t
             self._discover_halos(skeys, own, gravity)
+            sorted_done = set(disc)
         else:
             self.n_lo = self.n_hi = 0
             self.halo_send_idx = []
+            sorted_done = set()
 
         total = self.n_lo + n_own + self.n_hi
         d.resize(total, keep=False)
         self.start, self.end, self.n_with_halos = self.n_lo, self.n_lo + n_own, total
-        for f in names:
+        # reorder the remaining fields a few at a time straight into place: the transient is a few fields, not a
+        # second copy of every conserved field (own[f] may alias d's buffers on one rank: each gather completes before
+        # its copy, stream-ordered)
+        rest = [f for f in names if f not in sorted_done]
+        for c in range(0, len(rest), REORDER_BATCH):
+            batch = rest[c:c + REORDER_BATCH]
+            for f, t in zip(batch, sfc_ops.gather_many(perm, [own[f] for f in batch])):
+                d.buffer(f)[self.start:self.end].copy_(t)
+        for f in sorted_done:
             d.buffer(f)[self.start:self.end].copy_(own[f])
+        del own
         d.buffer("keys")[self.start:self.end].copy_(skeys)
 
         if self.size > 1:
