@@ -67,6 +67,8 @@ class Domain:
         self.sfc_kind = sfc_kind
         self.halo_cut_boxes = halo_cut_boxes
         self.check_halos = check_halos
+        # peer pruning costs one host copy per step and pays off only when many ranks are far apart
+        self.peer_prune_min_ranks = 16
 
         self.start = 0
         self.end = 0
@@ -280,10 +282,16 @@ class Domain:
             outside = torch.zeros(ot.num_nodes, dtype=torch.uint8, device=x.device)
             grav_ops.mark_outside_range(ot, self.assignment_keys[self.rank], self.assignment_keys[self.rank + 1],
                                         outside)
+        # peer pruning (reference traversal/peers.hpp: only ranks whose domains interact exchange halos): a rank whose
+        # search boxes do not reach this rank's particle bounding box receives no SPH halos, and its marking pass is
+        # skipped (with gravity every rank still gets the LET multipoles, so all ranks stay peers)
+        prune = not gravity and self.size >= self.peer_prune_min_ranks
+        peers = self._halo_peers(all_boxes, ot) if prune else set(range(self.size))
+        self.stats["peers"] = len(peers - {self.rank})
         send_idx: List[torch.Tensor] = []
         mp_send: List[torch.Tensor] = []
         for q in range(self.size):
-            if q == self.rank or all_boxes[q].shape[0] == 0 or skeys.numel() == 0:
+            if q == self.rank or q not in peers or all_boxes[q].shape[0] == 0 or skeys.numel() == 0:
                 send_idx.append(torch.empty(0, dtype=torch.int64, device=skeys.device))
                 mp_send.append(torch.empty(0, dtype=torch.int64, device=skeys.device))
                 continue
@@ -304,6 +312,32 @@ class Domain:
         self.n_hi = sum(self.halo_recv_counts[self.rank + 1:])
         self._halo_send_rel = send_idx  # relative to own block, converted to absolute below
         self.halo_send_idx = [t + self.n_lo for t in send_idx]
+
+    def _halo_peers(self, all_boxes, ot) -> set:
+        """ranks whose search-box union overlaps this rank's particle bounding box (periodic images included)"""
+        if ot.num_nodes == 0:
+            return set()
+        dev = all_boxes[self.rank].device
+        ext = []
+        for q in range(self.size):
+            bq = all_boxes[q]
+            if bq.shape[0] == 0:
+                ext.append(torch.full((6,), float("nan"), dtype=torch.float64, device=dev))
+            else:
+                ext.append(torch.cat([(bq[:, :3] - bq[:, 3:]).min(0).values, (bq[:, :3] + bq[:, 3:]).max(0).values]))
+        own_c, own_h = ot.center[:3].to(dev), ot.half[:3].to(dev)
+        ext.append(torch.cat([own_c - own_h, own_c + own_h]))
+        e = torch.stack(ext).cpu().tolist()  # one host copy for all ranks
+        mine = e[-1]
+        peers = {self.rank}
+        for q in range(self.size):
+            lo_q, hi_q = e[q][:3], e[q][3:]
+            if any(math.isnan(v) for v in lo_q):
+                continue
+            if all(_interval_overlap(lo_q[k], hi_q[k], mine[k], mine[3 + k], self.box.lengths()[k],
+                                     self.box.bc[k] == PERIODIC) for k in range(3)):
+                peers.add(q)
+        return peers
 
     def _check_halo_ownership(self, keys: torch.Tensor):
         """every halo received from rank q must carry an SFC key inside q's assigned range, and no halo may fall into
@@ -374,6 +408,11 @@ def _rebalance_replicated(tree: torch.Tensor, gcounts: torch.Tensor, bucket: int
     c_np = gcounts.clamp(max=2**32 - 1).to(torch.int64).cpu().numpy().astype(np.uint32)
     new, changed = _lib.cpu().rebalance(t_np, c_np, bucket)
     return torch.from_numpy(new.view(np.int64)).to(tree.device), bool(changed)
+
+
+def _interval_overlap(a0: float, a1: float, b0: float, b1: float, length: float, periodic: bool) -> bool:
+    shifts = (-length, 0.0, length) if periodic else (0.0,)
+    return any(a0 <= b1 + s and b0 + s <= a1 for s in shifts)
 
 
 def _search_boxes(ot, x, y, z, h, factor: float):
