@@ -122,6 +122,11 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("gather_multi",
           [](int64_t n, Ptr perm, const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst, int es, Ptr s)
           { gatherMulti(n, P<int32_t>(perm), src, dst, es, St(s)); });
+    m.def("row_bytes", [](const std::vector<int>& sizes) { return rowBytes(sizes); });
+    m.def("pack_rows", [](int64_t n, Ptr idx, const std::vector<uintptr_t>& src, const std::vector<int>& sizes, Ptr rows,
+                          Ptr s) { packRows(n, P<int64_t>(idx), src, sizes, P<void>(rows), St(s)); });
+    m.def("unpack_rows", [](int64_t n, Ptr rows, const std::vector<uintptr_t>& dst, const std::vector<int>& sizes,
+                            int64_t off, Ptr s) { unpackRows(n, P<void>(rows), dst, sizes, off, St(s)); });
     m.def("scan_temp_bytes", [](int64_t n) { return scanTempBytes(n); });
     m.def("exclusive_scan_i64", [](Ptr in, Ptr out, int64_t n, Ptr tmp, size_t tb, Ptr s)
           { exclusiveScanI64(P<int64_t>(in), P<int64_t>(out), n, P<void>(tmp), tb, St(s)); });

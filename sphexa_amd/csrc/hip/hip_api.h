@@ -52,6 +52,12 @@ void sortKeys(int64_t n, const KeyT* keysIn, KeyT* keysOut, int32_t* perm, void*
 void gather(int64_t n, const int32_t* perm, const void* src, void* dst, int elemSize, hipStream_t s);
 void gatherMulti(int64_t n, const int32_t* perm, const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,
                  int elemSize, hipStream_t s);
+//! halo message rows of several fields (8-byte fields first, rows padded to 8 bytes); idx == nullptr: rows 0..n-1
+int rowBytes(const std::vector<int>& sizes);
+void packRows(int64_t n, const int64_t* idx, const std::vector<uintptr_t>& src, const std::vector<int>& sizes,
+              void* rows, hipStream_t s);
+void unpackRows(int64_t n, const void* rows, const std::vector<uintptr_t>& dst, const std::vector<int>& sizes,
+                int64_t dstOffset, hipStream_t s);
 size_t scanTempBytes(int64_t n);
 void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s);
 

@@ -135,6 +135,95 @@ void gatherMulti(int64_t n, const int32_t* perm, const std::vector<uintptr_t>& s
     SPHX_LAUNCH_CHECK();
 }
 
+/*! @brief halo message rows: field k of row r at byte offset off[k] of a row of rowWords 4-byte words (8-byte fields
+ *         first, so every field is naturally aligned); one thread per row, all fields of a message in one launch
+ */
+struct RowFields
+{
+    uintptr_t ptr[kMaxGatherFields];
+    int words[kMaxGatherFields]; // 1 (4-byte) or 2 (8-byte) words
+    int off[kMaxGatherFields];   // word offset in the row
+};
+
+__global__ void packRowsKernel(int64_t n, const int64_t* __restrict__ idx, RowFields f, int nf, int rowWords,
+                               uint32_t* __restrict__ rows)
+{
+    int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int64_t j = idx ? idx[r] : r;
+    uint32_t* row   = rows + r * rowWords;
+    for (int k = 0; k < nf; ++k)
+    {
+        if (f.words[k] == 2)
+            *reinterpret_cast<uint2*>(row + f.off[k]) = reinterpret_cast<const uint2*>(f.ptr[k])[j];
+        else row[f.off[k]] = reinterpret_cast<const uint32_t*>(f.ptr[k])[j];
+    }
+}
+
+__global__ void unpackRowsKernel(int64_t n, const uint32_t* __restrict__ rows, RowFields f, int nf, int rowWords,
+                                 int64_t dstOffset)
+{
+    int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t* row = rows + r * rowWords;
+    const int64_t i     = dstOffset + r;
+    for (int k = 0; k < nf; ++k)
+    {
+        if (f.words[k] == 2)
+            reinterpret_cast<uint2*>(f.ptr[k])[i] = *reinterpret_cast<const uint2*>(row + f.off[k]);
+        else reinterpret_cast<uint32_t*>(f.ptr[k])[i] = row[f.off[k]];
+    }
+}
+
+static RowFields rowFields(const std::vector<uintptr_t>& ptrs, const std::vector<int>& sizes, int& rowWords)
+{
+    if (ptrs.size() > size_t(kMaxGatherFields) || ptrs.size() != sizes.size())
+        throw std::runtime_error("row packing: bad field list");
+    RowFields f{};
+    int w = 0;
+    for (int pass = 0; pass < 2; ++pass) // 8-byte fields first: natural alignment of every field in the row
+        for (size_t k = 0; k < ptrs.size(); ++k)
+            if ((sizes[k] == 8) == (pass == 0))
+            {
+                if (sizes[k] != 4 && sizes[k] != 8) throw std::runtime_error("row packing: element size");
+                f.ptr[k]   = ptrs[k];
+                f.words[k] = sizes[k] / 4;
+                f.off[k]   = w;
+                w += sizes[k] / 4;
+            }
+    rowWords = (w + 1) & ~1; // rows of whole 8-byte words
+    return f;
+}
+
+int rowBytes(const std::vector<int>& sizes)
+{
+    std::vector<uintptr_t> p(sizes.size(), 0);
+    int w;
+    rowFields(p, sizes, w);
+    return 4 * w;
+}
+
+void packRows(int64_t n, const int64_t* idx, const std::vector<uintptr_t>& src, const std::vector<int>& sizes,
+              void* rows, hipStream_t s)
+{
+    if (n <= 0) return;
+    int w;
+    RowFields f = rowFields(src, sizes, w);
+    packRowsKernel<<<gridFor(n, 256), 256, 0, s>>>(n, idx, f, int(src.size()), w, static_cast<uint32_t*>(rows));
+    SPHX_LAUNCH_CHECK();
+}
+
+void unpackRows(int64_t n, const void* rows, const std::vector<uintptr_t>& dst, const std::vector<int>& sizes,
+                int64_t dstOffset, hipStream_t s)
+{
+    if (n <= 0) return;
+    int w;
+    RowFields f = rowFields(dst, sizes, w);
+    unpackRowsKernel<<<gridFor(n, 256), 256, 0, s>>>(n, static_cast<const uint32_t*>(rows), f, int(dst.size()), w,
+                                                     dstOffset);
+    SPHX_LAUNCH_CHECK();
+}
+
 size_t scanTempBytes(int64_t n)
 {
     size_t bytes = 0;

@@ -266,7 +266,10 @@ class Domain:
     def _discover_halos(self, skeys, own, gravity: bool = False):
         """push-based halo discovery against the other ranks' search boxes (+ LET selection with gravity)"""
         x, y, z, h = own["x"], own["y"], own["z"], own["h"]
-        tree, counts = octree_ops.update_tree(None, skeys, self.bucket_size_focus)
+        # the own-particle tree of the previous step is the starting point (one rebalance round instead of one per level
+        # from the root, each a host round trip)
+        tree, counts = octree_ops.update_tree(getattr(self, "_own_tree", None), skeys, self.bucket_size_focus)
+        self._own_tree = tree
         ot = octree_ops.build_octree(tree, counts, skeys, x, y, z, 0)
         c, hf = _search_boxes(ot, x, y, z, h, 2.0)
         cut = _coarse_cut(ot, c, hf, self.halo_cut_boxes)
@@ -290,6 +293,7 @@ class Domain:
         self.stats["peers"] = len(peers - {self.rank})
         send_idx: List[torch.Tensor] = []
         mp_send: List[torch.Tensor] = []
+        flag_rows = None
         for q in range(self.size):
             if q == self.rank or q not in peers or all_boxes[q].shape[0] == 0 or skeys.numel() == 0:
                 send_idx.append(torch.empty(0, dtype=torch.int64, device=skeys.device))
@@ -302,8 +306,16 @@ class Domain:
                 send_idx.append(torch.nonzero(pflags, as_tuple=False).flatten())
                 mp_send.append(nodes)
             else:
-                flags = _mark_in_boxes(ot, all_boxes[q], x, y, z, self.box)
-                send_idx.append(torch.nonzero(flags, as_tuple=False).flatten())
+                # flags of every peer first, indices after the loop: one host round trip instead of one per rank
+                if flag_rows is None:
+                    flag_rows = torch.zeros((self.size, skeys.numel()), dtype=torch.uint8, device=skeys.device)
+                _mark_in_boxes(ot, all_boxes[q], x, y, z, self.box, out=flag_rows[q])
+                send_idx.append(None)
+        if flag_rows is not None:
+            nz = torch.nonzero(flag_rows, as_tuple=False)
+            per = torch.bincount(nz[:, 0], minlength=self.size).cpu().tolist()
+            parts = torch.split(nz[:, 1], per)
+            send_idx = [parts[q] if t is None else t for q, t in enumerate(send_idx)]
         if gravity:
             self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes)
         self.halo_send_counts = [int(t.numel()) for t in send_idx]
@@ -312,6 +324,7 @@ class Domain:
         self.n_hi = sum(self.halo_recv_counts[self.rank + 1:])
         self._halo_send_rel = send_idx  # relative to own block, converted to absolute below
         self.halo_send_idx = [t + self.n_lo for t in send_idx]
+        self._halo_send_cat = None  # concatenated once per sync by exchange_halos
 
     def _halo_peers(self, all_boxes, ot) -> set:
         """ranks whose search-box union overlaps this rank's particle bounding box (periodic images included)"""
@@ -383,7 +396,10 @@ class Domain:
             return
         if not fields:
             return
-        send_idx = torch.cat(self.halo_send_idx) if self.halo_send_idx else None
+        send_idx = getattr(self, "_halo_send_cat", None)
+        if send_idx is None or send_idx.numel() != sum(self.halo_send_counts):
+            send_idx = torch.cat(self.halo_send_idx) if self.halo_send_idx else None
+            self._halo_send_cat = send_idx
         tensors = [d[f] for f in fields]
         packed = _pack_rows(tensors, send_idx)
         rowbytes = packed.shape[1]
@@ -440,26 +456,30 @@ def _search_boxes(ot, x, y, z, h, factor: float):
 
 def _coarse_cut(ot, center, half, max_boxes: int) -> torch.Tensor:
     """node indices of a tree cut with at most ~max_boxes non-empty nodes (nodes at the cut level + shallower
-    leaves)"""
-    lv = ot.node_levels()
+    leaves): the deepest level whose cut still fits, from per-level counts gathered in one host copy"""
+    lv = ot.node_levels().long()
     is_leaf = ot.node_to_leaf >= 0
     nonempty = half.view(-1, 3)[:, 0] >= 0
-    best = None
-    for cut in range(0, octree_ops.MAX_LEVEL + 1):
-        sel = ((lv == cut) | (is_leaf & (lv < cut))) & nonempty
-        cnt = int(sel.sum().item())
-        if cnt > max_boxes and best is not None:
+    nl = octree_ops.MAX_LEVEL + 1
+    at_level = torch.bincount(lv[nonempty], minlength=nl)[:nl]
+    leaves_at = torch.bincount(lv[nonempty & is_leaf], minlength=nl)[:nl]
+    # cut(c) = nonempty nodes at level c + nonempty leaves above c
+    leaves_above = torch.cumsum(leaves_at, 0) - leaves_at
+    sizes = (at_level + leaves_above).cpu().tolist()
+    best = 0
+    for c in range(0, min(nl, ot.max_depth() + 2)):
+        if sizes[c] > max_boxes and c > 0:
             break
-        best = sel
-        if cut > ot.max_depth():
-            break
-    return torch.nonzero(best, as_tuple=False).flatten()
+        best = c
+    sel = ((lv == best) | (is_leaf & (lv < best))) & nonempty
+    return torch.nonzero(sel, as_tuple=False).flatten()
 
 
-def _mark_in_boxes(ot, boxes: torch.Tensor, x, y, z, box: Box) -> torch.Tensor:
-    """flags[i] = particle i lies inside any of ``boxes`` (rows: center[3], half[3]); PBC aware"""
+def _mark_in_boxes(ot, boxes: torch.Tensor, x, y, z, box: Box, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """flags[i] = particle i lies inside any of ``boxes`` (rows: center[3], half[3]); PBC aware. ``out``: a zeroed
+    contiguous uint8 row to fill"""
     n = x.numel()
-    flags = torch.zeros(n, dtype=torch.uint8, device=x.device)
+    flags = torch.zeros(n, dtype=torch.uint8, device=x.device) if out is None else out
     bc = boxes[:, :3].contiguous().view(-1)
     bh = boxes[:, 3:].contiguous().view(-1)
     nb = boxes.shape[0]
@@ -474,7 +494,19 @@ def _mark_in_boxes(ot, boxes: torch.Tensor, x, y, z, box: Box) -> torch.Tensor:
 
 
 def _pack_rows(tensors: Sequence[torch.Tensor], idx: Optional[torch.Tensor]) -> torch.Tensor:
-    """gather rows idx of several 1-D fields into one (n, rowbytes) uint8 matrix"""
+    """gather rows idx of several 1-D fields into one (n, rowbytes) uint8 matrix. On the GPU one kernel packs every
+    field (8-byte fields first, rows padded to 8 bytes: csrc/hip/sfc_sort.hip packRows); the CPU path concatenates
+    the fields' bytes in the given order. All ranks use the same path, so both ends agree on the row layout."""
+    if tensors and tensors[0].is_cuda:
+        hp = _lib.hip()
+        sizes = [t.element_size() for t in tensors]
+        n = idx.numel() if idx is not None else tensors[0].numel()
+        rows = torch.empty((n, hp.row_bytes(sizes)), dtype=torch.uint8, device=tensors[0].device)
+        if idx is not None:
+            idx = idx.to(torch.int64).contiguous()
+        hp.pack_rows(n, 0 if idx is None else idx.data_ptr(), [t.data_ptr() for t in tensors], sizes,
+                     rows.data_ptr(), _stream())
+        return rows
     cols = []
     for t in tensors:
         sel = t.index_select(0, idx) if idx is not None else t
@@ -485,6 +517,11 @@ def _pack_rows(tensors: Sequence[torch.Tensor], idx: Optional[torch.Tensor]) -> 
 def _unpack_rows(rows: torch.Tensor, tensors: Sequence[torch.Tensor], offset: int):
     n = rows.shape[0]
     if n == 0:
+        return
+    if rows.is_cuda:
+        rows = rows.contiguous()
+        _lib.hip().unpack_rows(n, rows.data_ptr(), [t.data_ptr() for t in tensors],
+                               [t.element_size() for t in tensors], int(offset), _stream())
         return
     col = 0
     for t in tensors:
