@@ -190,6 +190,10 @@ class ParticlesData:
         if self.is_allocated(name):
             self[name] = value
 
+    @property
+    def capacity(self) -> int:
+        return self._capacity
+
     def buffer(self, name: str) -> torch.Tensor:
         """the full-capacity storage of a field (used to swap in reordered data)"""
         return self._buf[name]

@@ -81,10 +81,15 @@ def gather(perm: torch.Tensor, src: torch.Tensor, out: torch.Tensor | None = Non
     return out
 
 
-def gather_many(perm: torch.Tensor, srcs: Sequence[torch.Tensor]):
-    """gather several fields with the same permutation; on the GPU all fields of one element size share a launch"""
+def gather_many(perm: torch.Tensor, srcs: Sequence[torch.Tensor], outs: Sequence[torch.Tensor] | None = None):
+    """gather several fields with the same permutation; on the GPU all fields of one element size share a launch.
+    ``outs``: optional contiguous destinations (e.g. slices of new field buffers)"""
     n = perm.numel()
-    outs = [torch.empty(n, dtype=s.dtype, device=s.device) for s in srcs]
+    if outs is None:
+        outs = [torch.empty(n, dtype=s.dtype, device=s.device) for s in srcs]
+    else:
+        outs = list(outs)
+        assert all(o.is_contiguous() and o.numel() == n for o in outs)
     if n == 0 or not srcs:
         return outs
     if srcs[0].is_cuda:

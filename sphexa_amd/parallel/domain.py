@@ -164,14 +164,18 @@ class Domain:
         total = self.n_lo + n_own + self.n_hi
         d.resize(total, keep=False)
         self.start, self.end, self.n_with_halos = self.n_lo, self.n_lo + n_own, total
-        # reorder the remaining fields a few at a time straight into place: the transient is a few fields, not a
-        # second copy of every conserved field (own[f] may alias d's buffers on one rank: each gather completes before
-        # its copy, stream-ordered)
+        # reorder the remaining fields a few at a time into fresh buffers that replace the old ones: no copy back, and
+        # the transient is a few fields, not a second copy of every conserved field (own[f] may view the old buffers,
+        # which stay alive until their gather has been enqueued)
         rest = [f for f in names if f not in sorted_done]
+        cap = d.capacity
         for c in range(0, len(rest), REORDER_BATCH):
             batch = rest[c:c + REORDER_BATCH]
-            for f, t in zip(batch, sfc_ops.gather_many(perm, [own[f] for f in batch])):
-                d.buffer(f)[self.start:self.end].copy_(t)
+            bufs = [torch.empty(cap, dtype=d.buffer(f).dtype, device=d.device) for f in batch]
+            sfc_ops.gather_many(perm, [own[f] for f in batch], [b[self.start:self.end] for b in bufs])
+            for f, b in zip(batch, bufs):
+                own[f] = None
+                d.set_buffer(f, b)
         for f in sorted_done:
             d.buffer(f)[self.start:self.end].copy_(own[f])
         del own
