@@ -116,3 +116,26 @@ def test_nan_watchdog(tmp_path, monkeypatch):
         sphexa.main(args)
     # disabled: the run completes (and carries the NaN)
     assert sphexa.main(args + ["--no-watchdog"]) == 0
+
+
+def test_restart_matches_uninterrupted(tmp_path):
+    """checkpoint -> restart continues the run as if it had not been interrupted: 4 uninterrupted steps
+    vs 2 steps + snapshot + restart + 2 steps, compared field by field in key order"""
+    full = str(tmp_path / "full.h5")
+    half = str(tmp_path / "half.h5")
+    _run_cli(["--init", "sedov", "-n", "10", "-s", "4", "-w", "4", "-o", full, "--device", "cpu", "--quiet"])
+    _run_cli(["--init", "sedov", "-n", "10", "-s", "2", "-w", "2", "-o", half, "--device", "cpu", "--quiet"])
+    sim = Simulation(half, device="cpu")
+    sim.run(2)
+    rd = H5PartReader()
+    rd.set_step(full, -1, collective=False)
+    ref = {f: rd.read_field(f, "d") for f in ("x", "y", "z", "temp", "vx", "h")}
+    it = int(np.asarray(rd.step_attributes()["iteration"]).ravel()[0])
+    rd.close_step()
+    assert sim.d.iteration - 1 == it == 4
+    o_ref = np.lexsort((ref["z"], ref["y"], ref["x"]))
+    got = {f: sim.local(f).double().numpy() for f in ref}
+    o_got = np.lexsort((got["z"], got["y"], got["x"]))
+    for f in ref:
+        a, b = got[f][o_got], ref[f][o_ref]
+        assert np.abs(a - b).max() <= 1e-6 * max(np.abs(b).max(), 1e-30), f
