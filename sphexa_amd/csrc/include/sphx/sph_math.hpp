@@ -1026,8 +1026,10 @@ SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const G& box, const Idx* nbr, i
         HT dist    = r2 * invDist;
         HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
         HT rv   = rx * vxij + ry * vyij + rz * vzij;
-        HT vsij = HT(0);
-        if (rv < HT(0)) { vsij = ci + pj.c - HT(3) * rv * invDist; }
+        // branch-free: a branch here lets the compiler sink the load of pj.c into it, behind a full vmcnt(0) that
+        // serializes the batched gathers (AV 36 % slower than IAD before, profiles/r2_perf_log.md)
+        HT vst  = ci + pj.c - HT(3) * rv * invDist;
+        HT vsij = rv < HT(0) ? vst : HT(0);
         vsig   = smax(vsig, vsij);
         HT W   = HT(K) * hInv3 * kf.w(dist * hInv);
         HT tA0 = -(c11 * rx + c12 * ry + c13 * rz) * W;
@@ -1090,8 +1092,10 @@ SPHX_HD HT avSwitchesVJLoop(unsigned i, double K, const G& box, const Idx* nbr, 
         HT dist    = r2 * invDist;
         HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
         HT rv   = rx * vxij + ry * vyij + rz * vzij;
-        HT vsij = HT(0);
-        if (rv < HT(0)) { vsij = ci + pj.c - HT(3) * rv * invDist; }
+        // branch-free: a branch here lets the compiler sink the load of pj.c into it, behind a full vmcnt(0) that
+        // serializes the batched gathers (AV 36 % slower than IAD before, profiles/r2_perf_log.md)
+        HT vst  = ci + pj.c - HT(3) * rv * invDist;
+        HT vsij = rv < HT(0) ? vst : HT(0);
         vsig  = smax(vsig, vsij);
         HT wd = kf.w(dist * hInv) * pj.vd;
         T[0] += wd * rx;
