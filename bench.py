@@ -136,6 +136,13 @@ def main():
             if hasattr(d, "nc_rounds") and d.nc_rounds > 0:
                 print(f"# neighbor search: {d.nc_rounds:.2f} rounds and {d.nc_leaves:.1f} candidate leaves per "
                       f"64-particle group (last step), {getattr(d, 'nc_spilled', 0)} spilled groups", file=sys.stderr)
+            for k, v in prop.timer.mem_peak.items():
+                print(f"# memory peak in {k:28s} {v / max(d.numParticlesGlobal / size, 1):8.0f} B/particle",
+                      file=sys.stderr)
+            nl = getattr(prop, "nl", None)
+            if nl is not None and nl.grouped and nl.nidx is not None:
+                print(f"# neighbor lists: {nl.nidx.numel() * 4 / max(nl.last - nl.first, 1):.0f} B/particle "
+                      f"(packed rows used {nl.rows_used}, pool plan {nl.plan})", file=sys.stderr)
             if prop.gravity is not None and prop.gravity.stats:
                 print(f"# gravity stats {prop.gravity.stats}", file=sys.stderr)
             if device.type == "cuda":

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Census of the device memory a test case holds between steps: particle fields, neighbor lists, record workspaces,
+tree and scratch, in bytes per particle (memory item of the round-2 plan).
+
+  python scripts/mem_census.py --init sedov -n 200 --steps 2
+"""
+
+import argparse
+import gc
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--init", default="sedov")
+    ap.add_argument("-n", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=2)
+    args = ap.parse_args()
+    from sphexa_amd.app.simulation import Simulation
+    from sphexa_amd.parallel.comm import init_distributed
+
+    comm = init_distributed("nccl")
+    sim = Simulation(args.init, n=args.n, prop="ve", device=torch.device("cuda", 0), comm=comm, out=None, quiet=True)
+    for _ in range(args.steps):
+        sim.step()
+    torch.cuda.synchronize()
+    n = sim.d.numParticlesGlobal
+    d = sim.d
+    names = {}
+    for f, t in d._buf.items():
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            names[t.untyped_storage().data_ptr()] = f"field {f} ({'active' if d._state.get(f) else 'released'})"
+    for attr, v in vars(d).items():
+        if isinstance(v, torch.Tensor) and v.is_cuda:
+            names.setdefault(v.untyped_storage().data_ptr(), f"d.{attr}")
+    nl = getattr(sim.propagator, "nl", None)
+    if nl is not None and nl.nidx is not None and nl.nidx.is_cuda:
+        names[nl.nidx.untyped_storage().data_ptr()] = "neighbor lists"
+    seen = {}
+    for o in gc.get_objects():
+        try:
+            if isinstance(o, torch.Tensor) and o.is_cuda:
+                st = o.untyped_storage()
+                seen[st.data_ptr()] = (st.nbytes(), tuple(o.shape), o.dtype)
+        except Exception:
+            pass
+    total = sum(v[0] for v in seen.values())
+    print(f"{args.init} -n {args.n}: {n} particles; live tensors {total / 2**30:.2f} GiB ({total / n:.0f} B/particle); "
+          f"allocator: allocated {torch.cuda.memory_allocated() / 2**30:.2f} GiB, peak "
+          f"{torch.cuda.max_memory_allocated() / 2**30:.2f} GiB ({torch.cuda.max_memory_allocated() / n:.0f} B/particle)")
+    rows = sorted(seen.items(), key=lambda kv: -kv[1][0])
+    for ptr, (nb, shape, dt) in rows[:40]:
+        print(f"{nb / n:8.1f} B/p  {nb / 2**20:10.1f} MiB  {str(dt):14s} {str(shape):22s} {names.get(ptr, '')}")
+
+
+if __name__ == "__main__":
+    main()

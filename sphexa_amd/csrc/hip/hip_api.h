@@ -94,11 +94,13 @@ struct XmFuse
     KernelFn kf;
 };
 // stats: [0] h-iteration failures, [1] groups overflowing even the spill storage, [2] spilled groups
-size_t neighborScratchBytes(int64_t n);
+size_t neighborScratchBytes(int64_t n, unsigned ngmax);
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
-                   const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int32_t* nc,
-                   int iterateH, unsigned long long* stats, void* scratch, int testFrontCap, const XmFuse& xf,
-                   hipStream_t s);
+                   const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int home,
+                   int ovStride, int32_t* nc, int iterateH, unsigned long long* stats, void* scratch,
+                   int testFrontCap, const XmFuse& xf, hipStream_t s);
+//! overflow-row stripes of the packed-list pool; stats must hold 8 + 32 * stripes counters
+int neighborRowStripes();
 
 // hydro.hip
 struct MomFields

@@ -7,8 +7,9 @@
  *   * every neighbor loop first packs the source fields it needs into a 16-byte aligned array of records (one
  *     streaming pass), so a neighbor costs 2-8 dwordx4 loads of one contiguous 32-128 B record instead of up to 21
  *     scattered 4/8-byte gathers;
- *   * neighbor lists come from the wave64 search in 4-entry blocks per lane (kBlockedList), so the indices of four
- *     steps are one coalesced 1 KiB load per wave;
+ *   * neighbor lists come from the wave64 search as 16-bit delta-coded rows per 64-particle group (packed_list.hpp,
+ *     ~190 B/particle instead of 608 for int32 at the ngmax stride), so the indices of eight steps are one coalesced
+ *     1 KiB load per wave;
  *   * blocks are remapped so each XCD walks a contiguous SFC range of target groups (shared neighbors stay in that
  *     XCD's L2);
  *   * IAD and the velocity divergence/curl run in one kernel (c_ij of the target is all divv needs).
@@ -25,22 +26,29 @@ namespace sphx::hip
 
 constexpr int kBlock = 256;
 
-/*! @brief target of this thread and its neighbor list. Threads past the last target stay alive with an empty list
- *         and a clamped index (the cooperative gathers need all 64 lanes of a wave); they store nothing.
+/*! @brief target of this thread and its neighbor list (packed rows of its 64-particle group, packed_list.hpp).
+ *         Threads past the last target stay alive with an empty list and a clamped index (the cooperative gathers
+ *         need all 64 lanes of a wave); they store nothing. `n` is the neighbor count (excluding self, capped).
  */
-__device__ __forceinline__ bool targetOf(const NbrArgs& a, int64_t& i, const int32_t*& nbr, unsigned& n)
+__device__ __forceinline__ bool targetOf(const NbrArgs& a, int64_t& i, PackedLane& pl, unsigned& n)
 {
-    unsigned lb = xcdRemap(blockIdx.x, gridDim.x);
-    int64_t t   = int64_t(lb) * kBlock + threadIdx.x;
-    i           = a.first + t;
-    int64_t g   = t >> 6;
-    nbr         = a.nidx + g * int64_t((a.ngmax + 3) & ~3u) * 64 + (t & 63) * 4; // kBlockedList layout
+    unsigned lb     = xcdRemap(blockIdx.x, gridDim.x);
+    int64_t t       = int64_t(lb) * kBlock + threadIdx.x;
+    i               = a.first + t;
+    const int64_t g = t >> 6;
+    const int64_t G = (a.last - a.first + 63) / 64;
+    pl.tab  = a.nidx + g * int64_t(packedTableInts(a.ngmax));
+    pl.rows = reinterpret_cast<const int4*>(a.nidx + packedTableRegion(G, a.ngmax)) + (t & 63);
+    // wave-uniform: waves past the last group have no table
+    pl.nblk = g < G ? unsigned(*(const __attribute__((address_space(4))) int32_t*)(pl.tab)) : 0u;
     if (i >= a.last)
     {
-        i = a.last - 1;
-        n = 0;
+        i       = a.last - 1;
+        pl.self = unsigned(i);
+        n       = 0;
         return false;
     }
+    pl.self = unsigned(i);
     int cnt = a.nc[i] - 1;
     n       = unsigned(cnt < 0 ? 0 : (unsigned(cnt) < a.ngmax ? cnt : a.ngmax));
     return true;
@@ -304,10 +312,10 @@ __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, B
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcPos>::S];
     int64_t i;
-    const int32_t* nbr;
+    PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, nbr, n);
-    float v = xmassJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], coopOf(rec, tile, i, a),
+    const bool valid = targetOf(a, i, pl, n);
+    float v = xmassJLoop(unsigned(i), sc.K, box, &pl, 0, n, h[i], coopOf(rec, tile, i, a),
                          KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice});
     if (valid) xm[i] = v;
 }
@@ -319,15 +327,15 @@ __global__ __launch_bounds__(kBlock) void xmassQKernel(NbrArgs a, SphConsts sc, 
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcPosQ>::S];
     int64_t i;
-    const int32_t* nbr;
+    PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, nbr, n);
+    const bool valid = targetOf(a, i, pl, n);
     const auto ld    = coopOf(rec, tile, i, a);
     const KernelFn kf{wh, nullptr, sc.sincIndex, sc.kernelChoice};
     const SrcPosQ pi = ld(unsigned(i));
     const float hi = h[i], hInv = 1.f / hi, h3Inv = hInv * hInv * hInv;
     float rho0 = pi.m;
-    forEachNeighbor<SPHX_BATCH_POS>(nbr, kBlockedList, n, ld, [&](unsigned, const SrcPosQ& pj) {
+    forEachNeighbor<SPHX_BATCH_POS>(&pl, 0, n, ld, [&](unsigned, const SrcPosQ& pj) {
         const float rx   = float(int32_t(pi.x - pj.x)) * q.inv[0];
         const float ry   = float(int32_t(pi.y - pj.y)) * q.inv[1];
         const float rz   = float(int32_t(pi.z - pj.z)) * q.inv[2];
@@ -346,11 +354,11 @@ __global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts 
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
-    const int32_t* nbr;
+    PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, nbr, n);
+    const bool valid = targetOf(a, i, pl, n);
     float k, g;
-    veDefGradhJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], coopOf(rec, tile, i, a),
+    veDefGradhJLoop(unsigned(i), sc.K, box, &pl, 0, n, h[i], coopOf(rec, tile, i, a),
                     KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice}, k, g, mUniform);
     if (!valid) return;
     kx[i]    = k;
@@ -418,11 +426,11 @@ __global__ __launch_bounds__(kBlock) void iadKernel(NbrArgs a, SphConsts sc, Box
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcIad>::S];
     int64_t i;
-    const int32_t* nbr;
+    PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, nbr, n);
+    const bool valid = targetOf(a, i, pl, n);
     float c[6];
-    iadJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], coopOf(rec, tile, i, a),
+    iadJLoop(unsigned(i), sc.K, box, &pl, 0, n, h[i], coopOf(rec, tile, i, a),
              KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c);
     if (!valid) return;
     for (int k = 0; k < 6; ++k)
@@ -441,11 +449,11 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConst
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
-    const int32_t* nbr;
+    PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, nbr, n);
+    const bool valid = targetOf(a, i, pl, n);
     float c[6], g[6], dvi, cvi, S[3];
-    iadDivvCurlvJLoop<kAvS>(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], kx[i], coopOf(rec, tile, i, a),
+    iadDivvCurlvJLoop<kAvS>(unsigned(i), sc.K, box, &pl, 0, n, h[i], kx[i], coopOf(rec, tile, i, a),
                             KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, g, S);
     if (!valid) return;
     for (int k = 0; k < 6; ++k)
@@ -466,11 +474,11 @@ __global__ __launch_bounds__(kBlock) void avSwitchesKernel(NbrArgs a, SphConsts 
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcIad>::S];
     int64_t i;
-    const int32_t* nbr;
+    PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, nbr, n);
+    const bool valid = targetOf(a, i, pl, n);
     float ci[6] = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
-    float al    = avSwitchesJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, h[i], ci, coopOf(rec, tile, i, a),
+    float al    = avSwitchesJLoop(unsigned(i), sc.K, box, &pl, 0, n, h[i], ci, coopOf(rec, tile, i, a),
                                   KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt, sc.alphamin, sc.alphamax,
                                   sc.decayConstant, alpha[i]);
     if (valid) alpha[i] = al;
@@ -485,11 +493,11 @@ __global__ __launch_bounds__(kBlock) void avSwitchesQKernel(NbrArgs a, SphConsts
                                                             float* __restrict__ alpha)
 {
     int64_t i;
-    const int32_t* nbr;
+    PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, nbr, n);
+    const bool valid = targetOf(a, i, pl, n);
     float ci[6] = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
-    float al    = avSwitchesJLoop(unsigned(i), sc.K, q, nbr, kBlockedList, n, h[i], ci, AvQLoader{rec, divv},
+    float al    = avSwitchesJLoop(unsigned(i), sc.K, q, &pl, 0, n, h[i], ci, AvQLoader{rec, divv},
                                   KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt, sc.alphamin, sc.alphamax,
                                   sc.decayConstant, alpha[i]);
     if (valid) alpha[i] = al;
@@ -506,13 +514,13 @@ __global__ __launch_bounds__(kBlock) void avSwitchesVKernel(NbrArgs a, SphConsts
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcAvV>::S];
     int64_t i;
-    const int32_t* nbr;
+    PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, nbr, n);
+    const bool valid = targetOf(a, i, pl, n);
     float ci[6]    = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
     const float4 s = avS[i - a.first];
     const float S[3] = {s.x, s.y, s.z};
-    float al = avSwitchesVJLoop(unsigned(i), sc.K, q, nbr, kBlockedList, n, h[i], ci, divv[i], S,
+    float al = avSwitchesVJLoop(unsigned(i), sc.K, q, &pl, 0, n, h[i], ci, divv[i], S,
                                 coopOf(rec, tile, i, a), KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt,
                                 sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
     if (valid) alpha[i] = al;
@@ -547,23 +555,20 @@ struct GradVLoader
 };
 
 template<bool avClean, class R, class G>
-__global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphConsts sc, G box,
-                                                                 const R* __restrict__ rec,
-                                                                 const SrcGradV* __restrict__ gv,
-                                                                 const float* __restrict__ wh,
-                                                                 float* __restrict__ ax, float* __restrict__ ay,
-                                                                 float* __restrict__ az, double* __restrict__ du,
-                                                                 float* __restrict__ minDt)
+__device__ __forceinline__ void momentumEnergyVeBody(const NbrArgs& a, const SphConsts& sc, const G& box,
+                                                     const R* __restrict__ rec, const SrcGradV* __restrict__ gv,
+                                                     const float* __restrict__ wh, float* __restrict__ ax,
+                                                     float* __restrict__ ay, float* __restrict__ az,
+                                                     double* __restrict__ du, float* __restrict__ minDt, float4* tile)
 {
-    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
-    const int32_t* nbr;
+    PackedLane pl;
     unsigned n;
-    bool valid = targetOf(a, i, nbr, n);
+    bool valid = targetOf(a, i, pl, n);
     float dti  = FLT_MAX;
     float mvs, axi, ayi, azi;
     double dui;
-    momentumEnergyJLoop<avClean>(unsigned(i), sc, box, nbr, kBlockedList, n, coopOf(rec, tile, i, a), GradVLoader{gv},
+    momentumEnergyJLoop<avClean>(unsigned(i), sc, box, &pl, 0, n, coopOf(rec, tile, i, a), GradVLoader{gv},
                                  KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui, mvs);
     if (valid)
     {
@@ -577,6 +582,30 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphC
     reduceMinDt(dti, minDt);
 }
 
+template<bool avClean, class R, class G>
+__global__ __launch_bounds__(kBlock) void momentumEnergyVeKernel(NbrArgs a, SphConsts sc, G box,
+                                                                 const R* __restrict__ rec,
+                                                                 const SrcGradV* __restrict__ gv,
+                                                                 const float* __restrict__ wh,
+                                                                 float* __restrict__ ax, float* __restrict__ ay,
+                                                                 float* __restrict__ az, double* __restrict__ du,
+                                                                 float* __restrict__ minDt)
+{
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
+    momentumEnergyVeBody<avClean>(a, sc, box, rec, gv, wh, ax, ay, az, du, minDt, tile);
+}
+
+//! @brief the production instance (fixed-point records, no AV cleaning) held at 4 waves per SIMD (128 VGPRs, no
+//!        spills; the packed-list decoding would otherwise push it to 138 VGPRs and 3 waves)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void momentumEnergyVeQKernel(
+    NbrArgs a, SphConsts sc, QFrame box, const SrcMomQ* __restrict__ rec, const float* __restrict__ wh,
+    float* __restrict__ ax, float* __restrict__ ay, float* __restrict__ az, double* __restrict__ du,
+    float* __restrict__ minDt)
+{
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcMomQ>::S];
+    momentumEnergyVeBody<false>(a, sc, box, rec, nullptr, wh, ax, ay, az, du, minDt, tile);
+}
+
 __global__ __launch_bounds__(kBlock) void momentumEnergyStdKernel(NbrArgs a, SphConsts sc, Box box,
                                                                   const SrcStd* __restrict__ rec,
                                                                   const float* __restrict__ wh,
@@ -586,13 +615,13 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyStdKernel(NbrArgs a, Sph
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcStd>::S];
     int64_t i;
-    const int32_t* nbr;
+    PackedLane pl;
     unsigned n;
-    bool valid = targetOf(a, i, nbr, n);
+    bool valid = targetOf(a, i, pl, n);
     float dti  = FLT_MAX;
     float mvs, axi, ayi, azi;
     double dui;
-    momentumEnergyStdJLoop(unsigned(i), sc.K, box, nbr, kBlockedList, n, coopOf(rec, tile, i, a),
+    momentumEnergyStdJLoop(unsigned(i), sc.K, box, &pl, 0, n, coopOf(rec, tile, i, a),
                            KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui, mvs);
     if (valid)
     {
@@ -869,8 +898,8 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
             momentumEnergyVeKernel<true>
                 <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, (const SrcMomQ*)rec, gv, wh, ax, ay, az, du, minDt);
         else
-            momentumEnergyVeKernel<false>
-                <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, (const SrcMomQ*)rec, nullptr, wh, ax, ay, az, du, minDt);
+            momentumEnergyVeQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, (const SrcMomQ*)rec, wh, ax,
+                                                              ay, az, du, minDt);
     }
     SPHX_LAUNCH_CHECK();
 }

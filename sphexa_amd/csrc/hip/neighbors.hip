@@ -16,11 +16,17 @@
  *      fp64 with the reference's minimum-image formula, so the neighbor sets equal the fp64 CPU search exactly
  *   4. lanes whose count is out of [ng0/4, ngmax+1] update h and the wave repeats
  *
- * List storage (sphx::kBlockedList): a lane's entries 4b..4b+3 form one int4 at nidx + g*ngmax4*64 + 256 b + 4 lane,
- * so step k of a pair loop reads one coalesced 1 KiB block per four steps. Hits go to a per-lane ring of 8 slots in
- * LDS; whenever some lane's ring is full, every lane holding >= 4 pending entries writes one block (dwordx4): the
- * wave issues a few dozen list stores per group instead of one partially masked store per candidate source (the
- * search was bound by those stores in the texture data path).
+ * Lists: hits go to a per-lane ring of 16 slots in LDS; whenever some lane's ring is nearly full, every lane holding
+ * >= 4 pending entries writes one int4 block of raw indices to the wave's scratch slot (the wave issues a few dozen
+ * list stores per group instead of one partially masked store per candidate source: the search was bound by those
+ * stores in the texture data path). After the last h-iteration round the group's raw lists are encoded into packed
+ * rows (sphx/packed_list.hpp: 16-bit delta slots, ~190 B/particle instead of 608 for int32 at the ngmax stride).
+ * The search runs in chunks of 16384 groups alternating between two streams; every group has its own raw-list slot
+ * in its chunk's buffer and encodes it after its last round, so raw lists exist for two chunks only. Measured on Sedov -n 400 (search alone, profiles/r2_perf_log.md): encoding
+ * inside the candidate loop 57 ms vs 35 (the flush code grew the hot loop past the compiler's unroll threshold and
+ * register budget); one pool counter for all groups 145 ms (12 M atomics on one address); per-group scratch slots
+ * guarded by lock words 88 ms (a device-scope CAS + release per group); persistent waves with private slots 79 ms;
+ * chunks with a separate encode kernel 44 ms.
  *
  * Optional fused XMass (XmFuse, the reference computes rho0 inside its traversal, xmass_gpu.cu:54-101): the ring also
  * keeps each hit's squared distance and the flushing lanes sum m_j w(r_ij/h_i) over their block. Measured on MI355X
@@ -32,6 +38,7 @@
 #include "common.h"
 #include "hip_api.h"
 #include "sphx/box.hpp"
+#include "sphx/packed_list.hpp"
 #include "sphx/sph_math.hpp"
 
 namespace sphx::hip
@@ -93,6 +100,143 @@ __device__ __forceinline__ int32_t ldList(const int32_t* p)
     else { return *p; }
 }
 
+//! overflow-row stripes (one allocation counter each, 256 B apart)
+constexpr int kRowStripes = 64;
+//! target groups per search chunk (raw lists of two chunks in flight: 2 x 16384 x 38 KB at ngmax 150)
+#ifndef SPHX_NS_CHUNK
+#define SPHX_NS_CHUNK 16384
+#endif
+constexpr int64_t kChunkGroups = SPHX_NS_CHUNK;
+
+/*! @brief packed-list output of the search (packed_list.hpp). Rows of group g: its `home` rows g*home.. (no atomics),
+ *         then overflow rows from stripe g % kRowStripes (counter ctr[32 s], rows ovBase + s*ovStride ..). A group
+ *         allocating past its stripe gets no rows; the host sees the counter and repeats the search with more.
+ */
+struct PackedOut
+{
+    int32_t* tab;                // group tables
+    int4* rows;                  // row 0
+    unsigned rowsMax;            // rows a group may use
+    unsigned tabInts;            // ints per group table
+    unsigned home;               // home rows per group
+    unsigned ovStride;           // rows per overflow stripe
+    unsigned long long ovBase;   // first overflow row (groups * home)
+    unsigned long long poolRows; // rows in the buffer
+    unsigned long long* ctr;     // stripe counters
+};
+
+/*! @brief encode the final raw lists of one group (int4 blocks of 4 indices per lane at raw[64 b]) into packed rows
+ *         and write its table. The wave walks the raw blocks in step (three prefetched ahead: the reads are latency
+ *         bound otherwise); each lane shifts the slots of its 4 entries into a 4-VGPR block accumulator and stores
+ *         every completed block. Rows are taken as blocks complete: home rows without atomics, then the stripe.
+ */
+__device__ void encodeGroup(int64_t g, unsigned self, unsigned cnt, const int4* __restrict__ raw, const PackedOut& po,
+                            unsigned long long* __restrict__ stats)
+{
+    const unsigned lane = threadIdx.x & 63;
+    unsigned rowReg = 0, nAlloc = 0;
+    // rows for list blocks < need (per lane) exist afterwards; called by the whole wave
+    auto ensureRows = [&](unsigned need)
+    {
+        need = min(need, po.rowsMax);
+        if (ballot(need > nAlloc))
+        {
+            const unsigned m = unsigned(__builtin_amdgcn_readfirstlane(waveMax(int(need))));
+            if (lane >= nAlloc && lane < min(m, po.home)) rowReg = unsigned(g) * po.home + lane;
+            const unsigned from = max(nAlloc, po.home);
+            if (m > from)
+            {
+                const unsigned stripe = unsigned(g) & (kRowStripes - 1);
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(po.ctr + 32 * stripe, (unsigned long long)(m - from));
+                const unsigned k0 = unsigned(__builtin_amdgcn_readfirstlane(int(unsigned(base)))) + (lane - from);
+                if (lane >= from && lane < m)
+                    rowReg = k0 < po.ovStride ? unsigned(po.ovBase) + stripe * po.ovStride + k0 : 0xFFFFFFFFu;
+            }
+            nAlloc = m;
+        }
+    };
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    unsigned ns = 0, fb = 0, nst = 0, rowA = 0, rowB = 0;
+    bool ovf = false;
+    auto put = [&](unsigned slot)
+    {
+        a0 = __builtin_amdgcn_alignbit(a1, a0, 16);
+        a1 = __builtin_amdgcn_alignbit(a2, a1, 16);
+        a2 = __builtin_amdgcn_alignbit(a3, a2, 16);
+        a3 = (a3 >> 16) | (slot << 16);
+        if (++ns == 8)
+        {
+            const unsigned r = nst == 0 ? rowA : rowB;
+            if (nst < 2 && fb < po.rowsMax)
+            {
+                if (r < po.poolRows) po.rows[size_t(r) * 64 + lane] = make_int4(int(a0), int(a1), int(a2), int(a3));
+            }
+            else ovf = true;
+            ++nst;
+            ++fb;
+            ns = 0;
+        }
+    };
+    const unsigned nb    = (cnt + 3) >> 2;
+    const unsigned nbMax = unsigned(__builtin_amdgcn_readfirstlane(waveMax(int(nb))));
+    // (explicit branches: a ?: over two int4 lvalues becomes a pointer select, i.e. a stack copy of the zero)
+    int4 q0 = make_int4(0, 0, 0, 0), q1 = q0, q2 = q0;
+    if (nb > 0) q0 = raw[0];
+    if (nb > 1) q1 = raw[64];
+    if (nb > 2) q2 = raw[128];
+    unsigned prev = self;
+    for (unsigned kb = 0; kb < nbMax; ++kb)
+    {
+        const int4 cur = q0;
+        q0             = q1;
+        q1             = q2;
+        if (kb + 3 < nb) q2 = raw[size_t(kb + 3) * 64];
+        const unsigned m = kb < nb ? min(4u, cnt - 4 * kb) : 0u;
+        const unsigned e[4] = {unsigned(cur.x), unsigned(cur.y), unsigned(cur.z), unsigned(cur.w)};
+        unsigned slots = 0, pv = prev;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+        {
+            if (unsigned(u) < m)
+            {
+                slots += slotsFor(int(e[u] - pv));
+                pv = e[u];
+            }
+        }
+        ensureRows(fb + ((ns + slots) >> 3));
+        rowA = unsigned(__shfl(int(rowReg), int(min(fb, 63u))));
+        rowB = unsigned(__shfl(int(rowReg), int(min(fb + 1, 63u))));
+        nst  = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+        {
+            if (unsigned(u) < m)
+            {
+                encodeStep(int(e[u] - prev), put);
+                prev = e[u];
+            }
+        }
+    }
+    // pad the partial block with no-op slots, then give every lane the group's row count (zero blocks)
+    ensureRows(ns > 0 ? fb + 1 : 0u);
+    rowA = unsigned(__shfl(int(rowReg), int(min(fb, 63u))));
+    nst  = 0;
+    while (ns != 0)
+        put(0u);
+    const unsigned nRows = min(unsigned(__builtin_amdgcn_readfirstlane(waveMax(int(fb)))), po.rowsMax);
+    for (unsigned b = 0; b < nRows; ++b)
+    {
+        const unsigned r = unsigned(__builtin_amdgcn_readlane(int(rowReg), int(b)));
+        if (b >= fb && r < po.poolRows) po.rows[size_t(r) * 64 + lane] = make_int4(0, 0, 0, 0);
+    }
+    int32_t* tab = po.tab + g * int64_t(po.tabInts);
+    if (lane == 0) tab[0] = int32_t(nRows);
+    if (lane + 1 < po.tabInts) tab[1 + lane] = lane < nAlloc && rowReg < po.poolRows ? int32_t(rowReg) : 0;
+    const uint64_t bad = ballot(ovf);
+    if (lane == 0 && bad) atomicAdd(&stats[5], (unsigned long long)__popcll(bad));
+}
+
 struct TreeView
 {
     const int32_t* __restrict__ child;
@@ -110,7 +254,8 @@ template<bool kSpill, bool kXm>
 __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t last, const double* __restrict__ x,
                                             const double* __restrict__ y, const double* __restrict__ z,
                                             float* __restrict__ h, const NsTree& tree, const Box& box, unsigned ng0,
-                                            unsigned ngmax, int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
+                                            unsigned ngmax, int32_t* __restrict__ rawSlot, const PackedOut& po,
+                                            int32_t* __restrict__ nc,
                                             int iterateH, unsigned long long* __restrict__ stats, int32_t* frontA,
                                             int32_t* frontB, int32_t* leaves, int frontCap, int leafCap,
                                             int32_t* work, const XmFuse& xf)
@@ -129,8 +274,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         zi = z[i];
         hi = h[i];
     }
-    const unsigned ngmax4 = (ngmax + 3) & ~3u;
-    int4* nlist           = reinterpret_cast<int4*>(nidx + g * int64_t(ngmax4) * 64) + lane;
+    int4* nlist = reinterpret_cast<int4*>(rawSlot) + lane; // the wave's raw-list scratch slot
     // hit ring and staging ring alias the frontiers (fast path): they are only live in the candidate phase
     constexpr int kRing    = ringSlots<kXm>();
     constexpr int kRingPad = ringStride<kXm>() - 1;
@@ -374,6 +518,10 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         if (repeat) hi = sphx::updateH<float>(ng0, ncSph, hi);
     }
 
+    // packed rows from the raw lists of the final round (the wave's own raw slot: no other wave touches it)
+#ifndef SPHX_NS_NOENCODE // timing experiments only (no usable lists)
+    encodeGroup(g, unsigned(valid ? i : first), valid ? min(ncSph - 1, ngmax) : 0u, nlist, po, stats);
+#endif
     if (lane == 0 && round >= 10) atomicAdd(&stats[0], 1ull);
     if (lane == 0 && (iterateH & 2)) // statistics (opt-in): search rounds and candidate leaves, summed over groups
     {
@@ -395,32 +543,33 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     return true;
 }
 
-//! fast path: frontier and leaf list in LDS; overflowing groups are queued for the spill kernel
+//! fast path: frontier and leaf list in LDS; overflowing groups are queued for the spill kernel. One launch per chunk
+//! of groups [g0, g0 + gCount); group g keeps its raw lists in slot g - g0 of the chunk's scratch
 template<bool kXm>
 __global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_t last, const double* __restrict__ x,
                                                            const double* __restrict__ y,
                                                            const double* __restrict__ z, float* __restrict__ h,
                                                            NsTree t, Box box, unsigned ng0, unsigned ngmax,
-                                                           int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
+                                                           int64_t g0, int64_t gCount, int32_t* __restrict__ raw,
+                                                           int64_t slotInts, PackedOut po, int32_t* __restrict__ nc,
                                                            int iterateH, unsigned long long* __restrict__ stats,
                                                            int32_t* __restrict__ spillList, int frontCap, XmFuse xf)
 {
     __shared__ __attribute__((aligned(16))) int32_t work[kWavesPerBlock][workWords<kXm>()];
     __shared__ int32_t leaves[kWavesPerBlock][kLeafCap];
 
-    const int wave          = threadIdx.x >> 6;
-    const int64_t numGroups = (last - first + 63) / 64;
-    const unsigned lb       = xcdRemap(blockIdx.x, gridDim.x);
-    const int64_t g         = int64_t(lb) * kWavesPerBlock + wave;
-    if (g >= numGroups) return;
-
-    bool ok = searchGroup<false, kXm>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
-                                      work[wave], work[wave] + kFrontCap, leaves[wave], frontCap, kLeafCap, work[wave],
-                                      xf);
+    const int wave     = threadIdx.x >> 6;
+    const unsigned lb  = xcdRemap(blockIdx.x, gridDim.x);
+    const int64_t gl   = int64_t(lb) * kWavesPerBlock + wave;
+    if (gl >= gCount) return;
+    const int64_t g = g0 + gl;
+    bool ok = searchGroup<false, kXm>(g, first, last, x, y, z, h, t, box, ng0, ngmax, raw + gl * slotInts, po, nc,
+                                      iterateH, stats, work[wave], work[wave] + kFrontCap, leaves[wave], frontCap,
+                                      kLeafCap, work[wave], xf);
     if (!ok && (threadIdx.x & 63) == 0)
     {
-        unsigned long long slot = atomicAdd(&stats[2], 1ull);
-        spillList[slot] = int32_t(g);
+        unsigned long long k = atomicAdd(&stats[2], 1ull);
+        spillList[k] = int32_t(g);
     }
 }
 
@@ -437,7 +586,8 @@ __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, in
                                                                const double* __restrict__ y,
                                                                const double* __restrict__ z, float* __restrict__ h,
                                                                NsTree t, Box box, unsigned ng0, unsigned ngmax,
-                                                               int32_t* __restrict__ nidx, int32_t* __restrict__ nc,
+                                                               PackedOut po, int32_t* __restrict__ rawSpill,
+                                                               int64_t slotInts, int32_t* __restrict__ nc,
                                                                int iterateH, unsigned long long* __restrict__ stats,
                                                                const int32_t* __restrict__ spillList,
                                                                int32_t* __restrict__ scratch, XmFuse xf)
@@ -450,46 +600,109 @@ __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, in
     for (int64_t k = blockIdx.x; k < numSpill; k += gridDim.x)
     {
         int64_t g = spillList[k];
-        bool ok   = searchGroup<true, kXm>(g, first, last, x, y, z, h, t, box, ng0, ngmax, nidx, nc, iterateH, stats,
-                                           frontA, frontB, leaves, kSpillFront, kSpillLeaves, work, xf);
+        bool ok   = searchGroup<true, kXm>(g, first, last, x, y, z, h, t, box, ng0, ngmax,
+                                           rawSpill + int64_t(blockIdx.x) * slotInts, po, nc, iterateH, stats, frontA,
+                                           frontB, leaves, kSpillFront, kSpillLeaves, work, xf);
         if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
     }
 }
 
-size_t neighborScratchBytes(int64_t n)
+//! scratch layout (ints): spill list | spill frontiers | spill raw slots | raw lists of two chunks
+static void scratchLayout(int64_t n, unsigned ngmax, int64_t& spillMemOff, int64_t& spillRawOff, int64_t& rawOff,
+                          int64_t& chunkInts, int64_t& total, int64_t& slotInts)
 {
-    int64_t groups = (n + 63) / 64;
-    return size_t(groups) * sizeof(int32_t) + size_t(kSpillWaves) * (2 * kSpillFront + kSpillLeaves) * sizeof(int32_t);
+    const int64_t groups = (n + 63) / 64;
+    const int64_t chunk  = groups < kChunkGroups ? groups : kChunkGroups;
+    slotInts             = int64_t((ngmax + 3) & ~3u) * 64;
+    spillMemOff          = (groups + 63) / 64 * 64;
+    spillRawOff          = spillMemOff + int64_t(kSpillWaves) * (2 * kSpillFront + kSpillLeaves);
+    rawOff               = spillRawOff + int64_t(kSpillWaves) * slotInts;
+    chunkInts            = chunk * slotInts;
+    total                = rawOff + (groups > chunk ? 2 : 1) * chunkInts;
+}
+
+int neighborRowStripes() { return kRowStripes; }
+
+size_t neighborScratchBytes(int64_t n, unsigned ngmax)
+{
+    int64_t a, b, c, d, total, slotInts;
+    scratchLayout(n, ngmax, a, b, c, d, total, slotInts);
+    return size_t(total) * sizeof(int32_t);
 }
 
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
-                   const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int32_t* nc,
-                   int iterateH, unsigned long long* stats, void* scratch, int testFrontCap, const XmFuse& xf,
-                   hipStream_t s)
+                   const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int home,
+                   int ovStride, int32_t* nc, int iterateH, unsigned long long* stats, void* scratch,
+                   int testFrontCap, const XmFuse& xf, hipStream_t s)
 {
     int64_t n = last - first;
     if (n <= 0) return;
-    int64_t groups     = (n + 63) / 64;
+    int64_t groups = (n + 63) / 64;
+    if (packedTableInts(ngmax) > 64 || home < 0 || ovStride < 1)
+        throw std::invalid_argument("findNeighbors: ngmax too large for packed lists or bad row pool");
+    const unsigned long long ovBase = (unsigned long long)groups * home;
+    const PackedOut po{nidx,
+                       reinterpret_cast<int4*>(nidx + packedTableRegion(groups, ngmax)),
+                       packedRowsMax(ngmax),
+                       packedTableInts(ngmax),
+                       unsigned(home),
+                       unsigned(ovStride),
+                       ovBase,
+                       ovBase + (unsigned long long)kRowStripes * ovStride,
+                       stats + 8};
+    int64_t spillMemOff, spillRawOff, rawOff, chunkInts, total, slotInts;
+    scratchLayout(n, ngmax, spillMemOff, spillRawOff, rawOff, chunkInts, total, slotInts);
     int32_t* spillList = static_cast<int32_t*>(scratch);
-    int32_t* spillMem  = spillList + ((groups + 63) / 64) * 64;
-    unsigned grid      = unsigned((groups + kWavesPerBlock - 1) / kWavesPerBlock);
+    int32_t* spillMem  = spillList + spillMemOff;
+    int32_t* rawSpill  = spillList + spillRawOff;
     const int fc       = testFrontCap > 0 ? min(testFrontCap, kFrontCap) : kFrontCap;
+
+    // chunks alternate between s and a side stream, each with its own raw-list buffer: the two streams overlap each
+    // other's tails
+    static thread_local hipStream_t side = nullptr;
+    static thread_local hipEvent_t fork = nullptr, join = nullptr;
+    if (!side)
+    {
+        SPHX_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+        SPHX_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+        SPHX_CHECK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+    }
+    const int64_t chunk = groups < kChunkGroups ? groups : kChunkGroups;
+    const bool twoStreams = groups > chunk;
+    if (twoStreams)
+    {
+        SPHX_CHECK(hipEventRecord(fork, s));
+        SPHX_CHECK(hipStreamWaitEvent(side, fork, 0));
+    }
+    for (int64_t g0 = 0, c = 0; g0 < groups; g0 += chunk, ++c)
+    {
+        const int64_t gc    = groups - g0 < chunk ? groups - g0 : chunk;
+        hipStream_t st      = (c & 1) ? side : s;
+        int32_t* raw        = spillList + rawOff + (c & 1) * chunkInts;
+        const unsigned grid = unsigned((gc + kWavesPerBlock - 1) / kWavesPerBlock);
+        if (xf.xm)
+            findNeighborsKernel<true><<<grid, 64 * kWavesPerBlock, 0, st>>>(first, last, x, y, z, h, t, box, ng0,
+                                                                            ngmax, g0, gc, raw, slotInts, po, nc,
+                                                                            iterateH, stats, spillList, fc, xf);
+        else
+            findNeighborsKernel<false><<<grid, 64 * kWavesPerBlock, 0, st>>>(first, last, x, y, z, h, t, box, ng0,
+                                                                             ngmax, g0, gc, raw, slotInts, po, nc,
+                                                                             iterateH, stats, spillList, fc, xf);
+        SPHX_LAUNCH_CHECK();
+    }
+    if (twoStreams)
+    {
+        SPHX_CHECK(hipEventRecord(join, side));
+        SPHX_CHECK(hipStreamWaitEvent(s, join, 0));
+    }
     if (xf.xm)
-    {
-        findNeighborsKernel<true><<<grid, 64 * kWavesPerBlock, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax,
-                                                                       nidx, nc, iterateH, stats, spillList, fc, xf);
-        SPHX_LAUNCH_CHECK();
-        findNeighborsSpillKernel<true><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax, nidx,
-                                                                  nc, iterateH, stats, spillList, spillMem, xf);
-    }
+        findNeighborsSpillKernel<true><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax, po,
+                                                                  rawSpill, slotInts, nc, iterateH, stats, spillList,
+                                                                  spillMem, xf);
     else
-    {
-        findNeighborsKernel<false><<<grid, 64 * kWavesPerBlock, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax,
-                                                                        nidx, nc, iterateH, stats, spillList, fc, xf);
-        SPHX_LAUNCH_CHECK();
-        findNeighborsSpillKernel<false><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax,
-                                                                   nidx, nc, iterateH, stats, spillList, spillMem, xf);
-    }
+        findNeighborsSpillKernel<false><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax, po,
+                                                                   rawSpill, slotInts, nc, iterateH, stats,
+                                                                   spillList, spillMem, xf);
     SPHX_LAUNCH_CHECK();
 }
 

@@ -14,7 +14,7 @@
  * or two cache lines instead of up to 21 scattered 4-byte gathers. Fields that the reference derives per pair
  * (xm/kx, kx*m/xm) are packed already derived — bit-identical because the same fp32 operations are applied.
  * The neighbor list accessor is (nbr, stride): neighbor k is nbr[k*stride] with stride 1 on the CPU; on the GPU
- * (stride == kBlockedList) a lane's entries 4b..4b+3 are one int4 at nbr + 256 b (listAt).
+ * nbr is the lane's PackedLane (16-bit delta-coded lists in per-group rows, packed_list.hpp).
  */
 #pragma once
 
@@ -23,6 +23,7 @@
 
 #include "annotation.hpp"
 #include "box.hpp"
+#include "packed_list.hpp"
 
 namespace sphx
 {
@@ -630,35 +631,54 @@ struct CoopLoader
     __device__ __forceinline__ float4 own(int p) const { return tile[(threadIdx.x & 63) * S + p]; }
 };
 
-/*! @brief per-lane gather loop of the small records (any loader returning a record by value): one list block
- *         (4 indices) and its records in flight per step */
-template<class Idx, class Ld, class F>
-__device__ void forEachNeighborDirect(const Idx* nbr, int stride, unsigned nc, const Ld& ld, F&& f)
+/*! @brief keep a loaded record in registers at this point. The packed-list loops skip entries equal to the target
+ *         (jump/padding slots); a record whose fields are only used under that test would have its load sunk into
+ *         the branch behind a full vmcnt(0) wait, serializing the batched gathers (measured on the AV loop). */
+template<class T>
+__device__ __forceinline__ void pinRegs(T& v)
 {
-    // small records (cooperative path measured slower for 32 B): per-lane gathers, one list block (4 indices)
-    // and its records in flight (a deeper software pipeline measured slower: more VGPRs, same texture work)
-    // (B is ignored: the direct path always consumes one 4-entry list block per batch)
-    unsigned k = 0;
-    const int4* blk = reinterpret_cast<const int4*>(nbr);
-    int4 v = blk[0]; // next block prefetched while the current one is evaluated (A/B: beats per-step block
-                     // loads and per-entry index loads by 5 %)
-    for (; k + 4 <= nc; k += 4)
+    static_assert(sizeof(T) % 4 == 0, "records are whole dwords");
+    uint32_t w[sizeof(T) / 4];
+    __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+    for (unsigned k = 0; k < sizeof(T) / 4; ++k)
+        asm volatile("" : "+v"(w[k]));
+    __builtin_memcpy(&v, w, sizeof(T));
+}
+
+/*! @brief per-lane gather loop of the small records (any loader returning a record by value) over a packed list:
+ *         one list block (8 entries) decoded per row, its records gathered 4 at a time */
+template<class Ld, class F>
+__device__ void forEachNeighborDirect(const PackedLane& pl, const Ld& ld, F&& f)
+{
+    // small records (cooperative path measured slower for 32 B): per-lane gathers, four records in flight (a
+    // deeper software pipeline measured slower: more VGPRs, same texture work); the next list block is prefetched
+    const unsigned nblk = pl.nblk;
+    if (nblk == 0) return;
+    unsigned prev = pl.self;
+    int4 w        = pl.block(0);
+    auto batch    = [&](int w0, int w1)
     {
-        const int4 vn       = blk[size_t((k >> 2) + 1) * 64];
-        const unsigned j[4] = {unsigned(v.x), unsigned(v.y), unsigned(v.z), unsigned(v.w)};
-        v                   = vn;
+        unsigned j[4];
+        decodeWord(w0, prev, pl.self, j[0], j[1]);
+        decodeWord(w1, prev, pl.self, j[2], j[3]);
         decltype(ld(0u)) rr[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             rr[u] = ld(j[u]);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            f(j[u], rr[u]);
-    }
-    for (; k < nc; ++k)
+        {
+            pinRegs(rr[u]);
+            if (j[u] != pl.self) f(j[u], rr[u]);
+        }
+    };
+    for (unsigned b = 0; b < nblk; ++b)
     {
-        unsigned j = unsigned(listAt(nbr, stride, k));
-        f(j, ld(j));
+        const int4 wn = pl.block(b + 1);
+        batch(w.x, w.y);
+        batch(w.z, w.w);
+        w = wn;
     }
 }
 
@@ -690,31 +710,30 @@ struct AvQLoader
     }
 };
 
-template<int B, class Idx, class F>
-__device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const AvQLoader& ld, F&& f)
+template<int B, class F>
+__device__ void forEachNeighbor(const PackedLane* pl, int, unsigned, const AvQLoader& ld, F&& f)
 {
-    forEachNeighborDirect(nbr, stride, nc, ld, f);
+    forEachNeighborDirect(*pl, ld, f);
 }
 
-template<int B, class Idx, class R, class F>
-__device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const CoopLoader<R>& ld, F&& f)
+template<int B, class R, class F>
+__device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const CoopLoader<R>& ld, F&& f)
 {
     constexpr int C = CoopLoader<R>::C;
     constexpr bool direct = C < SPHX_COOP_MIN_CHUNKS;
+    const PackedLane& pl = *plp;
     if constexpr (direct)
     {
-        forEachNeighborDirect(nbr, stride, nc, ld, f);
+        forEachNeighborDirect(pl, ld, f);
         return;
     }
-    unsigned ncMax  = nc;
-    for (int o = 32; o > 0; o >>= 1)
-        ncMax = max(ncMax, unsigned(__shfl_xor(int(ncMax), o)));
-    ncMax = __builtin_amdgcn_readfirstlane(ncMax);
-    if (ncMax == 0) return;
-    // Neighbor indices come in 4-entry list blocks (one coalesced 1 KiB load per four steps, two blocks ahead), are
-    // spread to the chunk lanes with ds_bpermute two steps ahead, and the chunk data is gathered one step ahead of
-    // the evaluation. Unrolled by four with ping-pong buffers (A/B data, I1/I2 indices): no register rotation.
-    auto consume = [&](const float4 (&raw)[C], unsigned j, unsigned k)
+    const unsigned nblk = pl.nblk;
+    if (nblk == 0) return;
+    // Neighbor indices come in 8-entry packed list blocks (one coalesced 1 KiB load per eight steps, one block
+    // ahead), are spread to the chunk lanes with ds_bpermute two steps ahead, and the chunk data is gathered one
+    // step ahead of the evaluation. Unrolled by eight with ping-pong buffers (A/B data, I1/I2
+    // indices): no register rotation. Jump/padding slots decode to the target itself: gathered, not evaluated.
+    auto consume = [&](const float4 (&raw)[C], unsigned j)
     {
         float4 o[C];
 #pragma unroll
@@ -731,56 +750,56 @@ __device__ void forEachNeighbor(const Idx* nbr, int stride, unsigned nc, const C
             asm volatile("" : "+v"(o[p].x), "+v"(o[p].y), "+v"(o[p].z), "+v"(o[p].w));
 #endif
         const R rec = coopUnpack<R>(o);
-        if (k < nc) f(j, rec);
+        if (j != pl.self) f(j, rec);
     };
-    const int4* blk = reinterpret_cast<const int4*>(nbr); // block b at blk[64 b]
-    // entry e of a block for step k; entries past the lane's count are garbage: use the lane's own record
-    auto pick = [&](unsigned v, unsigned k) { return k < nc ? v : ld.self; };
-    int4 B0 = blk[0], B1 = blk[64];
+    unsigned prev = pl.self;
+    unsigned D[8];
+    decodeBlock(pl.block(0), prev, pl.self, D);
     unsigned I1[C], I2[C];
     float4 A[C], Bf[C];
-    {
-        const unsigned j0 = pick(unsigned(B0.x), 0), j1 = pick(unsigned(B0.y), 1);
 #pragma unroll
-        for (int q = 0; q < C; ++q)
-        {
-            A[q]  = ld.issue(ld.spread(j0, q), q);
-            I1[q] = ld.spread(j1, q);
-        }
+    for (int q = 0; q < C; ++q)
+    {
+        A[q]  = ld.issue(ld.spread(D[0], q), q);
+        I1[q] = ld.spread(D[1], q);
     }
-    for (unsigned k = 0; k < ncMax; k += 4)
+    for (unsigned b = 0; b < nblk; ++b)
     {
-        const int4 B2 = blk[size_t((k >> 2) + 2) * 64]; // list allocation carries two spare block rows
+        const int4 W = pl.block(b + 1); // past the list: row 0 (valid memory), entries replaced below
+        const bool more = b + 1 < nblk;
 #pragma unroll
-        for (int q = 0; q < C; ++q)
+        for (int u = 0; u < 8; u += 2)
         {
-            I2[q] = ld.spread(pick(unsigned(B0.z), k + 2), q);
-            Bf[q] = ld.issue(I1[q], q);
-        }
-        consume(A, pick(unsigned(B0.x), k), k);
+            unsigned jA, jB;
+            if (u < 6)
+            {
+                jA = D[u + 2];
+                jB = D[u + 3];
+            }
+            else
+            {
+                // steps 6, 7 spread the first two entries of the next block (the target's own record past the list)
+                unsigned p = prev;
+                decodeWord(W.x, p, pl.self, jA, jB);
+                jA = more ? jA : pl.self;
+                jB = more ? jB : pl.self;
+            }
 #pragma unroll
-        for (int q = 0; q < C; ++q)
-        {
-            I1[q] = ld.spread(pick(unsigned(B0.w), k + 3), q);
-            A[q]  = ld.issue(I2[q], q);
-        }
-        consume(Bf, pick(unsigned(B0.y), k + 1), k + 1);
+            for (int q = 0; q < C; ++q)
+            {
+                I2[q] = ld.spread(jA, q);
+                Bf[q] = ld.issue(I1[q], q);
+            }
+            consume(A, D[u]);
 #pragma unroll
-        for (int q = 0; q < C; ++q)
-        {
-            I2[q] = ld.spread(pick(unsigned(B1.x), k + 4), q);
-            Bf[q] = ld.issue(I1[q], q);
+            for (int q = 0; q < C; ++q)
+            {
+                I1[q] = ld.spread(jB, q);
+                A[q]  = ld.issue(I2[q], q);
+            }
+            consume(Bf, D[u + 1]);
         }
-        consume(A, pick(unsigned(B0.z), k + 2), k + 2);
-#pragma unroll
-        for (int q = 0; q < C; ++q)
-        {
-            I1[q] = ld.spread(pick(unsigned(B1.y), k + 5), q);
-            A[q]  = ld.issue(I2[q], q);
-        }
-        consume(Bf, pick(unsigned(B0.w), k + 3), k + 3);
-        B0 = B1;
-        B1 = B2;
+        decodeBlock(W, prev, pl.self, D);
     }
 }
 #endif

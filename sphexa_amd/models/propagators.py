@@ -53,6 +53,9 @@ class Propagator:
         self.timer.device = d.device
 
     def sync(self, domain, d):
+        # the pair loops' record workspaces are idle until the first loop after the search: releasing them lets the
+        # sync's transients (keys, sort, reorder batches) and the search reuse that memory (step high-water mark)
+        H.release_workspaces(d)
         domain.sync(d, self.conserved_fields(), self.dependent, gravity=d.g != 0.0)
 
     def step(self, domain, d):
@@ -76,7 +79,7 @@ class Propagator:
         first, last = domain.start_index(), domain.end_index()
         fuse = xmass_field is not None and d.device.type == "cuda" and FUSE_XMASS
         self.nl = find_neighbors(d, domain.octree, domain.box, first, last,
-                                 nidx=self.nl.nidx if self.nl is not None else None,
+                                 prev=self.nl,  # (not nidx=: an argument would pin the old GPU buffer)
                                  xmass_out=d[xmass_field] if fuse else None,
                                  m_uniform=H.uniform_mass(d) if fuse else 0.0)
         if d.device.type == "cuda":

@@ -46,14 +46,25 @@ def _is_gpu(d):
     return d.device.type == "cuda"
 
 
+def release_workspaces(d):
+    """drop the record workspaces (re-allocated by the next loop; the caching allocator hands the blocks back)"""
+    d._rec0 = None
+    d._rec1 = None
+
+
 def _rec(d, which: int = 0, loop: str = "mom"):
-    """per-dataset record workspace on the GPU (grow-only; particle count incl. halos times the record size)"""
+    """per-dataset record workspace on the GPU (grow-only within a step; particle count incl. halos times the record
+    size). Workspace 1 holds the AV loop's S_i (float4) or the AV-cleaning SrcGradV (32 B)."""
     name = "_rec%d" % which
-    per = REC_BYTES[loop][1 if getattr(d, "fixedPoint", 1) else 0] if which == 0 else 32
+    if which == 0:
+        per = REC_BYTES[loop][1 if getattr(d, "fixedPoint", 1) else 0]
+    else:
+        per = 32 if loop == "gradv" else 16
     need = d.size * per
     buf = getattr(d, name, None)
     if buf is None or buf.numel() < need:
-        setattr(d, name, None)  # release before the larger allocation
+        buf = None
+        setattr(d, name, None)  # release before the larger allocation (no reference may survive)
         buf = torch.empty(int(need * 1.05) + 4096, dtype=torch.uint8, device=d.device)
         setattr(d, name, buf)
     return buf
@@ -237,6 +248,7 @@ def compute_av_switches(d, nl: NeighborList, box: Box):
         avs = _rec(d, 1, "av").data_ptr() if (getattr(d, "_av_s_valid", False) and d.fixedPoint) else 0
         _lib.hip().av_switches(*args, *_gpu_tail(d, "av"), avs)
         d._av_s_valid = False
+        d._rec1 = None  # S_i consumed (stream-ordered reuse): not held through the momentum loop
     else:
         _lib.cpu().av_switches(*args)
 
@@ -252,7 +264,8 @@ def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = F
               d["ax"].data_ptr(), d["ay"].data_ptr(), d["az"].data_ptr(), d["du"].data_ptr())
     if _is_gpu(d):
         dt = torch.full((1,), math.inf, dtype=torch.float32, device=d.device)
-        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), *_gpu_tail(d, "mom", (0, 1)))
+        gv = _rec(d, 1, "gradv").data_ptr() if av_clean else 0  # SrcGradV records (AV cleaning only)
+        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), d.size, _rec(d, 0, "mom").data_ptr(), gv, _stream())
         d.minDtCourant_dev = dt
         d.minDtCourant = None
     else:

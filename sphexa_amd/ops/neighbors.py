@@ -7,9 +7,10 @@ loop (the reference GPU path re-traverses the tree in each of its five kernels).
 
 Storage layouts
   * CPU:  ``nidx[(i - first) * ngmax + k]``
-  * HIP:  target groups of 64 consecutive particles (one wave64 per group), entries in 4-entry blocks per lane:
-          ``nidx[g * ngmax4 * 64 + (k // 4) * 256 + lane * 4 + k % 4]`` (ngmax4 = ngmax rounded up to 4), so that
-          four steps of a pair loop are one coalesced 1 KiB load per wave and the search writes whole blocks.
+  * HIP:  packed lists (csrc/include/sphx/packed_list.hpp): target groups of 64 consecutive particles (one wave64 per
+          group); per lane 16-bit delta-coded slots, 8 per 16-byte block, 64 lanes' blocks = one 1-KiB row; rows are
+          allocated per group from a pool (group table: row count, row numbers). ~190 B/particle at ng0 100 instead
+          of 608 for int32 lists at the ngmax stride. ``decode_packed`` / ``pack_lists`` are the Python codec.
 ``nc`` (a particle field) counts neighbors *including* self, as in the reference.
 """
 
@@ -27,25 +28,113 @@ from ..utils.box import Box
 GROUP = 64
 
 
-def _round4(v: int) -> int:
-    return (v + 3) // 4 * 4
-
-
 def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
 @dataclass
 class NeighborList:
-    nidx: torch.Tensor
+    nidx: torch.Tensor  # CPU: int32 lists at the ngmax stride; HIP: packed list buffer (tables + rows)
     first: int
     last: int
     ngmax: int
-    grouped: bool  # True: HIP wave64-interleaved layout
+    grouped: bool  # True: HIP packed layout
+    rows_used: int = 0  # HIP: list rows the search took from the pool
+    plan: tuple | None = None  # HIP: (groups, home rows, overflow rows per stripe) for the next search
+    hist: tuple = ()  # HIP: rows needed by recent searches (pool sizing)
 
     @property
     def stride(self):
         return GROUP if self.grouped else 1
+
+
+# ------------------------------------------------------------------------------------------- packed list codec
+# mirrors csrc/include/sphx/packed_list.hpp (slot: bit 0 emit flag, bits 1..15 signed step; jumps move by step*2^14)
+SLOT_FINE = 16383
+JUMP_SHIFT = 14
+LIST_JUMP_SLACK = 32
+
+
+def packed_rows_max(ngmax: int) -> int:
+    return (ngmax + LIST_JUMP_SLACK + 7) // 8
+
+
+def packed_table_ints(ngmax: int) -> int:
+    return (packed_rows_max(ngmax) + 3 + 3) & ~3
+
+
+def packed_table_region(groups: int, ngmax: int) -> int:
+    return (groups * packed_table_ints(ngmax) + 255) // 256 * 256
+
+
+def encode_step(delta: int) -> list:
+    out = []
+    while delta < -SLOT_FINE - 1 or delta > SLOT_FINE:
+        J = (delta + (1 << (JUMP_SHIFT - 1))) >> JUMP_SHIFT
+        J = max(-SLOT_FINE - 1, min(SLOT_FINE, J))
+        out.append((J * 2) & 0xFFFF)
+        delta -= J << JUMP_SHIFT
+    out.append(((delta * 2) | 1) & 0xFFFF)
+    return out
+
+
+def pack_lists(lists, first: int, ngmax: int, device=None) -> NeighborList:
+    """packed GPU lists from per-target index lists (target first + t gets lists[t]); rows in group order"""
+    import numpy as np
+    n = len(lists)
+    groups = max((n + GROUP - 1) // GROUP, 1)
+    T, region = packed_table_ints(ngmax), packed_table_region(groups, ngmax)
+    lane_slots = []
+    for t, lst in enumerate(lists):
+        prev, sl = first + t, []
+        for j in lst:
+            sl += encode_step(int(j) - prev)
+            prev = int(j)
+        if len(sl) > 8 * packed_rows_max(ngmax):
+            raise ValueError("list too long for the packed rows")
+        lane_slots.append(sl)
+    nrows = [max([(len(s) + 7) // 8 for s in lane_slots[g * GROUP:(g + 1) * GROUP]] + [0]) for g in range(groups)]
+    total = max(sum(nrows), 1)
+    buf = np.zeros(region + total * 256, dtype=np.int32)
+    tab = buf[:groups * T].reshape(groups, T)
+    rows16 = buf[region:].view(np.uint16).reshape(total, GROUP, 8)
+    r0 = 0
+    for g in range(groups):
+        tab[g, 0] = nrows[g]
+        tab[g, 1:1 + nrows[g]] = np.arange(r0, r0 + nrows[g])
+        for lane in range(GROUP):
+            t = g * GROUP + lane
+            if t >= n:
+                break
+            sl = lane_slots[t]
+            for k, v in enumerate(sl):
+                rows16[r0 + k // 8, lane, k % 8] = v
+        r0 += nrows[g]
+    out = torch.from_numpy(buf)
+    return NeighborList(out.to(device) if device is not None else out, first, first + n, ngmax, True, total)
+
+
+def decode_packed(nl: NeighborList):
+    """(indices int64 [n, S], valid bool [n, S]) of a packed list: slot k of target first + t"""
+    buf = nl.nidx.cpu()
+    n = nl.last - nl.first
+    groups = max((n + GROUP - 1) // GROUP, 1)
+    T, region = packed_table_ints(nl.ngmax), packed_table_region(groups, nl.ngmax)
+    tab = buf[:groups * T].view(groups, T).long()
+    nrows = tab[:, 0]
+    R = max(int(nrows.max()), 1)
+    rows = tab[:, 1:1 + R]
+    data = buf[region:].view(-1, GROUP, 4)
+    blk = data[rows.clamp(0, data.shape[0] - 1)].contiguous()  # (groups, R, 64, 4)
+    slots = blk.view(torch.int16).permute(0, 2, 1, 3).reshape(groups, GROUP, R * 8).long()
+    live = (torch.arange(R * 8) // 8).view(1, 1, -1) < nrows.view(-1, 1, 1)
+    slots = torch.where(live, slots, 0).reshape(groups * GROUP, R * 8)
+    e = (slots & 1) == 1
+    d = slots >> 1
+    inc = torch.where(e, d, d << JUMP_SHIFT)
+    self_idx = nl.first + torch.arange(groups * GROUP, dtype=torch.int64)
+    idx = self_idx.view(-1, 1) + torch.cumsum(inc, dim=1)
+    return idx[:n], e[:n]
 
 
 class NeighborSearchError(RuntimeError):
@@ -81,14 +170,40 @@ def _scratch(nbytes: int, device) -> torch.Tensor:
     return t
 
 
+def _pool_plan(prev: NeighborList | None, groups: int, ng0: int, stripes: int):
+    """(home rows per group, rows per overflow stripe) of the packed-list pool: the previous search's choice for
+    this group count, else ng0/8 home rows and 0.35 ng0/8 overflow rows per group (on lattices the neighbor count
+    jumps to ~1.3 ng0 at shell steps)"""
+    if prev is not None and prev.grouped and prev.plan is not None and prev.plan[0] == groups:
+        return prev.plan[1], prev.plan[2]
+    return max(1, round(ng0 / 8)), max(8, -(-int(0.35 * ng0 / 8 * groups + 0.5) // stripes))
+
+
+def _next_plan(buf: torch.Tensor, groups: int, ngmax: int, home: int, stripes: int):
+    """rows per group of this search (table column 0) -> the pool plan of the next one, chosen among home +- 2 for
+    the fewest rows (home rows of every group + stripe capacity for the longest stripe's overflow, +10 %); returns
+    device tensors [5] of (home candidates, total rows)"""
+    T = packed_table_ints(ngmax)
+    nr = buf[:groups * T].view(groups, T)[:, 0].to(torch.int32)
+    pad = (-groups) % stripes
+    if pad:
+        nr = torch.cat([nr, torch.zeros(pad, dtype=torch.int32, device=nr.device)])
+    cand = (torch.arange(-2, 3, device=nr.device) + home).clamp(min=1)
+    # one candidate at a time: a (5, groups) temporary would be 40 B/particle at the search's memory high-water mark
+    over = torch.stack([(nr - cand[k]).clamp_(min=0).view(-1, stripes).sum(dim=0).amax() for k in range(5)])
+    ov = (over.double() * 1.1).long() + 8
+    return cand, ov, cand * groups + stripes * ov
+
+
 def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
                    nidx: torch.Tensor | None = None, xmass_out: torch.Tensor | None = None,
-                   m_uniform: float = 0.0) -> NeighborList:
+                   m_uniform: float = 0.0, prev: NeighborList | None = None) -> NeighborList:
     """search neighbors of particles [first, last) within 2h, adjusting h towards ng0 neighbors.
 
     ``xmass_out`` (GPU only): also compute the VE XMass loop's xm = m / rho0 (reference xmass_kern.hpp) inside the
     search from the distances of the stored entries (``m_uniform`` > 0: common mass, else per-particle masses), so
     the separate XMass pass over the lists is skipped.
+    ``prev``: the previous step's lists; on the GPU its buffer is reused when it has the right size.
     """
     x, y, z, h, nc = d["x"], d["y"], d["z"], d["h"], d["nc"]
     n = last - first
@@ -97,29 +212,71 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         raise ValueError("ng0 should be smaller than ngmax")
     if x.is_cuda:
         hp = _lib.hip()
-        num_groups = (n + GROUP - 1) // GROUP
-        # + 2 block rows: the pair loops prefetch list blocks two ahead
-        need = max(num_groups, 1) * GROUP * _round4(ngmax) + 2 * 4 * GROUP
-        if nidx is None or nidx.numel() < need:
-            nidx = torch.empty(need, dtype=torch.int32, device=x.device)
-        stats = torch.zeros(8, dtype=torch.int64, device=x.device)
-        scratch = _scratch(hp.neighbor_scratch_bytes(n), x.device)
-        hp.find_neighbors(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), tree.num_nodes,
-                          tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
-                          tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
-                          d.ng0, ngmax, nidx.data_ptr(), nc.data_ptr(), int(iterate_h) | (2 if COLLECT_STATS else 0),
-                          stats.data_ptr(),
-                          scratch.data_ptr(), TEST_FRONT_CAP, _stream(),
-                          xm=xmass_out.data_ptr() if xmass_out is not None else 0, m=d["m"].data_ptr(),
-                          m_uniform=float(m_uniform), wh=d.wh.data_ptr(), consts=d.consts_array())
-        st = stats.cpu()
+        num_groups = max((n + GROUP - 1) // GROUP, 1)
+        if packed_table_ints(ngmax) > 64:
+            raise ValueError(f"ngmax {ngmax} too large for the packed GPU lists (at most {8 * 62 - LIST_JUMP_SLACK - 8})")
+        region = packed_table_region(num_groups, ngmax)
+        K = hp.neighbor_row_stripes()
+        home, ov = _pool_plan(prev, num_groups, d.ng0, K)
+        want = num_groups * home + K * ov
+        buf = prev.nidx if (prev is not None and prev.grouped) else nidx
+        have = (buf.numel() - region) // 256 if buf is not None else 0
+        # reuse a buffer with up to 25 % spare rows (they become overflow rows); else release it first
+        if buf is None or have < want or have > 1.25 * want:
+            buf = nidx = None
+            if prev is not None:
+                prev.nidx = None
+            buf = torch.empty(region + want * 256, dtype=torch.int32, device=x.device)
+        scratch = _scratch(hp.neighbor_scratch_bytes(n, ngmax), x.device)
+        for _attempt in range(2):
+            ov = ((buf.numel() - region) // 256 - num_groups * home) // K
+            stats = torch.zeros(8 + 32 * K, dtype=torch.int64, device=x.device)
+            hp.find_neighbors(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), tree.num_nodes,
+                              tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
+                              tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
+                              d.ng0, ngmax, buf.data_ptr(), nc.data_ptr(),
+                              int(iterate_h) | (2 if COLLECT_STATS else 0), stats.data_ptr(),
+                              scratch.data_ptr(), TEST_FRONT_CAP, _stream(),
+                              xm=xmass_out.data_ptr() if xmass_out is not None else 0, m=d["m"].data_ptr(),
+                              m_uniform=float(m_uniform), wh=d.wh.data_ptr(), consts=d.consts_array(),
+                              home=home, ov_stride=ov)
+            ctr = stats[8::32][:K]
+            cand, cand_ov, cand_rows = _next_plan(buf, num_groups, ngmax, home, K)
+            host = torch.cat([stats[:8], ctr.amax().view(1), ctr.sum().view(1), cand, cand_ov, cand_rows]).cpu()
+            st = host[:8]
+            if int(host[8]) <= ov:
+                break
+            # an overflow stripe ran out: the search left h converged, repeat it with enough rows
+            buf = nidx = None
+            if prev is not None:
+                prev.nidx = None
+            buf = torch.empty(region + (num_groups * home + K * (int(int(host[8]) * 1.1) + 8)) * 256,
+                              dtype=torch.int32, device=x.device)
+        else:
+            raise NeighborSearchError("packed neighbor lists: overflow rows exhausted twice")
+        used = num_groups * home + int(host[9])
+        best = int(torch.argmin(host[20:25]))
+        plan_home, plan_ov = int(host[10 + best]), int(host[15 + best])
+        # size the next pool for the largest need of the last 32 searches: neighbor counts on lattices jump between
+        # shells every few steps (Sedov: 12 -> 16 rows per group for one step), and a pool sized for the last step
+        # alone would make those steps repeat the search
+        need = num_groups * plan_home + K * plan_ov
+        same = prev is not None and prev.grouped and prev.plan is not None and prev.plan[0] == num_groups
+        # (the first search's pool is a guess that covers shell steps: it stays in the history)
+        hist = ((prev.hist if same else (num_groups * home + K * ov,)) + (need,))[-32:]
+        if max(hist) > need:
+            plan_ov = -(-(max(hist) - num_groups * plan_home) // K)
+        plan = (num_groups, plan_home, plan_ov)
         if int(st[1]) > 0:
             raise NeighborSearchError(f"GPU traversal stack overflow in {int(st[1])} groups")
+        if int(st[5]) > 0 and not ALLOW_NC_FAIL:
+            raise NeighborSearchError(f"{int(st[5])} neighbor lists exceed the packed rows (ngmax {ngmax} + "
+                                      f"{LIST_JUMP_SLACK} jump slots)")
         _check_convergence(d, int(st[0]))
         d.nc_spilled = int(st[2])
-        d.nc_rounds = int(st[3]) / max(num_groups, 1)  # mean search rounds per group (h iteration)
-        d.nc_leaves = int(st[4]) / max(num_groups, 1)  # mean candidate leaves per group and step
-        return NeighborList(nidx, first, last, ngmax, True)
+        d.nc_rounds = int(st[3]) / num_groups  # mean search rounds per group (h iteration)
+        d.nc_leaves = int(st[4]) / num_groups  # mean candidate leaves per group and step
+        return NeighborList(buf, first, last, ngmax, True, used, plan, hist)
 
     need = max(n, 1) * ngmax
     if nidx is None or nidx.numel() < need:
@@ -136,16 +293,19 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
 def neighbor_lists_as_sets(nl: NeighborList, nc: torch.Tensor):
     """debug/test helper: python sets of neighbor indices per target (capped lists)"""
     out = []
-    nidx = nl.nidx.cpu()
     ncc = nc.cpu()
+    if nl.grouped:
+        idx, valid = decode_packed(nl)
+        for t in range(nl.last - nl.first):
+            lst = idx[t][valid[t]].tolist()
+            cnt = min(int(ncc[nl.first + t]) - 1, nl.ngmax)
+            if len(lst) != max(cnt, 0):
+                raise AssertionError(f"packed list of target {nl.first + t}: {len(lst)} entries, nc says {cnt}")
+            out.append(set(lst))
+        return out
+    nidx = nl.nidx.cpu()
     for i in range(nl.first, nl.last):
         cnt = min(int(ncc[i]) - 1, nl.ngmax)
-        if nl.grouped:
-            g, lane = divmod(i - nl.first, GROUP)
-            base = g * _round4(nl.ngmax) * GROUP + lane * 4
-            s = {int(nidx[base + (k // 4) * 4 * GROUP + k % 4]) for k in range(cnt)}
-        else:
-            base = (i - nl.first) * nl.ngmax
-            s = set(int(v) for v in nidx[base:base + cnt].tolist())
-        out.append(s)
+        base = (i - nl.first) * nl.ngmax
+        out.append(set(int(v) for v in nidx[base:base + cnt].tolist()))
     return out

@@ -46,6 +46,9 @@ class Timer:
         self.num_start = 0         # start() calls since the last write_timings (the reference's numStartCalled)
         self.step_times: List[float] = []  # every step() duration since the last write_timings, in call order
         self.pm = None  # optional utils.pm_reader.PmReader sampled at every boundary
+        # SPHX_MEM_TRACE=1: device-memory peak of every substep (max over steps), to locate the step's high-water mark
+        self.mem_trace = os.environ.get("SPHX_MEM_TRACE") == "1"
+        self.mem_peak: Dict[str, int] = OrderedDict()
 
     def _now(self):
         if self.sync and self.device is not None and self.device.type == "cuda":
@@ -71,6 +74,9 @@ class Timer:
         self.steps[name] = self.steps.get(name, 0.0) + dt
         self.step_times.append(dt)
         self.accum[name] = self.accum.get(name, 0.0) + dt
+        if self.mem_trace and self.device is not None and self.device.type == "cuda":
+            self.mem_peak[name] = max(self.mem_peak.get(name, 0), torch.cuda.max_memory_allocated(self.device))
+            torch.cuda.reset_peak_memory_stats(self.device)
         if self.active and self.out is not None:
             print(f"# {name}: {dt:.6f}s", file=self.out)
         r = _roctx()

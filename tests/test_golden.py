@@ -195,15 +195,12 @@ def _dataset(dev, n, vals, fields=VE_FIELDS):
 
 
 def _neighbor_list(d, n):
-    """particle 0 against 1..n-1 in the operator's list layout (CPU rows / GPU 4-entry lane blocks)"""
-    from sphexa_amd.ops.neighbors import GROUP, NeighborList
+    """particle 0 against 1..n-1 in the operator's list layout (CPU rows / GPU packed lists)"""
+    from sphexa_amd.ops.neighbors import NeighborList, pack_lists
 
     k = np.arange(n - 1)
     if d.device.type == "cuda":
-        ng4 = (d.ngmax + 3) // 4 * 4
-        nidx = np.zeros(GROUP * ng4 + 2 * 4 * GROUP, dtype=np.int32)
-        nidx[(k // 4) * 4 * GROUP + k % 4] = k + 1
-        return NeighborList(torch.from_numpy(nidx).to(d.device), 0, 1, d.ngmax, True)
+        return pack_lists([(k + 1).tolist()], 0, d.ngmax, d.device)
     return NeighborList(torch.from_numpy((k + 1).astype(np.int32)), 0, 1, d.ngmax, False)
 
 
