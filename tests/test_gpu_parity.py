@@ -278,3 +278,24 @@ def test_ve_step_fp64_records_matches_cpu(gpu, monkeypatch):
     for f in ("ax", "du"):
         assert _rel(g[f], c[f]) < 2e-3, f
 
+
+
+def test_packed_list_overflow_rows_and_repeat(gpu, monkeypatch):
+    """packed lists with 1 home row per group: every other row comes from the overflow stripes, and a first attempt
+    with 8 rows per stripe runs out, so the search repeats with a larger pool; lists and the VE loops must not change
+    (ops/neighbors.py _pool_plan, neighbors.hip encodeGroup)"""
+    from sphexa_amd.ops import neighbors as N
+
+    dg, pg, domg = _setup(gpu, 16, jitter=0.01)
+    pg.sync(domg, dg)
+    nl_ref = find_neighbors(dg, domg.octree, domg.box, 0, dg.size)
+    sets_ref = neighbor_lists_as_sets(nl_ref, dg["nc"])
+    H.compute_xmass(dg, nl_ref, domg.box)
+    xm_ref = dg["xm"].clone()
+    monkeypatch.setattr(N, "_pool_plan", lambda prev, groups, ng0, stripes: (1, 8))
+    nl = find_neighbors(dg, domg.octree, domg.box, 0, dg.size)
+    groups = (dg.size + 63) // 64
+    assert nl.rows_used > groups  # overflow rows were taken
+    assert neighbor_lists_as_sets(nl, dg["nc"]) == sets_ref
+    H.compute_xmass(dg, nl, domg.box)
+    assert torch.equal(dg["xm"], xm_ref)
