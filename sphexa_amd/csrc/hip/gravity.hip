@@ -352,11 +352,19 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
                     const float rQr = rx * Qx[r] + ry * Qy[r] + rz * Qz[r];
                     const float Mir = C[r].w * ir;
                     const float t1  = rQr * ir5;
+#ifdef SPHX_M2P_FMA
+                    const float cmb = __builtin_fmaf(-2.5f, t1, -Mir) * ir2;
+                    ph[tb]          = __builtin_fmaf(-0.5f, t1, ph[tb] - Mir);
+                    ax[tb]          = __builtin_fmaf(cmb, rx, __builtin_fmaf(ir5, Qx[r], ax[tb]));
+                    ay[tb]          = __builtin_fmaf(cmb, ry, __builtin_fmaf(ir5, Qy[r], ay[tb]));
+                    az[tb]          = __builtin_fmaf(cmb, rz, __builtin_fmaf(ir5, Qz[r], az[tb]));
+#else
                     const float cmb = (-2.5f * t1 - Mir) * ir2;
                     ph[tb] -= Mir + 0.5f * t1;
                     ax[tb] += ir5 * Qx[r] + cmb * rx;
                     ay[tb] += ir5 * Qy[r] + cmb * ry;
                     az[tb] += ir5 * Qz[r] + cmb * rz;
+#endif
                 }
             }
         }
@@ -381,6 +389,161 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
     acc[1] += v[1];
     acc[2] += v[2];
     acc[3] += v[3];
+}
+
+//! float4 slots of the per-wave staging area used by evalM2PMfma2 (64 nodes per batch)
+constexpr int kM2P2Stage = 64 + 16 + 256 + 128;
+
+/*! @brief M2P with every bilinear part of the pair on the matrix cores: separation, quadrupole-vector product and the
+ *         quadratic form, leaving the VALU the radial factors and the accumulation.
+ *
+ * With t the target and c the node center (both relative to the group center) and Q traceless (p2m/addQuadrupole):
+ *     R2[n][t]  = |t|^2 + sum_k [-2c_x, -2c_y, -2c_z, |c|^2]_k [t_x, t_y, t_z, 1]_k              (C input |t|^2)
+ *     Qr_a[n][t] = sum_k [Q_ax, Q_ay, Q_az, -(Q c)_a]_k [t_x, t_y, t_z, 1]_k                        (= (Q r)_a)
+ *     rQr[n][t] = c.Qc + [Q_xx, Q_yy, 2Q_xy, 2Q_xz | 2Q_yz, -2(Qc)_x, -2(Qc)_y, -2(Qc)_z]
+ *                      . [t_x^2 - t_z^2, t_y^2 - t_z^2, t_x t_y, t_x t_z | t_y t_z, t_x, t_y, t_z]    (C input c.Qc)
+ * i.e. six v_mfma_f32_16x16x4_f32 per 16-node x 16-target block. The acceleration sum_n (r5 Qr + comb r) is kept as
+ * sum_n (r5 Qr - comb c) + t sum_n comb, so no per-pair separation vector is formed: 16 VALU + one rsqrt per pair
+ * instead of 25 (evalM2PMfma). The expansions carry rounding ~eps (|t| + |c|)^2 against |r|^2, and |c| <= |r| + |t| for
+ * nodes accepted by the MAC against the group box. Padding nodes: center 1e10 away, zero mass and quadrupole.
+ */
+__device__ inline void evalM2PMfma2(const int32_t* list, int n, const GravTree& t, const double tcv[3], float xr,
+                                    float yr, float zr, float4* stage, float acc[4])
+{
+    n = __builtin_amdgcn_readfirstlane(n);
+    if (n <= 0) return;
+    // the group center is wave-uniform: keep it in SGPRs (VGPR copies are spilled around the batch loop)
+    double tc[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+    {
+        const uint64_t u = __builtin_bit_cast(uint64_t, tcv[d]);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(u)), hi = __builtin_amdgcn_readfirstlane(uint32_t(u >> 32));
+        tc[d] = __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+    }
+    const int lane = laneId(), kq = lane >> 4, col = lane & 15;
+    float4* sC = stage;                                      // 64 x {-c_x, -c_y, -c_z, M}
+    float* sD  = reinterpret_cast<float*>(stage + 64);       // 64 x c.Qc
+    float4* sA = stage + 80;                                 // (node, k) -> {Qr_x, Qr_y, Qr_z, R2} A operands
+    float2* sB = reinterpret_cast<float2*>(stage + 336);     // (node, k) -> the two rQr A operands
+    float bT[4], b2a[4], b2b[4], tt[4];
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+    {
+        const int src = tb * 16 + col;
+        const float X = __shfl(xr, src), Y = __shfl(yr, src), Z = __shfl(zr, src);
+        bT[tb]  = kq == 0 ? X : (kq == 1 ? Y : (kq == 2 ? Z : 1.f));
+        b2a[tb] = kq == 0 ? X * X - Z * Z : (kq == 1 ? Y * Y - Z * Z : (kq == 2 ? X * Y : X * Z));
+        b2b[tb] = kq == 0 ? Y * Z : (kq == 1 ? X : (kq == 2 ? Y : Z));
+        tt[tb]  = X * X + Y * Y + Z * Z;
+    }
+    float ph[4] = {0, 0, 0, 0}, ax[4] = {0, 0, 0, 0}, ay[4] = {0, 0, 0, 0}, az[4] = {0, 0, 0, 0};
+    float sc[4] = {0, 0, 0, 0};
+
+    double rc[3];
+    float4 q0, q1;
+    auto gather = [&](int32_t nd)
+    {
+        const double* c = t.centers + 4 * nd;
+        const float4* q = reinterpret_cast<const float4*>(t.mp + nd);
+        rc[0] = c[0], rc[1] = c[1], rc[2] = c[2];
+        q0 = q[0], q1 = q[1];
+    };
+    int32_t idxN  = lane < n ? list[lane] : 0;
+    int32_t idxNN = 64 + lane < n ? list[64 + lane] : 0;
+    gather(idxN);
+    for (int b0 = 0; b0 < n; b0 += 64)
+    {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // previous batch fully read before it is overwritten
+        {
+            const bool live = b0 + lane < n;
+            const float cx = live ? float(rc[0] - tc[0]) : 1e10f, cy = live ? float(rc[1] - tc[1]) : 1e10f,
+                        cz = live ? float(rc[2] - tc[2]) : 1e10f;
+            const float M   = live ? q0.x : 0.f;
+            const float Qxx = live ? q0.y : 0.f, Qxy = live ? q0.z : 0.f, Qxz = live ? q0.w : 0.f;
+            const float Qyy = live ? q1.x : 0.f, Qyz = live ? q1.y : 0.f, Qzz = live ? q1.z : 0.f;
+            const float Qcx = Qxx * cx + Qxy * cy + Qxz * cz;
+            const float Qcy = Qxy * cx + Qyy * cy + Qyz * cz;
+            const float Qcz = Qxz * cx + Qyz * cy + Qzz * cz;
+            sC[lane]         = make_float4(-cx, -cy, -cz, M);
+            sD[lane]         = cx * Qcx + cy * Qcy + cz * Qcz;
+            sA[4 * lane + 0] = make_float4(Qxx, Qxy, Qxz, -2.f * cx);
+            sA[4 * lane + 1] = make_float4(Qxy, Qyy, Qyz, -2.f * cy);
+            sA[4 * lane + 2] = make_float4(Qxz, Qyz, Qzz, -2.f * cz);
+            sA[4 * lane + 3] = make_float4(-Qcx, -Qcy, -Qcz, cx * cx + cy * cy + cz * cz);
+            sB[4 * lane + 0] = make_float2(Qxx, 2.f * Qyz);
+            sB[4 * lane + 1] = make_float2(Qyy, -2.f * Qcx);
+            sB[4 * lane + 2] = make_float2(2.f * Qxy, -2.f * Qcy);
+            sB[4 * lane + 3] = make_float2(2.f * Qxz, -2.f * Qcz);
+        }
+        idxN  = idxNN;
+        idxNN = b0 + 128 + lane < n ? list[b0 + 128 + lane] : 0;
+        gather(idxN);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int ntile = (min(64, n - b0) + 15) >> 4;
+        for (int tile = 0; tile < ntile; ++tile)
+        {
+            const float4 A  = sA[4 * (16 * tile + col) + kq];
+            const float2 A2 = sB[4 * (16 * tile + col) + kq];
+            const float4 D  = reinterpret_cast<const float4*>(sD)[4 * tile + kq]; // c.Qc of rows 4 kq + r
+            float4 C[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                C[r] = sC[16 * tile + 4 * kq + r];
+            const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+            const f32x4 cQc  = {D.x, D.y, D.z, D.w};
+#pragma unroll
+            for (int tb = 0; tb < 4; ++tb)
+            {
+                const f32x4 cT  = {tt[tb], tt[tb], tt[tb], tt[tb]};
+                const f32x4 R2  = __builtin_amdgcn_mfma_f32_16x16x4f32(A.w, bT[tb], cT, 0, 0, 0);
+                const f32x4 Qx  = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[tb], zero, 0, 0, 0);
+                const f32x4 Qy  = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[tb], zero, 0, 0, 0);
+                const f32x4 Qz  = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[tb], zero, 0, 0, 0);
+                const f32x4 rQa = __builtin_amdgcn_mfma_f32_16x16x4f32(A2.x, b2a[tb], cQc, 0, 0, 0);
+                const f32x4 rQr = __builtin_amdgcn_mfma_f32_16x16x4f32(A2.y, b2b[tb], rQa, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    // explicit fmas: a + (b*c + d*e) would cost a multiply, an fma and an add
+                    const float ir  = __builtin_amdgcn_rsqf(R2[r]);
+                    const float ir2 = ir * ir;
+                    const float ir5 = ir2 * (ir2 * ir);
+                    const float Mir = C[r].w * ir;
+                    const float t1  = rQr[r] * ir5;
+                    const float cmb = __builtin_fmaf(-2.5f, t1, -Mir) * ir2;
+                    ph[tb]          = __builtin_fmaf(-0.5f, t1, ph[tb] - Mir);
+                    ax[tb]          = __builtin_fmaf(cmb, C[r].x, __builtin_fmaf(ir5, Qx[r], ax[tb]));
+                    ay[tb]          = __builtin_fmaf(cmb, C[r].y, __builtin_fmaf(ir5, Qy[r], ay[tb]));
+                    az[tb]          = __builtin_fmaf(cmb, C[r].z, __builtin_fmaf(ir5, Qz[r], az[tb]));
+                    sc[tb] += cmb;
+                }
+#ifndef SPHX_M2P2_NOBARRIER
+                __builtin_amdgcn_sched_barrier(0); // one block's MFMA results live at a time (4 waves per SIMD)
+#endif
+            }
+        }
+    }
+    // partials of target 16 tb + col sit in the four lane groups kq: sum them, lane L keeps target L
+    const int myTb = lane >> 4;
+    float v[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+    {
+        float p[5] = {ph[tb], ax[tb], ay[tb], az[tb], sc[tb]};
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+        {
+            float s = p[q];
+            s += __shfl_xor(s, 16);
+            s += __shfl_xor(s, 32);
+            v[q] = (tb == myTb) ? s : v[q];
+        }
+    }
+    acc[0] += v[0];
+    acc[1] += v[1] + xr * v[4];
+    acc[2] += v[2] + yr * v[4];
+    acc[3] += v[3] + zr * v[4];
 }
 
 
@@ -926,7 +1089,11 @@ __global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t 
                                                            double* __restrict__ out,
                                                            unsigned long long* __restrict__ stats, GravSlabs S)
 {
+#ifdef SPHX_GRAV_M2P_MFMA2
+    __shared__ float4 stage[kGWaves][kM2P2Stage];
+#else
     __shared__ float4 stage[kGWaves][5 * 64];
+#endif
     __shared__ double red[kGWaves];
     const int wave          = threadIdx.x >> 6;
     const int64_t numGroups = (last - first + 63) / 64;
@@ -939,6 +1106,8 @@ __global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t 
         float acc[4] = {0, 0, 0, 0};
 #ifdef SPHX_GRAV_VALU_M2P
         evalM2P(S.mlist + g * S.capM, nm, t, e.tc, e.xr, e.yr, e.zr, stage[wave], acc);
+#elif defined(SPHX_GRAV_M2P_MFMA2)
+        evalM2PMfma2(S.mlist + g * S.capM, nm, t, e.tc, e.xr, e.yr, e.zr, stage[wave], acc);
 #else
         evalM2PMfma(S.mlist + g * S.capM, nm, t, e.tc, e.xr, e.yr, e.zr, stage[wave], acc);
 #endif
