@@ -11,6 +11,10 @@ particles every iteration, so a Catalyst/Ascent/ParaView bridge (or any analysis
     def finalize(): ...
 
 A module exposing only one callable may be given as ``module:function`` (used as ``execute``).
+
+``--insitu ascent`` runs the built-in adaptor with the reference's Ascent actions (``app/ascent.py``: threshold
+pipeline, pseudocolor render, relay extract), ``--insitu ascent:actions.yaml`` an Ascent action file (pipelines,
+binning queries, scenes, extracts, triggers).
 """
 
 from __future__ import annotations
@@ -20,10 +24,17 @@ from typing import Optional
 
 
 class InsituHook:
-    def __init__(self, spec: Optional[str], constants=None):
+    def __init__(self, spec: Optional[str], constants=None, comm=None, out_dir: str = "."):
         self.mod = None
         self.exec_fn = None
+        self.builtin = None
         if not spec:
+            return
+        if spec == "ascent" or spec.startswith("ascent:"):
+            from .ascent import AscentAdaptor
+
+            path = spec.partition(":")[2] or None
+            self.builtin = AscentAdaptor(actions_path=path, comm=comm, out_dir=out_dir)
             return
         name, _, fn = spec.partition(":")
         self.mod = importlib.import_module(name)
@@ -34,10 +45,13 @@ class InsituHook:
 
     @property
     def active(self) -> bool:
-        return self.exec_fn is not None
+        return self.exec_fn is not None or self.builtin is not None
 
     def execute(self, d, domain):
         if not self.active:
+            return
+        if self.builtin is not None:
+            self.builtin.execute(d, domain.start_index(), domain.end_index(), domain.box)
             return
         s, e = domain.start_index(), domain.end_index()
         fields = {n: d[n][s:e] for n in d.allocated_fields()}

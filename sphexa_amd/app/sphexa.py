@@ -52,7 +52,8 @@ Where possible options are:
                         [/sys/cray/pm_counters]; the amdgpu hwmon sensor is used for the GPU when absent
     -o PATH             Location of generated output files
     --device DEV        cuda (default when a GPU is present) or cpu (OpenMP reference path)
-    --insitu MOD[:FN]   In-situ adaptor module called every iteration with the local particle fields
+    --insitu MOD[:FN]   In-situ adaptor module called every iteration with the local particle fields;
+                        'ascent' / 'ascent:actions.yaml' for the built-in Ascent-action adaptor
     --no-watchdog       Do not abort on non-finite energies or time steps
 """
 
@@ -140,7 +141,7 @@ def main(argv=None) -> int:
         print(f"Domain synchronized, nLocalParticles {domain.n_particles()}", flush=True)
     from .insitu import InsituHook
 
-    viz = InsituHook(parser.get("--insitu", None), sim_init.constants())
+    viz = InsituHook(parser.get("--insitu", None), sim_init.constants(), comm, os.path.dirname(out_file) or ".")
 
     start_iteration = d.iteration
     while not stop_simulation(d.iteration - 1, d.ttot, max_step):
