@@ -176,7 +176,10 @@ void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, do
 #endif
 
 constexpr int kGWaves = 4;
-constexpr int kGStack = 2048;
+#ifndef SPHX_GSTACK
+#define SPHX_GSTACK 2048
+#endif
+constexpr int kGStack = SPHX_GSTACK; // LDS traversal stack (node ids) per wave of the list kernel
 constexpr int kGM2P   = 256;
 constexpr int kGP2P   = 512; // particle indices queued for P2P per wave
 
@@ -979,7 +982,7 @@ __global__ __launch_bounds__(256) void gravityListKernel(int64_t first, int64_t 
     int32_t* ml = S.mlist + g * S.capM;
     int32_t* ll = S.llist + g * S.capL;
     int sp = 1, nm = 0, nl = 0, np = 0;
-    bool ok = true;
+    bool ok = true, slabFull = false;
     if (lane == 0) stack[0] = 0;
     gWaveSync<false>();
     while (sp > 0)
@@ -993,26 +996,30 @@ __global__ __launch_bounds__(256) void gravityListKernel(int64_t first, int64_t 
         }
         uint64_t bm = ballot(isM2P), bl = ballot(isLeaf);
         int cm = __popcll(bm), cl = __popcll(bl);
-        if (nm + cm > S.capM || nl + cl > S.capL)
+        // a group that outgrows its slabs finishes the traversal counting only, so the host learns the whole
+        // demand ([6] leaves, [7] M2P nodes) and sizes the slabs for it in one step (the group itself falls back)
+        slabFull = slabFull || nm + cm > S.capM || nl + cl > S.capL;
+        if (!slabFull)
         {
-            // record the demand seen so far ([6] leaves, [7] M2P nodes) so the host can grow the slabs
-            if (lane == 0)
+            if (isM2P) ml[nm + __popcll(bm & lanemaskLt())] = nd;
+            if (isLeaf)
             {
-                atomicMax(&stats[6], (unsigned long long)(nl + cl));
-                atomicMax(&stats[7], (unsigned long long)(nm + cm));
+                ll[nl + __popcll(bl & lanemaskLt())] = nd;
+                np += t.ne[nd] - t.ns[nd];
             }
-            ok = false;
-            break;
-        }
-        if (isM2P) ml[nm + __popcll(bm & lanemaskLt())] = nd;
-        if (isLeaf)
-        {
-            ll[nl + __popcll(bl & lanemaskLt())] = nd;
-            np += t.ne[nd] - t.ns[nd];
         }
         nm += cm;
         nl += cl;
         gWaveSync<false>();
+    }
+    if (slabFull)
+    {
+        if (lane == 0)
+        {
+            atomicMax(&stats[6], (unsigned long long)nl);
+            atomicMax(&stats[7], (unsigned long long)nm);
+        }
+        ok = false;
     }
     np = waveSum(np);
     if (lane == 0)
