@@ -166,6 +166,8 @@ class HydroVeProp(Propagator):
         t.step("domain::sync")
         box = domain.box
         first, last = domain.start_index(), domain.end_index()
+        # velocity halos are not read before the IAD loop: their exchange overlaps the search, XMass and Gradh
+        vel_halos = domain.exchange_halos_start(d, ["vx", "vy", "vz"])
         fused = self._neighbors(domain, d, "xm")
         t.step("FindNeighbors")
         nl = self.nl
@@ -182,7 +184,8 @@ class HydroVeProp(Propagator):
         t.step("Normalization & Gradh")
         H.compute_eos_ve(d, first, last)
         t.step("EquationOfState")
-        domain.exchange_halos(d, ["vx", "vy", "vz", "prho", "c", "kx"])
+        domain.exchange_halos(d, ["prho", "c", "kx"])
+        domain.exchange_halos_finish(vel_halos)
         t.step("mpi::synchronizeHalos")
 
         d.release("gradh", "az")
@@ -190,7 +193,10 @@ class HydroVeProp(Propagator):
         H.compute_iad_divv_curlv(d, nl, box, self.av_clean)
         d.minDtRho = self.rho_timestep(d, first, last)
         t.step("IadVelocityDivCurl")
-        domain.exchange_halos(d, ["c11", "c12", "c13", "c22", "c23", "c33", "divv"])
+        # the AV switches read divv of the neighbors but the IAD coefficients of the target only: the coefficient
+        # halos (needed by the momentum loop) are exchanged while the AV loop runs
+        domain.exchange_halos(d, ["divv"])
+        iad_halos = domain.exchange_halos_start(d, ["c11", "c12", "c13", "c22", "c23", "c33"])
         t.step("mpi::synchronizeHalos")
 
         H.compute_av_switches(d, nl, box)
@@ -200,6 +206,7 @@ class HydroVeProp(Propagator):
             domain.exchange_halos(d, ["dV11", "dV12", "dV13", "dV22", "dV23", "dV33", "alpha"])
         else:
             domain.exchange_halos(d, ["alpha"])
+        domain.exchange_halos_finish(iad_halos)
         t.step("mpi::synchronizeHalos")
 
         d.release("divv", "curlv")
@@ -262,6 +269,7 @@ class HydroProp(Propagator):
         t = self.timer
         box = domain.box
         first, last = domain.start_index(), domain.end_index()
+        vel_halos = domain.exchange_halos_start(d, ["vx", "vy", "vz"])  # overlaps the search and density loop
         fused = self._neighbors(domain, d, "rho")
         t.step("FindNeighbors")
         nl = self.nl
@@ -270,7 +278,8 @@ class HydroProp(Propagator):
         t.step("Density")
         H.compute_eos_std(d, first, last)
         t.step("EquationOfState")
-        domain.exchange_halos(d, ["vx", "vy", "vz", "rho", "p", "c"])
+        domain.exchange_halos(d, ["rho", "p", "c"])
+        domain.exchange_halos_finish(vel_halos)
         t.step("mpi::synchronizeHalos")
         H.compute_iad(d, nl, box, "m", "rho")
         t.step("IAD")

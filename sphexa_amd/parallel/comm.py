@@ -145,6 +145,25 @@ class Comm:
                                input_split_sizes=list(send_counts), group=self.group)
         return (recv.to(send.device) if staged else recv), list(recv_counts)
 
+    def alltoallv_start(self, send: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int]
+                        ) -> "PendingExchange":
+        """``alltoallv`` with known receive counts, issued without waiting: over RCCL the all-to-all runs on the
+        communicator's stream while the caller's stream keeps computing; ``PendingExchange.wait()`` makes the
+        caller's stream wait for it (no host synchronization). Over gloo, host tensors move asynchronously on gloo's
+        worker threads; device tensors are staged through host memory synchronously."""
+        if self.size == 1:
+            return PendingExchange(send[: int(send_counts[0])].clone(), None, send.device, None)
+        send_counts = [int(v) for v in send_counts]
+        recv_counts = [int(v) for v in recv_counts]
+        shape = (sum(recv_counts),) + tuple(send.shape[1:])
+        staged = self._staged(send)
+        src = send.contiguous().cpu() if staged else send.contiguous()
+        recv = torch.empty(shape, dtype=send.dtype, device=src.device)
+        self._audit("alltoallv", src, recv, splits=(send_counts, recv_counts))
+        work = dist.all_to_all_single(recv, src, output_split_sizes=recv_counts, input_split_sizes=send_counts,
+                                      group=self.group, async_op=not staged)
+        return PendingExchange(recv, work, send.device, src)
+
     def allgather_var(self, t: torch.Tensor) -> List[torch.Tensor]:
         """gather tensors of different first-dimension sizes from all ranks"""
         if self.size == 1:
@@ -163,6 +182,21 @@ class Comm:
         outs = [torch.empty_like(pad) for _ in range(self.size)]
         dist.all_gather(outs, pad, group=self.group)
         return [o[:s] for o, s in zip(outs, sizes)]
+
+
+class PendingExchange:
+    """an all-to-all in flight: ``wait()`` returns the received rows on the sender's device"""
+
+    def __init__(self, recv: torch.Tensor, work, device, keep):
+        self.recv, self.work, self.device = recv, work, device
+        self._keep = keep  # the packed send buffer stays alive until the exchange has completed
+
+    def wait(self) -> torch.Tensor:
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        self._keep = None
+        return self.recv if self.recv.device == self.device else self.recv.to(self.device)
 
 
 def init_distributed(backend: str | None = None) -> Comm:

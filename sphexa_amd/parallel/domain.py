@@ -396,23 +396,30 @@ class Domain:
 
     def exchange_halos(self, d, fields: Sequence[str]):
         """fill halo slots of ``fields`` from their owners. One packed all_to_all per call (all fields fused)."""
-        if self.size == 1:
-            return
-        if not fields:
-            return
+        self.exchange_halos_finish(self.exchange_halos_start(d, fields))
+
+    def exchange_halos_start(self, d, fields: Sequence[str]):
+        """pack the owned rows of ``fields`` and start their halo all-to-all without waiting for it (overlap with
+        work that neither reads the halos of these fields nor writes their owned rows); complete it with
+        ``exchange_halos_finish`` before the halos are read. Ranks must start and finish in the same order."""
+        if self.size == 1 or not fields:
+            return None
         send_idx = getattr(self, "_halo_send_cat", None)
         if send_idx is None or send_idx.numel() != sum(self.halo_send_counts):
             send_idx = torch.cat(self.halo_send_idx) if self.halo_send_idx else None
             self._halo_send_cat = send_idx
         tensors = [d[f] for f in fields]
         packed = _pack_rows(tensors, send_idx)
-        rowbytes = packed.shape[1]
-        recv, _ = self.comm.alltoallv(packed, self.halo_send_counts, self.halo_recv_counts)
-        lo = recv[: self.n_lo]
-        hi = recv[self.n_lo:]
-        _unpack_rows(lo, tensors, 0)
-        _unpack_rows(hi, tensors, self.end)
-        del rowbytes
+        pending = self.comm.alltoallv_start(packed, self.halo_send_counts, self.halo_recv_counts)
+        return pending, tensors, self.n_lo, self.end
+
+    def exchange_halos_finish(self, handle):
+        if handle is None:
+            return
+        pending, tensors, n_lo, end = handle
+        recv = pending.wait()
+        _unpack_rows(recv[:n_lo], tensors, 0)
+        _unpack_rows(recv[n_lo:], tensors, end)
 
     # ---------------------------------------------------------------------------------------- diagnostics
     def global_tree_size(self) -> int:
