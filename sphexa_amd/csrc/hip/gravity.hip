@@ -1172,7 +1172,7 @@ __global__ __launch_bounds__(256, SPHX_P2P_WAVES) void gravityP2PKernel(int64_t 
     blockEnergy(upot, red, kGWaves, out);
 }
 
-//! @brief add the P2P partials (computed concurrently with the M2P kernel on a second stream) to the outputs
+//! @brief add the P2P partials (kept apart from the M2P sums, optionally computed on a second stream) to the outputs
 __global__ void gravityCombineKernel(int64_t first, int64_t last, const float4* __restrict__ pacc,
                                      const float* __restrict__ m, float G, float* __restrict__ ax,
                                      float* __restrict__ ay, float* __restrict__ az, double* __restrict__ ugrav)
@@ -1281,18 +1281,20 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
     unsigned grid  = unsigned((groups + kGWaves - 1) / kGWaves);
     gravityExpandKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, c.S, poff, pidx);
     SPHX_LAUNCH_CHECK();
-    // the M2P kernel (register-light, latency bound) and the MFMA P2P kernel run concurrently: P2P on a side stream
-    // forked from and joined back into s; its partials land in pacc and are added by gravityCombineKernel
-    static thread_local hipStream_t side = nullptr;
+    // P2P partials land in pacc and are added by gravityCombineKernel. The two evaluation kernels run one after the
+    // other on s: run concurrently (P2P on a side stream, SPHX_GRAV_CONCURRENT) they compete for the same SIMDs and
+    // the step is ~1 ms slower on Evrard -n 200 (37.4 vs 38.4 ms, profiles/r2_perf_log.md)
+    hipStream_t side = s;
     static thread_local hipEvent_t fork = nullptr, join = nullptr;
-    if (!side)
+    if (!fork)
     {
-        SPHX_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
         SPHX_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
         SPHX_CHECK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
     }
-#ifdef SPHX_GRAV_SERIAL
-    side = s;
+#ifdef SPHX_GRAV_CONCURRENT
+    static thread_local hipStream_t sideStream = nullptr;
+    if (!sideStream) SPHX_CHECK(hipStreamCreateWithFlags(&sideStream, hipStreamNonBlocking));
+    side = sideStream;
 #endif
     SPHX_CHECK(hipEventRecord(fork, s));
     SPHX_CHECK(hipStreamWaitEvent(side, fork, 0));
