@@ -18,6 +18,8 @@ from ..models.propagators import propagator_factory
 from ..parallel.comm import Comm
 from ..parallel.domain import Domain
 
+from ..ops import _lib
+
 
 class Simulation:
     def __init__(self, init: str, n: int = 50, prop: str = "ve", device=None, glass=None, av_clean=False,
@@ -46,6 +48,7 @@ class Simulation:
 
     def step(self):
         self.propagator.step(self.domain, self.d)
+        _lib.raise_on_device_check(f"iteration {self.d.iteration}")  # SPHX_DEVICE_CHECKS=1 builds only
         self.d.iteration += 1
 
     def run(self, steps: int):

@@ -19,6 +19,7 @@ from ..models import particles as P
 from ..models.init import initializer_factory
 from ..models.observables import TimeAndEnergy
 from ..models.propagators import propagator_factory
+from ..ops import _lib
 from ..parallel.comm import init_distributed
 from ..parallel.domain import Domain
 from ..utils import io as sio
@@ -146,6 +147,7 @@ def main(argv=None) -> int:
     start_iteration = d.iteration
     while not stop_simulation(d.iteration - 1, d.ttot, max_step):
         propagator.step(domain, d)
+        _lib.raise_on_device_check(f"iteration {d.iteration}")  # SPHX_DEVICE_CHECKS=1 builds only
         box = domain.box
         observables.compute_and_write(d, domain, comm)
         if watchdog:

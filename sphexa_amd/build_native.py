@@ -188,6 +188,12 @@ def build_all(verbose=False, hip=True):
     return [o for o in out if o]
 
 
+def build_dcheck(verbose=False):
+    """device-check build of the HIP module (csrc/hip/common.h SPHX_DCHECK) into _native/variants/dcheck/, loaded
+    when SPHX_DEVICE_CHECKS=1: failed range checks are flagged and reported after the step instead of faulting"""
+    return build_hip(verbose=verbose, variant="dcheck", defines=["-DSPHX_DEVICE_CHECKS"])
+
+
 if __name__ == "__main__":
     if "--variant" in sys.argv:
         i = sys.argv.index("--variant")
@@ -197,6 +203,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if "--sanitize" in sys.argv:
         print("ok", build_cpu(verbose=True, sanitize=True))
+        sys.exit(0)
+    if "--dcheck" in sys.argv:
+        print("ok", build_dcheck(verbose=True))
         sys.exit(0)
     skip_hip = "--no-hip" in sys.argv
     for t in build_all(verbose=True, hip=not skip_hip):

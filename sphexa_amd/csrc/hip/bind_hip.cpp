@@ -398,6 +398,9 @@ PYBIND11_MODULE(_sphx_hip, m)
                                  capM, capL, P<int64_t>(poff), P<int32_t>(pidx), P<void>(pacc), St(s));
           });
     m.def("gravity_scratch_bytes", [](int64_t n, int capM, int capL) { return gravityScratchBytes(n, capM, capL); });
+    m.def("device_checks_enabled", &deviceChecksEnabled);
+    m.def("device_check_flags", []() { return dcheckHydro() | dcheckSfc() | dcheckGravity(); },
+          "read and clear the failed device-check bits (always 0 unless built with SPHX_DEVICE_CHECKS)");
     m.def("gravity_particle_counts", [](Ptr scratch, int64_t n, int capM, int capL)
           { return reinterpret_cast<uintptr_t>(gravityParticleCounts(P<void>(scratch), n, capM, capL)); });
     m.def("direct_sum",

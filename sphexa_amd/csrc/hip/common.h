@@ -24,6 +24,43 @@
 
 #define SPHX_LAUNCH_CHECK() SPHX_CHECK(hipGetLastError())
 
+/*! Device-side checks (debug build: build_native --dcheck -> _native/variants/dcheck, loaded when
+ *  SPHX_DEVICE_CHECKS=1). A failed check sets bit `bit` of this translation unit's flag word (one vector atomic) and
+ *  the kernel continues with a safe value (e.g. an out-of-range neighbor index is replaced by the target itself), so
+ *  a corrupted input is reported by the host after the step (ops/_lib.py: raise_on_device_check) instead of faulting
+ *  the GPU. Compiled out otherwise.
+ *  bits: 0 neighbor index >= record count, 1 packed-list rows of a group > rowsMax, 2 gather permutation index out of
+ *        range, 3 gravity interaction list longer than its slab, 4 halo pack index out of range */
+#ifdef SPHX_DEVICE_CHECKS
+namespace sphx::hip
+{
+static __device__ unsigned g_dcheckFlags = 0;
+}
+#define SPHX_DCHECK(cond, bit)                                                                                        \
+    do                                                                                                                \
+    {                                                                                                                 \
+        if (!(cond)) atomicOr(&::sphx::hip::g_dcheckFlags, 1u << (bit));                                             \
+    } while (0)
+//! host reader of this translation unit's flags (read and clear)
+#define SPHX_DCHECK_READER(name)                                                                                      \
+    unsigned name()                                                                                                   \
+    {                                                                                                                 \
+        unsigned v = 0, z = 0;                                                                                        \
+        SPHX_CHECK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_dcheckFlags), sizeof(v), 0, hipMemcpyDeviceToHost));          \
+        SPHX_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_dcheckFlags), &z, sizeof(z), 0, hipMemcpyHostToDevice));            \
+        return v;                                                                                                     \
+    }
+#define SPHX_DCHECK_ENABLED 1
+#else
+#define SPHX_DCHECK(cond, bit)                                                                                        \
+    do                                                                                                                \
+    {                                                                                                                 \
+    } while (0)
+#define SPHX_DCHECK_READER(name)                                                                                      \
+    unsigned name() { return 0; }
+#define SPHX_DCHECK_ENABLED 0
+#endif
+
 namespace sphx::hip
 {
 

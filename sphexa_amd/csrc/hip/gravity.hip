@@ -1106,7 +1106,11 @@ __global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t 
     const int64_t numGroups = (last - first + 63) / 64;
     const int64_t g         = int64_t(xcdRemap(blockIdx.x, gridDim.x)) * kGWaves + wave;
     double upot             = 0;
-    const int nm            = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[2 * g]) : -1;
+    int nm                  = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[2 * g]) : -1;
+    SPHX_DCHECK(nm <= S.capM, 3);
+#ifdef SPHX_DEVICE_CHECKS
+    nm = min(nm, S.capM);
+#endif
     if (nm >= 0)
     {
         EvalTarget e = evalTarget(g, first, last, x, y, z, h);
@@ -1495,5 +1499,7 @@ void m2pFlat(int64_t first, int64_t last, const double* x, const double* y, cons
         first, last, x, y, z, m, M, mc, (const Quadrupole*)mp, G, ax, ay, az, ugrav, out);
     SPHX_LAUNCH_CHECK();
 }
+
+SPHX_DCHECK_READER(dcheckGravity)
 
 } // namespace sphx::hip

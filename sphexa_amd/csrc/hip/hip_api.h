@@ -182,6 +182,12 @@ void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, do
 // Barnes-Hut in two phases: interaction lists (+ per-group P2P particle counts), then evaluation given the
 // exclusive scan poff (groups + 1 entries) of those counts and a pidx buffer of poff[groups] entries
 size_t gravityScratchBytes(int64_t n, int capM, int capL);
+
+// device-check build (common.h SPHX_DCHECK): read and clear the failed-check bits of each translation unit
+unsigned dcheckHydro();
+unsigned dcheckSfc();
+unsigned dcheckGravity();
+bool deviceChecksEnabled();
 int32_t* gravityParticleCounts(void* scratch, int64_t n, int capM, int capL);
 void computeGravityLists(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
                          const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,

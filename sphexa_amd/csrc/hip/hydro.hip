@@ -41,6 +41,11 @@ __device__ __forceinline__ bool targetOf(const NbrArgs& a, int64_t& i, PackedLan
     pl.rows = reinterpret_cast<const int4*>(a.nidx + packedTableRegion(G, a.ngmax)) + (t & 63);
     // wave-uniform: waves past the last group have no table
     pl.nblk = g < G ? unsigned(*(const __attribute__((address_space(4))) int32_t*)(pl.tab)) : 0u;
+#ifdef SPHX_DEVICE_CHECKS
+    pl.ntot = a.ntot;
+    SPHX_DCHECK(pl.nblk <= packedRowsMax(a.ngmax), 1);
+    pl.nblk = min(pl.nblk, packedRowsMax(a.ngmax));
+#endif
     if (i >= a.last)
     {
         i       = a.last - 1;
@@ -938,5 +943,7 @@ void conservedQuantities(int64_t first, int64_t last, const double* x, const dou
     conservedKernel<<<grid, 256, 0, s>>>(first, last, x, y, z, vx, vy, vz, m, temp, u, nc, cv, out);
     SPHX_LAUNCH_CHECK();
 }
+
+SPHX_DCHECK_READER(dcheckHydro)
 
 } // namespace sphx::hip

@@ -100,6 +100,10 @@ __global__ void gatherMultiKernel(int64_t n, const int32_t* __restrict__ perm, F
     int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     int32_t p = perm[i];
+    SPHX_DCHECK(p >= 0 && p < n, 2);
+#ifdef SPHX_DEVICE_CHECKS
+    p = (p >= 0 && p < n) ? p : int32_t(i);
+#endif
 #pragma unroll 4
     for (int k = 0; k < numFields; ++k)
         f.dst[k][i] = f.src[k][p];
@@ -150,8 +154,12 @@ __global__ void packRowsKernel(int64_t n, const int64_t* __restrict__ idx, RowFi
 {
     int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (r >= n) return;
-    const int64_t j = idx ? idx[r] : r;
-    uint32_t* row   = rows + r * rowWords;
+    int64_t j     = idx ? idx[r] : r;
+    SPHX_DCHECK(j >= 0, 4);
+#ifdef SPHX_DEVICE_CHECKS
+    j = j >= 0 ? j : 0;
+#endif
+    uint32_t* row = rows + r * rowWords;
     for (int k = 0; k < nf; ++k)
     {
         if (f.words[k] == 2)
@@ -237,5 +245,8 @@ void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, siz
     size_t bytes = tmpBytes;
     SPHX_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, int(n), s));
 }
+
+SPHX_DCHECK_READER(dcheckSfc)
+bool deviceChecksEnabled() { return SPHX_DCHECK_ENABLED != 0; }
 
 } // namespace sphx::hip

@@ -100,6 +100,10 @@ __device__ __forceinline__ void decodeBlock(int4 w, unsigned& prev, unsigned sel
     decodeWord(w.w, prev, self, j[6], j[7]);
 }
 
+#ifndef SPHX_DCHECK // translation units without the kernels' common.h (host bindings): checks compile to nothing
+#define SPHX_DCHECK(cond, bit) ((void)0)
+#endif
+
 //! @brief one lane's view of its group's packed list (see the file comment)
 struct PackedLane
 {
@@ -107,6 +111,20 @@ struct PackedLane
     const int4* rows;   // first row + lane
     unsigned self;      // target index: decoded jump/padding slots, skipped by the loops
     unsigned nblk;      // list rows of the group (wave-uniform)
+#ifdef SPHX_DEVICE_CHECKS
+    unsigned ntot; // source records (device-check build: decoded indices are checked against it)
+#endif
+
+    //! the decoded index j, or the target itself if j is out of range (device-check build: reported, bit 0)
+    __device__ __forceinline__ unsigned checked(unsigned j) const
+    {
+#ifdef SPHX_DEVICE_CHECKS
+        SPHX_DCHECK(j < ntot, 0);
+        return j < ntot ? j : self;
+#else
+        return j;
+#endif
+    }
 
     __device__ __forceinline__ int4 block(unsigned b) const
     {

@@ -662,6 +662,11 @@ __device__ void forEachNeighborDirect(const PackedLane& pl, const Ld& ld, F&& f)
         unsigned j[4];
         decodeWord(w0, prev, pl.self, j[0], j[1]);
         decodeWord(w1, prev, pl.self, j[2], j[3]);
+#ifdef SPHX_DEVICE_CHECKS
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            j[u] = pl.checked(j[u]);
+#endif
         decltype(ld(0u)) rr[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -754,7 +759,17 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const Coop
     };
     unsigned prev = pl.self;
     unsigned D[8];
-    decodeBlock(pl.block(0), prev, pl.self, D);
+    // (the block decoded after the last one lies past the list and is never used: not checked)
+    auto decodeChecked = [&](int4 w, bool used)
+    {
+        decodeBlock(w, prev, pl.self, D);
+#ifdef SPHX_DEVICE_CHECKS
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            D[u] = used ? pl.checked(D[u]) : D[u];
+#endif
+    };
+    decodeChecked(pl.block(0), true);
     unsigned I1[C], I2[C];
     float4 A[C], Bf[C];
 #pragma unroll
@@ -781,8 +796,8 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const Coop
                 // steps 6, 7 spread the first two entries of the next block (the target's own record past the list)
                 unsigned p = prev;
                 decodeWord(W.x, p, pl.self, jA, jB);
-                jA = more ? jA : pl.self;
-                jB = more ? jB : pl.self;
+                jA = more ? pl.checked(jA) : pl.self;
+                jB = more ? pl.checked(jB) : pl.self;
             }
 #pragma unroll
             for (int q = 0; q < C; ++q)
@@ -799,7 +814,7 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const Coop
             }
             consume(Bf, D[u + 1]);
         }
-        decodeBlock(W, prev, pl.self, D);
+        decodeChecked(W, more);
     }
 }
 #endif

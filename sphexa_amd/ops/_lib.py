@@ -21,6 +21,8 @@ def _load(name: str):
         return _cache[name]
     path = os.path.join(_NATIVE_DIR, name + _EXT)
     variant = os.environ.get("SPHX_HIP_VARIANT") if name == "_sphx_hip" else None
+    if name == "_sphx_hip" and os.environ.get("SPHX_DEVICE_CHECKS") == "1":
+        variant = "dcheck"  # device-check build (build_native --dcheck)
     if name == "_sphx_cpu" and os.environ.get("SPHX_CPU_VARIANT") == "sanitize":
         # ASan/UBSan build of the OpenMP module (build_native --sanitize)
         path = os.path.join(_NATIVE_DIR, "sanitize", name + _EXT)
@@ -72,3 +74,24 @@ def golden():
 def native_paths():
     """the .so files this process has loaded (for diagnostics / smoke tests)"""
     return {k: getattr(v, "__file__", None) for k, v in _cache.items()}
+
+
+class DeviceCheckError(RuntimeError):
+    """a device-side check of the SPHX_DEVICE_CHECKS build failed (see csrc/hip/common.h for the bits)"""
+
+
+DEVICE_CHECK_BITS = {0: "neighbor index out of range", 1: "packed-list rows of a group above rowsMax",
+                     2: "gather permutation index out of range", 3: "gravity interaction list longer than its slab",
+                     4: "halo pack index out of range"}
+
+
+def raise_on_device_check(where: str = ""):
+    """with SPHX_DEVICE_CHECKS=1 (device-check HIP build loaded): raise if any device check failed since the last
+    call. A no-op otherwise (no device synchronization)."""
+    if os.environ.get("SPHX_DEVICE_CHECKS") != "1" or "_sphx_hip" not in _cache:
+        return
+    flags = int(_cache["_sphx_hip"].device_check_flags())
+    if flags:
+        names = [v for b, v in DEVICE_CHECK_BITS.items() if flags >> b & 1]
+        raise DeviceCheckError(f"device checks failed{(' in ' + where) if where else ''}: {', '.join(names)} "
+                               f"(flags {flags:#x})")

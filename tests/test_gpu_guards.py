@@ -78,3 +78,23 @@ def test_evrard_takes_fp64_records_and_fixed_point_stays_close(gpu):
         err = (fx[f] - f64[f]).abs().max().item() / scale
         print(f"fixed-point vs fp64 records, {f}: max rel err {err:.3e}")
         assert err < tol, (f, err)
+
+
+@pytest.mark.parametrize("mode", ["clean", "corrupt"])
+def test_device_check_build(mode):
+    """device-check HIP build (build_native --dcheck, SPHX_DEVICE_CHECKS=1): range checks in the pair loops, gathers,
+    halo packing and gravity lists report a corrupted input after the step instead of faulting (common.h)"""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SPHX_DEVICE_CHECKS="1")
+    env.pop("SPHX_HIP_VARIANT", None)
+    p = subprocess.run([sys.executable, os.path.join(root, "tests", "helpers", "dcheck_run.py"), mode], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    if mode == "clean":
+        assert "clean ok" in p.stdout
+    else:
+        assert "caught: device checks failed in corrupted list: neighbor index out of range" in p.stdout
