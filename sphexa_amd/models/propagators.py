@@ -98,15 +98,29 @@ class Propagator:
             self.timer.step("Gravity")
 
     def compute_timestep(self, domain, d, *extra):
-        """min of Courant, rho, acceleration and 1.1x previous dt; global MIN (reference sph/timestep.hpp)"""
+        """min of Courant, rho, acceleration and 1.1x previous dt; global MIN (reference sph/timestep.hpp). The
+        device-resident inputs (Courant minimum of the momentum loop, max divv, max |a|^2) come to the host in one
+        copy per step."""
         first, last = domain.start_index(), domain.end_index()
+        dev = []
         if d.minDtCourant is None:
-            d.minDtCourant = float(d.minDtCourant_dev.item())
+            dev.append(d.minDtCourant_dev.reshape(()))
+        rho_dev = torch.is_tensor(d.minDtRho)
+        if rho_dev:
+            dev.append(d.minDtRho)  # max divv of the owned particles (rho_timestep)
+        grav = d.g != 0.0 and last > first
+        if grav:
+            dev.append((d["ax"][first:last].double() ** 2 + d["ay"][first:last].double() ** 2 +
+                        d["az"][first:last].double() ** 2).max())
+        vals = torch.stack([v.to(torch.float64) for v in dev]).tolist() if dev else []
+        if d.minDtCourant is None:
+            d.minDtCourant = float(vals.pop(0))
+        if rho_dev:
+            mx = abs(float(vals.pop(0)))
+            d.minDtRho = d.Krho / mx if mx != 0 else math.inf
         dt_acc = math.inf
-        if d.g != 0.0 and last > first:
-            a2 = (d["ax"][first:last].double() ** 2 + d["ay"][first:last].double() ** 2 +
-                  d["az"][first:last].double() ** 2).max()
-            max_acc = math.sqrt(float(a2))
+        if grav:
+            max_acc = math.sqrt(float(vals.pop(0)))
             if max_acc > 0:
                 dt_acc = d.etaAcc * math.sqrt(d.eps / max_acc)
         dt_loc = min([dt_acc, d.minDtCourant, d.minDtRho, d.maxDtIncrease * d.minDt] + list(extra))
@@ -116,10 +130,10 @@ class Propagator:
         d.minDt = dt
 
     def rho_timestep(self, d, first, last):
+        """max divv of the owned particles as a device scalar; compute_timestep turns it into Krho / |max divv|"""
         if last <= first:
             return math.inf
-        mx = float(d["divv"][first:last].max())
-        return d.Krho / abs(mx) if mx != 0 else math.inf
+        return d["divv"][first:last].max()
 
     def print_iteration_timings(self, domain, d):
         if self.out is None:

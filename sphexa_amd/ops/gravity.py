@@ -96,7 +96,9 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
                         m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
                         0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), st_dev.data_ptr(),
                         scratch.data_ptr(), cap_m, cap_l, poff.data_ptr(), pidx.data_ptr(), pacc.data_ptr(), s)
-        st = st_dev.cpu()
+        host = torch.cat([st_dev.to(torch.float64), out]).cpu()  # stats (exact below 2^53) + energy: one copy
+        st = host[:8].to(torch.int64)
+        energy = float(host[8])
         if TEST_CAPS is None and int(st[5]) > 0:
             # groups fell back to the (slow, serial) fused kernel: grow the slabs to the observed demand while the
             # slab memory stays below ~6% of the device (it is 4 B x groups x (capM + capL))
@@ -110,7 +112,7 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
                          fallback=int(st[5]), caps=(cap_m, cap_l))
         if int(st[1]) > 0:
             raise RuntimeError(f"gravity traversal stack overflow in {int(st[1])} groups")
-        return float(out[0].item())
+        return energy
     st = torch.zeros(2, dtype=torch.int64)
     e = float(_lib.cpu().compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
                                          tree.node_start.data_ptr(), tree.node_end.data_ptr(), centers.data_ptr(),

@@ -106,13 +106,23 @@ def invalidate_h_cache(d):
 
 
 def set_global_h_min(d, comm):
-    """smallest h over all ranks (own + halo particles), so every rank takes the same record path in a step"""
+    """smallest h over all ranks (own + halo particles), so every rank takes the same record path in a step. The
+    mass extremes for uniform_mass ride along in the same reduction and host copy (global: every rank then takes the
+    same Gradh record type too)."""
     h = d["h"][: d.size]
-    loc = h.min().to(torch.float64).reshape(1) if h.numel() else torch.full((1,), math.inf, dtype=torch.float64,
-                                                                              device=h.device)
+    m = d["m"][: d.size]
+    if h.numel():
+        lo, hi = torch.aminmax(m)
+        loc = torch.stack([h.min().to(torch.float64), lo.to(torch.float64), -hi.to(torch.float64)])
+    else:
+        loc = torch.full((3,), math.inf, dtype=torch.float64, device=h.device)
     if comm is not None and comm.size > 1:
         comm.allreduce(loc, "min")
-    d._h_min_global = float(loc.item())
+    hmin, mlo, mhi = loc.tolist()
+    mhi = -mhi
+    d._h_min_global = float(hmin)
+    val = float(mlo) if (mlo == mhi and mlo > 0) else 0.0
+    d._m_uniform = ((m.data_ptr(), m.numel(), m._version), val)
 
 
 def quantum(box: Box) -> float:

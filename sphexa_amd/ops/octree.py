@@ -178,10 +178,11 @@ def _build_octree_hip(tree, counts, keys, x, y, z, offset) -> Octree:
     ne = torch.empty(N, dtype=torch.int32, device=dev)
     center = torch.empty(3 * N, dtype=torch.float64, device=dev)
     half = torch.empty(3 * N, dtype=torch.float64, device=dev)
-    lr = [int(v) for v in level_range.cpu().tolist()]
     h.node_ranges(codes_s.data_ptr(), N, keys.data_ptr(), n, offset, ns.data_ptr(), ne.data_ptr(), s)
     h.leaf_boxes(vals_s.data_ptr(), N, ns.data_ptr(), ne.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(),
                  center.data_ptr(), half.data_ptr(), s)
+    # the level ranges (host copy) are read while the node-range and leaf-box kernels run
+    lr = [int(v) for v in level_range.cpu().tolist()]
     for l in range(MAX_LEVEL, -1, -1):
         a, b = lr[l], lr[l + 1]
         if b > a:
