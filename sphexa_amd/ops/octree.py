@@ -158,7 +158,10 @@ def _build_octree_hip(tree, counts, keys, x, y, z, offset) -> Octree:
     h.internal_counts(tree.data_ptr(), L, icount.data_ptr(), s)
     tmp = torch.empty(h.scan_temp_bytes(L + 1), dtype=torch.uint8, device=dev)
     h.exclusive_scan_i64(icount.data_ptr(), icount.data_ptr(), L + 1, tmp.data_ptr(), tmp.numel(), s)
-    Ni = int(icount[L].item())
+    # every internal node of a cornerstone octree has eight children: L = 7 Ni + 1 (no host copy of icount[L])
+    if (L - 1) % 7 != 0:
+        raise ValueError(f"not a cornerstone leaf array: {L} leaves")
+    Ni = (L - 1) // 7
     N = Ni + L
     codes = torch.empty(N, dtype=torch.int64, device=dev)
     vals = torch.empty(N, dtype=torch.int32, device=dev)
