@@ -54,3 +54,23 @@ def test_native_h_writers_invalidate_the_cache():
     assert getattr(d, "_h_min_global", None) is None
     assert H.fixed_point_ok(d, box)
     assert H.fixed_point_ok(d, box) and d._h_min[1] > 4e-3
+
+
+def test_global_h_min_carries_the_uniform_mass():
+    """set_global_h_min reduces h min and the mass extremes in one copy and primes uniform_mass's cache"""
+    from sphexa_amd.models import particles as P
+
+    d = P.ParticlesData("cpu")
+    d.set_conserved("x", "y", "z", "h", "m")
+    d.resize(32)
+    d["h"] = torch.linspace(0.01, 0.02, 32, dtype=torch.float32)
+    d["m"] = 0.5
+    H.set_global_h_min(d, None)
+    assert abs(d._h_min_global - 0.01) < 1e-9
+    key, val = d._m_uniform
+    assert val == 0.5 and key[0] == d["m"].data_ptr()
+    assert H.uniform_mass(d) == 0.5
+    d["m"][3] = 0.25  # in-place change bumps the version: recomputed, no longer uniform
+    assert H.uniform_mass(d) == 0.0
+    H.set_global_h_min(d, None)
+    assert d._m_uniform[1] == 0.0
