@@ -1274,7 +1274,7 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
                         const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
                         const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
                         double* ugrav, double* out, unsigned long long* stats, void* scratch, int capM, int capL,
-                        const int64_t* poff, int32_t* pidx, void* paccBuf, hipStream_t s)
+                        const int64_t* poff, int32_t* pidx, void* paccBuf, hipStream_t s, int phase)
 {
     float4* pacc = static_cast<float4*>(paccBuf);
     int64_t n = last - first;
@@ -1283,6 +1283,15 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
     int64_t groups = (n + 63) / 64;
     GravScratch c  = carve(scratch, groups, capM, capL);
     unsigned grid  = unsigned((groups + kGWaves - 1) / kGWaves);
+    // phase 1: M2P only (needs no particle index list), phase 2: the P2P part, 0: both. Split so that the host
+    // reads the P2P list size while the M2P kernel runs (ops/gravity.py)
+    if (phase == 1)
+    {
+        gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
+                                                       stats, c.S);
+        SPHX_LAUNCH_CHECK();
+        return;
+    }
     gravityExpandKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, c.S, poff, pidx);
     SPHX_LAUNCH_CHECK();
     // P2P partials land in pacc and are added by gravityCombineKernel. The two evaluation kernels run one after the
@@ -1306,9 +1315,12 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
                                                       stats, c.S, poff, pidx, pacc);
     SPHX_LAUNCH_CHECK();
     SPHX_CHECK(hipEventRecord(join, side));
-    gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
-                                                   c.S);
-    SPHX_LAUNCH_CHECK();
+    if (phase == 0)
+    {
+        gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
+                                                       stats, c.S);
+        SPHX_LAUNCH_CHECK();
+    }
     SPHX_CHECK(hipStreamWaitEvent(s, join, 0));
     gravityCombineKernel<<<gridFor(n, 256), 256, 0, s>>>(first, last, pacc, m, G, ax, ay, az, ugrav);
     SPHX_LAUNCH_CHECK();

@@ -197,7 +197,7 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
                         const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
                         const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
                         double* ugrav, double* out, unsigned long long* stats, void* scratch, int capM, int capL,
-                        const int64_t* poff, int32_t* pidx, void* pacc, hipStream_t s);
+                        const int64_t* poff, int32_t* pidx, void* pacc, hipStream_t s, int phase = 0);
 void directSum(int64_t first, int64_t last, int64_t n, const double* x, const double* y, const double* z,
                const float* h, const float* m, float G, float* ax, float* ay, float* az, double* ugrav, double* out,
                hipStream_t s);

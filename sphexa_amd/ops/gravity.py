@@ -63,6 +63,17 @@ def upsweep(tree: Octree, x, y, z, m, box: Box, theta: float, sfc_kind: int = 0)
     return centers, mp
 
 
+_PINNED: dict = {}
+
+
+def _pinned_total() -> torch.Tensor:
+    """one pinned int64 host word per process (device-to-host copies into it are asynchronous)"""
+    t = _PINNED.get("total")
+    if t is None:
+        t = _PINNED["total"] = torch.empty(1, dtype=torch.int64, pin_memory=True)
+    return t
+
+
 def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h, m, G: float, ax, ay, az,
                     ugrav=None, stats: dict | None = None) -> float:
     """add G * a_grav to ax, ay, az for targets [first, last); returns this rank's 0.5 * sum G m phi.
@@ -88,14 +99,23 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         pcount = _int32_view(hp.gravity_particle_counts(scratch.data_ptr(), n, cap_m, cap_l), groups, scratch)
         poff = torch.zeros(groups + 1, dtype=torch.int64, device=x.device)
         torch.cumsum(pcount, 0, out=poff[1:])
-        total = int(poff[-1].item())
-        pidx = torch.empty(max(total, 1), dtype=torch.int32, device=x.device)
         pacc = torch.empty(4 * n, dtype=torch.float32, device=x.device)  # P2P partials (phi, a) per target
-        # phase 2: expand leaves to particle runs, M2P, MFMA P2P, fused fallback for overflowing groups
-        hp.gravity_eval(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
-                        m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
-                        0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), st_dev.data_ptr(),
-                        scratch.data_ptr(), cap_m, cap_l, poff.data_ptr(), pidx.data_ptr(), pacc.data_ptr(), s)
+        # the P2P list size goes to pinned host memory ahead of the M2P kernel: the host waits for that copy only,
+        # and enqueues the P2P part while M2P runs (no idle gap on the GPU)
+        total_h = _pinned_total()
+        total_h.copy_(poff[-1:], non_blocking=True)
+        copied = torch.cuda.Event()
+        copied.record()
+        eval_args = (first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), m.data_ptr(),
+                     float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(), 0 if ugrav is None else ugrav.data_ptr(),
+                     out.data_ptr(), st_dev.data_ptr(), scratch.data_ptr(), cap_m, cap_l, poff.data_ptr())
+        # phase 2a: M2P of the accepted nodes
+        hp.gravity_eval(*eval_args, 0, pacc.data_ptr(), s, phase=1)
+        copied.synchronize()
+        total = int(total_h[0])
+        pidx = torch.empty(max(total, 1), dtype=torch.int32, device=x.device)
+        # phase 2b: expand leaves to particle runs, MFMA P2P, combine, fused fallback for overflowing groups
+        hp.gravity_eval(*eval_args, pidx.data_ptr(), pacc.data_ptr(), s, phase=2)
         host = torch.cat([st_dev.to(torch.float64), out]).cpu()  # stats (exact below 2^53) + energy: one copy
         st = host[:8].to(torch.int64)
         energy = float(host[8])
