@@ -317,9 +317,12 @@ SPHX_HD void pairDelta(CT xi, CT yi, CT zi, CT xj, CT yj, CT zj, HT hi, const Bo
 
 /*! @brief fixed-point coordinate frame of the gfx950 source records: coordinates become 32-bit offsets in the box.
  *         Periodic dimensions span the full 2^32 range, so the wrapping int32 difference of two offsets IS the
- *         minimum image (no fold); open dimensions use 2^30 per box length (|dx| < 2L stays in range). The pair
- *         separation is exact in the integers and rounds once when converted to fp32 (quantum <= 1e-9 L), i.e. to
- *         the accuracy of the fp64 difference rounded to fp32. Records shrink by 12 B, which is what lets XMass,
+ *         minimum image (no fold); open dimensions use 2^30 per box length (|dx| < 2L stays in range). Quantizing
+ *         the positions costs at most one quantum q (L/2^32 periodic, L/2^30 open) per separation component; the
+ *         integer difference is then exact and rounds once to fp32. The host admits this path only while
+ *         q <= 2^-22 h_min (ops/hydro.py FIXED_POINT_REL_QUANTUM), i.e. within 2-4x of the reference's fp32 rounding
+ *         of its fp64 difference at the kernel support of the smallest particle, and below it for h >= 4 h_min;
+ *         otherwise the loops read fp64-coordinate records. Records shrink by 12 B, which is what lets XMass,
  *         Gradh (uniform mass), IAD and momentum drop one 16-B gather chunk per neighbor.
  */
 struct QFrame
@@ -353,7 +356,8 @@ SPHX_HD void pairSep(const Box& box, const R& pi, const R& pj, HT hi, HT& rx, HT
     pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
 }
 
-//! @brief pair separation of two fixed-point records (QFrame): wrapping integer difference, one rounding
+//! @brief pair separation of two fixed-point records (QFrame): wrapping integer difference, one fp32 rounding (plus the
+//!        position quantization of the records, see QFrame)
 template<class R>
 SPHX_HD void pairSep(const QFrame& q, const R& pi, const R& pj, HT, HT& rx, HT& ry, HT& rz)
 {
