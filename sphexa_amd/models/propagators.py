@@ -78,12 +78,15 @@ class Propagator:
         into its final round, ops/neighbors.py), and the return value says whether that happened"""
         first, last = domain.start_index(), domain.end_index()
         fuse = xmass_field is not None and d.device.type == "cuda" and FUSE_XMASS
+        gpu = d.device.type == "cuda"
         self.nl = find_neighbors(d, domain.octree, domain.box, first, last,
                                  prev=self.nl,  # (not nidx=: an argument would pin the old GPU buffer)
                                  xmass_out=d[xmass_field] if fuse else None,
-                                 m_uniform=H.uniform_mass(d) if fuse else 0.0)
-        if d.device.type == "cuda":
-            H.set_global_h_min(d, domain.comm)
+                                 m_uniform=H.uniform_mass(d) if fuse else 0.0,
+                                 # global h minimum + mass extremes come back with the search statistics
+                                 ride_along=(lambda: H.global_h_min_device(d, domain.comm)) if gpu else None)
+        if gpu:
+            H.apply_global_h_min(d, self.nl.ride_along)
         return fuse
 
     def _gravity(self, domain, d):

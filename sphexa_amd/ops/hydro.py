@@ -105,10 +105,8 @@ def invalidate_h_cache(d):
     d._h_min_global = None
 
 
-def set_global_h_min(d, comm):
-    """smallest h over all ranks (own + halo particles), so every rank takes the same record path in a step. The
-    mass extremes for uniform_mass ride along in the same reduction and host copy (global: every rank then takes the
-    same Gradh record type too)."""
+def global_h_min_device(d, comm) -> torch.Tensor:
+    """[min h, min m, -max m] over all ranks as a float64 device tensor (no host copy; see set_global_h_min)"""
     h = d["h"][: d.size]
     m = d["m"][: d.size]
     if h.numel():
@@ -118,11 +116,25 @@ def set_global_h_min(d, comm):
         loc = torch.full((3,), math.inf, dtype=torch.float64, device=h.device)
     if comm is not None and comm.size > 1:
         comm.allreduce(loc, "min")
-    hmin, mlo, mhi = loc.tolist()
+    return loc
+
+
+def apply_global_h_min(d, vals):
+    """store the host values of global_h_min_device: the per-step h minimum of the fixed-point guard and the
+    uniform-mass cache keyed on the current mass tensor"""
+    hmin, mlo, mhi = (float(v) for v in vals)
     mhi = -mhi
-    d._h_min_global = float(hmin)
-    val = float(mlo) if (mlo == mhi and mlo > 0) else 0.0
+    m = d["m"][: d.size]
+    d._h_min_global = hmin
+    val = mlo if (mlo == mhi and mlo > 0) else 0.0
     d._m_uniform = ((m.data_ptr(), m.numel(), m._version), val)
+
+
+def set_global_h_min(d, comm):
+    """smallest h over all ranks (own + halo particles), so every rank takes the same record path in a step. The
+    mass extremes for uniform_mass ride along in the same reduction and host copy (global: every rank then takes the
+    same Gradh record type too)."""
+    apply_global_h_min(d, global_h_min_device(d, comm).tolist())
 
 
 def quantum(box: Box) -> float:

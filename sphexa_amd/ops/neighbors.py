@@ -42,6 +42,7 @@ class NeighborList:
     rows_used: int = 0  # HIP: list rows the search took from the pool
     plan: tuple | None = None  # HIP: (groups, home rows, overflow rows per stripe) for the next search
     hist: tuple = ()  # HIP: rows needed by recent searches (pool sizing)
+    ride_along: list | None = None  # HIP: host values of find_neighbors' ride_along tensor
 
     @property
     def stride(self):
@@ -197,13 +198,15 @@ def _next_plan(buf: torch.Tensor, groups: int, ngmax: int, home: int, stripes: i
 
 def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
                    nidx: torch.Tensor | None = None, xmass_out: torch.Tensor | None = None,
-                   m_uniform: float = 0.0, prev: NeighborList | None = None) -> NeighborList:
+                   m_uniform: float = 0.0, prev: NeighborList | None = None, ride_along=None) -> NeighborList:
     """search neighbors of particles [first, last) within 2h, adjusting h towards ng0 neighbors.
 
     ``xmass_out`` (GPU only): also compute the VE XMass loop's xm = m / rho0 (reference xmass_kern.hpp) inside the
     search from the distances of the stored entries (``m_uniform`` > 0: common mass, else per-particle masses), so
     the separate XMass pass over the lists is skipped.
     ``prev``: the previous step's lists; on the GPU its buffer is reused when it has the right size.
+    ``ride_along`` (GPU): a callable returning a float64 device tensor computed after the search; its values reach
+    the host in the same copy as the search statistics (``NeighborList.ride_along``), saving a synchronization.
     """
     x, y, z, h, nc = d["x"], d["y"], d["z"], d["h"], d["nc"]
     n = last - first
@@ -228,6 +231,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                 prev.nidx = None
             buf = torch.empty(region + want * 256, dtype=torch.int32, device=x.device)
         scratch = _scratch(hp.neighbor_scratch_bytes(n, ngmax), x.device)
+        ride_host = None
         for _attempt in range(2):
             ov = ((buf.numel() - region) // 256 - num_groups * home) // K
             stats = torch.zeros(8 + 32 * K, dtype=torch.int64, device=x.device)
@@ -242,7 +246,15 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               home=home, ov_stride=ov)
             ctr = stats[8::32][:K]
             cand, cand_ov, cand_rows = _next_plan(buf, num_groups, ngmax, home, K)
-            host = torch.cat([stats[:8], ctr.amax().view(1), ctr.sum().view(1), cand, cand_ov, cand_rows]).cpu()
+            # evaluated once per call (it may issue a collective, so every rank calls it exactly once); a repeated
+            # search keeps the converged h of the first one, so the first values stay valid
+            first_try = _attempt == 0
+            ex = (ride_along().to(torch.float64).reshape(-1).view(torch.int64)
+                  if (ride_along is not None and first_try) else None)
+            parts = [stats[:8], ctr.amax().view(1), ctr.sum().view(1), cand, cand_ov, cand_rows]
+            host = torch.cat(parts + ([ex] if ex is not None else [])).cpu()
+            if ex is not None:
+                ride_host = host[25:].view(torch.float64).tolist()
             st = host[:8]
             if int(host[8]) <= ov:
                 break
@@ -276,7 +288,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         d.nc_spilled = int(st[2])
         d.nc_rounds = int(st[3]) / num_groups  # mean search rounds per group (h iteration)
         d.nc_leaves = int(st[4]) / num_groups  # mean candidate leaves per group and step
-        return NeighborList(buf, first, last, ngmax, True, used, plan, hist)
+        return NeighborList(buf, first, last, ngmax, True, used, plan, hist, ride_host)
 
     need = max(n, 1) * ngmax
     if nidx is None or nidx.numel() < need:
