@@ -24,6 +24,9 @@ class MultipoleHolder:
         self.centers = None
         self.multipoles = None
         self.stats = {}
+        self.pending = []
+        self._rstats = None
+        self._host_energy = 0.0
 
     def upsweep(self, d, domain):
         ot = domain.octree
@@ -31,16 +34,37 @@ class MultipoleHolder:
                                                   domain.sfc_kind)
 
     def traverse(self, d, domain):
+        """accelerations now; on the GPU the energy and statistics stay on the device until the propagator's time
+        step copies them to the host together with its own inputs (``pending`` / ``finish``)"""
+        self.finish_sync(d)  # a previous step's values, if nobody collected them
         first, last = domain.start_index(), domain.end_index()
         ot = domain.octree
-        egrav = G.compute_gravity(ot, self.centers, self.multipoles, first, last, d["x"], d["y"], d["z"], d["h"],
-                                  d["m"], d.g, d["ax"], d["ay"], d["az"], stats=self.stats)
+        parts = [G.compute_gravity(ot, self.centers, self.multipoles, first, last, d["x"], d["y"], d["z"], d["h"],
+                                   d["m"], d.g, d["ax"], d["ay"], d["az"], stats=self.stats, defer=True)]
+        self._rstats = None
         if domain.size > 1 and getattr(domain, "remote_tree", None) is not None:
             rt, rc, rmp = domain.remote_tree
-            rstats = {}
-            egrav += G.compute_gravity(rt, rc, rmp, first, last, d["x"], d["y"], d["z"], d["h"], d["m"], d.g,
-                                       d["ax"], d["ay"], d["az"], stats=rstats)
-            self.stats["remote_m2p"] = rstats.get("m2p", 0)
-            self.stats["remote_p2p"] = rstats.get("p2p", 0)
+            self._rstats = {}
+            parts.append(G.compute_gravity(rt, rc, rmp, first, last, d["x"], d["y"], d["z"], d["h"], d["m"], d.g,
+                                           d["ax"], d["ay"], d["az"], stats=self._rstats, defer=True))
+        self.pending = [p for p in parts if isinstance(p, G.GravityPending)]
+        self._host_energy = sum(float(p) for p in parts if not isinstance(p, G.GravityPending))
+        if not self.pending:
+            self._finalize(d, [])
+
+    def finish(self, d, host_vals):
+        """host values of ``pending`` (one list per pending evaluation, in order)"""
+        energies = [p.finish(v) for p, v in zip(self.pending, host_vals)]
+        self.pending = []
+        self._finalize(d, energies)
+
+    def finish_sync(self, d):
+        if getattr(self, "pending", None):
+            self.finish(d, [p.dev.cpu().tolist() for p in self.pending])
+
+    def _finalize(self, d, energies):
+        if self._rstats is not None:
+            self.stats["remote_m2p"] = self._rstats.get("m2p", 0)
+            self.stats["remote_p2p"] = self._rstats.get("p2p", 0)
         # rank-local share; the observables reduction sums it over ranks (as the reference's MPI_Reduce does)
-        d.egrav = egrav
+        d.egrav = self._host_energy + sum(energies)

@@ -115,7 +115,14 @@ class Propagator:
         if grav:
             dev.append((d["ax"][first:last].double() ** 2 + d["ay"][first:last].double() ** 2 +
                         d["az"][first:last].double() ** 2).max())
-        vals = torch.stack([v.to(torch.float64) for v in dev]).tolist() if dev else []
+        # the gravity statistics and energy of this step (GravityPending) ride along in the same copy
+        pend = list(getattr(self.gravity, "pending", None) or [])
+        flat = [v.to(torch.float64).reshape(-1) for v in dev] + [p.dev for p in pend]
+        vals = torch.cat(flat).tolist() if flat else []
+        if pend:
+            k = len(vals) - 10 * len(pend)
+            self.gravity.finish(d, [vals[k + 10 * i: k + 10 * (i + 1)] for i in range(len(pend))])
+            vals = vals[:k]
         if d.minDtCourant is None:
             d.minDtCourant = float(vals.pop(0))
         if rho_dev:

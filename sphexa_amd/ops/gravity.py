@@ -74,10 +74,36 @@ def _pinned_total() -> torch.Tensor:
     return t
 
 
+class GravityPending:
+    """statistics and energy of a GPU gravity evaluation still on the device (compute_gravity(defer=True)): the
+    caller brings ``dev`` (float64 [10]) to the host with other per-step values and calls ``finish``"""
+
+    def __init__(self, dev, groups: int, caps, stats, device):
+        self.dev, self.groups, self.caps, self.stats, self.device = dev, groups, caps, stats, device
+
+    def finish(self, vals) -> float:
+        st = [int(v) for v in vals[:8]]  # exact: counts below 2^53
+        energy = float(vals[8])
+        if TEST_CAPS is None and st[5] > 0:
+            # groups fell back to the (slow, serial) fused kernel: grow the slabs to the observed demand while the
+            # slab memory stays below ~6% of the device (it is 4 B x groups x (capM + capL))
+            budget = torch.cuda.get_device_properties(self.device).total_memory // 16
+            cm = min(max(_CAPS["m"], _round64(1.25 * st[7])), 16384)
+            cl = min(max(_CAPS["l"], _round64(1.25 * st[6])), 8192)
+            if 4 * self.groups * (cm + cl) <= budget:
+                _CAPS["m"], _CAPS["l"] = cm, cl
+        if self.stats is not None:
+            self.stats.update(p2p=st[0], m2p=st[2], max_p2p=st[3], max_m2p=st[4], fallback=st[5], caps=self.caps)
+        if st[1] > 0:
+            raise RuntimeError(f"gravity traversal stack overflow in {st[1]} groups")
+        return energy
+
+
 def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h, m, G: float, ax, ay, az,
-                    ugrav=None, stats: dict | None = None) -> float:
+                    ugrav=None, stats: dict | None = None, defer: bool = False):
     """add G * a_grav to ax, ay, az for targets [first, last); returns this rank's 0.5 * sum G m phi.
-    On the GPU ``stats`` (if given) receives p2p/m2p (summed over targets) and max_p2p/max_m2p (per target)."""
+    On the GPU ``stats`` (if given) receives p2p/m2p (summed over targets) and max_p2p/max_m2p (per target).
+    ``defer`` (GPU): return a GravityPending instead of copying the energy and statistics to the host here."""
     if last <= first:
         return 0.0
     if x.is_cuda:
@@ -116,23 +142,10 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         pidx = torch.empty(max(total, 1), dtype=torch.int32, device=x.device)
         # phase 2b: expand leaves to particle runs, MFMA P2P, combine, fused fallback for overflowing groups
         hp.gravity_eval(*eval_args, pidx.data_ptr(), pacc.data_ptr(), s, phase=2)
-        host = torch.cat([st_dev.to(torch.float64), out]).cpu()  # stats (exact below 2^53) + energy: one copy
-        st = host[:8].to(torch.int64)
-        energy = float(host[8])
-        if TEST_CAPS is None and int(st[5]) > 0:
-            # groups fell back to the (slow, serial) fused kernel: grow the slabs to the observed demand while the
-            # slab memory stays below ~6% of the device (it is 4 B x groups x (capM + capL))
-            budget = torch.cuda.get_device_properties(x.device).total_memory // 16
-            cm = min(max(_CAPS["m"], _round64(1.25 * int(st[7]))), 16384)
-            cl = min(max(_CAPS["l"], _round64(1.25 * int(st[6]))), 8192)
-            if 4 * groups * (cm + cl) <= budget:
-                _CAPS["m"], _CAPS["l"] = cm, cl
-        if stats is not None:
-            stats.update(p2p=int(st[0]), m2p=int(st[2]), max_p2p=int(st[3]), max_m2p=int(st[4]),
-                         fallback=int(st[5]), caps=(cap_m, cap_l))
-        if int(st[1]) > 0:
-            raise RuntimeError(f"gravity traversal stack overflow in {int(st[1])} groups")
-        return energy
+        pending = GravityPending(torch.cat([st_dev.to(torch.float64), out]), groups, (cap_m, cap_l), stats, x.device)
+        if defer:
+            return pending
+        return pending.finish(pending.dev.cpu().tolist())
     st = torch.zeros(2, dtype=torch.int64)
     e = float(_lib.cpu().compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
                                          tree.node_start.data_ptr(), tree.node_end.data_ptr(), centers.data_ptr(),
