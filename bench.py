@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Headline benchmark: particle-updates/s of the reference's test cases (BASELINE.json).
 
-Default: VE-SPH Sedov blast ``--init sedov -n 400`` (64 M particles, regular-lattice initial conditions).
-``--init evrard -n 200`` runs the second headline config (Evrard collapse with Barnes-Hut self-gravity, glass ICs).
+Default: both headline configs of BASELINE.json in one invocation, each with its own W warmup and K timed steps:
+VE-SPH Sedov blast ``--init sedov -n 400`` (64 M particles, regular-lattice initial conditions) -> ``value`` /
+``ms_per_step``, then the Evrard collapse ``-n 200`` with Barnes-Hut self-gravity (glass ICs) -> ``evrard_value`` /
+``evrard_ms_per_step``. The Sedov state is freed before Evrard starts. ``--init CASE`` runs one case only.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 the driver starts one process per
 GPU with torch.distributed.run. W untimed steps, then exactly K timed steps bracketed by barrier + device sync,
@@ -60,7 +62,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--init", default="sedov", help="test case (sedov, evrard, noh, ...)")
+    ap.add_argument("--init", default=None,
+                    help="one test case (sedov, evrard, noh, ...); default: the headline pair, Sedov -n 400 then "
+                         "Evrard -n 200 with self-gravity")
     ap.add_argument("-n", type=int, default=None, help="particles per dimension (default 400 sedov, 200 evrard)")
     ap.add_argument("--prop", default="ve")
     ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
@@ -68,9 +72,7 @@ def main():
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_self_launch(args.gpus))
-    n = args.n if args.n is not None else (200 if args.init == "evrard" else 400)
 
-    from sphexa_amd.app.simulation import Simulation
     from sphexa_amd.parallel.comm import init_distributed
 
     use_cuda = args.device == "cuda" or (args.device == "auto" and torch.cuda.is_available())
@@ -85,7 +87,49 @@ def main():
     else:
         device = torch.device("cpu")
 
-    sim = Simulation(args.init, n=n, prop=args.prop, device=device, comm=comm,
+    # -n without --init applies to both cases (plumbing runs on small sizes)
+    cases = [(args.init, args.n)] if args.init else [("sedov", args.n), ("evrard", args.n)]
+    results = [_run_case(init, n if n is not None else (200 if init == "evrard" else 400), args, comm, device)
+               for init, n in cases]
+    head = results[0]
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": head["value"],
+            "unit": "particle-updates/s",
+            "n_gpus": size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": head["ms"],
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": (head["value"] / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "fp64 coordinates + fp32 hydro (reference precision mix)",
+            "data": "synthetic (built-in " + " and ".join(f"{r['init']} {r['ic']}" for r in results) +
+                    " initial conditions)",
+            "config": {"model": head["model"], "global_batch": head["particles"], "seq_len": 1,
+                       "parallelism": f"sfc-domain-decomposition x{size}", "ranks": size,
+                       "backend": comm.backend or "none"},
+            "peak_mem_gib": head["peak_gib"],
+        }
+        for r in results[1:]:
+            p = r["init"]
+            out.update({f"{p}_value": r["value"], f"{p}_ms_per_step": r["ms"], f"{p}_particles": r["particles"],
+                        f"{p}_model": r["model"], f"{p}_peak_mem_gib": r["peak_gib"]})
+        print(json.dumps(out), flush=True)
+
+
+def _run_case(init: str, n: int, args, comm, device) -> dict:
+    """W untimed steps, then exactly K steps between barrier + device synchronizations (max over ranks)"""
+    import gc
+
+    from sphexa_amd.app.simulation import Simulation
+
+    rank, size = comm.rank, comm.size
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats()
+    sim = Simulation(init, n=n, prop=args.prop, device=device, comm=comm,
                      out=sys.stdout if (args.verbose and rank == 0) else None, quiet=not args.verbose)
     prop, d = sim.propagator, sim.d
     prop.timer.sync = args.verbose
@@ -107,48 +151,34 @@ def main():
     dt = comm.allreduce_scalar(dt, "max", device=device)
     ms = 1000.0 * dt / max(args.steps, 1)
     value = d.numParticlesGlobal * args.steps / dt
-    if rank == 0:
-        grav = " + Barnes-Hut self-gravity" if d.g != 0 else ""
-        ic = "glass" if args.init != "sedov" else "lattice"
-        out = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "particle-updates/s",
-            "n_gpus": size,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms,
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "fp64 coordinates + fp32 hydro (reference precision mix)",
-            "data": f"synthetic (built-in {args.init} {ic} initial conditions)",
-            "config": {"model": f"{args.init} -n {n} --prop {args.prop}{grav} ({int(d.numParticlesGlobal)} particles)",
-                       "global_batch": int(d.numParticlesGlobal), "seq_len": 1,
-                       "parallelism": f"sfc-domain-decomposition x{size}", "ranks": size,
-                       "backend": comm.backend or "none"},
-        }
-        print(json.dumps(out), flush=True)
-        if args.verbose:
-            nsteps = max(prop.timer.num_accum, 1)
-            for k, v in prop.timer.accum.items():
-                print(f"# substep {k:28s} {1000.0 * v / nsteps:10.3f} ms/step", file=sys.stderr)
-            if hasattr(d, "nc_rounds") and d.nc_rounds > 0:
-                print(f"# neighbor search: {d.nc_rounds:.2f} rounds and {d.nc_leaves:.1f} candidate leaves per "
-                      f"64-particle group (last step), {getattr(d, 'nc_spilled', 0)} spilled groups", file=sys.stderr)
-            for k, v in prop.timer.mem_peak.items():
-                print(f"# memory peak in {k:28s} {v / max(d.numParticlesGlobal / size, 1):8.0f} B/particle",
-                      file=sys.stderr)
-            nl = getattr(prop, "nl", None)
-            if nl is not None and nl.grouped and nl.nidx is not None:
-                print(f"# neighbor lists: {nl.nidx.numel() * 4 / max(nl.last - nl.first, 1):.0f} B/particle "
-                      f"(packed rows used {nl.rows_used}, pool plan {nl.plan})", file=sys.stderr)
-            if prop.gravity is not None and prop.gravity.stats:
-                print(f"# gravity stats {prop.gravity.stats}", file=sys.stderr)
-            if device.type == "cuda":
-                print(f"# max memory allocated {torch.cuda.max_memory_allocated() / 2**30:.2f} GiB "
-                      f"({torch.cuda.max_memory_allocated() / max(d.numParticlesGlobal / size, 1):.0f} B/particle), "
-                      f"held between steps {torch.cuda.memory_allocated() / 2**30:.2f} GiB", file=sys.stderr)
+    peak = torch.cuda.max_memory_allocated() / 2**30 if device.type == "cuda" else 0.0
+    grav = " + Barnes-Hut self-gravity" if d.g != 0 else ""
+    res = dict(init=init, ic="glass" if init != "sedov" else "lattice", value=value, ms=ms,
+               particles=int(d.numParticlesGlobal), peak_gib=round(peak, 2),
+               model=f"{init} -n {n} --prop {args.prop}{grav} ({int(d.numParticlesGlobal)} particles)")
+    if rank == 0 and args.verbose:
+        print(f"# case {res['model']}: {ms:.3f} ms/step", file=sys.stderr)
+        nsteps = max(prop.timer.num_accum, 1)
+        for k, v in prop.timer.accum.items():
+            print(f"# substep {k:28s} {1000.0 * v / nsteps:10.3f} ms/step", file=sys.stderr)
+        if hasattr(d, "nc_rounds") and d.nc_rounds > 0:
+            print(f"# neighbor search: {d.nc_rounds:.2f} rounds and {d.nc_leaves:.1f} touched leaves per "
+                  f"64-particle group (last step), {getattr(d, 'nc_spilled', 0)} spilled groups", file=sys.stderr)
+        for k, v in prop.timer.mem_peak.items():
+            print(f"# memory peak in {k:28s} {v / max(d.numParticlesGlobal / size, 1):8.0f} B/particle",
+                  file=sys.stderr)
+        nl = getattr(prop, "nl", None)
+        if nl is not None and nl.grouped and nl.nidx is not None:
+            print(f"# neighbor lists: {nl.nidx.numel() * 4 / max(nl.last - nl.first, 1):.0f} B/particle "
+                  f"(rows used {nl.rows_used}, pool plan {nl.plan})", file=sys.stderr)
+        if prop.gravity is not None and prop.gravity.stats:
+            print(f"# gravity stats {prop.gravity.stats}", file=sys.stderr)
+        if device.type == "cuda":
+            print(f"# max memory allocated {peak:.2f} GiB ({peak * 2**30 / max(d.numParticlesGlobal / size, 1):.0f} "
+                  f"B/particle), held between steps {torch.cuda.memory_allocated() / 2**30:.2f} GiB", file=sys.stderr)
+    del sim, prop, d
+    gc.collect()
+    return res
 
 
 if __name__ == "__main__":

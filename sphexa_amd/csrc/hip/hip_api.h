@@ -83,22 +83,13 @@ void markInBoxes(int64_t nb, const double* bc, const double* bh, const int32_t* 
                  const double* y, const double* z, const Box& box, uint8_t* flags, hipStream_t s);
 
 // neighbors.hip
-//! XMass fused into the search (xm == nullptr: lists only): xm_i = m_i / (K h_i^-3 (m_i + sum_j m_j w_ij)) over the
-//! stored neighbors of the final h-iteration round, from the distances the search already computed
-struct XmFuse
-{
-    float* xm;
-    const float* m;  // masses: m_i always, m_j when mUniform == 0
-    float mUniform;  // common particle mass, or 0
-    float K;
-    KernelFn kf;
-};
-// stats: [0] h-iteration failures, [1] groups overflowing even the spill storage, [2] spilled groups
+// stats: [0] h-iteration failures, [1] groups overflowing even the spill storage, [2] spilled groups, [3]/[4] rounds /
+// touched leaves (opt-in), [6] groups over the chunk-table capacity, [8 + 32 k] overflow-row stripe counters
 size_t neighborScratchBytes(int64_t n, unsigned ngmax);
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int home,
                    int ovStride, int32_t* nc, int iterateH, unsigned long long* stats, void* scratch,
-                   int testFrontCap, const XmFuse& xf, hipStream_t s);
+                   int testFrontCap, hipStream_t s);
 //! overflow-row stripes of the packed-list pool; stats must hold 8 + 32 * stripes counters
 int neighborRowStripes();
 

@@ -7,9 +7,9 @@
  *   * every neighbor loop first packs the source fields it needs into a 16-byte aligned array of records (one
  *     streaming pass), so a neighbor costs 2-8 dwordx4 loads of one contiguous 32-128 B record instead of up to 21
  *     scattered 4/8-byte gathers;
- *   * neighbor lists come from the wave64 search as 16-bit delta-coded rows per 64-particle group (packed_list.hpp,
- *     ~190 B/particle instead of 608 for int32 at the ngmax stride), so the indices of eight steps are one coalesced
- *     1 KiB load per wave;
+ *   * neighbor lists come from the wave64 search as 16-bit chunk codes in rows per 64-particle group (packed_list.hpp,
+ *     2 B per entry instead of 4 for int32 at the ngmax stride), so the indices of eight steps are one coalesced
+ *     1 KiB load per wave, decoded through the group's chunk table in LDS;
  *   * blocks are remapped so each XCD walks a contiguous SFC range of target groups (shared neighbors stay in that
  *     XCD's L2);
  *   * IAD and the velocity divergence/curl run in one kernel (c_ij of the target is all divv needs).
@@ -26,25 +26,46 @@ namespace sphx::hip
 
 constexpr int kBlock = 256;
 
-/*! @brief target of this thread and its neighbor list (packed rows of its 64-particle group, packed_list.hpp).
- *         Threads past the last target stay alive with an empty list and a clamped index (the cooperative gathers
- *         need all 64 lanes of a wave); they store nothing. `n` is the neighbor count (excluding self, capped).
+/*! @brief target of this thread and its neighbor list (chunk-coded rows of its 64-particle group, packed_list.hpp).
+ *         The wave loads its group's chunk table into LDS (nch entries, one coalesced load per 64). Threads past the
+ *         last target stay alive with an empty list and a clamped index (the cooperative gathers need all 64 lanes of
+ *         a wave); they store nothing. `n` is the neighbor count (excluding self, capped).
  */
 __device__ __forceinline__ bool targetOf(const NbrArgs& a, int64_t& i, PackedLane& pl, unsigned& n)
 {
+    __shared__ uint32_t ctabAll[kBlock / 64][kChunkCap];
     unsigned lb     = xcdRemap(blockIdx.x, gridDim.x);
     int64_t t       = int64_t(lb) * kBlock + threadIdx.x;
     i               = a.first + t;
     const int64_t g = t >> 6;
     const int64_t G = (a.last - a.first + 63) / 64;
-    pl.tab  = a.nidx + g * int64_t(packedTableInts(a.ngmax));
-    pl.rows = reinterpret_cast<const int4*>(a.nidx + packedTableRegion(G, a.ngmax)) + (t & 63);
+    const unsigned lane = threadIdx.x & 63;
+    const int32_t* tab  = a.nidx + g * int64_t(packedTableInts(a.ngmax));
+    const int32_t* rowsInt = a.nidx + packedTableRegion(G, a.ngmax);
     // wave-uniform: waves past the last group have no table
-    pl.nblk = g < G ? unsigned(*(const __attribute__((address_space(4))) int32_t*)(pl.tab)) : 0u;
+    unsigned nch = 0, T = 0;
+    pl.nblk = 0;
+    if (g < G)
+    {
+        pl.nblk          = unsigned(*(const __attribute__((address_space(4))) int32_t*)(tab));
+        const unsigned w = unsigned(*(const __attribute__((address_space(4))) int32_t*)(tab + 1));
+        nch              = min(w & 0xFFFFu, kChunkCap);
+        T                = w >> 16;
+    }
+    pl.tab  = tab + 2 + T;
+    pl.rows = reinterpret_cast<const int4*>(rowsInt) + lane;
+    uint32_t* ctab = ctabAll[threadIdx.x >> 6];
+    for (unsigned e = lane; e < nch; e += 64)
+    {
+        const int32_t r = *(const __attribute__((address_space(4))) int32_t*)(tab + 2 + (e >> 8));
+        ctab[e]         = uint32_t(rowsInt[size_t(r) * 256 + (e & 255)]);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    pl.ctab = ctab;
 #ifdef SPHX_DEVICE_CHECKS
     pl.ntot = a.ntot;
-    SPHX_DCHECK(pl.nblk <= packedRowsMax(a.ngmax), 1);
-    pl.nblk = min(pl.nblk, packedRowsMax(a.ngmax));
+    SPHX_DCHECK(pl.nblk <= listBlocksMax(a.ngmax), 1);
+    pl.nblk = min(pl.nblk, listBlocksMax(a.ngmax));
 #endif
     if (i >= a.last)
     {

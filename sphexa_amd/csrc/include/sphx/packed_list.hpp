@@ -1,27 +1,31 @@
-/*! Packed neighbor lists of the GPU path: 16-bit delta-coded entries in 1-KiB list rows allocated per target group.
+/*! Chunk-coded neighbor lists of the GPU path: one 16-bit code per entry, 8 per 16-byte block, in 1-KiB rows
+ *  allocated per 64-particle target group.
  *
  * The reference keeps no neighbor lists on the GPU (each of its five SPH kernels re-traverses the tree,
  * sph/hydro_ve/*_gpu.cu); here the search stores them once per step and every pair loop streams them. Stored as
- * int32 at a fixed ngmax stride they cost 608 B/particle (ngmax 150), two thirds of the whole footprint. Entries of a
- * lane's list are ascending SFC indices of a compact neighborhood, so consecutive entries are close: on the Sedov
- * lattice (64 M particles) 99.46 % of the steps between consecutive entries (the first one measured from the target)
- * fit 15 bits (profiles/r2_list_stats.md).
+ * int32 at a fixed ngmax stride they cost 608 B/particle (ngmax 150).
  *
- * Slot (16 bit): bit 0 = emit flag, bits 1..15 = signed d.
- *   emit: prev += d, the entry is prev                  (|step| <= 16383: one slot)
- *   jump: prev += d * 2^14, no entry                    (larger steps: jump slots, then one emit slot)
- *   0x0000 is a jump by 0: padding. A jump can move by +-2^28, so any 31-bit index step is a few slots.
- * A decoded jump or padding slot yields the target's own index, which is never one of its neighbors: the pair loops
- * skip an entry equal to the target.
+ * The search of a group tests the sources of its candidate leaves in chunks of at most 64 consecutive particles
+ * (one chunk = one wave-wide coalesced load, lane k holds particle c0 + k). Every chunk that holds a candidate gets a
+ * slot s in the group's chunk table (table[s] = c0); a neighbor is then the 16-bit code
+ *     code = s | k << 10        (s < kChunkCap <= 1024, k < 64)   ->   j = table[s] + k.
+ * Slot 0 is the group's own first particle, so code (lane << 10) decodes to the target itself: that is the padding
+ * code of a lane's last block, and the lists also hold the target itself (the search counts it, as the reference's
+ * nc does, instead of excluding it per candidate). The pair loops skip entries equal to the target. Lanes past the
+ * last particle of a partial group pad with the last particle (the loops clamp them to it: a valid record).
+ * A code is final when the candidate test finds the hit: the search writes list blocks straight from its hit ring,
+ * without raw index lists, read-back or a delta-encoding pass; entries are independent (no prefix chain to decode).
  *
  * Layout of one search's list buffer (int32):
- *   [ group tables: G x kTab ints, padded to 256 ints ][ rows: 1 KiB each = 64 lanes x int4 (8 slots per lane) ]
- *   group table: [0] = number of list rows of the group (wave-uniform trip count of the pair loops),
- *                [1 + b] = row of list block b; entries past the group's rows name row 0 (valid memory: the pair
- *                loops prefetch two blocks ahead).
+ *   [ group tables: G x packedTableInts ints, padded to 256 ints ][ rows: 1 KiB each = 64 lanes x int4 ]
+ *   group table: [0] = list blocks nblk (wave-uniform trip count of the pair loops), [1] = nch | T << 16 with nch the
+ *                chunk-table entries and T its rows, [2 + r] = row of ordinal r. Ordinals 0 .. T-1 hold the chunk
+ *                table (256 ints per row; the search reserves T from an upper bound of nch), ordinals T .. T+nblk-1
+ *                the list blocks (row of 64 lanes x 8 codes). Entries past them name row 0 (valid memory: the pair
+ *                loops prefetch a block ahead).
  * Rows: group g owns `home` rows (g*home ..), chosen by the host from the previous search's row counts; rows past
- * those come from one of 64 overflow stripes through an atomic counter per stripe (neighbors.hip PackedOut). The
- * host reads the counters, and repeats the search with more overflow rows if a stripe ran out.
+ * those come from one of 64 overflow stripes through an atomic counter per stripe (neighbors.hip). The host reads
+ * the counters and repeats the search with more overflow rows if a stripe ran out.
  */
 #pragma once
 
@@ -33,84 +37,61 @@
 namespace sphx
 {
 
-//! slots per lane a list may use beyond ngmax entries (jump slots); a lane needing more re-iterates h
-constexpr unsigned kListJumpSlack = 32;
-//! list rows (8 slots per lane) a group may use
-SPHX_HD constexpr unsigned packedRowsMax(unsigned ngmax) { return (ngmax + kListJumpSlack + 7) / 8; }
-//! ints per group table: row count + rows + 2 prefetch entries, rounded to 4 (16-B aligned tables)
-SPHX_HD constexpr unsigned packedTableInts(unsigned ngmax) { return (packedRowsMax(ngmax) + 3 + 3) & ~3u; }
+//! chunk-table capacity per target group (the pair loops keep the table in LDS: 4 B per slot and wave)
+constexpr unsigned kChunkCap = 512;
+constexpr unsigned kChunkSlotBits = 10;
+constexpr unsigned kChunkSlotMask = (1u << kChunkSlotBits) - 1;
+//! rows of a chunk table at capacity
+constexpr unsigned kChunkTabRowsMax = (kChunkCap + 255) / 256;
+//! list blocks a lane may fill: ngmax neighbors + the target itself
+SPHX_HD constexpr unsigned listBlocksMax(unsigned ngmax) { return (ngmax + 1 + 7) / 8; }
+//! rows a group may use (chunk table + list blocks)
+SPHX_HD constexpr unsigned packedRowsMax(unsigned ngmax) { return listBlocksMax(ngmax) + kChunkTabRowsMax; }
+//! ints per group table: counts + rows + 2 prefetch entries, rounded to 4 (16-B aligned tables)
+SPHX_HD constexpr unsigned packedTableInts(unsigned ngmax) { return (2 + packedRowsMax(ngmax) + 2 + 3) & ~3u; }
 //! ints of the table region of a list buffer for `groups` target groups (rows start 1-KiB aligned)
 SPHX_HD constexpr int64_t packedTableRegion(int64_t groups, unsigned ngmax)
 {
     return (groups * int64_t(packedTableInts(ngmax)) + 255) / 256 * 256;
 }
-
-constexpr int kSlotFine = 16383; // largest |d| of an emit slot
-constexpr int kJumpShift = 14;
-
-//! number of slots that encode a step of `delta` (1 emit slot + jump slots)
-SPHX_HD unsigned slotsFor(int delta)
-{
-    unsigned n = 1;
-    while (delta < -kSlotFine - 1 || delta > kSlotFine)
-    {
-        int J = (delta + (1 << (kJumpShift - 1))) >> kJumpShift;
-        J     = J < -kSlotFine - 1 ? -kSlotFine - 1 : (J > kSlotFine ? kSlotFine : J);
-        delta -= J * (1 << kJumpShift);
-        ++n;
-    }
-    return n;
-}
-
-//! emit the slots of one step (jumps first, then the emit slot) through put(uint16 slot)
-template<class Put>
-SPHX_HD void encodeStep(int delta, Put&& put)
-{
-    while (delta < -kSlotFine - 1 || delta > kSlotFine)
-    {
-        int J = (delta + (1 << (kJumpShift - 1))) >> kJumpShift;
-        J     = J < -kSlotFine - 1 ? -kSlotFine - 1 : (J > kSlotFine ? kSlotFine : J);
-        put(unsigned(J * 2) & 0xFFFFu);
-        delta -= J * (1 << kJumpShift);
-    }
-    put((unsigned(delta * 2) | 1u) & 0xFFFFu);
-}
+//! rows of a chunk table with nch entries
+SPHX_HD constexpr unsigned chunkTabRows(unsigned nch) { return (nch + 255) / 256; }
+//! code of particle c0 + k of chunk slot s
+SPHX_HD constexpr uint32_t chunkCode(unsigned s, unsigned k) { return s | (k << kChunkSlotBits); }
 
 #if defined(__HIPCC__)
-//! @brief slot -> entry (or `self` for jumps/padding); `prev` carries the running index
-__device__ __forceinline__ unsigned decodeSlot(int d, unsigned e, unsigned& prev, unsigned self)
-{
-    prev += unsigned(e ? d : d * (1 << kJumpShift));
-    return e ? prev : self;
-}
-
-//! @brief the 2 entries of one word of a list block (slot 2q in the low half of word q)
-__device__ __forceinline__ void decodeWord(int w, unsigned& prev, unsigned self, unsigned& j0, unsigned& j1)
-{
-    j0 = decodeSlot(__builtin_amdgcn_sbfe(w, 1, 15), unsigned(w) & 1u, prev, self);
-    j1 = decodeSlot(w >> 17, (unsigned(w) >> 16) & 1u, prev, self);
-}
-
-//! @brief the 8 entries of one list block (int4 = 8 slots)
-__device__ __forceinline__ void decodeBlock(int4 w, unsigned& prev, unsigned self, unsigned (&j)[8])
-{
-    decodeWord(w.x, prev, self, j[0], j[1]);
-    decodeWord(w.y, prev, self, j[2], j[3]);
-    decodeWord(w.z, prev, self, j[4], j[5]);
-    decodeWord(w.w, prev, self, j[6], j[7]);
-}
 
 #ifndef SPHX_DCHECK // translation units without the kernels' common.h (host bindings): checks compile to nothing
 #define SPHX_DCHECK(cond, bit) ((void)0)
 #endif
 
-//! @brief one lane's view of its group's packed list (see the file comment)
+//! @brief the 2 entries of one word of a list block (code 2q in the low half of word q). The slot is masked to the
+//!        table capacity, so a corrupted code stays inside the LDS table (device-check builds then flag the index).
+__device__ __forceinline__ void decodeWord(int w, const uint32_t* ctab, unsigned& j0, unsigned& j1)
+{
+    static_assert((kChunkCap & (kChunkCap - 1)) == 0 && kChunkCap <= (1u << kChunkSlotBits), "table capacity");
+    j0 = ctab[unsigned(w) & (kChunkCap - 1)] + __builtin_amdgcn_ubfe(unsigned(w), kChunkSlotBits, 6);
+    j1 = ctab[__builtin_amdgcn_ubfe(unsigned(w), 16, kChunkSlotBits) & (kChunkCap - 1)] +
+         (unsigned(w) >> (16 + kChunkSlotBits));
+}
+
+//! @brief the 8 entries of one list block (int4 = 8 codes)
+__device__ __forceinline__ void decodeBlock(int4 w, const uint32_t* ctab, unsigned (&j)[8])
+{
+    decodeWord(w.x, ctab, j[0], j[1]);
+    decodeWord(w.y, ctab, j[2], j[3]);
+    decodeWord(w.z, ctab, j[4], j[5]);
+    decodeWord(w.w, ctab, j[6], j[7]);
+}
+
+//! @brief one lane's view of its group's list (see the file comment)
 struct PackedLane
 {
-    const int32_t* tab; // group table (wave-uniform address: scalar loads)
-    const int4* rows;   // first row + lane
-    unsigned self;      // target index: decoded jump/padding slots, skipped by the loops
-    unsigned nblk;      // list rows of the group (wave-uniform)
+    const int32_t* tab;   // row ordinals of the list blocks (group table + 2 + T; wave-uniform: scalar loads)
+    const int4* rows;     // first row + lane
+    const uint32_t* ctab; // the group's chunk table in this wave's LDS
+    unsigned self;        // target index: padding codes decode to it, the loops skip it
+    unsigned nblk;        // list blocks of the group (wave-uniform)
 #ifdef SPHX_DEVICE_CHECKS
     unsigned ntot; // source records (device-check build: decoded indices are checked against it)
 #endif
@@ -128,8 +109,15 @@ struct PackedLane
 
     __device__ __forceinline__ int4 block(unsigned b) const
     {
-        const int32_t r = *(const __attribute__((address_space(4))) int32_t*)(tab + 1 + b);
+        const int32_t r = *(const __attribute__((address_space(4))) int32_t*)(tab + b);
         return rows[size_t(r) * 64];
+    }
+
+    __device__ __forceinline__ void decode(int w, unsigned& j0, unsigned& j1) const
+    {
+        decodeWord(w, ctab, j0, j1);
+        j0 = checked(j0);
+        j1 = checked(j1);
     }
 };
 #endif

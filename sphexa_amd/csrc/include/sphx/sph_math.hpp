@@ -659,18 +659,12 @@ __device__ void forEachNeighborDirect(const PackedLane& pl, const Ld& ld, F&& f)
     // deeper software pipeline measured slower: more VGPRs, same texture work); the next list block is prefetched
     const unsigned nblk = pl.nblk;
     if (nblk == 0) return;
-    unsigned prev = pl.self;
-    int4 w        = pl.block(0);
-    auto batch    = [&](int w0, int w1)
+    int4 w     = pl.block(0);
+    auto batch = [&](int w0, int w1)
     {
         unsigned j[4];
-        decodeWord(w0, prev, pl.self, j[0], j[1]);
-        decodeWord(w1, prev, pl.self, j[2], j[3]);
-#ifdef SPHX_DEVICE_CHECKS
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            j[u] = pl.checked(j[u]);
-#endif
+        pl.decode(w0, j[0], j[1]);
+        pl.decode(w1, j[2], j[3]);
         decltype(ld(0u)) rr[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -738,10 +732,11 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const Coop
     }
     const unsigned nblk = pl.nblk;
     if (nblk == 0) return;
-    // Neighbor indices come in 8-entry packed list blocks (one coalesced 1 KiB load per eight steps, one block
-    // ahead), are spread to the chunk lanes with ds_bpermute two steps ahead, and the chunk data is gathered one
-    // step ahead of the evaluation. Unrolled by eight with ping-pong buffers (A/B data, I1/I2
-    // indices): no register rotation. Jump/padding slots decode to the target itself: gathered, not evaluated.
+    // Neighbor indices come in 8-entry list blocks (one coalesced 1 KiB load per eight steps, one block ahead,
+    // decoded through the group's chunk table in LDS), are spread to the chunk lanes with ds_bpermute two steps
+    // ahead, and the chunk data is gathered one step ahead of the evaluation. Unrolled by eight with ping-pong
+    // buffers (A/B data, I1/I2 indices): no register rotation. Padding codes and the target's own entry decode to
+    // the target itself: gathered, not evaluated.
     auto consume = [&](const float4 (&raw)[C], unsigned j)
     {
         float4 o[C];
@@ -761,12 +756,11 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const Coop
         const R rec = coopUnpack<R>(o);
         if (j != pl.self) f(j, rec);
     };
-    unsigned prev = pl.self;
     unsigned D[8];
     // (the block decoded after the last one lies past the list and is never used: not checked)
     auto decodeChecked = [&](int4 w, bool used)
     {
-        decodeBlock(w, prev, pl.self, D);
+        decodeBlock(w, pl.ctab, D);
 #ifdef SPHX_DEVICE_CHECKS
 #pragma unroll
         for (int u = 0; u < 8; ++u)
@@ -798,8 +792,7 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const Coop
             else
             {
                 // steps 6, 7 spread the first two entries of the next block (the target's own record past the list)
-                unsigned p = prev;
-                decodeWord(W.x, p, pl.self, jA, jB);
+                decodeWord(W.x, pl.ctab, jA, jB);
                 jA = more ? pl.checked(jA) : pl.self;
                 jB = more ? pl.checked(jB) : pl.self;
             }

@@ -111,11 +111,10 @@ class HydroCoolingProp(HydroProp):
         t = self.timer
         box = domain.box
         first, last = domain.start_index(), domain.end_index()
-        fused = self._neighbors(domain, d, "rho")
+        self._neighbors(domain, d)
         t.step("FindNeighbors")
         nl = self.nl
-        if not fused:
-            H.compute_density(d, nl, box)
+        H.compute_density(d, nl, box)
         t.step("Density")
         self.cooler.gamma = d.gamma
         self.cooler.eos(d, first, last)

@@ -27,7 +27,6 @@ from ..utils.timer import Timer
 # XMass (STD: density) computed inside the GPU neighbor search instead of a separate pass over the lists. Off by
 # default: measured on Sedov -n 400 the search grows by 26 ms (flush-time kernel evaluations are divergent: a wave
 # evaluates whenever any lane flushes a block) while the XMass pass it replaces costs 11 ms (csrc/hip/neighbors.hip).
-FUSE_XMASS = os.environ.get("SPHX_FUSE_XMASS", "0") == "1"
 
 
 class Propagator:
@@ -73,21 +72,16 @@ class Propagator:
         pass
 
     # ---------------------------------------------------------------------------------------------- shared
-    def _neighbors(self, domain, d, xmass_field: str | None = None):
-        """neighbor search + h iteration; on the GPU ``xmass_field`` is filled by the search itself (XMass fused
-        into its final round, ops/neighbors.py), and the return value says whether that happened"""
+    def _neighbors(self, domain, d):
+        """neighbor search + h iteration"""
         first, last = domain.start_index(), domain.end_index()
-        fuse = xmass_field is not None and d.device.type == "cuda" and FUSE_XMASS
         gpu = d.device.type == "cuda"
         self.nl = find_neighbors(d, domain.octree, domain.box, first, last,
                                  prev=self.nl,  # (not nidx=: an argument would pin the old GPU buffer)
-                                 xmass_out=d[xmass_field] if fuse else None,
-                                 m_uniform=H.uniform_mass(d) if fuse else 0.0,
                                  # global h minimum + mass extremes come back with the search statistics
                                  ride_along=(lambda: H.global_h_min_device(d, domain.comm)) if gpu else None)
         if gpu:
             H.apply_global_h_min(d, self.nl.ride_along)
-        return fuse
 
     def _gravity(self, domain, d):
         if d.g != 0.0:
@@ -192,12 +186,11 @@ class HydroVeProp(Propagator):
         first, last = domain.start_index(), domain.end_index()
         # velocity halos are not read before the IAD loop: their exchange overlaps the search, XMass and Gradh
         vel_halos = domain.exchange_halos_start(d, ["vx", "vy", "vz"])
-        fused = self._neighbors(domain, d, "xm")
+        self._neighbors(domain, d)
         t.step("FindNeighbors")
         nl = self.nl
 
-        if not fused:
-            H.compute_xmass(d, nl, box)
+        H.compute_xmass(d, nl, box)
         t.step("XMass")
         domain.exchange_halos(d, ["xm"])
         t.step("mpi::synchronizeHalos")
@@ -294,11 +287,10 @@ class HydroProp(Propagator):
         box = domain.box
         first, last = domain.start_index(), domain.end_index()
         vel_halos = domain.exchange_halos_start(d, ["vx", "vy", "vz"])  # overlaps the search and density loop
-        fused = self._neighbors(domain, d, "rho")
+        self._neighbors(domain, d)
         t.step("FindNeighbors")
         nl = self.nl
-        if not fused:
-            H.compute_density(d, nl, box)
+        H.compute_density(d, nl, box)
         t.step("Density")
         H.compute_eos_std(d, first, last)
         t.step("EquationOfState")

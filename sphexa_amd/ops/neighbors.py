@@ -7,10 +7,11 @@ loop (the reference GPU path re-traverses the tree in each of its five kernels).
 
 Storage layouts
   * CPU:  ``nidx[(i - first) * ngmax + k]``
-  * HIP:  packed lists (csrc/include/sphx/packed_list.hpp): target groups of 64 consecutive particles (one wave64 per
-          group); per lane 16-bit delta-coded slots, 8 per 16-byte block, 64 lanes' blocks = one 1-KiB row; rows are
-          allocated per group from a pool (group table: row count, row numbers). ~190 B/particle at ng0 100 instead
-          of 608 for int32 lists at the ngmax stride. ``decode_packed`` / ``pack_lists`` are the Python codec.
+  * HIP:  chunk-coded lists (csrc/include/sphx/packed_list.hpp): target groups of 64 consecutive particles (one wave64
+          per group); per lane 16-bit codes (chunk slot | offset) decoded through the group's chunk table, 8 per
+          16-byte block, 64 lanes' blocks = one 1-KiB row; rows are allocated per group from a pool (group table:
+          block count, chunk entries, row numbers). 2 B per entry instead of 4 for int32 lists at the ngmax stride.
+          ``decode_packed`` / ``pack_lists`` are the Python codec.
 ``nc`` (a particle field) counts neighbors *including* self, as in the reference.
 """
 
@@ -50,92 +51,111 @@ class NeighborList:
 
 
 # ------------------------------------------------------------------------------------------- packed list codec
-# mirrors csrc/include/sphx/packed_list.hpp (slot: bit 0 emit flag, bits 1..15 signed step; jumps move by step*2^14)
-SLOT_FINE = 16383
-JUMP_SHIFT = 14
-LIST_JUMP_SLACK = 32
+# mirrors csrc/include/sphx/packed_list.hpp: code = slot | k << 10 -> j = chunk_table[slot] + k; slot 0 = the group's
+# first particle (code lane << 10 is the padding code and decodes to the target itself)
+CHUNK_CAP = 512
+CHUNK_SLOT_BITS = 10
+CHUNK_TAB_ROWS_MAX = (CHUNK_CAP + 255) // 256
+
+
+def list_blocks_max(ngmax: int) -> int:
+    return (ngmax + 1 + 7) // 8
 
 
 def packed_rows_max(ngmax: int) -> int:
-    return (ngmax + LIST_JUMP_SLACK + 7) // 8
+    return list_blocks_max(ngmax) + CHUNK_TAB_ROWS_MAX
 
 
 def packed_table_ints(ngmax: int) -> int:
-    return (packed_rows_max(ngmax) + 3 + 3) & ~3
+    return (2 + packed_rows_max(ngmax) + 2 + 3) & ~3
 
 
 def packed_table_region(groups: int, ngmax: int) -> int:
     return (groups * packed_table_ints(ngmax) + 255) // 256 * 256
 
 
-def encode_step(delta: int) -> list:
-    out = []
-    while delta < -SLOT_FINE - 1 or delta > SLOT_FINE:
-        J = (delta + (1 << (JUMP_SHIFT - 1))) >> JUMP_SHIFT
-        J = max(-SLOT_FINE - 1, min(SLOT_FINE, J))
-        out.append((J * 2) & 0xFFFF)
-        delta -= J << JUMP_SHIFT
-    out.append(((delta * 2) | 1) & 0xFFFF)
-    return out
+def group_rows(tab: torch.Tensor) -> torch.Tensor:
+    """rows used per group from the group tables [G, T] (list blocks + chunk-table rows)"""
+    return tab[:, 0] + (tab[:, 1] >> 16)
 
 
 def pack_lists(lists, first: int, ngmax: int, device=None) -> NeighborList:
-    """packed GPU lists from per-target index lists (target first + t gets lists[t]); rows in group order"""
+    """GPU list buffer from per-target index lists (target first + t gets lists[t], entries in the given order);
+    chunk tables of 64-aligned bases, rows in group order"""
     import numpy as np
     n = len(lists)
     groups = max((n + GROUP - 1) // GROUP, 1)
-    T, region = packed_table_ints(ngmax), packed_table_region(groups, ngmax)
-    lane_slots = []
-    for t, lst in enumerate(lists):
-        prev, sl = first + t, []
-        for j in lst:
-            sl += encode_step(int(j) - prev)
-            prev = int(j)
-        if len(sl) > 8 * packed_rows_max(ngmax):
-            raise ValueError("list too long for the packed rows")
-        lane_slots.append(sl)
-    nrows = [max([(len(s) + 7) // 8 for s in lane_slots[g * GROUP:(g + 1) * GROUP]] + [0]) for g in range(groups)]
+    T_I, region = packed_table_ints(ngmax), packed_table_region(groups, ngmax)
+    per_group = []
+    for g in range(groups):
+        glists = [list(map(int, lists[t])) for t in range(g * GROUP, min((g + 1) * GROUP, n))]
+        if any(len(lst) > 8 * list_blocks_max(ngmax) for lst in glists):
+            raise ValueError("list too long for the list blocks")
+        bases = sorted({j & ~63 for lst in glists for j in lst})
+        if len(bases) + 1 > CHUNK_CAP:
+            raise ValueError("too many chunks for the chunk table")
+        table = [first + g * GROUP] + bases
+        slot = {b: s + 1 for s, b in enumerate(bases)}
+        codes = [[slot[j & ~63] | ((j & 63) << CHUNK_SLOT_BITS) for j in lst] for lst in glists]
+        nblk = max([(len(c) + 7) // 8 for c in codes] + [0])
+        per_group.append((table, codes, nblk))
+    nrows = [-(-len(tb) // 256) + nb for tb, _, nb in per_group]
     total = max(sum(nrows), 1)
     buf = np.zeros(region + total * 256, dtype=np.int32)
-    tab = buf[:groups * T].reshape(groups, T)
+    tab = buf[:groups * T_I].reshape(groups, T_I)
+    rows = buf[region:].reshape(total, 256)
     rows16 = buf[region:].view(np.uint16).reshape(total, GROUP, 8)
     r0 = 0
-    for g in range(groups):
-        tab[g, 0] = nrows[g]
-        tab[g, 1:1 + nrows[g]] = np.arange(r0, r0 + nrows[g])
+    for g, (table, codes, nblk) in enumerate(per_group):
+        T = -(-len(table) // 256)
+        tab[g, 0] = nblk
+        tab[g, 1] = len(table) | (T << 16)
+        tab[g, 2:2 + T + nblk] = np.arange(r0, r0 + T + nblk)
+        for e, v in enumerate(table):
+            rows[r0 + e // 256, e % 256] = v
         for lane in range(GROUP):
-            t = g * GROUP + lane
-            if t >= n:
-                break
-            sl = lane_slots[t]
-            for k, v in enumerate(sl):
-                rows16[r0 + k // 8, lane, k % 8] = v
-        r0 += nrows[g]
+            c = codes[lane] if lane < len(codes) else []
+            # padding decodes to the target itself; lanes past the last target to the last target (a valid record)
+            pad = lane if lane < len(codes) else len(codes) - 1
+            c = c + [pad << CHUNK_SLOT_BITS] * (8 * nblk - len(c))
+            for k, v in enumerate(c):
+                rows16[r0 + T + k // 8, lane, k % 8] = v
+        r0 += T + nblk
     out = torch.from_numpy(buf)
     return NeighborList(out.to(device) if device is not None else out, first, first + n, ngmax, True, total)
 
 
 def decode_packed(nl: NeighborList):
-    """(indices int64 [n, S], valid bool [n, S]) of a packed list: slot k of target first + t"""
+    """(indices int64 [n, S], valid bool [n, S]) of a GPU list buffer: entry k of target first + t (padding and the
+    target's own entry are not valid)"""
     buf = nl.nidx.cpu()
     n = nl.last - nl.first
     groups = max((n + GROUP - 1) // GROUP, 1)
-    T, region = packed_table_ints(nl.ngmax), packed_table_region(groups, nl.ngmax)
-    tab = buf[:groups * T].view(groups, T).long()
-    nrows = tab[:, 0]
-    R = max(int(nrows.max()), 1)
-    rows = tab[:, 1:1 + R]
-    data = buf[region:].view(-1, GROUP, 4)
-    blk = data[rows.clamp(0, data.shape[0] - 1)].contiguous()  # (groups, R, 64, 4)
-    slots = blk.view(torch.int16).permute(0, 2, 1, 3).reshape(groups, GROUP, R * 8).long()
-    live = (torch.arange(R * 8) // 8).view(1, 1, -1) < nrows.view(-1, 1, 1)
-    slots = torch.where(live, slots, 0).reshape(groups * GROUP, R * 8)
-    e = (slots & 1) == 1
-    d = slots >> 1
-    inc = torch.where(e, d, d << JUMP_SHIFT)
-    self_idx = nl.first + torch.arange(groups * GROUP, dtype=torch.int64)
-    idx = self_idx.view(-1, 1) + torch.cumsum(inc, dim=1)
-    return idx[:n], e[:n]
+    T_I, region = packed_table_ints(nl.ngmax), packed_table_region(groups, nl.ngmax)
+    tab = buf[:groups * T_I].view(groups, T_I).long()
+    nblk = tab[:, 0]
+    nch = tab[:, 1] & 0xFFFF
+    T = tab[:, 1] >> 16
+    R = max(int(nblk.max()), 1)
+    data = buf[region:].view(-1, 256)
+    nrows_all = data.shape[0]
+    # chunk tables [G, 256 * max T]
+    TM = max(int(T.max()), 1)
+    trow = tab[:, 2:2 + TM].clamp(0, nrows_all - 1)
+    ctab = data[trow].reshape(groups, TM * 256).long()
+    ctab = torch.where(torch.arange(TM * 256).view(1, -1) < nch.view(-1, 1), ctab, 0)
+    # list blocks [G, R, 64, 8] codes
+    bidx = (2 + T.view(-1, 1) + torch.arange(R).view(1, -1)).clamp(max=T_I - 1)
+    brow = torch.gather(tab, 1, bidx).clamp(0, nrows_all - 1)
+    codes = data[brow].view(torch.int16).view(groups, R, GROUP, 8).long() & 0xFFFF
+    codes = codes.permute(0, 2, 1, 3).reshape(groups, GROUP, R * 8)
+    slot = (codes & (CHUNK_CAP - 1)).clamp(max=TM * 256 - 1)  # (blocks past nblk hold other rows: masked below)
+    k = codes >> CHUNK_SLOT_BITS
+    idx = torch.gather(ctab, 1, slot.view(groups, -1)).view(groups, GROUP, R * 8) + k
+    live = (torch.arange(R * 8) // 8).view(1, 1, -1) < nblk.view(-1, 1, 1)
+    self_idx = (nl.first + torch.arange(groups * GROUP, dtype=torch.int64)).view(groups, GROUP, 1)
+    valid = live & (idx != self_idx)
+    return idx.reshape(groups * GROUP, R * 8)[:n], valid.reshape(groups * GROUP, R * 8)[:n]
 
 
 class NeighborSearchError(RuntimeError):
@@ -172,12 +192,12 @@ def _scratch(nbytes: int, device) -> torch.Tensor:
 
 
 def _pool_plan(prev: NeighborList | None, groups: int, ng0: int, stripes: int):
-    """(home rows per group, rows per overflow stripe) of the packed-list pool: the previous search's choice for
-    this group count, else ng0/8 home rows and 0.35 ng0/8 overflow rows per group (on lattices the neighbor count
-    jumps to ~1.3 ng0 at shell steps)"""
+    """(home rows per group, rows per overflow stripe) of the list-row pool: the previous search's choice for this
+    group count, else ng0/8 + 1 home rows (list blocks + one chunk-table row) and 0.35 ng0/8 overflow rows per group
+    (on lattices the neighbor count jumps to ~1.3 ng0 at shell steps)"""
     if prev is not None and prev.grouped and prev.plan is not None and prev.plan[0] == groups:
         return prev.plan[1], prev.plan[2]
-    return max(1, round(ng0 / 8)), max(8, -(-int(0.35 * ng0 / 8 * groups + 0.5) // stripes))
+    return max(1, round(ng0 / 8) + 1), max(8, -(-int(0.35 * ng0 / 8 * groups + 0.5) // stripes))
 
 
 def _next_plan(buf: torch.Tensor, groups: int, ngmax: int, home: int, stripes: int):
@@ -185,7 +205,7 @@ def _next_plan(buf: torch.Tensor, groups: int, ngmax: int, home: int, stripes: i
     the fewest rows (home rows of every group + stripe capacity for the longest stripe's overflow, +10 %); returns
     device tensors [5] of (home candidates, total rows)"""
     T = packed_table_ints(ngmax)
-    nr = buf[:groups * T].view(groups, T)[:, 0].to(torch.int32)
+    nr = group_rows(buf[:groups * T].view(groups, T)).to(torch.int32)
     pad = (-groups) % stripes
     if pad:
         nr = torch.cat([nr, torch.zeros(pad, dtype=torch.int32, device=nr.device)])
@@ -197,13 +217,10 @@ def _next_plan(buf: torch.Tensor, groups: int, ngmax: int, home: int, stripes: i
 
 
 def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
-                   nidx: torch.Tensor | None = None, xmass_out: torch.Tensor | None = None,
-                   m_uniform: float = 0.0, prev: NeighborList | None = None, ride_along=None) -> NeighborList:
+                   nidx: torch.Tensor | None = None, prev: NeighborList | None = None,
+                   ride_along=None) -> NeighborList:
     """search neighbors of particles [first, last) within 2h, adjusting h towards ng0 neighbors.
 
-    ``xmass_out`` (GPU only): also compute the VE XMass loop's xm = m / rho0 (reference xmass_kern.hpp) inside the
-    search from the distances of the stored entries (``m_uniform`` > 0: common mass, else per-particle masses), so
-    the separate XMass pass over the lists is skipped.
     ``prev``: the previous step's lists; on the GPU its buffer is reused when it has the right size.
     ``ride_along`` (GPU): a callable returning a float64 device tensor computed after the search; its values reach
     the host in the same copy as the search statistics (``NeighborList.ride_along``), saving a synchronization.
@@ -217,7 +234,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         hp = _lib.hip()
         num_groups = max((n + GROUP - 1) // GROUP, 1)
         if packed_table_ints(ngmax) > 64:
-            raise ValueError(f"ngmax {ngmax} too large for the packed GPU lists (at most {8 * 62 - LIST_JUMP_SLACK - 8})")
+            raise ValueError(f"ngmax {ngmax} too large for the GPU lists")
         region = packed_table_region(num_groups, ngmax)
         K = hp.neighbor_row_stripes()
         home, ov = _pool_plan(prev, num_groups, d.ng0, K)
@@ -240,10 +257,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
                               d.ng0, ngmax, buf.data_ptr(), nc.data_ptr(),
                               int(iterate_h) | (2 if COLLECT_STATS else 0), stats.data_ptr(),
-                              scratch.data_ptr(), TEST_FRONT_CAP, _stream(),
-                              xm=xmass_out.data_ptr() if xmass_out is not None else 0, m=d["m"].data_ptr(),
-                              m_uniform=float(m_uniform), wh=d.wh.data_ptr(), consts=d.consts_array(),
-                              home=home, ov_stride=ov)
+                              scratch.data_ptr(), TEST_FRONT_CAP, _stream(), home=home, ov_stride=ov)
             ctr = stats[8::32][:K]
             cand, cand_ov, cand_rows = _next_plan(buf, num_groups, ngmax, home, K)
             # evaluated once per call (it may issue a collective, so every rank calls it exactly once); a repeated
@@ -281,9 +295,9 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         plan = (num_groups, plan_home, plan_ov)
         if int(st[1]) > 0:
             raise NeighborSearchError(f"GPU traversal stack overflow in {int(st[1])} groups")
-        if int(st[5]) > 0 and not ALLOW_NC_FAIL:
-            raise NeighborSearchError(f"{int(st[5])} neighbor lists exceed the packed rows (ngmax {ngmax} + "
-                                      f"{LIST_JUMP_SLACK} jump slots)")
+        if int(st[6]) > 0:
+            raise NeighborSearchError(f"{int(st[6])} target groups touch more than {CHUNK_CAP - 1} source chunks "
+                                      f"(chunk-table capacity of the GPU lists)")
         _check_convergence(d, int(st[0]))
         d.nc_spilled = int(st[2])
         d.nc_rounds = int(st[3]) / num_groups  # mean search rounds per group (h iteration)

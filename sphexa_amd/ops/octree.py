@@ -51,6 +51,12 @@ class Octree:
     def device(self):
         return self.tree.device
 
+    def to(self, device) -> "Octree":
+        """copy with every tensor on ``device`` (e.g. a host copy of a GPU tree for CPU oracles)"""
+        import dataclasses
+        return dataclasses.replace(self, **{f.name: getattr(self, f.name).to(device) for f in dataclasses.fields(self)
+                                            if isinstance(getattr(self, f.name), torch.Tensor)})
+
     def max_depth(self) -> int:
         for l in range(MAX_LEVEL, -1, -1):
             if self.level_range[l + 1] > self.level_range[l]:

@@ -31,3 +31,7 @@ def test_bench_json_contract(gpus):
     assert out["steps"] == 2 and out["warmup"] == 1 and out["value"] > 0
     assert out["config"]["global_batch"] == 12**3
     assert abs(out["value"] - 12**3 * 1000.0 / out["ms_per_step"]) < 1e-6 * out["value"]
+    # the second headline config (Evrard with self-gravity) is timed in the same invocation
+    assert out["evrard_value"] > 0 and out["evrard_ms_per_step"] > 0 and out["evrard_particles"] > 0
+    assert abs(out["evrard_value"] - out["evrard_particles"] * 1000.0 / out["evrard_ms_per_step"]) < \
+        1e-6 * out["evrard_value"]

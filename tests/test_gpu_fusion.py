@@ -1,5 +1,5 @@
-"""Fused GPU paths vs their unfused forms (same inputs): the XMass sum inside the neighbor search, and the AV switches
-on vd = vol*divv records with the IAD loop's S_i (sph_math.hpp SrcAvV). Tolerances: fp32 summation-order level."""
+"""GPU paths vs their reference forms (same inputs): the h-iterating search vs the CPU search, and the AV switches on
+vd = vol*divv records with the IAD loop's S_i (sph_math.hpp SrcAvV). Tolerances: fp32 summation-order level."""
 
 import pytest
 import torch
@@ -38,21 +38,22 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("mass_spread,h_scale", [(0.0, 1.0), (0.1, 1.0), (0.0, 1.35)])
-def test_fused_xmass_matches_loop(gpu, mass_spread, h_scale):
-    """h_scale 1.35 starts far from ng0 neighbors: several h-iteration rounds, the sum must be the final round's"""
+def test_search_h_iteration_matches_cpu(gpu, mass_spread, h_scale):
+    """h_scale 1.35 starts far from ng0 neighbors: several h-iteration rounds whose chunk tables and list blocks are
+    rewritten in place; the final lists and counts must equal the CPU search at the final h"""
     d, prop, dom = _setup(gpu, mass_spread=mass_spread, h_scale=h_scale)
-    h0 = d["h"].clone()
-    nl = find_neighbors(d, dom.octree, dom.box, dom.start_index(), dom.end_index(), xmass_out=d["xm"],
-                        m_uniform=H.uniform_mass(d))
-    xm_fused = d["xm"].clone()
-    nc_f, h_f = d["nc"].clone(), d["h"].clone()
-    d["xm"].zero_()
-    d["h"].copy_(h0)
-    nl2 = find_neighbors(d, dom.octree, dom.box, dom.start_index(), dom.end_index())
-    assert torch.equal(d["nc"], nc_f) and torch.equal(d["h"], h_f)
-    assert neighbor_lists_as_sets(nl, nc_f) == neighbor_lists_as_sets(nl2, d["nc"])
-    H.compute_xmass(d, nl2, dom.box)
-    assert _rel(xm_fused, d["xm"]) < 3e-6
+    dc, propc, domc = _setup("cpu", mass_spread=mass_spread, h_scale=h_scale)
+    assert torch.equal(dc["keys"], d["keys"].cpu())
+    nl = find_neighbors(d, dom.octree, dom.box, dom.start_index(), dom.end_index())
+    # the CPU oracle searches at the GPU's final h (the h iteration's float pow differs by an ulp between host and
+    # device, which can move a boundary neighbor after several rounds)
+    assert torch.allclose(dc["h"], d["h"].cpu(), rtol=1e-3) or h_scale != 1.0
+    dc["h"] = d["h"].cpu()
+    nlc = find_neighbors(dc, domc.octree, domc.box, domc.start_index(), domc.end_index(), iterate_h=False)
+    assert torch.equal(dc["nc"], d["nc"].cpu())
+    assert neighbor_lists_as_sets(nl, d["nc"]) == neighbor_lists_as_sets(nlc, dc["nc"])
+    H.compute_xmass(d, nl, dom.box)
+    assert torch.isfinite(d["xm"]).all()
 
 
 def test_av_vd_records_match_loop(gpu):

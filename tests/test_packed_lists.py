@@ -1,12 +1,13 @@
-"""Packed GPU neighbor-list codec (csrc/include/sphx/packed_list.hpp; Python mirror in ops/neighbors.py): 16-bit
-delta slots with jump slots for large steps, per-group rows. The GPU search writes this format and the pair loops
-decode it (tests/test_gpu_parity.py compares the decoded GPU lists with the CPU search)."""
+"""Chunk-coded GPU neighbor-list codec (csrc/include/sphx/packed_list.hpp; Python mirror in ops/neighbors.py): 16-bit
+codes slot | k << 10 decoded through a per-group chunk table (slot 0 = the group's first particle, so padding decodes
+to the target itself), 8 codes per lane and block, one 1-KiB row per block index of a group. The GPU search writes
+this format and the pair loops decode it (tests/test_gpu_parity.py compares the decoded GPU lists with the CPU search)."""
 
 import numpy as np
 import pytest
 
-from sphexa_amd.ops.neighbors import (GROUP, decode_packed, encode_step, pack_lists, packed_rows_max,
-                                      packed_table_ints)
+from sphexa_amd.ops.neighbors import (CHUNK_CAP, GROUP, decode_packed, group_rows, list_blocks_max, pack_lists,
+                                      packed_rows_max, packed_table_ints)
 
 
 def _roundtrip(lists, first, ngmax=150):
@@ -17,14 +18,6 @@ def _roundtrip(lists, first, ngmax=150):
     return nl, idx, valid
 
 
-def test_small_steps_one_slot_each():
-    for d in (1, -1, 16383, -16384, 7, -300):
-        assert len(encode_step(d)) == 1
-    for d in (16384, -16385, 1 << 27, -(1 << 27)):
-        assert len(encode_step(d)) == 2
-    assert len(encode_step(1 << 30)) >= 3  # beyond one jump's +-2^28
-
-
 def test_roundtrip_random_lists():
     rng = np.random.default_rng(3)
     first = 1000
@@ -33,26 +26,46 @@ def test_roundtrip_random_lists():
     for t in range(n):
         k = int(rng.integers(0, 120))
         near = first + t + rng.integers(-3000, 3000, size=k)
-        far = rng.integers(0, 1 << 30, size=int(rng.integers(0, 4)))
-        lst = np.unique(np.concatenate([near, far]).clip(0, None))
+        lst = np.unique(near.clip(0, None))
         lst = lst[lst != first + t][:140]
         lists.append(lst.tolist())
     nl, idx, valid = _roundtrip(lists, first)
-    assert nl.rows_used <= n * packed_rows_max(150)
+    assert nl.rows_used <= ((n + GROUP - 1) // GROUP) * packed_rows_max(150)
 
 
-def test_unsorted_and_descending_entries():
+def test_unsorted_and_far_entries():
     _roundtrip([[5, 2, 900000, 1, 2 ** 31 - 2, 3], [], [7]], first=10)
+
+
+def test_padding_and_self_entries_are_not_valid():
+    lists = [[0, 3]] * 3  # target 0 lists itself: the codec keeps it, the decoder reports it as the target
+    nl = pack_lists(lists, 0, 150)
+    idx, valid = decode_packed(nl)
+    assert idx[0][valid[0]].tolist() == [3]
+    assert idx[1][valid[1]].tolist() == [0, 3]
+    # padding past the two entries decodes to the target itself
+    assert (idx[2][2:8] == 2).all() and not valid[2][2:8].any()
 
 
 def test_rows_follow_the_longest_lane_of_a_group():
     lists = [[1]] * GROUP
-    lists[5] = list(range(100, 130))  # 30 entries -> 4 rows of 8 slots
+    lists[5] = list(range(100, 130))  # 30 entries -> 4 list blocks, + 1 chunk-table row
     nl = pack_lists(lists, 0, 150)
-    assert nl.nidx[0].item() == 4 and nl.rows_used == 4
+    assert nl.nidx[0].item() == 4 and nl.rows_used == 5
+    T = packed_table_ints(150)
+    assert group_rows(nl.nidx[:T].view(1, T)).item() == 5
     assert packed_table_ints(150) % 4 == 0
 
 
-def test_list_too_long_is_rejected():
+def test_chunk_table_over_one_row():
+    # 300 distinct 64-aligned chunks in one group: the table takes two rows
+    lists = [[64 * k for k in range(300)][t::GROUP] for t in range(GROUP)]
+    nl, _, _ = _roundtrip(lists, 10 ** 6)
+    assert (nl.nidx[1].item() >> 16) == 2
+
+
+def test_limits_are_rejected():
     with pytest.raises(ValueError):
-        pack_lists([list(range(1, 2 ** 30, 2 ** 22))], 0, 150)  # 256 jump+emit pairs
+        pack_lists([list(range(0, 8 * list_blocks_max(150) + 1))], 0, 150)
+    with pytest.raises(ValueError):
+        pack_lists([[64 * k for k in range(CHUNK_CAP)]], 0, 150)
