@@ -177,20 +177,22 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("find_neighbors",
           [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr h, int64_t numNodes, Ptr child, Ptr n2l, Ptr ns,
              Ptr ne, Ptr center, Ptr half, const BoxArr& box, unsigned ng0, unsigned ngmax, Ptr nidx, Ptr nc,
-             int iterateH, Ptr stats, Ptr scratch, int testFrontCap, Ptr s, int home, int ovStride)
+             int iterateH, Ptr stats, Ptr scratch, int testFrontCap, Ptr s, int home, int ovStride, Ptr mm,
+             int64_t ntot, Ptr rec)
           {
               (void)numNodes;
               NsTree t{P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne), P<double>(center),
                        P<double>(half)};
               findNeighbors(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(h), t, toBox(box), ng0,
                             ngmax, P<int32_t>(nidx), home, ovStride, P<int32_t>(nc), iterateH,
-                            P<unsigned long long>(stats), P<void>(scratch), testFrontCap, St(s));
+                            P<unsigned long long>(stats), P<void>(scratch), testFrontCap, P<float>(mm), ntot,
+                            P<void>(rec), St(s));
           },
           py::arg("first"), py::arg("last"), py::arg("x"), py::arg("y"), py::arg("z"), py::arg("h"),
           py::arg("numNodes"), py::arg("child"), py::arg("n2l"), py::arg("ns"), py::arg("ne"), py::arg("center"),
           py::arg("half"), py::arg("box"), py::arg("ng0"), py::arg("ngmax"), py::arg("nidx"), py::arg("nc"),
           py::arg("iterateH"), py::arg("stats"), py::arg("scratch"), py::arg("testFrontCap"), py::arg("s"),
-          py::arg("home") = 0, py::arg("ov_stride") = 1);
+          py::arg("home") = 0, py::arg("ov_stride") = 1, py::arg("m") = 0, py::arg("ntot") = 0, py::arg("rec") = 0);
     m.def("neighbor_row_stripes", []() { return neighborRowStripes(); });
     m.def("packed_table_ints", [](unsigned ngmax) { return packedTableInts(ngmax); });
     m.def("packed_rows_max", [](unsigned ngmax) { return packedRowsMax(ngmax); });

@@ -30,7 +30,8 @@
  *  a corrupted input is reported by the host after the step (ops/_lib.py: raise_on_device_check) instead of faulting
  *  the GPU. Compiled out otherwise.
  *  bits: 0 neighbor index >= record count, 1 packed-list rows of a group > rowsMax, 2 gather permutation index out of
- *        range, 3 gravity interaction list longer than its slab, 4 halo pack index out of range */
+ *        range, 3 gravity interaction list longer than its slab, 4 halo pack index out of range, 5 search band
+ *        re-test source index out of range */
 #ifdef SPHX_DEVICE_CHECKS
 namespace sphx::hip
 {

@@ -89,7 +89,10 @@ size_t neighborScratchBytes(int64_t n, unsigned ngmax);
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int home,
                    int ovStride, int32_t* nc, int iterateH, unsigned long long* stats, void* scratch,
-                   int testFrontCap, hipStream_t s);
+                   int testFrontCap, const float* m, int64_t ntot, void* rec, hipStream_t s);
+//! fixed-point {x, y, z, m} records (QFrame of the box) of particles [0, n): the search and the XMass loop read them
+void packPosQ(int64_t n, const double* x, const double* y, const double* z, const float* m, const QFrame& q,
+              SrcPosQ* out, hipStream_t s);
 //! overflow-row stripes of the packed-list pool; stats must hold 8 + 32 * stripes counters
 int neighborRowStripes();
 

@@ -766,6 +766,14 @@ __global__ void conservedKernel(int64_t first, int64_t last, const double* __res
 
 // --------------------------------------------------------------------------------------------------- launchers
 
+void packPosQ(int64_t n, const double* x, const double* y, const double* z, const float* m, const QFrame& q,
+              SrcPosQ* out, hipStream_t s)
+{
+    if (n <= 0) return;
+    packPosQKernel<<<gridFor(n, 256), 256, 0, s>>>(n, x, y, z, m, q, out);
+    SPHX_LAUNCH_CHECK();
+}
+
 void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x, const double* y,
            const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s)
 {

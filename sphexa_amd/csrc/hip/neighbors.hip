@@ -40,15 +40,33 @@
 namespace sphx::hip
 {
 
-constexpr int kWavesPerBlock = 4;
+// one wave (target group) per block: a block's LDS and wave slots are released when its last wave finishes, and the
+// groups of one block take very different times (A/B Sedov -n 400 search: 4 waves/block 43.4 ms, 1 wave 32.4 ms)
+#ifndef SPHX_NS_WPB
+#define SPHX_NS_WPB 1
+#endif
+constexpr int kWavesPerBlock = SPHX_NS_WPB;
 constexpr int kFrontCap      = 512;
-constexpr int kLeafCap       = 512; // LDS candidate-leaf list per wave (A/B: 1024 costs occupancy, 512 spills few groups)
+// 256 candidate leaves + <= 96 VGPRs: 7.5 KiB LDS per wave, 5 waves per SIMD (A/B: 32.4 -> 29.4 ms)
+#ifndef SPHX_NS_LEAFCAP
+#define SPHX_NS_LEAFCAP 256
+#endif
+#ifndef SPHX_NS_ROUNDED // rounded core-box prefilter of the staged candidates
+#define SPHX_NS_ROUNDED 1
+#endif
+#ifndef SPHX_NS_DOT // dot-product form of the candidate test
+#define SPHX_NS_DOT 1
+#endif
+#ifndef SPHX_NS_WAVES_EU
+#define SPHX_NS_WAVES_EU 5
+#endif
+constexpr int kLeafCap = SPHX_NS_LEAFCAP; // LDS candidate-leaf list per wave (overflowing groups take the spill path)
 constexpr int kRing          = 16;  // hit-ring entries per lane (two list blocks)
 constexpr int kStagePairs    = 64;  // staged candidate pairs (128 candidates)
 constexpr int kCbase         = 128; // chunk bases of the most recent slots (band re-test: the staging window spans
                                     // at most 128 chunks with candidates)
 constexpr int kRingWords     = kRing * 64;
-constexpr int kStageWords    = kStagePairs * 8;
+constexpr int kStageWords    = kStagePairs * 10; // per 2 pairs {x0 x1 y0 y1} {z0 z1 cc0 cc1} x2 + 4 codes
 constexpr int kCandWords     = kRingWords + kStageWords + kCbase;
 //! per-wave LDS work area: the traversal frontiers, then (candidate phase) ring + staging + chunk bases
 constexpr int kWorkWords = 2 * kFrontCap > kCandWords ? 2 * kFrontCap : kCandWords;
@@ -172,6 +190,7 @@ __device__ __forceinline__ bool boxesOverlapF(const double c1[3], const double s
 template<bool kSpill, bool kCapped>
 __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t last, const double* __restrict__ x,
                                             const double* __restrict__ y, const double* __restrict__ z,
+                                            const SrcPosQ* __restrict__ xq, const QFrame& qf, uint32_t ntot,
                                             float* __restrict__ h, const NsTree& tree, const Box& box, unsigned ng0,
                                             unsigned ngmax, const PackedOut& po, int32_t* __restrict__ nc,
                                             int iterateH, unsigned long long* __restrict__ stats, int32_t* frontA,
@@ -185,13 +204,20 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     const bool valid    = i < last;
     double xi = 0, yi = 0, zi = 0;
     float hi  = 0;
+    uint32_t qi[3] = {0, 0, 0};
     if (valid)
     {
         xi = x[i];
         yi = y[i];
         zi = z[i];
         hi = h[i];
+        const SrcPosQ r = xq[i];
+        qi[0] = r.x;
+        qi[1] = r.y;
+        qi[2] = r.z;
     }
+    // one coordinate quantum (largest dimension): the fixed-point positions carry at most this error
+    const float qmax = fmaxf(qf.inv[0], fmaxf(qf.inv[1], qf.inv[2]));
     // candidate-phase LDS (aliases the frontiers): hit ring [kRing][64], staging pairs, chunk bases
     uint32_t* ring     = reinterpret_cast<uint32_t*>(work);
     float* stage       = reinterpret_cast<float*>(work + kRingWords);
@@ -206,6 +232,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
 
     RowAlloc ra;
     unsigned ncSph = 1, cnt = 0, fb = 0, T = 0, slot = 1, nT = 0;
+    unsigned long long nStagedLast = 0, nSubLast = 0;
     uint32_t selfCode = padCode;
     int round = 0;
     bool chunkOvf = false;
@@ -277,13 +304,21 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
             R = fmax(R, gs[d]);
             if (box.bc[d] == kPeriodic && 2.0 * gs[d] > 0.45 * box.len(d)) relOk = false;
         }
-        const float xir = float(fold(xi - gc[0], 0));
-        const float yir = float(fold(yi - gc[1], 1));
-        const float zir = float(fold(zi - gc[2], 2));
+        // group frame from the fixed-point positions (QFrame): int32 difference to the quantized group center (in
+        // periodic dimensions the wrapping difference is the minimum image), one fp32 rounding
+        uint32_t gq[3];
+        for (int d = 0; d < 3; ++d)
+            gq[d] = uint32_t(__builtin_amdgcn_readfirstlane(int(quantize(gc[d], qf.lo[d], qf.s[d]))));
+        const float xir = float(int32_t(qi[0] - gq[0])) * qf.inv[0];
+        const float yir = float(int32_t(qi[1] - gq[1])) * qf.inv[1];
+        const float zir = float(int32_t(qi[2] - gq[2])) * qf.inv[2];
         const float r2f = 4.0f * hi * hi;
-        // rounding of the fp32 distance^2 around the radius: coordinates carry |err| <= delta each
-        const float delta = float(R) * 6.0e-7f + 1e-30f;
-        const float band  = relOk ? 8.0f * hi * delta + 4.0f * delta * delta : 3.4e38f;
+        // rounding of the fp32 distance^2 around the radius: coordinates carry |err| <= delta each (quantization of
+        // the positions + fp32 rounding of the separation)
+        const float delta = float(R) * 6.0e-7f + qmax + 1e-30f;
+        // (without a valid fp32 frame every candidate takes the fp64 test; the bound stays finite so that the +inf
+        // staging sentinels never do)
+        const float band  = relOk ? 8.0f * hi * delta + 4.0f * delta * delta : 1.0e37f;
         const double radiusSq = double(r2f);
         // thresholds: d2 < lo is a hit, lo <= d2 <= hi goes to the fp64 re-test; lanes past the group never hit
         const float thLo = valid ? r2f - band : -1.0f;
@@ -291,6 +326,46 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         const double ip[3] = {xi, yi, zi};
         // group search box half sizes in the relative fp32 frame, widened by the coordinate rounding
         const float gsf[3] = {float(gs[0]) + 2.0f * delta, float(gs[1]) + 2.0f * delta, float(gs[2]) + 2.0f * delta};
+        // rounded core box: the box of the group's particles (relative frame) grown by the largest search radius with
+        // rounded edges and corners. Any neighbor of any lane lies inside it; it excludes the corners of the group
+        // search box that no sphere reaches (~23 % of the candidates of a compact lattice group), at a few VALU per
+        // 64 sources in the staging instead of a full test step per candidate
+        float ccr[3], csr[3];
+        {
+            const float pr[3] = {xir, yir, zir};
+            for (int d = 0; d < 3; ++d)
+            {
+                const float a = waveMin(valid ? pr[d] : 3.4e38f), b = waveMax(valid ? pr[d] : -3.4e38f);
+                ccr[d]        = 0.5f * (a + b);
+                csr[d]        = 0.5f * (b - a) + 2.0f * delta;
+            }
+        }
+        const float rcore  = 2.0f * waveMax(valid ? hi : 0.0f) + 4.0f * delta;
+        const float rcore2 = rcore * rcore;
+        // statistics (opt-in): rounded boxes of the eight 8-lane sub-groups (what-if filter, counted only)
+        float sbc[3] = {0, 0, 0}, sbh[3] = {0, 0, 0}, sbr = 0;
+        unsigned long long nStaged = 0, nSub = 0;
+#ifdef SPHX_NS_STATS
+        if (iterateH & 2)
+        {
+            const float pr[3] = {xir, yir, zir};
+            for (int d = 0; d < 3; ++d)
+            {
+                float a = valid ? pr[d] : 3.4e38f, b = valid ? pr[d] : -3.4e38f;
+                for (int o = 1; o < 8; o <<= 1)
+                {
+                    a = fminf(a, __shfl_xor(a, o));
+                    b = fmaxf(b, __shfl_xor(b, o));
+                }
+                sbc[d] = 0.5f * (a + b);
+                sbh[d] = 0.5f * (b - a) + 2.0f * delta;
+            }
+            float hm = valid ? hi : 0.0f;
+            for (int o = 1; o < 8; o <<= 1)
+                hm = fmaxf(hm, __shfl_xor(hm, o));
+            sbr = 2.0f * hm + 4.0f * delta;
+        }
+#endif
 
         // 3. touched leaves, compacted in place; chunk count -> rows of the chunk table
         {
@@ -331,83 +406,179 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         fb       = 0;
         slot     = 1;
         selfCode = padCode;
-        // store one block (8 ring entries from ring slot s0, entries k >= nv replaced by the padding code) for every
-        // lane in `who`
-        unsigned cnt8 = 0; // entries << 8
-        const unsigned cap8 = cap << 8;
+        // Hit ring: linear, [slot][lane] (a store's bank is its lane whatever the slot). wp = this lane's byte address
+        // of its next free slot, so an append is one ds_write + one v_add. A flush stores slots 0..7 as one list
+        // block and moves slots 8..15 down.
+        typedef __attribute__((address_space(3))) uint32_t LdsU32;
+        const uint32_t laneBase = uint32_t(reinterpret_cast<uintptr_t>((LdsU32*)(ring + lane)));
+        uint32_t wp             = laneBase;
+        const uint32_t wFlush   = laneBase + 12u * 256u; // a lane at 12 pending entries triggers a flush
+        unsigned fbDrop = 0; // blocks of a lane past its list capacity (a round that repeats): counted, not stored
+        unsigned extra  = 0; // capped lists (no h iteration): hits past the cap, counted, not stored
+        // rows: home rows exist without atomics; more only when a flush might need them
+        ra.ensure(min(po.home, po.rowsMax), g, po);
+        ra.ensure(T, g, po);
+        unsigned flushes = 0; // flush events of this round (a lane's block count is at most this)
+        // store one block (ring slots 0..7, slots k >= nv replaced by the padding code) for every lane in `who` and
+        // shift its remaining entries down
         auto storeBlock = [&](bool who, unsigned nv)
         {
-            who                 = who && fb < blocksMax;
-            const unsigned need = T + unsigned(__builtin_amdgcn_readfirstlane(waveMax(int(who ? fb + 1 : 0u))));
-            ra.ensure(need, g, po);
-            const unsigned s0 = (8 * fb) & (kRing - 1);
-            uint32_t e[8];
+            const bool can = who && fb < blocksMax;
+            ++flushes;
+            if (T + flushes > ra.n) // (rare: past the home rows) exact need
+                ra.ensure(T + unsigned(__builtin_amdgcn_readfirstlane(waveMax(int(who ? fb + 1 : 0u)))), g, po);
+            uint32_t e[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                e[k] = *reinterpret_cast<LdsU32*>(uintptr_t(laneBase + 256u * k));
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-            {
-                const uint32_t v = ring[(s0 + k) * 64 + lane];
-                e[k]             = unsigned(k) < nv ? v : padCode;
-            }
-            const unsigned rw = ra.row(T + fb);
-            if (who && rw < po.poolRows)
+                e[k] = unsigned(k) < nv ? e[k] : padCode;
+            const unsigned ord = T + fb;
+            const unsigned rw  = ballot(can && ord >= po.home) ? ra.row(ord) : unsigned(g) * po.home + ord;
+            if (can && rw < po.poolRows)
                 po.rows[size_t(rw) * 64 + lane] = make_int4(int(e[0] | e[1] << 16), int(e[2] | e[3] << 16),
                                                             int(e[4] | e[5] << 16), int(e[6] | e[7] << 16));
-            fb += who ? 1u : 0u;
+            if (who)
+            {
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    *reinterpret_cast<LdsU32*>(uintptr_t(laneBase + 256u * k)) = e[8 + k];
+                wp -= 8u * 256u;
+                if (can) fb += 1;
+                else fbDrop += 1;
+            }
         };
-        // test `count` (a multiple of 4) staged candidates against every lane; one flush check per four candidates
-        // (pending <= 11 after a check, <= 15 before the next: fits the ring)
-        unsigned sHead = 0, sTail = 0; // wave-uniform candidate positions in the staging ring
-        const f2 xr2 = {xir, xir}, yr2 = {yir, yir}, zr2 = {zir, zir};
-        // hit ring address of the lane's next entry: cnt8 = cnt << 8 is the byte offset of ring slot cnt & 15 in the
-        // [slot][lane] layout; entries past the cap land in the slot after the last pending one (never stored)
-        char* ringLane = reinterpret_cast<char*>(ring + lane);
-        auto testOne   = [&](float d2, uint32_t code)
+        // staging: groups of four candidates (two pairs) as five float4 {x0 x1 y0 y1} {z0 z1 cc0 cc1} x2 + {codes},
+        // so one pointer walks a test with immediate offsets
+        auto stagePut = [&](unsigned p, float xr, float yr, float zr, uint32_t code)
         {
-            bool hit        = d2 < thLo;
-            const bool band = d2 <= thHi; // hit implies band
-            if (ballot(band) != ballot(hit)) // rare: fp64 re-test of candidates in the rounding band
+            const unsigned q = (p >> 2) & (kStagePairs / 2 - 1), r = p & 3;
+            float* e         = stage + q * 20 + (r >> 1) * 8 + (r & 1);
+            e[0]             = xr;
+            e[2]             = yr;
+            e[4]             = zr;
+            e[6]             = xr * xr + yr * yr + zr * zr;
+            reinterpret_cast<uint32_t*>(stage)[q * 20 + 16 + r] = code;
+        };
+        unsigned sHead = 0, sTail = 0; // wave-uniform candidate positions in the staging ring
+        // dot-product form of the distance test: d2 = cc_j - 2 c_j.x_i + |x_i|^2 with cc_j = |c_j|^2 staged per
+        // candidate, so a pair of candidates costs three v_pk_fma_f32 and |x_i|^2 moves into the thresholds. The
+        // cancellation (terms up to the squared group extent Rg^2) widens the rounding band by 8 ulp of 4 Rg^2; the fp64
+        // re-test keeps the sets exact
+        const f2 mx2 = {-2.0f * xir, -2.0f * xir}, my2 = {-2.0f * yir, -2.0f * yir}, mz2 = {-2.0f * zir, -2.0f * zir};
+        const float ii  = xir * xir + yir * yir + zir * zir;
+        const float rg2 = float(gs[0] * gs[0] + gs[1] * gs[1] + gs[2] * gs[2]) + 3.0f * delta;
+        const float bandDot = relOk ? 2.0e-6f * rg2 : 0.0f;
+        const float thLoI = valid ? thLo - bandDot - ii : -3.4e38f;
+        const float thHiI = valid ? thHi + bandDot - ii : -3.4e38f;
+        // fp64 re-test of a candidate in the rounding band of some lane (rare): returns the corrected hit mask
+        auto bandRetest = [&](float d2, uint32_t code, uint64_t hm) -> uint64_t
+        {
+            bool hit = (hm >> lane) & 1;
+            const uint32_t cu = uint32_t(__builtin_amdgcn_readfirstlane(int(code)));
+            const int32_t ju  = __builtin_amdgcn_readfirstlane(cbase[(cu & kChunkSlotMask) & (kCbase - 1)]) +
+                               int32_t(cu >> kChunkSlotBits);
+            SPHX_DCHECK(uint32_t(ju) < ntot, 5);
+            if (uint32_t(ju) < ntot) // (always, for staged sources; a guard against wild scalar loads)
             {
-                const uint32_t cu = uint32_t(__builtin_amdgcn_readfirstlane(int(code)));
-                const int32_t ju  = __builtin_amdgcn_readfirstlane(cbase[(cu & kChunkSlotMask) & (kCbase - 1)]) +
-                                   int32_t(cu >> kChunkSlotBits);
                 const double d64 = distanceSqPbc(ldConst(x + ju), ldConst(y + ju), ldConst(z + ju), xi, yi, zi, box);
-                hit              = hit || (band && d64 < radiusSq);
+                hit              = hit || (d2 <= thHiI && d64 < radiusSq);
             }
-            if (hit)
+            return ballot(hit);
+        };
+        // append `code` for the lanes in `hm`: exec-masked and branch-free (the compiler placed the store blocks out of
+        // line behind a taken branch per candidate). The LDS store is not counted by the compiler's lgkmcnt waits; the
+        // ring is only read by later LDS loads of this wave, which the in-order LDS queue orders after it.
+        auto append = [&](uint64_t hm, uint32_t code)
+        {
+            uint64_t save;
+            if constexpr (kCapped)
             {
-                // with the h iteration (kCapped false) a lane past the cap repeats the round, and only the final
-                // round's lists are kept: no clamp needed on the hot path
-                const unsigned c8 = kCapped ? min(cnt8, cap8) : cnt8;
-                *reinterpret_cast<uint32_t*>(ringLane + (c8 & 0xF00u)) = code;
-                cnt8 += 256;
+                // (no h iteration: test and tool runs) keep the first cap entries, count the rest
+                if ((hm >> lane) & 1)
+                {
+                    if (8 * fb + ((wp - laneBase) >> 8) < cap)
+                    {
+                        *reinterpret_cast<LdsU32*>(uintptr_t(wp)) = code;
+                        wp += 256u;
+                    }
+                    else extra += 1;
+                }
+            }
+            else
+            {
+                // with the h iteration a lane past the cap repeats the round, and only the final round's lists are
+                // kept: its blocks past the capacity are dropped (storeBlock), so the ring never overflows
+                asm volatile("s_and_saveexec_b64 %[sv], %[m]\n"
+                             "ds_write_b32 %[wp], %[code]\n"
+                             "v_add_u32_e32 %[wp], 0x100, %[wp]\n"
+                             "s_or_b64 exec, exec, %[sv]"
+                             : [wp] "+v"(wp), [sv] "=&s"(save)
+                             : [m] "s"(hm), [code] "v"(code)
+                             : "memory");
             }
         };
+        /* Test `count` (a multiple of 4, <= 64) staged candidates against every lane: four candidates (five broadcast
+         * ds_read_b128) per step, one ring check per step. A test always starts at a half of the staging ring (sHead
+         * is a multiple of 64) and never wraps. Measured alternative (profiles/r3_perf_log.md): per-lane hit masks
+         * built with one v_addc per candidate and appended in batches of 32 made the loop VALU-bound in the append
+         * (+18 % VALU, search 31.9 -> 37.9 ms). */
         auto testStaged = [&](unsigned count)
         {
-            // four candidates (two pairs, four broadcast ds_read_b128) per step; four waves per SIMD hide the reads
-            const float4* sp = reinterpret_cast<const float4*>(stage);
+#ifdef SPHX_NS_TIMING_NOTEST // timing experiments only (no usable lists)
+            sHead += count;
+            return;
+#endif
+            const float4* sp = reinterpret_cast<const float4*>(stage) + ((sHead >> 2) & (kStagePairs / 2 - 1)) * 5;
+#pragma nounroll
             for (unsigned k = 0; k < count; k += 4)
             {
-                float4 C[4];
+                float4 C[5];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    C[u] = sp[((((sHead + k) >> 1) + (u >> 1)) & (kStagePairs - 1)) * 2 + (u & 1)];
+                for (int u = 0; u < 5; ++u)
+                    C[u] = sp[u];
+                sp += 5;
+                float dd[4];
 #pragma unroll
                 for (int p = 0; p < 2; ++p)
                 {
                     const float4 A = C[2 * p], B = C[2 * p + 1];
-                    const f2 dx = f2{A.x, A.y} - xr2;
-                    const f2 dy = f2{A.z, A.w} - yr2;
-                    const f2 dz = f2{B.x, B.y} - zr2;
-                    const f2 d2 = dx * dx + dy * dy + dz * dz;
-                    testOne(d2.x, __float_as_uint(B.z));
-                    testOne(d2.y, __float_as_uint(B.w));
+                    f2 t = f2{B.z, B.w};
+                    t    = __builtin_elementwise_fma(f2{A.x, A.y}, mx2, t);
+                    t    = __builtin_elementwise_fma(f2{A.z, A.w}, my2, t);
+                    t    = __builtin_elementwise_fma(f2{B.x, B.y}, mz2, t);
+                    dd[2 * p]     = t.x;
+                    dd[2 * p + 1] = t.y;
                 }
-                const unsigned pend8 = min(cnt8, cap8) - 2048 * fb; // (rounds past the cap: flushes stop at the cap)
-                if (ballot(pend8 >= unsigned(kRing - 4) * 256)) storeBlock(pend8 >= 8 * 256, 8);
+                const uint32_t code[4] = {__float_as_uint(C[4].x), __float_as_uint(C[4].y), __float_as_uint(C[4].z),
+                                          __float_as_uint(C[4].w)};
+                // hit masks (SGPRs) of the four candidates; one rarely taken branch covers their band re-tests, so the
+                // common path runs straight through (a taken branch per candidate cost more)
+                uint64_t hm[4];
+                uint64_t anyBand = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                {
+                    hm[u] = ballot(dd[u] < thLoI);
+                    anyBand |= ballot(dd[u] <= thHiI) ^ hm[u]; // (lane masks: SALU only)
+                }
+                if (__builtin_expect(anyBand != 0, 0))
+                {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (ballot(dd[u] <= thHiI) != hm[u]) hm[u] = bandRetest(dd[u], code[u], hm[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    append(hm[u], code[u]);
+                if (ballot(wp >= wFlush)) storeBlock(wp >= laneBase + 8u * 256u, 8);
             }
             sHead += count;
         };
+#ifdef SPHX_NS_TIMING_NOCAND // timing experiments only (no usable lists)
+        nT = 0;
+#endif
         for (unsigned l = 0; l < nT; ++l)
         {
             const int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + l));
@@ -420,14 +591,40 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                 bool inBox = false;
                 if (j < b)
                 {
-                    xr = float(fold(x[j] - gc[0], 0));
-                    yr = float(fold(y[j] - gc[1], 1));
-                    zr = float(fold(z[j] - gc[2], 2));
+                    const SrcPosQ rj = xq[j];
+                    xr               = float(int32_t(rj.x - gq[0])) * qf.inv[0];
+                    yr               = float(int32_t(rj.y - gq[1])) * qf.inv[1];
+                    zr               = float(int32_t(rj.z - gq[2])) * qf.inv[2];
                     // only sources inside the group search box can be a neighbor of any lane
+                    const float ax = fmaxf(fabsf(xr - ccr[0]) - csr[0], 0.0f);
+                    const float ay = fmaxf(fabsf(yr - ccr[1]) - csr[1], 0.0f);
+                    const float az = fmaxf(fabsf(zr - ccr[2]) - csr[2], 0.0f);
+#if SPHX_NS_ROUNDED
+                    inBox = !relOk || (fabsf(xr) <= gsf[0] && fabsf(yr) <= gsf[1] && fabsf(zr) <= gsf[2] &&
+                                       ax * ax + ay * ay + az * az <= rcore2);
+#else
                     inBox = !relOk || (fabsf(xr) <= gsf[0] && fabsf(yr) <= gsf[1] && fabsf(zr) <= gsf[2]);
+                    (void)ax, (void)ay, (void)az;
+#endif
                 }
                 const uint64_t m = ballot(inBox);
                 if (!m) continue;
+#ifdef SPHX_NS_STATS
+                if (iterateH & 2) // statistics: staged candidates, and those inside some sub-group rounded box
+                {
+                    bool inSub = false;
+                    for (int q = 0; q < 8; ++q)
+                    {
+                        const float ax = fmaxf(fabsf(xr - readLaneF(sbc[0], 8 * q)) - readLaneF(sbh[0], 8 * q), 0.f);
+                        const float ay = fmaxf(fabsf(yr - readLaneF(sbc[1], 8 * q)) - readLaneF(sbh[1], 8 * q), 0.f);
+                        const float az = fmaxf(fabsf(zr - readLaneF(sbc[2], 8 * q)) - readLaneF(sbh[2], 8 * q), 0.f);
+                        const float rq = readLaneF(sbr, 8 * q);
+                        inSub = inSub || ax * ax + ay * ay + az * az <= rq * rq;
+                    }
+                    nStaged += __popcll(m);
+                    nSub += __popcll(ballot(inBox && inSub));
+                }
+#endif
                 const unsigned s = slot++;
                 if (lane == 0)
                 {
@@ -437,15 +634,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                 }
                 if (int64_t(c0) <= i && i < int64_t(c0) + 64) selfCode = chunkCode(s, unsigned(i - c0));
                 // compact the in-box sources into the staging pairs (source order kept: deterministic lists)
-                if (inBox)
-                {
-                    const unsigned p = sTail + unsigned(__popcll(m & lanemaskLt()));
-                    float* e         = stage + ((p >> 1) & (kStagePairs - 1)) * 8 + (p & 1);
-                    e[0]             = xr;
-                    e[2]             = yr;
-                    e[4]             = zr;
-                    e[6]             = __uint_as_float(chunkCode(s, lane));
-                }
+                if (inBox) stagePut(sTail + unsigned(__popcll(m & lanemaskLt())), xr, yr, zr, chunkCode(s, lane));
                 sTail += unsigned(__popcll(m));
                 if (sTail - sHead >= 64)
                 {
@@ -458,23 +647,17 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
             // pad the tail to a multiple of 4 with far-away sentinels (d2 = inf: never a hit, never in the band)
             const unsigned rem = sTail - sHead;
             const unsigned pad = (4 - (rem & 3)) & 3;
-            if (lane < pad)
-            {
-                const unsigned p = sTail + lane;
-                float* e         = stage + ((p >> 1) & (kStagePairs - 1)) * 8 + (p & 1);
-                e[0] = e[2] = e[4] = 1e30f;
-                e[6]               = __uint_as_float(padCode);
-            }
+            if (lane < pad) stagePut(sTail + lane, 0.0f, 0.0f, __builtin_inff(), padCode);
             waveSync<false>();
             testStaged(rem + pad);
         }
-        cnt   = cnt8 >> 8;
-        ncSph = cnt;
-        // remaining entries: at most 15 per lane, i.e. up to two blocks (the last one padded)
         {
-            const unsigned c = min(cnt, cap);
-            storeBlock(c > 8 * fb, min(c - 8 * fb, 8u));
-            storeBlock(c > 8 * fb, c - 8 * fb); // (after a partial first block 8 fb > c: no second one)
+            // entries: 8 per stored block + the pending ones (at most 15: up to two more blocks, the last one padded)
+            const unsigned pend = (wp - laneBase) >> 8;
+            cnt                 = 8 * (fb + fbDrop) + pend + extra;
+            ncSph               = cnt;
+            storeBlock(pend > 0, min(pend, 8u));
+            storeBlock(pend > 8, pend - 8);
         }
 
         // 5. smoothing length iteration
@@ -545,6 +728,18 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
             atomicAdd(&stats[4], (unsigned long long)nT);
         }
     }
+#ifdef SPHX_NS_STATS
+    if (iterateH & 2) // (stats[9..11] sit between the overflow-stripe counters at 8 + 32 k; build with SPHX_NS_STATS)
+    {
+        const unsigned long long hits = (unsigned long long)waveSum(int(valid ? cnt : 0u));
+        if (lane == 0)
+        {
+            atomicAdd(&stats[9], hits);
+            atomicAdd(&stats[10], nStagedLast);
+            atomicAdd(&stats[11], nSubLast);
+        }
+    }
+#endif
     if (valid)
     {
         nc[i] = int32_t(ncSph);
@@ -554,23 +749,28 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
 }
 
 //! fast path: frontier and leaf list in LDS; overflowing groups are queued for the spill kernel
+#define SPHX_NS_OCC __attribute__((amdgpu_waves_per_eu(SPHX_NS_WAVES_EU)))
 template<bool kCapped>
-__global__ __launch_bounds__(256) void findNeighborsKernel(int64_t first, int64_t last, const double* __restrict__ x,
+__global__ __launch_bounds__(64 * kWavesPerBlock) SPHX_NS_OCC void findNeighborsKernel(int64_t first, int64_t last, const double* __restrict__ x,
                                                            const double* __restrict__ y,
-                                                           const double* __restrict__ z, float* __restrict__ h,
+                                                           const double* __restrict__ z,
+                                                           const SrcPosQ* __restrict__ xq, QFrame qf,
+                                                           uint32_t ntot, float* __restrict__ h,
                                                            NsTree t, Box box, unsigned ng0, unsigned ngmax,
                                                            int64_t groups, PackedOut po, int32_t* __restrict__ nc,
                                                            int iterateH, unsigned long long* __restrict__ stats,
                                                            int32_t* __restrict__ spillList, int frontCap)
 {
-    __shared__ __attribute__((aligned(16))) int32_t work[kWavesPerBlock][kWorkWords];
+    // (4 KiB aligned: the hit ring at its start is addressed with v_and_or_b32, testOne)
+    static_assert(kWorkWords * 4 % 4096 == 0 || kWavesPerBlock == 1, "hit rings of the waves 4 KiB aligned");
+    __shared__ __attribute__((aligned(4096))) int32_t work[kWavesPerBlock][kWorkWords];
     __shared__ int32_t leaves[kWavesPerBlock][kLeafCap];
 
     const int wave    = threadIdx.x >> 6;
     const unsigned lb = xcdRemap(blockIdx.x, gridDim.x);
     const int64_t g   = int64_t(lb) * kWavesPerBlock + wave;
     if (g >= groups) return;
-    bool ok = searchGroup<false, kCapped>(g, first, last, x, y, z, h, t, box, ng0, ngmax, po, nc, iterateH, stats,
+    bool ok = searchGroup<false, kCapped>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po, nc, iterateH, stats,
                                  work[wave], work[wave] + kFrontCap, leaves[wave], frontCap, kLeafCap, work[wave]);
     if (!ok && (threadIdx.x & 63) == 0)
     {
@@ -590,14 +790,16 @@ template<bool kCapped>
 __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, int64_t last,
                                                                const double* __restrict__ x,
                                                                const double* __restrict__ y,
-                                                               const double* __restrict__ z, float* __restrict__ h,
-                                                               NsTree t, Box box, unsigned ng0, unsigned ngmax,
-                                                               PackedOut po, int32_t* __restrict__ nc, int iterateH,
+                                                               const double* __restrict__ z,
+                                                               const SrcPosQ* __restrict__ xq, QFrame qf,
+                                                               uint32_t ntot, float* __restrict__ h, NsTree t, Box box,
+                                                               unsigned ng0,
+                                                               unsigned ngmax, PackedOut po, int32_t* __restrict__ nc, int iterateH,
                                                                unsigned long long* __restrict__ stats,
                                                                const int32_t* __restrict__ spillList,
                                                                int32_t* __restrict__ scratch)
 {
-    __shared__ __attribute__((aligned(16))) int32_t work[kCandWords];
+    __shared__ __attribute__((aligned(4096))) int32_t work[kCandWords];
     const int64_t numSpill = int64_t(__hip_atomic_load(&stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     int32_t* frontA = scratch + int64_t(blockIdx.x) * (2 * kSpillFront + kSpillLeaves);
     int32_t* frontB = frontA + kSpillFront;
@@ -605,7 +807,7 @@ __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, in
     for (int64_t k = blockIdx.x; k < numSpill; k += gridDim.x)
     {
         int64_t g = spillList[k];
-        bool ok   = searchGroup<true, kCapped>(g, first, last, x, y, z, h, t, box, ng0, ngmax, po, nc, iterateH, stats,
+        bool ok   = searchGroup<true, kCapped>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po, nc, iterateH, stats,
                                       frontA, frontB, leaves, kSpillFront, kSpillLeaves, work);
         if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
     }
@@ -631,7 +833,7 @@ size_t neighborScratchBytes(int64_t n, unsigned)
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int home,
                    int ovStride, int32_t* nc, int iterateH, unsigned long long* stats, void* scratch,
-                   int testFrontCap, hipStream_t s)
+                   int testFrontCap, const float* m, int64_t ntot, void* rec, hipStream_t s)
 {
     int64_t n = last - first;
     if (n <= 0) return;
@@ -654,13 +856,18 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
     int32_t* spillMem  = spillList + spillMemOff;
     const int fc       = testFrontCap > 0 ? min(testFrontCap, kFrontCap) : kFrontCap;
     const unsigned grid = unsigned((groups + kWavesPerBlock - 1) / kWavesPerBlock);
+    // fixed-point source records {x, y, z, m} of every particle the tree covers (the XMass loop reads the same)
+    const QFrame qf     = qframeOf(box);
+    SrcPosQ* xq         = static_cast<SrcPosQ*>(rec);
+    packPosQ(ntot, x, y, z, m, qf, xq, s);
     auto launch = [&](auto capped)
     {
         constexpr bool kC = decltype(capped)::value;
-        findNeighborsKernel<kC><<<grid, 64 * kWavesPerBlock, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax,
+        findNeighborsKernel<kC><<<grid, 64 * kWavesPerBlock, 0, s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h, t,
+                                                                     box, ng0, ngmax,
                                                                      groups, po, nc, iterateH, stats, spillList, fc);
         SPHX_LAUNCH_CHECK();
-        findNeighborsSpillKernel<kC><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, h, t, box, ng0, ngmax, po, nc,
+        findNeighborsSpillKernel<kC><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h, t, box, ng0, ngmax, po, nc,
                                                                 iterateH, stats, spillList, spillMem);
         SPHX_LAUNCH_CHECK();
     };

@@ -80,9 +80,9 @@ class DeviceCheckError(RuntimeError):
     """a device-side check of the SPHX_DEVICE_CHECKS build failed (see csrc/hip/common.h for the bits)"""
 
 
-DEVICE_CHECK_BITS = {0: "neighbor index out of range", 1: "packed-list rows of a group above rowsMax",
+DEVICE_CHECK_BITS = {0: "neighbor index out of range", 1: "list blocks of a group above the maximum",
                      2: "gather permutation index out of range", 3: "gravity interaction list longer than its slab",
-                     4: "halo pack index out of range"}
+                     4: "halo pack index out of range", 5: "search band re-test source index out of range"}
 
 
 def raise_on_device_check(where: str = ""):

@@ -248,6 +248,10 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                 prev.nidx = None
             buf = torch.empty(region + want * 256, dtype=torch.int32, device=x.device)
         scratch = _scratch(hp.neighbor_scratch_bytes(n, ngmax), x.device)
+        # fixed-point {x, y, z, m} records of all particles (the search stages its candidates from them; 16 B each,
+        # in the XMass loop's record workspace)
+        from .hydro import _rec
+        rec = _rec(d, 0, "xmass")
         ride_host = None
         for _attempt in range(2):
             ov = ((buf.numel() - region) // 256 - num_groups * home) // K
@@ -257,7 +261,8 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
                               d.ng0, ngmax, buf.data_ptr(), nc.data_ptr(),
                               int(iterate_h) | (2 if COLLECT_STATS else 0), stats.data_ptr(),
-                              scratch.data_ptr(), TEST_FRONT_CAP, _stream(), home=home, ov_stride=ov)
+                              scratch.data_ptr(), TEST_FRONT_CAP, _stream(), home=home, ov_stride=ov,
+                              m=d["m"].data_ptr(), ntot=d.size, rec=rec.data_ptr())
             ctr = stats[8::32][:K]
             cand, cand_ov, cand_rows = _next_plan(buf, num_groups, ngmax, home, K)
             # evaluated once per call (it may issue a collective, so every rank calls it exactly once); a repeated
@@ -302,6 +307,9 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         d.nc_spilled = int(st[2])
         d.nc_rounds = int(st[3]) / num_groups  # mean search rounds per group (h iteration)
         d.nc_leaves = int(st[4]) / num_groups  # mean candidate leaves per group and step
+        if COLLECT_STATS:  # staged candidates and hits per group; candidates inside sub-group boxes (what-if)
+            extra = stats[9:12].cpu().tolist()
+            d.nc_hits, d.nc_staged, d.nc_subbox = (v / num_groups for v in extra)
         return NeighborList(buf, first, last, ngmax, True, used, plan, hist, ride_host)
 
     need = max(n, 1) * ngmax
