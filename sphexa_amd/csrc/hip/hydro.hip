@@ -24,7 +24,10 @@
 namespace sphx::hip
 {
 
-constexpr int kBlock = 256;
+#ifndef SPHX_PAIR_BLOCK
+#define SPHX_PAIR_BLOCK 256
+#endif
+constexpr int kBlock = SPHX_PAIR_BLOCK; // threads per block of the pair loops (4 target groups)
 
 /*! @brief target of this thread and its neighbor list (chunk-coded rows of its 64-particle group, packed_list.hpp).
  *         The wave loads its group's chunk table into LDS (nch entries, one coalesced load per 64). Threads past the

@@ -1198,8 +1198,14 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, 
     }
     HT etaCrit = cbrt(HT(32) * HT(M_PI) / HT(3) / HT(nc + 1));
 
-    HT maxvs = 0, mx = 0, my = 0, mz = 0, energy = 0, aviscE = 0;
+    // Sums with the kernel weights folded into per-pair coefficients (same terms as the reference's
+    // tA_i = -C_i r W_i, tA_j = -C_j r W_j form, regrouped):
+    //   a_i = -K sum_j (m_j prho_i a_mom W_i + av/2 W_i) (C_i r) + (m_j prho_j b_mom W_j + bv/2 W_j) (C_j r)
+    //   du_i = K (prho_i sum -m_j a_mom W_i v.(C_i r) + 1/2 max(0, -1/2 sum av W_i v.(C_i r) + bv W_j v.(C_j r)))
+    // so the six tA components are never formed (profiles/r3_perf_log.md: 144 -> ~100 VALU per pair)
+    HT maxvs = 0, mx = 0, my = 0, mz = 0, e1 = 0, e2 = 0;
     const HT Atmin = sc.Atmin, Atmax = sc.Atmax, ramp = sc.ramp;
+    const HT xmi2 = xmi * xmi;
 
     forEachNeighbor<SPHX_BATCH_MOM>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
@@ -1213,12 +1219,13 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, 
         HT Wi = hInv3 * kf.w(v1);
         HT Wj = hjInv * hjInv * hjInv * kf.w(v2);
 
-        HT tAi0 = -(pi.c11 * rx + pi.c12 * ry + pi.c13 * rz) * Wi;
-        HT tAi1 = -(pi.c12 * rx + pi.c22 * ry + pi.c23 * rz) * Wi;
-        HT tAi2 = -(pi.c13 * rx + pi.c23 * ry + pi.c33 * rz) * Wi;
-        HT tAj0 = -(pj.c11 * rx + pj.c12 * ry + pj.c13 * rz) * Wj;
-        HT tAj1 = -(pj.c12 * rx + pj.c22 * ry + pj.c23 * rz) * Wj;
-        HT tAj2 = -(pj.c13 * rx + pj.c23 * ry + pj.c33 * rz) * Wj;
+        // u = C r for the target and the neighbor
+        HT uix = pi.c11 * rx + pi.c12 * ry + pi.c13 * rz;
+        HT uiy = pi.c12 * rx + pi.c22 * ry + pi.c23 * rz;
+        HT uiz = pi.c13 * rx + pi.c23 * ry + pi.c33 * rz;
+        HT ujx = pj.c11 * rx + pj.c12 * ry + pj.c13 * rz;
+        HT ujy = pj.c12 * rx + pj.c22 * ry + pj.c23 * rz;
+        HT ujz = pj.c13 * rx + pj.c23 * ry + pj.c33 * rz;
 
         HT mj = pj.m, cj = pj.c, xmj = pj.xm, rhoj = pj.rho;
 
@@ -1238,7 +1245,7 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, 
         HT dRho = fabs(rhoi - rhoj), sRho = rhoi + rhoj;
         if (dRho < Atmin * sRho)
         {
-            a_mom = xmi * xmi;
+            a_mom = xmi2;
             b_mom = xmj * xmj;
         }
         else if (dRho > Atmax * sRho)
@@ -1251,31 +1258,29 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, 
             // xmi^(2-s) xmj^s = xmi^2 (xmj/xmi)^s and xmj^(2-s) xmi^s = xmj^2 (xmj/xmi)^-s
             HT sigma = ramp * (dRho * rcpF(sRho) - Atmin);
             HT e     = sigma * (log2(xmj) - log2xmi);
-            a_mom    = xmi * xmi * exp2(e);
+            a_mom    = xmi2 * exp2(e);
             b_mom    = xmj * xmj * exp2(-e);
         }
 
         HT av  = mj * invRhoi * visc;
         HT bv  = pj.mrho * visc;
-        HT avx = HT(0.5) * (av * tAi0 + bv * tAj0);
-        HT avy = HT(0.5) * (av * tAi1 + bv * tAj1);
-        HT avz = HT(0.5) * (av * tAi2 + bv * tAj2);
-        aviscE += avx * vxij + avy * vyij + avz * vzij;
-
-        energy += mj * a_mom * (vxij * tAi0 + vyij * tAi1 + vzij * tAi2);
-
-        HT momi = mj * prhoi * a_mom;
-        HT momj = mj * pj.prho * b_mom;
-        mx += momi * tAi0 + momj * tAj0 + avx;
-        my += momi * tAi1 + momj * tAj1 + avy;
-        mz += momi * tAi2 + momj * tAj2 + avz;
+        HT vui = vxij * uix + vyij * uiy + vzij * uiz;
+        HT vuj = vxij * ujx + vyij * ujy + vzij * ujz;
+        HT mja = mj * a_mom;
+        HT Ai  = (mja * prhoi + HT(0.5) * av) * Wi;
+        HT Aj  = (mj * pj.prho * b_mom + HT(0.5) * bv) * Wj;
+        mx += Ai * uix + Aj * ujx;
+        my += Ai * uiy + Aj * ujy;
+        mz += Ai * uiz + Aj * ujz;
+        e1 += mja * Wi * vui;
+        e2 += av * Wi * vui + bv * Wj * vuj;
     });
-    aviscE        = smax(HT(0), aviscE);
+    HT aviscE     = smax(HT(0), HT(-0.5) * e2);
     HT Kf         = HT(sc.K);
-    duOut         = double(Kf * (prhoi * energy + HT(0.5) * aviscE));
-    axOut         = -Kf * mx;
-    ayOut         = -Kf * my;
-    azOut         = -Kf * mz;
+    duOut         = double(Kf * (-prhoi * e1 + HT(0.5) * aviscE));
+    axOut         = Kf * mx;
+    ayOut         = Kf * my;
+    azOut         = Kf * mz;
     maxvsignalOut = maxvs;
 }
 
