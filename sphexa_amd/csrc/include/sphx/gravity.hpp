@@ -117,7 +117,11 @@ SPHX_HD void p2p(T dx, T dy, T dz, T mj, T hi, T hj, T acc[4])
     acc[3] += dz * w;
 }
 
-//! @brief true if the target box (center tc, half size ts) is closer to the source center than sqrt(macSq)
+/*! @brief true if the target box (center tc, half size ts) is closer to the source center than sqrt(macSq).
+ *         A negative macSq is the always-accept sentinel of received remote LET nodes (ops/gravity.py
+ *         FORCE_ACCEPT_MAC2): never violated, so the node is applied as one multipole even when its center lies inside
+ *         the target box (it has no particles here that a P2P could use instead).
+ */
 SPHX_HD bool macViolated(const double sc[3], double macSq, const double tc[3], const double ts[3])
 {
     double R2 = 0;
@@ -126,7 +130,7 @@ SPHX_HD bool macViolated(const double sc[3], double macSq, const double tc[3], c
         double dx = fabs(tc[d] - sc[d]) - ts[d];
         if (dx > 0) R2 += dx * dx;
     }
-    return R2 < fabs(macSq);
+    return R2 < macSq;
 }
 
 //! @brief geometric center and half size of the octree node with placeholder code @p code

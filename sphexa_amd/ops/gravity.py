@@ -216,9 +216,11 @@ def mark_outside_range(tree: Octree, lo: int, hi: int, failed: torch.Tensor):
     return failed
 
 
-# squared MAC radius of a received remote node: tiny but non-zero (zero marks an empty node), so the traversal
-# always applies it as one multipole. It passed the sender's vector MAC against every box of this rank's domain.
-FORCE_ACCEPT_MAC2 = 1e-300
+# squared MAC radius of a received remote node: negative = always accept (sphx/gravity.hpp macViolated; zero marks an
+# empty node), so the traversal applies it as one multipole even when its center of mass lies inside a target group
+# box: it has no particles on this rank, an opened remote leaf would drop its mass. It passed the sender's vector MAC
+# against the coarse boxes of this rank's domain.
+FORCE_ACCEPT_MAC2 = -1.0
 
 
 def remote_let_tree(codes: torch.Tensor, rcenters: torch.Tensor, rquads: torch.Tensor, box: Box, theta: float,

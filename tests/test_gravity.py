@@ -130,3 +130,45 @@ def test_let_kernels_gpu_match_cpu(gpu):
     for a, b in zip(out_c, out_g):
         assert torch.allclose(b.cpu(), a, rtol=1e-4, atol=1e-7)
     assert abs(eg - ec) < 1e-4 * abs(ec)
+
+
+def _remote_leaf_case(device):
+    """remote LET leaves (the leaves of a Plummer tree) whose centers of mass lie inside the boxes of a lattice of
+    targets filling the same cube: every received leaf must still be applied as one multipole (an opened
+    remote leaf has no particles here, so it would silently drop its mass)"""
+    n = 3000
+    box, ot, x, y, z, m, h = _setup(n)
+    cc, mc = G.upsweep(ot, x, y, z, m, box, 0.5)
+    leaves = ot.leaf_to_node.long()
+    codes = ot.prefixes[leaves].clone()
+    rcent = cc.view(-1, 4)[leaves, :3].contiguous()
+    rq = mc.view(-1, 8)[leaves].contiguous()
+    g = torch.linspace(-0.8, 0.8, 12, dtype=torch.float64)
+    T = torch.stack(torch.meshgrid(g, g, g, indexing="ij"), -1).view(-1, 3) + 1e-3  # off the lattice of centers
+    tk = sfc.compute_keys(T[:, 0].contiguous(), T[:, 1].contiguous(), T[:, 2].contiguous(), box)
+    _, p = sfc.sort_keys(tk)
+    T = T[p.long()]
+    nt = T.shape[0]
+    dev = torch.device(device)
+    tx, ty, tz = (T[:, k].contiguous().to(dev) for k in range(3))
+    tm = torch.full((nt,), 1e-3, dtype=torch.float32, device=dev)
+    th = torch.full((nt,), 1e-3, dtype=torch.float32, device=dev)
+    rt, rc, rmp = G.remote_let_tree(codes.to(dev), rcent.to(dev), rq.to(dev), box, 0.5)
+    a = [torch.zeros(nt, dtype=torch.float32, device=dev) for _ in range(3)]
+    e = G.compute_gravity(rt, rc, rmp, 0, nt, tx, ty, tz, th, tm, 1.0, *a)
+    r = [torch.zeros(nt, dtype=torch.float32) for _ in range(3)]
+    er = G.m2p_flat(0, nt, tx.cpu(), ty.cpu(), tz.cpu(), tm.cpu(), rcent, rq, 1.0, *r)
+    A = np.stack([t.cpu().numpy() for t in a], 1).astype(np.float64)
+    R = np.stack([t.numpy() for t in r], 1).astype(np.float64)
+    err = _errors(A, R)
+    assert err[nt // 2] < 1e-3 and err[-1] < 3e-2, (err[nt // 2], err[-1])
+    assert abs(e - er) < 1e-3 * abs(er)
+
+
+def test_remote_leaves_always_applied_cpu():
+    _remote_leaf_case("cpu")
+
+
+@pytest.mark.gpu
+def test_remote_leaves_always_applied_gpu(gpu):
+    _remote_leaf_case(gpu)
