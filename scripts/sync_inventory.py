@@ -1,8 +1,16 @@
 #!/usr/bin/env python3
 """Inventory of the host synchronizations of one time step (torch sync-debug mode): which lines of the package copy
-device values to the host, per step. usage: python scripts/sync_inventory.py [--init evrard] [-n 50]"""
+device values to the host, per step.
+
+  python scripts/sync_inventory.py [--init evrard] [-n 50]              one rank
+  python scripts/sync_inventory.py --ranks 2 [--init evrard] [-n 50]    N ranks sharing cuda:0 over gloo
+
+With several ranks the gloo staging copies of parallel/comm.py (host bounce buffers of a backend that RCCL replaces)
+are reported separately and not counted: the count is what an RCCL run synchronizes.
+"""
 import argparse
 import collections
+import json
 import os
 import sys
 import traceback
@@ -12,32 +20,90 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+STAGING = ("_stage_host", "_stage_dev")  # parallel/comm.py gloo bounce-buffer copies
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--init", default="evrard")
-    ap.add_argument("-n", type=int, default=50)
-    args = ap.parse_args()
+
+def inventory(init: str, n: int, steps_before: int = 2, comm=None):
+    """(counted sites, staging sites) of one step after ``steps_before`` steps"""
     from sphexa_amd.app.simulation import Simulation
 
-    sim = Simulation(args.init, n=args.n, prop="ve", device=torch.device("cuda", 0), out=None, quiet=True)
-    sim.run(2)
-    sites = collections.Counter()
+    sim = Simulation(init, n=n, prop="ve", device=torch.device("cuda", 0), comm=comm, out=None, quiet=True)
+    sim.run(steps_before)
+    sites, staged = collections.Counter(), collections.Counter()
 
     def hook(message, category, filename, lineno, file=None, line=None):
-        for fr in reversed(traceback.extract_stack()[:-1]):
-            if "sphexa_amd" in fr.filename:
-                sites[f"{os.path.relpath(fr.filename)}:{fr.lineno} {fr.line}"] += 1
-                break
+        frames = [fr for fr in traceback.extract_stack()[:-1] if "sphexa_amd" in fr.filename]
+        if not frames:
+            return
+        if frames[-1].name in STAGING:
+            fr = frames[-2] if len(frames) > 1 else frames[-1]
+            staged[f"{os.path.relpath(fr.filename)}:{fr.lineno}"] += 1
+            return
+        fr = frames[-1]
+        sites[f"{os.path.relpath(fr.filename)}:{fr.lineno} {fr.line}"] += 1
 
     warnings.showwarning = hook
     warnings.simplefilter("always")
     torch.cuda.set_sync_debug_mode("warn")
     sim.run(1)
     torch.cuda.set_sync_debug_mode("default")
-    print(f"{sum(sites.values())} synchronizing calls in one step ({args.init} -n {args.n}):")
-    for k, v in sites.most_common():
-        print(f"{v:4d}  {k}")
+    return sites, staged
+
+
+def _worker(rank, size, port, init, n, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(size))
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    from sphexa_amd.parallel.comm import Comm
+
+    sites, staged = inventory(init, n, comm=Comm())
+    q.put((rank, dict(sites), dict(staged)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def multi_rank(size: int, init: str, n: int):
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, size, port, init, n, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--init", default="evrard")
+    ap.add_argument("-n", type=int, default=50)
+    ap.add_argument("--ranks", type=int, default=1)
+    ap.add_argument("--json", action="store_true")
+    args = ap.parse_args()
+    if args.ranks == 1:
+        results = [(0,) + inventory(args.init, args.n)]
+    else:
+        results = multi_rank(args.ranks, args.init, args.n)
+    for rank, sites, staged in results:
+        sites, staged = collections.Counter(sites), collections.Counter(staged)
+        if args.json:
+            print(json.dumps({"rank": rank, "syncs": sum(sites.values()), "staging": sum(staged.values()),
+                              "sites": dict(sites)}))
+            continue
+        print(f"rank {rank}: {sum(sites.values())} synchronizing calls in one step ({args.init} -n {args.n}, "
+              f"{args.ranks} ranks; + {sum(staged.values())} gloo staging copies not counted):")
+        for k, v in sites.most_common():
+            print(f"{v:4d}  {k}")
 
 
 if __name__ == "__main__":

@@ -275,6 +275,7 @@ void markInBoxes(int64_t numBoxes, const double* bc, const double* bh, const Tre
     {
         const double* c = bc + 3 * b;
         const double* s = bh + 3 * b;
+        if (!(s[0] >= 0.0)) continue; // empty slot of a fixed-size box list (parallel/domain.py _coarse_cut)
         int32_t stack[256];
         int sp      = 0;
         stack[sp++] = 0;

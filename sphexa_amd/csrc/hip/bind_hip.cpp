@@ -202,22 +202,33 @@ PYBIND11_MODULE(_sphx_hip, m)
 
     // ---------------------------------------------------------------------------------------------- hydro
     // same argument lists as the OpenMP module, plus (ntot, record workspace(s), stream)
-    m.def("xmass", [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x,
-                      Ptr y, Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr xm, int64_t ntot, Ptr rec, Ptr s)
+    m.def("xmass",
+          [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
+             Ptr h, Ptr mm, Ptr wh, Ptr xm, int64_t ntot, Ptr rec, Ptr s, int inDone, Ptr out)
           {
               auto sc = toConsts(c);
               xmass(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y), P<double>(z),
-                    P<float>(h), P<float>(mm), P<float>(wh), P<void>(rec), P<float>(xm), St(s));
-          });
-    m.def("ve_def_gradh", [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc,
-                             Ptr x, Ptr y, Ptr z, Ptr h, Ptr mm, Ptr wh, Ptr whd, Ptr xm, Ptr kx, Ptr gradh,
-                             int64_t ntot, Ptr rec, Ptr s, double mUniform)
+                    P<float>(h), P<float>(mm), P<float>(wh), P<void>(rec), P<float>(xm), St(s), inDone, P<void>(out));
+          },
+          py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
+          py::arg("x"), py::arg("y"), py::arg("z"), py::arg("h"), py::arg("mm"), py::arg("wh"), py::arg("xm"),
+          py::arg("ntot"), py::arg("rec"), py::arg("s"), py::arg("inDone") = 0, py::arg("out") = 0);
+    m.def("ve_def_gradh",
+          [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
+             Ptr h, Ptr mm, Ptr wh, Ptr whd, Ptr xm, Ptr kx, Ptr gradh, int64_t ntot, Ptr rec, Ptr s, double mUniform,
+             int inDone, Ptr out, Ptr vx, Ptr vy, Ptr vz)
           {
               auto sc = toConsts(c);
               veDefGradh(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
                          P<double>(z), P<float>(h), P<float>(mm), P<float>(wh), P<float>(whd), P<float>(xm),
-                         P<void>(rec), P<float>(kx), P<float>(gradh), float(mUniform), St(s));
-          });
+                         P<void>(rec), P<float>(kx), P<float>(gradh), float(mUniform), St(s), inDone, P<void>(out),
+                         P<float>(vx), P<float>(vy), P<float>(vz));
+          },
+          py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
+          py::arg("x"), py::arg("y"), py::arg("z"), py::arg("h"), py::arg("mm"), py::arg("wh"), py::arg("whd"),
+          py::arg("xm"), py::arg("kx"), py::arg("gradh"), py::arg("ntot"), py::arg("rec"), py::arg("s"),
+          py::arg("mUniform"), py::arg("inDone") = 0, py::arg("out") = 0, py::arg("vx") = 0, py::arg("vy") = 0,
+          py::arg("vz") = 0);
     m.def("eos_ve", [](int64_t first, int64_t last, const ConstArr& c, Ptr temp, Ptr mm, Ptr kx, Ptr xm, Ptr gradh,
                        Ptr prho, Ptr cc, Ptr rho, Ptr p, Ptr s)
           {
@@ -244,7 +255,8 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("iad_divv_curlv",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
-             Ptr curlv, const std::array<Ptr, 6>& dV, int64_t ntot, Ptr rec, Ptr s, Ptr avS)
+             Ptr curlv, const std::array<Ptr, 6>& dV, int64_t ntot, Ptr rec, Ptr s, Ptr avS, int inDone, Ptr avOut,
+             Ptr momOut, Ptr cs, Ptr mm, Ptr prho)
           {
               auto sc = toConsts(c);
               auto cp = six(cij);
@@ -252,33 +264,36 @@ PYBIND11_MODULE(_sphx_hip, m)
               iadDivvCurlv(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
                            P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(wh),
                            P<float>(kx), P<float>(xm), P<void>(rec), cp.data(), P<float>(divv), P<float>(curlv),
-                           g.data(), P<void>(avS), St(s));
+                           g.data(), P<void>(avS), St(s), inDone, P<void>(avOut), P<void>(momOut), P<float>(cs),
+                           P<float>(mm), P<float>(prho));
           },
           py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
           py::arg("x"), py::arg("y"), py::arg("z"), py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("h"),
           py::arg("cij"), py::arg("wh"), py::arg("kx"), py::arg("xm"), py::arg("divv"), py::arg("curlv"),
-          py::arg("dV"), py::arg("ntot"), py::arg("rec"), py::arg("s"), py::arg("avS") = 0);
+          py::arg("dV"), py::arg("ntot"), py::arg("rec"), py::arg("s"), py::arg("avS") = 0, py::arg("inDone") = 0,
+          py::arg("avOut") = 0, py::arg("momOut") = 0, py::arg("cs") = 0, py::arg("mm") = 0, py::arg("prho") = 0);
     m.def("av_switches",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr cs, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
-             double dt, Ptr alpha, int64_t ntot, Ptr rec, Ptr s, Ptr avS)
+             double dt, Ptr alpha, int64_t ntot, Ptr rec, Ptr s, Ptr avS, int inDone, Ptr momOut)
           {
               auto sc = toConsts(c);
               auto cp = six(cij);
               avSwitches(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
                          P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(cs), cp.data(),
                          P<float>(wh), P<float>(kx), P<float>(xm), P<float>(divv), dt, P<void>(rec), P<void>(avS),
-                         P<float>(alpha), St(s));
+                         P<float>(alpha), St(s), inDone, P<void>(momOut));
           },
           py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
           py::arg("x"), py::arg("y"), py::arg("z"), py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("h"),
           py::arg("cs"), py::arg("cij"), py::arg("wh"), py::arg("kx"), py::arg("xm"), py::arg("divv"), py::arg("dt"),
-          py::arg("alpha"), py::arg("ntot"), py::arg("rec"), py::arg("s"), py::arg("avS") = 0);
+          py::arg("alpha"), py::arg("ntot"), py::arg("rec"), py::arg("s"), py::arg("avS") = 0, py::arg("inDone") = 0,
+          py::arg("momOut") = 0);
     m.def("momentum_energy_ve",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr prho, Ptr cs, const std::array<Ptr, 6>& cij, Ptr kx, Ptr xm,
              Ptr alpha, const std::array<Ptr, 6>& dV, Ptr wh, bool avClean, Ptr ax, Ptr ay, Ptr az, Ptr du,
-             Ptr minDt, int64_t ntot, Ptr rec, Ptr rec2, Ptr s)
+             Ptr minDt, int64_t ntot, Ptr rec, Ptr rec2, Ptr s, int inDone)
           {
               auto sc = toConsts(c);
               MomFields f;
@@ -302,8 +317,14 @@ PYBIND11_MODULE(_sphx_hip, m)
               f.alpha = P<float>(alpha);
               momentumEnergyVe(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, f, avClean, P<float>(wh),
                                P<void>(rec), P<void>(rec2), P<float>(ax), P<float>(ay), P<float>(az), P<double>(du),
-                               P<float>(minDt), St(s));
-          });
+                               P<float>(minDt), St(s), inDone);
+          },
+          py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
+          py::arg("x"), py::arg("y"), py::arg("z"), py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("h"),
+          py::arg("mm"), py::arg("prho"), py::arg("cs"), py::arg("cij"), py::arg("kx"), py::arg("xm"),
+          py::arg("alpha"), py::arg("dV"), py::arg("wh"), py::arg("avClean"), py::arg("ax"), py::arg("ay"),
+          py::arg("az"), py::arg("du"), py::arg("minDt"), py::arg("ntot"), py::arg("rec"), py::arg("rec2"),
+          py::arg("s"), py::arg("inDone") = 0);
     m.def("momentum_energy_std",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr rho, Ptr pp, Ptr cs, const std::array<Ptr, 6>& cij, Ptr wh,

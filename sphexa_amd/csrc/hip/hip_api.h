@@ -59,6 +59,12 @@ void packRows(int64_t n, const int64_t* idx, const std::vector<uintptr_t>& src, 
 void unpackRows(int64_t n, const void* rows, const std::vector<uintptr_t>& dst, const std::vector<int>& sizes,
                 int64_t dstOffset, hipStream_t s);
 size_t scanTempBytes(int64_t n);
+// hand-written sample sort and tile scans (sample_sort.hip)
+size_t sampleSortTempBytes(int64_t n);
+void sampleSortPairs(int64_t n, const uint64_t* keysIn, const uint32_t* valsIn, uint64_t* keysOut, uint32_t* valsOut,
+                     void* tmp, size_t tmpBytes, hipStream_t s);
+size_t exclusiveScanTempBytes(int64_t n);
+void exclusiveScanI64Hip(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s);
 void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s);
 
 // octree.hip
@@ -113,11 +119,17 @@ struct StdFields
     const float* cij[6];
 };
 
+// Record hand-offs of the fixed-point VE loops (hydro.hip packRanges): inDone = 0 pack all source records, 1 the own
+// range was written by the previous loop's epilogue, 2 all are written (the search's SrcPosQ); the *Out pointers are
+// the next loop's record arrays the epilogue fills for the own targets (null: none).
 void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x, const double* y,
-           const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s);
+           const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s,
+           int inDone = 0, void* xmOut = nullptr);
 void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                 const double* y, const double* z, const float* h, const float* m, const float* wh, const float* whd,
-                const float* xm, void* rec, float* kx, float* gradh, float mUniform, hipStream_t s);
+                const float* xm, void* rec, float* kx, float* gradh, float mUniform, hipStream_t s, int inDone = 0,
+                void* iadOut = nullptr, const float* vx = nullptr, const float* vy = nullptr,
+                const float* vz = nullptr);
 void eosPolytropic(int64_t first, int64_t last, const float* kx, const float* xm, const float* m, float* p, float* c,
                    hipStream_t s);
 void eosVe(int64_t first, int64_t last, const SphConsts& sc, const double* temp, const float* m, const float* kx,
@@ -130,14 +142,17 @@ void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, co
 void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                   const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                   const float* wh, const float* kx, const float* xm, void* rec, float* const cij[6], float* divv,
-                  float* curlv, float* const dV[6], void* avS, hipStream_t s);
+                  float* curlv, float* const dV[6], void* avS, hipStream_t s, int inDone = 0, void* avOut = nullptr,
+                  void* momOut = nullptr, const float* cs = nullptr, const float* m = nullptr,
+                  const float* prho = nullptr);
 void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                 const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                 const float* c, float* const cij[6], const float* wh, const float* kx, const float* xm,
-                const float* divv, double dt, void* rec, const void* avS, float* alpha, hipStream_t s);
+                const float* divv, double dt, void* rec, const void* avS, float* alpha, hipStream_t s, int inDone = 0,
+                void* momOut = nullptr);
 void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const MomFields& f,
                       bool avClean, const float* wh, void* rec, void* recGradV, float* ax, float* ay, float* az,
-                      double* du, float* minDt, hipStream_t s);
+                      double* du, float* minDt, hipStream_t s, int inDone = 0);
 void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const StdFields& f,
                        const float* wh, void* rec, float* ax, float* ay, float* az, double* du, float* minDt,
                        hipStream_t s);

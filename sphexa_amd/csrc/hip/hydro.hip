@@ -16,6 +16,7 @@
  * The pair math is sphx/sph_math.hpp, shared with the OpenMP path.
  */
 #include <cfloat>
+#include <type_traits>
 
 #include "common.h"
 #include "hip_api.h"
@@ -207,11 +208,11 @@ __global__ void packStdKernel(int64_t n, StdFields f, SrcStd* __restrict__ out)
 }
 
 //! @brief XMass source records on the fixed-point frame (QFrame, sph_math.hpp): one dwordx4 gather per neighbor
-__global__ void packPosQKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+__global__ void packPosQKernel(int64_t lo, int64_t n, const double* __restrict__ x, const double* __restrict__ y,
                                const double* __restrict__ z, const float* __restrict__ m, QFrame q,
                                SrcPosQ* __restrict__ out)
 {
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    int64_t i = lo + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     SrcPosQ r;
     r.x    = quantize(x[i], q.lo[0], q.s[0]);
@@ -221,11 +222,11 @@ __global__ void packPosQKernel(int64_t n, const double* __restrict__ x, const do
     out[i] = r;
 }
 
-__global__ void packXmQKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+__global__ void packXmQKernel(int64_t lo, int64_t n, const double* __restrict__ x, const double* __restrict__ y,
                               const double* __restrict__ z, const float* __restrict__ xm, QFrame q,
                               SrcXmQ* __restrict__ out)
 {
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    int64_t i = lo + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     SrcXmQ r;
     r.x    = quantize(x[i], q.lo[0], q.s[0]);
@@ -235,13 +236,13 @@ __global__ void packXmQKernel(int64_t n, const double* __restrict__ x, const dou
     out[i] = r;
 }
 
-__global__ void packIadQKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+__global__ void packIadQKernel(int64_t lo, int64_t n, const double* __restrict__ x, const double* __restrict__ y,
                                const double* __restrict__ z, const float* __restrict__ kx,
                                const float* __restrict__ vx, const float* __restrict__ vy,
                                const float* __restrict__ vz, const float* __restrict__ xm, QFrame q,
                                SrcIadQ* __restrict__ out)
 {
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    int64_t i = lo + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     SrcIadQ r;
     r.x    = quantize(x[i], q.lo[0], q.s[0]);
@@ -255,10 +256,10 @@ __global__ void packIadQKernel(int64_t n, const double* __restrict__ x, const do
     out[i] = r;
 }
 
-__global__ void packMomQKernel(int64_t n, MomFields f, QFrame q, SrcMomQ* __restrict__ out,
+__global__ void packMomQKernel(int64_t lo, int64_t n, MomFields f, QFrame q, SrcMomQ* __restrict__ out,
                                SrcGradV* __restrict__ gv)
 {
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    int64_t i = lo + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     SrcMomQ r;
     r.x     = quantize(f.x[i], q.lo[0], q.s[0]);
@@ -292,14 +293,14 @@ __global__ void packMomQKernel(int64_t n, MomFields f, QFrame q, SrcMomQ* __rest
     }
 }
 
-__global__ void packAvVKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+__global__ void packAvVKernel(int64_t lo, int64_t n, const double* __restrict__ x, const double* __restrict__ y,
                               const double* __restrict__ z, const float* __restrict__ kx,
                               const float* __restrict__ vx, const float* __restrict__ vy,
                               const float* __restrict__ vz, const float* __restrict__ xm,
                               const float* __restrict__ c, const float* __restrict__ divv, QFrame q,
                               SrcAvV* __restrict__ out)
 {
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    int64_t i = lo + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     SrcAvV r;
     r.x    = quantize(x[i], q.lo[0], q.s[0]);
@@ -335,6 +336,28 @@ __global__ void packAvQKernel(int64_t n, const double* __restrict__ x, const dou
 
 // ------------------------------------------------------------------------------------------------ VE loops
 
+/*! Record hand-offs of the fixed-point VE chain: a loop's epilogue writes the NEXT loop's source records for its own
+ *  targets (XMass -> SrcXmQ for Gradh, Gradh -> SrcIadQ for IAD, IAD -> SrcAvV for the AV switches and SrcMomQ for
+ *  momentum, AV -> the alpha slot of SrcMomQ), so the next launcher packs only the halo ranges (nothing on one rank)
+ *  instead of re-reading 4-20 fields of every particle. inDone: 0 pack all records, 1 the own range [first, last) is
+ *  written, 2 all are written (the search's SrcPosQ). */
+template<class L>
+void packRanges(int inDone, const NbrArgs& a, int64_t ntot, L&& launch)
+{
+    auto go = [&](int64_t lo, int64_t hi)
+    {
+        if (hi > lo) launch(lo, hi);
+    };
+    if (inDone == 2) return;
+    if (inDone == 0)
+    {
+        go(0, ntot);
+        return;
+    }
+    go(0, int64_t(a.first));
+    go(int64_t(a.last), ntot);
+}
+
 __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, Box box, const float* __restrict__ h,
                                                       const SrcPos* __restrict__ rec, const float* __restrict__ wh,
                                                       float* __restrict__ xm)
@@ -352,7 +375,7 @@ __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, B
 //! @brief XMass on fixed-point records (see SrcPosQ): same sum as xmassJLoop (sph_math.hpp), half the gathers
 __global__ __launch_bounds__(kBlock) void xmassQKernel(NbrArgs a, SphConsts sc, QFrame q, const float* __restrict__ h,
                                                        const SrcPosQ* __restrict__ rec, const float* __restrict__ wh,
-                                                       float* __restrict__ xm)
+                                                       float* __restrict__ xm, SrcXmQ* __restrict__ xmOut)
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcPosQ>::S];
     int64_t i;
@@ -371,7 +394,10 @@ __global__ __launch_bounds__(kBlock) void xmassQKernel(NbrArgs a, SphConsts sc, 
         const float dist = sqrtF(rx * rx + ry * ry + rz * rz);
         rho0 += kf.w(dist * hInv) * pj.m;
     });
-    if (valid) xm[i] = pi.m / (rho0 * float(sc.K) * h3Inv);
+    if (!valid) return;
+    const float v = pi.m / (rho0 * float(sc.K) * h3Inv);
+    xm[i]         = v;
+    if (xmOut) xmOut[i] = SrcXmQ{pi.x, pi.y, pi.z, v}; // Gradh's record of this target
 }
 
 template<class R, class G>
@@ -379,7 +405,9 @@ __global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts 
                                                            const float* __restrict__ h, const R* __restrict__ rec,
                                                            const float* __restrict__ wh, const float* __restrict__ whd,
                                                            float* __restrict__ kx, float* __restrict__ gradh,
-                                                           float mUniform)
+                                                           float mUniform, const float* __restrict__ vx,
+                                                           const float* __restrict__ vy, const float* __restrict__ vz,
+                                                           SrcIadQ* __restrict__ iadOut)
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
@@ -392,6 +420,15 @@ __global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts 
     if (!valid) return;
     kx[i]    = k;
     gradh[i] = g;
+    if constexpr (std::is_same_v<R, SrcXmQ>)
+    {
+        if (iadOut)
+        {
+            // the IAD loop's record of this target: vol = xm / kx (as packIadQKernel)
+            const SrcXmQ pi = rec[i];
+            iadOut[i]       = SrcIadQ{pi.x, pi.y, pi.z, pi.xm / k, vx[i], vy[i], vz[i], pi.xm};
+        }
+    }
 }
 
 __global__ void eosVeKernel(int64_t first, int64_t last, SphConsts sc, const double* __restrict__ temp,
@@ -474,7 +511,10 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConst
                                                              const R* __restrict__ rec,
                                                              const float* __restrict__ wh, Six cij,
                                                              float* __restrict__ divv, float* __restrict__ curlv,
-                                                             Six dV, int doGrad, float4* __restrict__ avS)
+                                                             Six dV, int doGrad, float4* __restrict__ avS,
+                                                             SrcAvV* __restrict__ avOut, SrcMomQ* __restrict__ momOut,
+                                                             const float* __restrict__ cs, const float* __restrict__ mm,
+                                                             const float* __restrict__ prho)
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
@@ -493,6 +533,42 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConst
     if (doGrad)
         for (int k = 0; k < 6; ++k)
             dV.p[k][i] = g[k];
+    if constexpr (std::is_same_v<R, SrcIadQ>)
+    {
+        // the AV loop's and the momentum loop's records of this target (as packAvVKernel / packMomQKernel; the
+        // momentum record's alpha is written by the AV loop)
+        if (avOut || momOut)
+        {
+            const SrcIadQ pi = rec[i];
+            const float ci   = cs[i];
+            if (avOut) avOut[i] = SrcAvV{pi.x, pi.y, pi.z, pi.vol * dvi, pi.vx, pi.vy, pi.vz, ci};
+            if (momOut)
+            {
+                SrcMomQ r;
+                r.x     = pi.x;
+                r.y     = pi.y;
+                r.z     = pi.z;
+                r.vx    = pi.vx;
+                r.vy    = pi.vy;
+                r.vz    = pi.vz;
+                r.ih    = 1.0f / h[i];
+                r.c11   = c[0];
+                r.c12   = c[1];
+                r.c13   = c[2];
+                r.c22   = c[3];
+                r.c23   = c[4];
+                r.c33   = c[5];
+                r.m     = mm[i];
+                r.c     = ci;
+                r.xm    = pi.xm;
+                r.rho   = kx[i] * r.m / pi.xm;
+                r.prho  = prho[i];
+                r.alpha = 0.f;
+                r.mrho  = r.m / r.rho;
+                momOut[i] = r;
+            }
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void avSwitchesKernel(NbrArgs a, SphConsts sc, Box box,
@@ -539,7 +615,7 @@ __global__ __launch_bounds__(kBlock) void avSwitchesVKernel(NbrArgs a, SphConsts
                                                             const float* __restrict__ divv,
                                                             const float4* __restrict__ avS,
                                                             const float* __restrict__ wh, double dt,
-                                                            float* __restrict__ alpha)
+                                                            float* __restrict__ alpha, SrcMomQ* __restrict__ momOut)
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcAvV>::S];
     int64_t i;
@@ -552,7 +628,9 @@ __global__ __launch_bounds__(kBlock) void avSwitchesVKernel(NbrArgs a, SphConsts
     float al = avSwitchesVJLoop(unsigned(i), sc.K, q, &pl, 0, n, h[i], ci, divv[i], S,
                                 coopOf(rec, tile, i, a), KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt,
                                 sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
-    if (valid) alpha[i] = al;
+    if (!valid) return;
+    alpha[i] = al;
+    if (momOut) momOut[i].alpha = al;
 }
 
 //! @brief block min of the Courant time step, then one atomic per block
@@ -773,12 +851,13 @@ void packPosQ(int64_t n, const double* x, const double* y, const double* z, cons
               SrcPosQ* out, hipStream_t s)
 {
     if (n <= 0) return;
-    packPosQKernel<<<gridFor(n, 256), 256, 0, s>>>(n, x, y, z, m, q, out);
+    packPosQKernel<<<gridFor(n, 256), 256, 0, s>>>(0, n, x, y, z, m, q, out);
     SPHX_LAUNCH_CHECK();
 }
 
 void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x, const double* y,
-           const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s)
+           const double* z, const float* h, const float* m, const float* wh, void* rec, float* xm, hipStream_t s,
+           int inDone, void* xmOut)
 {
     if (a.last <= a.first) return;
     if (!sc.fixedPoint)
@@ -789,29 +868,33 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
     else
     {
         const QFrame q = qframeOf(box);
-        packPosQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, q, (SrcPosQ*)rec);
-        xmassQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec, wh, xm);
+        packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
+                   { packPosQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, m, q, (SrcPosQ*)rec); });
+        xmassQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec, wh, xm,
+                                                 (SrcXmQ*)xmOut);
     }
     SPHX_LAUNCH_CHECK();
 }
 
 void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                 const double* y, const double* z, const float* h, const float* m, const float* wh, const float* whd,
-                const float* xm, void* rec, float* kx, float* gradh, float mUniform, hipStream_t s)
+                const float* xm, void* rec, float* kx, float* gradh, float mUniform, hipStream_t s, int inDone,
+                void* iadOut, const float* vx, const float* vy, const float* vz)
 {
     if (a.last <= a.first) return;
     if (mUniform > 0.f && sc.fixedPoint)
     {
         const QFrame q = qframeOf(box);
-        packXmQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, q, (SrcXmQ*)rec);
+        packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
+                   { packXmQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, xm, q, (SrcXmQ*)rec); });
         veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcXmQ*)rec, wh, whd, kx,
-                                                     gradh, mUniform);
+                                                     gradh, mUniform, vx, vy, vz, (SrcIadQ*)iadOut);
     }
     else
     {
         packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, xm, (SrcPos*)rec);
         veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcPos*)rec, wh, whd, kx,
-                                                     gradh, 0.f);
+                                                     gradh, 0.f, vx, vy, vz, nullptr);
     }
     SPHX_LAUNCH_CHECK();
 }
@@ -849,7 +932,8 @@ void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, co
 void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                   const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                   const float* wh, const float* kx, const float* xm, void* rec, float* const cij[6], float* divv,
-                  float* curlv, float* const dV[6], void* avS, hipStream_t s)
+                  float* curlv, float* const dV[6], void* avS, hipStream_t s, int inDone, void* avOut, void* momOut,
+                  const float* cs, const float* m, const float* prho)
 {
     if (a.last <= a.first) return;
     Six c, g;
@@ -863,19 +947,27 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
         packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, nullptr, nullptr,
                                                          (SrcIad*)rec);
         iadDivvCurlvKernel<false><<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, kx, (const SrcIad*)rec, wh,
-                                                              c, divv, curlv, g, dV[0] != nullptr, nullptr);
+                                                              c, divv, curlv, g, dV[0] != nullptr, nullptr, nullptr,
+                                                              nullptr, nullptr, nullptr, nullptr);
     }
     else
     {
         const QFrame q = qframeOf(box);
-        packIadQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, q, (SrcIadQ*)rec);
-        // fixed-point path: also the S_i of the AV loop (avSwitchesVJLoop) when a workspace is given
+        packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
+                   {
+                       packIadQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, kx, vx, vy, vz, xm, q,
+                                                                            (SrcIadQ*)rec);
+                   });
+        // fixed-point path: also the S_i of the AV loop (avSwitchesVJLoop) when a workspace is given, and the next
+        // loops' own records (avOut / momOut)
         if (avS)
             iadDivvCurlvKernel<true><<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh,
-                                                                 c, divv, curlv, g, dV[0] != nullptr, (float4*)avS);
+                                                                 c, divv, curlv, g, dV[0] != nullptr, (float4*)avS,
+                                                                 (SrcAvV*)avOut, (SrcMomQ*)momOut, cs, m, prho);
         else
             iadDivvCurlvKernel<false><<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec,
-                                                                  wh, c, divv, curlv, g, dV[0] != nullptr, nullptr);
+                                                                  wh, c, divv, curlv, g, dV[0] != nullptr, nullptr,
+                                                                  nullptr, (SrcMomQ*)momOut, cs, m, prho);
     }
     SPHX_LAUNCH_CHECK();
 }
@@ -883,7 +975,8 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
 void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                 const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                 const float* c, float* const cij[6], const float* wh, const float* kx, const float* xm,
-                const float* divv, double dt, void* rec, const void* avS, float* alpha, hipStream_t s)
+                const float* divv, double dt, void* rec, const void* avS, float* alpha, hipStream_t s, int inDone,
+                void* momOut)
 {
     if (a.last <= a.first) return;
     Six cc;
@@ -897,9 +990,13 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
     else if (avS)
     {
         const QFrame q = qframeOf(box);
-        packAvVKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, c, divv, q, (SrcAvV*)rec);
+        packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
+                   {
+                       packAvVKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, kx, vx, vy, vz, xm, c, divv,
+                                                                           q, (SrcAvV*)rec);
+                   });
         avSwitchesVKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, cc, (const SrcAvV*)rec, divv,
-                                                      (const float4*)avS, wh, dt, alpha);
+                                                      (const float4*)avS, wh, dt, alpha, (SrcMomQ*)momOut);
     }
     else
     {
@@ -913,7 +1010,7 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
 
 void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const MomFields& f,
                       bool avClean, const float* wh, void* rec, void* recGradV, float* ax, float* ay, float* az,
-                      double* du, float* minDt, hipStream_t s)
+                      double* du, float* minDt, hipStream_t s, int inDone)
 {
     if (a.last <= a.first) return;
     SrcGradV* gv = avClean ? (SrcGradV*)recGradV : nullptr;
@@ -930,7 +1027,9 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
     else
     {
         const QFrame q = qframeOf(box);
-        packMomQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, f, q, (SrcMomQ*)rec, gv);
+        // (the gradient records of AV cleaning are packed here: no hand-off then)
+        packRanges(gv ? 0 : inDone, a, ntot, [&](int64_t lo, int64_t hi)
+                   { packMomQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, f, q, (SrcMomQ*)rec, gv); });
         if (avClean)
             momentumEnergyVeKernel<true>
                 <<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, (const SrcMomQ*)rec, gv, wh, ax, ay, az, du, minDt);

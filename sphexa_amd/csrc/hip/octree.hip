@@ -266,6 +266,7 @@ __global__ void markInBoxesKernel(int64_t nb, const double* __restrict__ bc, con
     if (b >= nb) return;
     double c[3] = {bc[3 * b], bc[3 * b + 1], bc[3 * b + 2]};
     double s[3] = {bh[3 * b], bh[3 * b + 1], bh[3 * b + 2]};
+    if (!(s[0] >= 0.0)) return; // empty slot of a fixed-size box list (parallel/domain.py _coarse_cut)
     int32_t stack[192];
     int sp      = 0;
     stack[sp++] = 0;

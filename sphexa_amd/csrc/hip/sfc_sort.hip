@@ -2,9 +2,12 @@
  *
  * Parity: reference sfc/sfc_gpu.cu:38-54 (computeSfcKeysKernel), primitives/primitives_gpu.cu:85-91,270-338
  * (gatherGpu, sortByKeyGpu with CUB radix sort, exclusiveScanGpu), primitives/gather.cuh:44-113 (GpuSfcSorter).
- * Radix sorts go through hipCUB (rocPRIM onesweep on gfx950); keys use 63 bits so the sort runs over [0, 63).
+ * Sorts and scans are the hand-written sample sort / tile scans of sample_sort.hip (the hipCUB radix sort stays as
+ * the A/B variant SPHX_SORT_HIPCUB).
  */
+#ifdef SPHX_SORT_HIPCUB
 #include <hipcub/hipcub.hpp>
+#endif
 
 #include "common.h"
 #include "hip_api.h"
@@ -34,6 +37,8 @@ __global__ void iotaKernel(int64_t n, int32_t* out)
     if (i < n) out[i] = int32_t(i);
 }
 
+#ifdef SPHX_SORT_HIPCUB
+// library sorts (A/B variant: build_native --variant hipcub -DSPHX_SORT_HIPCUB)
 size_t sortPairsTempBytes(int64_t n)
 {
     size_t bytes = 0;
@@ -62,6 +67,23 @@ void sortKeys(int64_t n, const KeyT* keysIn, KeyT* keysOut, int32_t* perm, void*
     iotaKernel<<<gridFor(n, 256), 256, 0, s>>>(n, iota);
     sortPairs(n, keysIn, keysOut, iota, perm, static_cast<char*>(tmp) + iotaBytes, tmpBytes - iotaBytes, 0, 63, s);
 }
+#else
+// hand-written sample sort (sample_sort.hip): (key, value) ascending, keys compared on all 64 bits (the SFC keys and
+// octree codes leave the bits past endBit zero, so the bit range needs no handling)
+size_t sortPairsTempBytes(int64_t n) { return sampleSortTempBytes(n); }
+
+void sortPairs(int64_t n, const KeyT* keysIn, KeyT* keysOut, const int32_t* valsIn, int32_t* valsOut, void* tmp,
+               size_t tmpBytes, int, int, hipStream_t s)
+{
+    sampleSortPairs(n, keysIn, reinterpret_cast<const uint32_t*>(valsIn), keysOut, reinterpret_cast<uint32_t*>(valsOut),
+                    tmp, tmpBytes, s);
+}
+
+void sortKeys(int64_t n, const KeyT* keysIn, KeyT* keysOut, int32_t* perm, void* tmp, size_t tmpBytes, hipStream_t s)
+{
+    sampleSortPairs(n, keysIn, nullptr, keysOut, reinterpret_cast<uint32_t*>(perm), tmp, tmpBytes, s);
+}
+#endif
 
 template<class T>
 __global__ void gatherKernel(int64_t n, const int32_t* __restrict__ perm, const T* __restrict__ src,
@@ -232,6 +254,7 @@ void unpackRows(int64_t n, const void* rows, const std::vector<uintptr_t>& dst, 
     SPHX_LAUNCH_CHECK();
 }
 
+#ifdef SPHX_SORT_HIPCUB
 size_t scanTempBytes(int64_t n)
 {
     size_t bytes = 0;
@@ -245,6 +268,14 @@ void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, siz
     size_t bytes = tmpBytes;
     SPHX_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, int(n), s));
 }
+#else
+size_t scanTempBytes(int64_t n) { return exclusiveScanTempBytes(n); }
+
+void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s)
+{
+    exclusiveScanI64Hip(in, out, n, tmp, tmpBytes, s);
+}
+#endif
 
 SPHX_DCHECK_READER(dcheckSfc)
 bool deviceChecksEnabled() { return SPHX_DCHECK_ENABLED != 0; }

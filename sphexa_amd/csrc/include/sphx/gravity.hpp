@@ -174,6 +174,7 @@ SPHX_HD void markLetBox(const double qc[3], const double qs[3], const int32_t* c
                                const double* tcenter, const double* thalf, const double* gcenters, const Box& box,
                                uint8_t* failed)
 {
+    if (!(qs[0] >= 0.0)) return; // empty slot of a fixed-size box list (parallel/domain.py _coarse_cut)
     int32_t stack[192];
     int sp      = 0;
     stack[sp++] = 0;

@@ -29,15 +29,17 @@ class NbodyProp(Propagator):
         if d.g == 0.0:
             raise RuntimeError("--prop nbody needs a non-zero gravitational constant (--G)")
         self._gravity(domain, d)
+        d.minDtCourant = math.inf
+        d.minDtRho = math.inf
+        # (on the GPU the traversal statistics and energy arrive with the time-step copy: printed after it, so the
+        # line describes this step)
+        self.compute_timestep(domain, d)
+        t.step("Timestep")
         if self.out is not None and self.gravity is not None and self.gravity.stats:
             s = self.gravity.stats
             n = max(last - first, 1)
             print(f"numP2P {s.get('p2p', 0) / n:.1f} maxP2P {s.get('max_p2p', 0)} numM2P {s.get('m2p', 0) / n:.1f} "
                   f"maxM2P {s.get('max_m2p', 0)}", file=self.out)
-        d.minDtCourant = math.inf
-        d.minDtRho = math.inf
-        self.compute_timestep(domain, d)
-        t.step("Timestep")
         H.compute_positions(d, first, last, domain.box)
         t.step("UpdateQuantities")
         t.stop()

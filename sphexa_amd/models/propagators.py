@@ -95,40 +95,62 @@ class Propagator:
             self.timer.step("Gravity")
 
     def compute_timestep(self, domain, d, *extra):
-        """min of Courant, rho, acceleration and 1.1x previous dt; global MIN (reference sph/timestep.hpp). The
-        device-resident inputs (Courant minimum of the momentum loop, max divv, max |a|^2) come to the host in one
-        copy per step."""
+        """min of Courant, rho, acceleration and 1.1x previous dt; global MIN (reference sph/timestep.hpp). On the GPU
+        the local minimum is formed on the device from the device-resident inputs (Courant minimum of the momentum
+        loop, max divv, max |a|^2), reduced over ranks there, and comes to the host in ONE copy together with the
+        gravity statistics/energy (GravityPending) and the domain's deferred checks (Domain.pending_checks)."""
         first, last = domain.start_index(), domain.end_index()
-        dev = []
-        if d.minDtCourant is None:
-            dev.append(d.minDtCourant_dev.reshape(()))
-        rho_dev = torch.is_tensor(d.minDtRho)
-        if rho_dev:
-            dev.append(d.minDtRho)  # max divv of the owned particles (rho_timestep)
         grav = d.g != 0.0 and last > first
-        if grav:
-            dev.append((d["ax"][first:last].double() ** 2 + d["ay"][first:last].double() ** 2 +
-                        d["az"][first:last].double() ** 2).max())
-        # the gravity statistics and energy of this step (GravityPending) ride along in the same copy
         pend = list(getattr(self.gravity, "pending", None) or [])
-        flat = [v.to(torch.float64).reshape(-1) for v in dev] + [p.dev for p in pend]
-        vals = torch.cat(flat).tolist() if flat else []
-        if pend:
-            k = len(vals) - 10 * len(pend)
-            self.gravity.finish(d, [vals[k + 10 * i: k + 10 * (i + 1)] for i in range(len(pend))])
-            vals = vals[:k]
-        if d.minDtCourant is None:
-            d.minDtCourant = float(vals.pop(0))
-        if rho_dev:
-            mx = abs(float(vals.pop(0)))
-            d.minDtRho = d.Krho / mx if mx != 0 else math.inf
-        dt_acc = math.inf
-        if grav:
-            max_acc = math.sqrt(float(vals.pop(0)))
-            if max_acc > 0:
-                dt_acc = d.etaAcc * math.sqrt(d.eps / max_acc)
-        dt_loc = min([dt_acc, d.minDtCourant, d.minDtRho, d.maxDtIncrease * d.minDt] + list(extra))
-        dt = domain.comm.allreduce_scalar(dt_loc, MIN, device=d.device)
+        checks = domain.pending_checks() if hasattr(domain, "pending_checks") else None
+        if d.device.type == "cuda":
+            # (scalars enter as fills: torch.tensor(value, device=...) would be a synchronizing host-to-device copy)
+            f64 = dict(dtype=torch.float64, device=d.device)
+            inf = torch.full((), math.inf, **f64)
+            courant = (d.minDtCourant_dev.reshape(()).to(torch.float64) if d.minDtCourant is None
+                       else torch.full((), float(d.minDtCourant), **f64))
+            if torch.is_tensor(d.minDtRho):
+                mx = d.minDtRho.reshape(()).to(torch.float64).abs()  # max divv of the owned particles
+                rho = torch.where(mx != 0, d.Krho / mx, inf)
+            else:
+                rho = torch.full((), float(d.minDtRho), **f64)
+            acc = inf
+            if grav:
+                a2 = (d["ax"][first:last].double() ** 2 + d["ay"][first:last].double() ** 2 +
+                      d["az"][first:last].double() ** 2).max()
+                max_acc = torch.sqrt(a2)
+                acc = torch.where(max_acc > 0, d.etaAcc * torch.sqrt(d.eps / max_acc), inf)
+            others = min([d.maxDtIncrease * d.minDt] + [float(e) for e in extra])
+            loc = torch.minimum(torch.minimum(torch.minimum(acc, courant), rho), torch.full((), others, **f64))
+            glob = loc.reshape(1).clone()
+            domain.comm.allreduce(glob, MIN)
+            flat = [glob, courant.reshape(1), rho.reshape(1)] + [p.dev for p in pend]
+            if checks is not None:
+                flat.append(checks.to(torch.float64).reshape(-1))
+            vals = torch.cat(flat).tolist()
+            dt = vals[0]
+            d.minDtCourant, d.minDtRho = vals[1], vals[2]
+            k = 3 + 10 * len(pend)
+            if pend:
+                self.gravity.finish(d, [vals[3 + 10 * i: 3 + 10 * (i + 1)] for i in range(len(pend))])
+            if checks is not None:
+                domain.finish_checks(vals[k:])
+        else:
+            if pend:
+                self.gravity.finish(d, [p.dev.cpu().tolist() for p in pend])
+            if checks is not None:
+                domain.finish_checks(checks.reshape(-1).tolist())
+            if torch.is_tensor(d.minDtRho):
+                mx = abs(float(d.minDtRho))
+                d.minDtRho = d.Krho / mx if mx != 0 else math.inf
+            dt_acc = math.inf
+            if grav:
+                max_acc = math.sqrt(float((d["ax"][first:last].double() ** 2 + d["ay"][first:last].double() ** 2 +
+                                           d["az"][first:last].double() ** 2).max()))
+                if max_acc > 0:
+                    dt_acc = d.etaAcc * math.sqrt(d.eps / max_acc)
+            dt_loc = min([dt_acc, d.minDtCourant, d.minDtRho, d.maxDtIncrease * d.minDt] + list(extra))
+            dt = domain.comm.allreduce_scalar(dt_loc, MIN, device=d.device)
         d.ttot += dt
         d.minDt_m1 = d.minDt
         d.minDt = dt

@@ -190,18 +190,26 @@ def mark_let(tree: Octree, boxes: torch.Tensor, centers: torch.Tensor, box: Box)
     return failed
 
 
-def let_selection(tree: Octree, failed: torch.Tensor, mp: torch.Tensor):
-    """(particle flags over the tree's particles, node indices whose multipoles are sent) from the open flags"""
+def let_selection_masks(tree: Octree, failed: torch.Tensor, mp: torch.Tensor, n_particles: int | None = None):
+    """(particle flags over the tree's particles (uint8), node flags of the multipoles to send (bool)) from the open
+    flags: particles of opened leaves, and the first unopened non-empty node below an opened one. With the particle
+    count given there is no host copy."""
     N = tree.num_nodes
     f = failed.bool()
     leaf_open = f[tree.leaf_to_node.long()]
-    pflags = torch.repeat_interleave(leaf_open, tree.counts.long())
+    pflags = torch.repeat_interleave(leaf_open.to(torch.uint8), tree.counts.long(), output_size=n_particles)
     mass = mp.view(-1, 8)[:, 0]
     send = ~f & (mass > 0)
     if N > 1:
         parent = tree.parents.long()[torch.div(torch.arange(1, N, device=f.device) - 1, 8, rounding_mode="floor")]
         send[1:] &= f[parent]
-    return pflags, torch.nonzero(send, as_tuple=False).flatten()
+    return pflags, send
+
+
+def let_selection(tree: Octree, failed: torch.Tensor, mp: torch.Tensor):
+    """(particle flags over the tree's particles, node indices whose multipoles are sent) from the open flags"""
+    pflags, send = let_selection_masks(tree, failed, mp)
+    return pflags.bool(), torch.nonzero(send, as_tuple=False).flatten()
 
 
 def mark_outside_range(tree: Octree, lo: int, hi: int, failed: torch.Tensor):
@@ -228,26 +236,38 @@ def remote_let_tree(codes: torch.Tensor, rcenters: torch.Tensor, rquads: torch.T
     """Octree over the remote multipoles received from the other ranks (one leaf per received node, placeholder
     ``codes`` (M) int64, centers (M, 3) f64, quadrupoles (M, 8) f32), upswept so internal nodes carry the combined
     multipoles and vector-MAC radii. Returns (octree, centers N x 4, quadrupoles N x 8) for ``compute_gravity``: a
-    hierarchical far field instead of applying all M multipoles to every target."""
+    hierarchical far field instead of applying all M multipoles to every target.
+    The (small) tree structure is built on the host from one copy of the codes and goes back to the device through
+    pinned, non-blocking copies: one host synchronization."""
+    import dataclasses
+
     import numpy as np
 
     from .octree import build_octree
 
     dev = rcenters.device
     leaves, leaf_of = _lib.cpu().remote_leaf_array(codes.cpu().numpy().view(np.uint64))
-    tree = torch.from_numpy(leaves.view(np.int64).copy()).to(dev)
-    L = tree.numel() - 1
-    counts = torch.zeros(L, dtype=torch.int32, device=dev)
-    nokeys = torch.empty(0, dtype=torch.int64, device=dev)
-    nox = torch.empty(0, dtype=torch.float64, device=dev)
-    ot = build_octree(tree, counts, nokeys, nox, nox, nox, 0)
+    tree_h = torch.from_numpy(leaves.view(np.int64).copy())
+    L = tree_h.numel() - 1
+    nox = torch.empty(0, dtype=torch.float64)
+    ot_h = build_octree(tree_h, torch.zeros(L, dtype=torch.int32), torch.empty(0, dtype=torch.int64), nox, nox, nox,
+                        0)
+    if dev.type == "cuda":
+        def up(t):
+            return t.pin_memory().to(dev, non_blocking=True)
+
+        ot = dataclasses.replace(ot_h, **{f.name: up(getattr(ot_h, f.name)) for f in dataclasses.fields(ot_h)
+                                          if isinstance(getattr(ot_h, f.name), torch.Tensor)})
+        leaf_idx = up(torch.from_numpy(leaf_of.astype(np.int64)))
+    else:
+        ot, leaf_idx = ot_h, torch.from_numpy(leaf_of.astype(np.int64))
     N = ot.num_nodes
-    nodes = ot.leaf_to_node.long()[torch.from_numpy(leaf_of).to(dev)]
+    nodes = ot.leaf_to_node.long()[leaf_idx]
     centers = torch.zeros(N, 4, dtype=torch.float64, device=dev)
     mp = torch.zeros(N, 8, dtype=torch.float32, device=dev)
-    centers[nodes, :3] = rcenters
-    centers[nodes, 3] = rquads[:, 0].double()
-    mp[nodes] = rquads
+    centers[:, :3].index_copy_(0, nodes, rcenters)
+    centers[:, 3].index_copy_(0, nodes, rquads[:, 0].double())
+    mp.index_copy_(0, nodes, rquads)
     centers, mp = centers.view(-1), mp.view(-1)
     inv_theta = 1.0 / theta
     if dev.type == "cuda":
@@ -264,7 +284,7 @@ def remote_let_tree(codes: torch.Tensor, rcenters: torch.Tensor, rquads: torch.T
                                    ot.prefixes.data_ptr(), ot.node_start.data_ptr(), ot.node_end.data_ptr(), 0, 0, 0, 0,
                                    box.to_array(), sfc_kind, inv_theta, centers.data_ptr(), mp.data_ptr(),
                                    leavesGiven=True)
-    centers.view(-1, 4)[nodes, 3] = FORCE_ACCEPT_MAC2
+    centers.view(-1, 4)[:, 3].index_fill_(0, nodes, FORCE_ACCEPT_MAC2)
     return ot, centers, mp
 
 

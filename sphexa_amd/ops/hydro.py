@@ -27,7 +27,7 @@ DV = ("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")
 # runs: the fixed-point loops fall back to fp64-frame records in some cases (stored-mass Gradh: SrcPos 32 B; AV without
 # the IAD loop's S_i and STD IAD: SrcIad 48 B). The workspace is grow-only, so it settles at the momentum record:
 # SrcMom 96 B (fp64) or SrcMomQ 80 B (fixed point); SrcGradV (32 B) and the AV S_i (16 B) use the second buffer
-REC_BYTES = {"xmass": (32, 32), "gradh": (32, 32), "iad": (48, 48), "av": (48, 48), "mom": (96, 80), "std": (80, 80)}
+REC_BYTES = {"xmass": (32, 32), "gradh": (32, 32), "iad": (48, 48), "av": (48, 48), "mom": (96, 96), "std": (80, 80)}
 
 
 def _stream():
@@ -50,6 +50,72 @@ def release_workspaces(d):
     """drop the record workspaces (re-allocated by the next loop; the caching allocator hands the blocks back)"""
     d._rec0 = None
     d._rec1 = None
+    d._recB = None
+    d._recM = None
+    _handoff(d).clear()
+
+
+def _handoff(d) -> dict:
+    """record hand-offs of the fixed-point VE chain still valid in the workspaces (csrc/hip/hydro.hip packRanges):
+    'posq_all' (the search packed every SrcPosQ into workspace 0), 'xmq_own' (XMass wrote the own SrcXmQ into
+    workspace B), 'iadq_own' (Gradh wrote the own SrcIadQ into workspace 0), 'avv_own' / 'momq_iad' (IAD wrote the
+    own SrcAvV into B and SrcMomQ without alpha into M), 'momq_own' (AV added alpha). Every loop that does not take
+    part clears them (its records may overwrite the workspaces)."""
+    h = getattr(d, "_handoffs", None)
+    if h is None:
+        h = d._handoffs = {}
+    return h
+
+
+# fields a hand-off's records were built from: a Python-side change of any of them (new tensor or in-place write, seen
+# through the tensor version counter) between producer and consumer voids the hand-off
+_HANDOFF_FIELDS = {
+    "posq_all": ("x", "y", "z", "m"),
+    "xmq_own": ("x", "y", "z", "xm"),
+    "iadq_own": ("x", "y", "z", "vx", "vy", "vz", "xm", "kx"),
+    "avv_own": ("x", "y", "z", "vx", "vy", "vz", "xm", "kx", "c", "divv"),
+    "momq_iad": ("x", "y", "z", "vx", "vy", "vz", "h", "m", "c", "xm", "kx", "prho") + CIJ,
+    "momq_own": ("x", "y", "z", "vx", "vy", "vz", "h", "m", "c", "xm", "kx", "prho", "alpha") + CIJ,
+}
+
+
+def _sig(d, key):
+    out = []
+    for f in _HANDOFF_FIELDS[key]:
+        t = d[f]
+        out.append((t.data_ptr(), t._version, t.numel()))
+    return tuple(out)
+
+
+def handoff_mark(d, key: str):
+    _handoff(d)[key] = _sig(d, key)
+
+
+def handoff_take(d, key: str) -> bool:
+    """True if the hand-off ``key`` is pending and its source fields are unchanged (it is consumed either way)"""
+    sig = _handoff(d).pop(key, None)
+    return sig is not None and sig == _sig(d, key)
+
+
+def _wbuf(d, name: str, per: int):
+    """grow-only per-dataset byte workspace of ``per`` bytes per particle (incl. halos)"""
+    need = d.size * per
+    buf = getattr(d, name, None)
+    if buf is None or buf.numel() < need:
+        setattr(d, name, None)
+        buf = torch.empty(int(need * 1.05) + 4096, dtype=torch.uint8, device=d.device)
+        setattr(d, name, buf)
+    return buf
+
+
+def _recB(d):
+    """workspace B: SrcXmQ (XMass -> Gradh), then SrcAvV (IAD -> AV switches), 32 B per particle"""
+    return _wbuf(d, "_recB", 32)
+
+
+def _recM(d):
+    """workspace M: SrcMomQ records (IAD + AV -> momentum), 80 B per particle"""
+    return _wbuf(d, "_recM", 80)
 
 
 def _rec(d, which: int = 0, loop: str = "mom"):
@@ -71,6 +137,7 @@ def _rec(d, which: int = 0, loop: str = "mom"):
 
 
 def _gpu_tail(d, loop: str, which=(0,)):
+    _handoff(d).clear()  # a loop outside the hand-off chain may overwrite the workspaces
     return (d.size,) + tuple(_rec(d, w, loop).data_ptr() for w in which) + (_stream(),)
 
 
@@ -80,7 +147,14 @@ def compute_xmass(d, nl: NeighborList, box: Box, out_field: str = "xm"):
     args = (first, last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d[out_field].data_ptr())
     if _is_gpu(d):
-        _lib.hip().xmass(*args, *_gpu_tail(d, "xmass"))
+        ho = _handoff(d)
+        posq = handoff_take(d, "posq_all") and bool(d.fixedPoint)
+        # the VE chain: XMass writes Gradh's fixed-point records of its targets (uniform mass: the SrcXmQ path)
+        out = _recB(d).data_ptr() if (out_field == "xm" and d.fixedPoint and uniform_mass(d) > 0) else 0
+        ho.clear()
+        _lib.hip().xmass(*args, d.size, _rec(d, 0, "xmass").data_ptr(), _stream(), inDone=2 if posq else 0, out=out)
+        if out:
+            handoff_mark(d, "xmq_own")
     else:
         _lib.cpu().xmass(*args)
 
@@ -196,7 +270,19 @@ def compute_ve_def_gradh(d, nl: NeighborList, box: Box):
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d.whd.data_ptr(),
             d["xm"].data_ptr(), d["kx"].data_ptr(), d["gradh"].data_ptr())
     if _is_gpu(d):
-        _lib.hip().ve_def_gradh(*args, *_gpu_tail(d, "gradh"), uniform_mass(d))
+        mu = uniform_mass(d)
+        if d.fixedPoint and mu > 0:
+            # reads the SrcXmQ records in workspace B (own range from XMass), writes the IAD loop's own SrcIadQ
+            # records into workspace 0
+            ho = _handoff(d)
+            done = 1 if handoff_take(d, "xmq_own") else 0
+            ho.clear()
+            w0 = _rec(d, 0, "iad").data_ptr()
+            _lib.hip().ve_def_gradh(*args, d.size, _recB(d).data_ptr(), _stream(), mu, inDone=done, out=w0,
+                                    vx=d["vx"].data_ptr(), vy=d["vy"].data_ptr(), vz=d["vz"].data_ptr())
+            handoff_mark(d, "iadq_own")
+        else:
+            _lib.hip().ve_def_gradh(*args, *_gpu_tail(d, "gradh"), mu)
     else:
         _lib.cpu().ve_def_gradh(*args)
 
@@ -254,7 +340,22 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
     if _is_gpu(d):
         # the AV loop's S_i = sum_j vol_j w_ij r_ij goes to the second record workspace (dead until momentum), so the
         # AV switches read 32-B records with vd = vol divv (sph_math.hpp SrcAvV)
-        _lib.hip().iad_divv_curlv(*args, *_gpu_tail(d, "iad"), _rec(d, 1, "av").data_ptr())
+        if d.fixedPoint:
+            # fixed point: the epilogue also writes the AV loop's own SrcAvV (workspace B) and, without AV cleaning,
+            # the momentum loop's own SrcMomQ (workspace M, alpha from the AV loop)
+            ho = _handoff(d)
+            done = 1 if handoff_take(d, "iadq_own") else 0
+            ho.clear()
+            mom = 0 if av_clean else _recM(d).data_ptr()
+            _lib.hip().iad_divv_curlv(*args, d.size, _rec(d, 0, "iad").data_ptr(), _stream(),
+                                      _rec(d, 1, "av").data_ptr(), inDone=done, avOut=_recB(d).data_ptr(),
+                                      momOut=mom, cs=d["c"].data_ptr(), mm=d["m"].data_ptr(),
+                                      prho=d["prho"].data_ptr())
+            handoff_mark(d, "avv_own")
+            if mom:
+                handoff_mark(d, "momq_iad")
+        else:
+            _lib.hip().iad_divv_curlv(*args, *_gpu_tail(d, "iad"), _rec(d, 1, "av").data_ptr())
         d._av_s_valid = bool(d.fixedPoint)
     else:
         _lib.cpu().iad_divv_curlv(*args)
@@ -268,7 +369,17 @@ def compute_av_switches(d, nl: NeighborList, box: Box):
             d["xm"].data_ptr(), d["divv"].data_ptr(), float(d.minDt), d["alpha"].data_ptr())
     if _is_gpu(d):
         avs = _rec(d, 1, "av").data_ptr() if (getattr(d, "_av_s_valid", False) and d.fixedPoint) else 0
-        _lib.hip().av_switches(*args, *_gpu_tail(d, "av"), avs)
+        if avs:
+            # SrcAvV records in workspace B (own range from the IAD loop); alpha also into the momentum records
+            ho = _handoff(d)
+            done = 1 if handoff_take(d, "avv_own") else 0
+            mom = _recM(d).data_ptr() if handoff_take(d, "momq_iad") else 0
+            ho.clear()
+            _lib.hip().av_switches(*args, d.size, _recB(d).data_ptr(), _stream(), avs, inDone=done, momOut=mom)
+            if mom:
+                handoff_mark(d, "momq_own")
+        else:
+            _lib.hip().av_switches(*args, *_gpu_tail(d, "av"), avs)
         d._av_s_valid = False
         d._rec1 = None  # S_i consumed (stream-ordered reuse): not held through the momentum loop
     else:
@@ -287,7 +398,12 @@ def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = F
     if _is_gpu(d):
         dt = torch.full((1,), math.inf, dtype=torch.float32, device=d.device)
         gv = _rec(d, 1, "gradv").data_ptr() if av_clean else 0  # SrcGradV records (AV cleaning only)
-        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), d.size, _rec(d, 0, "mom").data_ptr(), gv, _stream())
+        ho = _handoff(d)
+        done = 1 if handoff_take(d, "momq_own") else 0
+        ho.clear()
+        # fixed point: SrcMomQ records in workspace M (own range from the IAD and AV loops)
+        rec = _recM(d) if d.fixedPoint else _rec(d, 0, "mom")
+        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), d.size, rec.data_ptr(), gv, _stream(), inDone=done)
         d.minDtCourant_dev = dt
         d.minDtCourant = None
     else:

@@ -250,7 +250,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         scratch = _scratch(hp.neighbor_scratch_bytes(n, ngmax), x.device)
         # fixed-point {x, y, z, m} records of all particles (the search stages its candidates from them; 16 B each,
         # in the XMass loop's record workspace)
-        from .hydro import _rec
+        from .hydro import _handoff, _rec, handoff_mark
         rec = _rec(d, 0, "xmass")
         ride_host = None
         for _attempt in range(2):
@@ -285,6 +285,9 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               dtype=torch.int32, device=x.device)
         else:
             raise NeighborSearchError("packed neighbor lists: overflow rows exhausted twice")
+        # the search packed every particle's SrcPosQ record into workspace 0: the XMass loop reads them as they are
+        _handoff(d).clear()
+        handoff_mark(d, "posq_all")
         used = num_groups * home + int(host[9])
         best = int(torch.argmin(host[20:25]))
         plan_home, plan_ov = int(host[10 + best]), int(host[15 + best])

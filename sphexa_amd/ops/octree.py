@@ -111,6 +111,85 @@ def update_tree(tree: Optional[torch.Tensor], keys: torch.Tensor, bucket: int, m
     return torch.from_numpy(t_out.view(np.int64)), torch.from_numpy(counts.view(np.int32))
 
 
+class TreeState:
+    """per-step octree of a particle set that changes a little every step (the domain's local and own-particle trees):
+    the cornerstone leaves are rebalanced lazily and the linked structure is cached.
+
+    * ``update``: the leaves of the previous step are kept and only their counts recomputed (device), unless the check
+      issued in the previous step found a leaf over the bucket (or under-full siblings to merge): then they are
+      rebalanced to convergence (the synchronous loop of ``update_tree``). The check for the next step (rebalance ops
+      -> changed flag) runs on the device and its flag lands in pinned host memory without a wait. Any cornerstone
+      leaf array is a valid octree, so a leaf one step over the bucket only costs search time; the reference likewise
+      rebalances once per step (domain/domain.hpp sync -> updateOctree).
+    * ``build``: with unchanged leaves the linked structure (placeholder codes, children, parents, level ranges) is
+      the previous step's; only the particle ranges and tight boxes are recomputed. No host copy in either case.
+    Steady state: no host synchronization per tree and step (two before: the changed flag, the level ranges)."""
+
+    def __init__(self):
+        self.tree: Optional[torch.Tensor] = None
+        self.octree: Optional["Octree"] = None
+        self._flag_h = None
+        self._event = None
+
+    def update(self, keys: torch.Tensor, bucket: int):
+        if not keys.is_cuda:
+            self.tree, counts = update_tree(self.tree, keys, bucket)
+            return self.tree, counts
+        redo = self.tree is None
+        if not redo and self._event is not None:
+            self._event.synchronize()  # recorded a step ago: long complete
+            redo = int(self._flag_h[0]) != 0
+        if redo:
+            self.tree, counts = update_tree(self.tree, keys, bucket)
+        else:
+            counts = node_counts(self.tree, keys)
+        h = _lib.hip()
+        L = self.tree.numel() - 1
+        ops = torch.empty(L + 1, dtype=torch.int64, device=keys.device)
+        flag = torch.zeros(1, dtype=torch.int32, device=keys.device)
+        h.rebalance_ops(self.tree.data_ptr(), counts.data_ptr(), L, bucket, ops.data_ptr(), flag.data_ptr(),
+                        _stream())
+        if self._flag_h is None:
+            self._flag_h = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._flag_h.copy_(flag, non_blocking=True)
+        self._event = torch.cuda.Event()
+        self._event.record()
+        return self.tree, counts
+
+    def build(self, tree: torch.Tensor, counts: torch.Tensor, keys: torch.Tensor, x, y, z, offset: int = 0):
+        prev = self.octree
+        if keys.is_cuda and prev is not None and prev.tree is tree:
+            ot = _refit_octree_hip(prev, counts, keys, x, y, z, offset)
+        else:
+            ot = build_octree(tree, counts, keys, x, y, z, offset)
+        self.octree = ot
+        return ot
+
+
+def _refit_octree_hip(prev: "Octree", counts, keys, x, y, z, offset) -> "Octree":
+    """the linked structure of ``prev`` (same leaves) with new particle ranges and tight boxes"""
+    h = _lib.hip()
+    dev = keys.device
+    N, n = prev.num_nodes, keys.numel()
+    s = _stream()
+    ns = torch.empty(N, dtype=torch.int32, device=dev)
+    ne = torch.empty(N, dtype=torch.int32, device=dev)
+    center = torch.empty(3 * N, dtype=torch.float64, device=dev)
+    half = torch.empty(3 * N, dtype=torch.float64, device=dev)
+    h.node_ranges(prev.prefixes.data_ptr(), N, keys.data_ptr(), n, offset, ns.data_ptr(), ne.data_ptr(), s)
+    h.leaf_boxes(prev.node_to_leaf.data_ptr(), N, ns.data_ptr(), ne.data_ptr(), x.data_ptr(), y.data_ptr(),
+                 z.data_ptr(), center.data_ptr(), half.data_ptr(), s)
+    lr = prev.level_range
+    for l in range(MAX_LEVEL, -1, -1):
+        a, b = lr[l], lr[l + 1]
+        if b > a:
+            h.upsweep_boxes(a, b, prev.node_to_leaf.data_ptr(), prev.child_offsets.data_ptr(), center.data_ptr(),
+                            half.data_ptr(), s)
+    import dataclasses
+    return dataclasses.replace(prev, counts=counts, node_start=ns, node_end=ne, center=center, half=half,
+                               offset=offset)
+
+
 def _root_np():
     return np.array([0, KEY_END], dtype=np.uint64)
 

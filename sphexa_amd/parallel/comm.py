@@ -38,6 +38,17 @@ class CommCheckError(RuntimeError):
     pass
 
 
+def _stage_host(t: torch.Tensor) -> torch.Tensor:
+    """gloo staging: device tensor -> host bounce buffer (a copy an RCCL run does not make; scripts/sync_inventory.py
+    leaves it out of the synchronization count)"""
+    return t.contiguous().cpu()
+
+
+def _stage_dev(t: torch.Tensor, device) -> torch.Tensor:
+    """gloo staging: host bounce buffer -> device"""
+    return t.to(device)
+
+
 class Comm:
     def __init__(self, group=None, check: bool | None = None):
         self.group = group
@@ -91,9 +102,9 @@ class Comm:
         if self.size > 1:
             self._audit("allreduce_" + op, t)
             if self._staged(t):
-                h = t.cpu()
+                h = _stage_host(t)
                 dist.all_reduce(h, op=_OPS[op], group=self.group)
-                t.copy_(h)
+                t.copy_(_stage_dev(h, t.device))
             else:
                 dist.all_reduce(t, op=_OPS[op], group=self.group)
         return t
@@ -127,6 +138,30 @@ class Comm:
         dist.all_to_all_single(r, s, group=self.group)
         return [int(v) for v in r.cpu().tolist()]
 
+    def exchange_counts_dev(self, counts: torch.Tensor) -> torch.Tensor:
+        """all-to-all of the rows of a (size, k) int64 tensor (row q goes to rank q), on the device: no host copy.
+        The caller brings send and receive counts to the host together (one synchronization)."""
+        if self.size == 1:
+            return counts.clone()
+        s = counts.contiguous()
+        staged = self._staged(s)
+        src = _stage_host(s) if staged else s
+        r = torch.empty_like(src)
+        self._audit("exchange_counts", src, r)
+        dist.all_to_all_single(r, src, group=self.group)
+        return _stage_dev(r, counts.device) if staged else r
+
+    def allgather_fixed(self, t: torch.Tensor) -> List[torch.Tensor]:
+        """all-gather of equal-shape tensors (no size exchange, no host copy over RCCL)"""
+        if self.size == 1:
+            return [t]
+        staged = self._staged(t)
+        src = _stage_host(t) if staged else t.contiguous()
+        outs = [torch.empty_like(src) for _ in range(self.size)]
+        self._audit("allgather", src)
+        dist.all_gather(outs, src, group=self.group)
+        return [_stage_dev(o, t.device) for o in outs] if staged else outs
+
     def alltoallv(self, send: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int] | None = None,
                   ) -> Tuple[torch.Tensor, List[int]]:
         """variable all-to-all along dim 0. ``send`` rows are grouped by destination rank in rank order."""
@@ -138,12 +173,12 @@ class Comm:
         recv_counts = [int(v) for v in recv_counts]
         shape = (sum(recv_counts),) + tuple(send.shape[1:])
         staged = self._staged(send)
-        src = send.contiguous().cpu() if staged else send.contiguous()
+        src = _stage_host(send) if staged else send.contiguous()
         recv = torch.empty(shape, dtype=send.dtype, device=src.device)
         self._audit("alltoallv", src, recv, splits=(send_counts, recv_counts))
         dist.all_to_all_single(recv, src, output_split_sizes=list(recv_counts),
                                input_split_sizes=list(send_counts), group=self.group)
-        return (recv.to(send.device) if staged else recv), list(recv_counts)
+        return (_stage_dev(recv, send.device) if staged else recv), list(recv_counts)
 
     def alltoallv_start(self, send: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int]
                         ) -> "PendingExchange":
@@ -157,7 +192,7 @@ class Comm:
         recv_counts = [int(v) for v in recv_counts]
         shape = (sum(recv_counts),) + tuple(send.shape[1:])
         staged = self._staged(send)
-        src = send.contiguous().cpu() if staged else send.contiguous()
+        src = _stage_host(send) if staged else send.contiguous()
         recv = torch.empty(shape, dtype=send.dtype, device=src.device)
         self._audit("alltoallv", src, recv, splits=(send_counts, recv_counts))
         work = dist.all_to_all_single(recv, src, output_split_sizes=recv_counts, input_split_sizes=send_counts,
@@ -169,12 +204,12 @@ class Comm:
         if self.size == 1:
             return [t]
         if self._staged(t):
-            return [o.to(t.device) for o in Comm.allgather_var(self, t.cpu())]
+            return [_stage_dev(o, t.device) for o in Comm.allgather_var(self, _stage_host(t))]
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
         self._audit("allgather_count", n)
         ns = [torch.empty_like(n) for _ in range(self.size)]
         dist.all_gather(ns, n, group=self.group)
-        sizes = [int(v.item()) for v in ns]
+        sizes = [int(v) for v in torch.cat(ns).cpu().tolist()]  # one host copy for all ranks
         mx = max(sizes)
         pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
@@ -196,7 +231,7 @@ class PendingExchange:
             self.work.wait()
             self.work = None
         self._keep = None
-        return self.recv if self.recv.device == self.device else self.recv.to(self.device)
+        return self.recv if self.recv.device == self.device else _stage_dev(self.recv, self.device)
 
 
 def init_distributed(backend: str | None = None) -> Comm:

@@ -89,6 +89,12 @@ class Domain:
         self.remote_codes: Optional[torch.Tensor] = None    # (M) int64 placeholder codes of the remote nodes
         self.remote_tree = None                             # (Octree, centers, quadrupoles) over the remote nodes
         self.stats: Dict[str, float] = {}
+        self._n_global: Optional[int] = None                # global particle count (from the replicated counts)
+        self._tree_np = None                                # host replica of the global tree (uint64 numpy)
+        self._pinned_keep: list = []                        # pinned host buffers of uploads in flight
+        self._pending_bad = None                            # deferred halo-ownership count (device int64)
+        self._local_state = octree_ops.TreeState()         # local (own + halo) octree: lazy rebalance, cached links
+        self._own_state = octree_ops.TreeState()           # own-particle octree of the halo discovery
 
     # ------------------------------------------------------------------------------------------------ queries
     def n_particles(self) -> int:
@@ -189,7 +195,13 @@ class Domain:
                     sfc_ops.compute_keys(d["x"][sl], d["y"][sl], d["z"][sl], self.box, self.sfc_kind,
                                          out=d["keys"][sl])
             if self.check_halos:
-                self._check_halo_ownership(d["keys"])
+                bad = self._halo_ownership_bad(d["keys"])
+                if bad is not None:
+                    if bad.is_cuda:
+                        # deferred: the count reaches the host with the propagator's time-step copy (pending_checks)
+                        self._pending_bad = bad if self._pending_bad is None else self._pending_bad + bad
+                    else:
+                        self._raise_bad_halos(int(bad))
         # native kernels write h in place (h iteration, h update) without bumping the tensor version: drop the
         # cached per-step reductions of h and m so the pair loops re-derive them for the new particle set
         d._h_min = None
@@ -197,8 +209,9 @@ class Domain:
         d._m_uniform = None
 
         all_keys = d["keys"]
-        self.local_tree, counts = octree_ops.update_tree(self.local_tree, all_keys, self.bucket_size_focus)
-        self.octree = octree_ops.build_octree(self.local_tree, counts, all_keys, d["x"], d["y"], d["z"], 0)
+        st = self._local_state
+        self.local_tree, counts = st.update(all_keys, self.bucket_size_focus)
+        self.octree = st.build(self.local_tree, counts, all_keys, d["x"], d["y"], d["z"], 0)
         self.stats["local_leaves"] = self.octree.num_leaves
         self.stats["halos"] = total - n_own
 
@@ -208,36 +221,61 @@ class Domain:
             return self.bucket_size
         return max(64, n_global // (100 * self.size))
 
-    def _distribute(self, keys, own: Dict[str, torch.Tensor], conserved):
-        """assign SFC ranges to ranks by equal particle counts and migrate particles (alltoallv)"""
-        skeys, perm = sfc_ops.sort_keys(keys)
-        n_global = int(self.comm.allreduce_scalar(float(skeys.numel()), SUM, device=keys.device))
-        bucket = self._global_bucket(n_global)
+    def _upload(self, arr, dev) -> torch.Tensor:
+        """host numpy array -> device tensor without a host synchronization (pinned staging buffer, non-blocking copy;
+        the buffer is kept until the next sync, by when the stream has consumed it)"""
+        t = torch.from_numpy(arr)
+        if dev.type != "cuda":
+            return t.clone()
+        pin = t.pin_memory()
+        self._pinned_keep.append(pin)
+        return pin.to(dev, non_blocking=True)
 
+    def _distribute(self, keys, own: Dict[str, torch.Tensor], conserved):
+        """assign SFC ranges to ranks by equal particle counts and migrate particles (alltoallv).
+
+        Host synchronizations: one copy of the global leaf counts per rebalance round (one round once the tree has
+        converged; the replicated tree itself stays on the host, so the uniform-bin cut search runs there), and one
+        copy of the send + receive counts. The global particle count is the sum of the replicated counts (the bucket
+        size uses the previous step's)."""
+        import numpy as np
+
+        self._pinned_keep = []
+        dev = keys.device
+        skeys, perm = sfc_ops.sort_keys(keys)
+        if self._n_global is None:
+            self._n_global = int(self.comm.allreduce_scalar(float(skeys.numel()), SUM, device=dev))
+        bucket = self._global_bucket(self._n_global)
+
+        tree_np = self._tree_np
         tree = self.global_tree
-        if tree is None:
-            tree = octree_ops.root_tree(skeys.device)
+        if tree_np is None or tree is None:
+            tree_np = np.array([0, octree_ops.KEY_END], dtype=np.uint64)
+            tree = self._upload(tree_np.view(np.int64), dev)
         for _ in range(64):
             # local counts on the replicated tree -> global counts -> identical rebalance on every rank
             gcounts = octree_ops.node_counts(tree, skeys).to(torch.int64)
             self.comm.allreduce(gcounts, SUM)
-            new_tree, changed = _rebalance_replicated(tree, gcounts, bucket)
+            c_np = gcounts.cpu().numpy()
+            new_np, changed = _lib.cpu().rebalance(tree_np, c_np.clip(max=2**32 - 1).astype(np.uint32), bucket)
             if not changed:
                 break
-            tree = new_tree
-        L = tree.numel() - 1
-        self.global_tree, self.global_counts = tree, gcounts
+            tree_np = new_np
+            tree = self._upload(tree_np.view(np.int64), dev)
+        L = tree_np.size - 1
+        self.global_tree, self.global_counts, self._tree_np = tree, gcounts, tree_np
+        n_global = int(c_np.sum())
+        self._n_global = n_global
 
-        # uniform bins over leaf counts
-        csum = torch.cumsum(gcounts, 0).cpu()
-        targets = torch.tensor([round(r * n_global / self.size) for r in range(1, self.size)], dtype=torch.int64)
-        cuts = torch.searchsorted(csum, targets, right=False).tolist()
+        # uniform bins over leaf counts (host: the counts and the tree are already there)
+        csum = np.cumsum(c_np)
+        targets = np.array([round(r * n_global / self.size) for r in range(1, self.size)], dtype=np.int64)
+        cuts = np.searchsorted(csum, targets, side="left").tolist()
         bounds = [0] + [min(c + 1, L) for c in cuts] + [L]
         for r in range(1, self.size + 1):
             bounds[r] = max(bounds[r], bounds[r - 1])
         self.assignment = bounds
-        tree_cpu = tree.cpu()
-        keys_b = [int(tree_cpu[b]) & 0xFFFFFFFFFFFFFFFF for b in bounds]  # the end key 2^63 is stored as int64 min
+        keys_b = [int(tree_np[b]) for b in bounds]
         old = self.assignment_keys
         if old is not None and len(old) == len(keys_b):
             # limitBoundaryShifts (reference domaindecomp.hpp:140-166): a rank can only grow into the old ranges
@@ -245,12 +283,16 @@ class Domain:
             for r in range(1, self.size):
                 keys_b[r] = min(max(keys_b[r], old[r - 1]), old[r + 1])
         self.assignment_keys = keys_b
-        bkeys = torch.tensor(keys_b[1:-1], dtype=torch.int64)
-        # send ranges: lower_bound of boundary keys in the sorted local keys
-        pos = torch.searchsorted(skeys, bkeys.to(skeys.device)).cpu().tolist()
-        edges = [0] + pos + [skeys.numel()]
-        send_counts = [edges[r + 1] - edges[r] for r in range(self.size)]
-        recv_counts = self.comm.exchange_counts(send_counts)
+        # send ranges: lower_bound of the boundary keys in the sorted local keys, on the device; send and receive
+        # counts come to the host in one copy
+        bkeys = self._upload(np.array(keys_b[1:-1], dtype=np.uint64).view(np.int64), dev)
+        pos = torch.searchsorted(skeys, bkeys)
+        edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), pos,
+                           torch.full((1,), skeys.numel(), dtype=torch.int64, device=dev)])
+        send_dev = (edges[1:] - edges[:-1]).view(-1, 1)
+        recv_dev = self.comm.exchange_counts_dev(send_dev)
+        counts = torch.cat([send_dev, recv_dev]).view(-1).cpu().tolist()
+        send_counts, recv_counts = counts[: self.size], counts[self.size:]
 
         names = list(own.keys())
         sorted_fields = sfc_ops.gather_many(perm, [own[f] for f in names])
@@ -272,13 +314,12 @@ class Domain:
         x, y, z, h = own["x"], own["y"], own["z"], own["h"]
         # the own-particle tree of the previous step is the starting point (one rebalance round instead of one per level
         # from the root, each a host round trip)
-        tree, counts = octree_ops.update_tree(getattr(self, "_own_tree", None), skeys, self.bucket_size_focus)
-        self._own_tree = tree
-        ot = octree_ops.build_octree(tree, counts, skeys, x, y, z, 0)
+        tree, counts = self._own_state.update(skeys, self.bucket_size_focus)
+        ot = self._own_state.build(tree, counts, skeys, x, y, z, 0)
         c, hf = _search_boxes(ot, x, y, z, h, 2.0)
-        cut = _coarse_cut(ot, c, hf, self.halo_cut_boxes)
-        boxes = torch.cat([c.view(-1, 3)[cut], hf.view(-1, 3)[cut]], dim=1)  # (nb, 6)
-        all_boxes = self.comm.allgather_var(boxes)
+        # a fixed-size list of coarse search boxes (empty slots: half < 0): no size exchange, no host copy
+        boxes = _coarse_cut(ot, c, hf, self.halo_cut_boxes)
+        all_boxes = self.comm.allgather_fixed(boxes)
 
         if gravity:
             from ..ops import gravity as grav_ops
@@ -295,35 +336,42 @@ class Domain:
         prune = not gravity and self.size >= self.peer_prune_min_ranks
         peers = self._halo_peers(all_boxes, ot) if prune else set(range(self.size))
         self.stats["peers"] = len(peers - {self.rank})
-        send_idx: List[torch.Tensor] = []
-        mp_send: List[torch.Tensor] = []
-        flag_rows = None
+        # per destination rank: particle flags (halos) and, with gravity, multipole-node flags; the counts of all
+        # ranks go through one device all-to-all and come to the host with the receive counts in ONE copy, then the
+        # index lists are extracted at their known sizes (nonzero_static: no further synchronization)
+        dev = skeys.device
+        n_own = skeys.numel()
+        flag_rows = torch.zeros((self.size, n_own), dtype=torch.uint8, device=dev)
+        node_rows = torch.zeros((self.size, ot.num_nodes), dtype=torch.bool, device=dev) if gravity else None
         for q in range(self.size):
-            if q == self.rank or q not in peers or all_boxes[q].shape[0] == 0 or skeys.numel() == 0:
-                send_idx.append(torch.empty(0, dtype=torch.int64, device=skeys.device))
-                mp_send.append(torch.empty(0, dtype=torch.int64, device=skeys.device))
+            if q == self.rank or q not in peers or n_own == 0:
                 continue
             if gravity:
                 failed = grav_ops.mark_let(ot, all_boxes[q], gcenters, self.box)
                 failed |= outside
-                pflags, nodes = grav_ops.let_selection(ot, failed, gquads)
-                send_idx.append(torch.nonzero(pflags, as_tuple=False).flatten())
-                mp_send.append(nodes)
+                pflags, nodes = grav_ops.let_selection_masks(ot, failed, gquads, n_own)
+                flag_rows[q] = pflags
+                node_rows[q] = nodes
             else:
-                # flags of every peer first, indices after the loop: one host round trip instead of one per rank
-                if flag_rows is None:
-                    flag_rows = torch.zeros((self.size, skeys.numel()), dtype=torch.uint8, device=skeys.device)
                 _mark_in_boxes(ot, all_boxes[q], x, y, z, self.box, out=flag_rows[q])
-                send_idx.append(None)
-        if flag_rows is not None:
-            nz = torch.nonzero(flag_rows, as_tuple=False)
-            per = torch.bincount(nz[:, 0], minlength=self.size).cpu().tolist()
-            parts = torch.split(nz[:, 1], per)
-            send_idx = [parts[q] if t is None else t for q, t in enumerate(send_idx)]
+        cnt = [flag_rows.sum(1, dtype=torch.int64)]
         if gravity:
-            self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes)
+            cnt.append(node_rows.sum(1, dtype=torch.int64))
+        send_dev = torch.stack(cnt, 1)  # (size, 1 or 2)
+        recv_dev = self.comm.exchange_counts_dev(send_dev)
+        host = torch.cat([send_dev, recv_dev]).cpu()
+        send_h, recv_h = host[: self.size], host[self.size:]
+        send_idx: List[torch.Tensor] = []
+        mp_send: List[torch.Tensor] = []
+        for q in range(self.size):
+            send_idx.append(torch.nonzero_static(flag_rows[q], size=int(send_h[q, 0])).flatten())
+            if gravity:
+                mp_send.append(torch.nonzero_static(node_rows[q], size=int(send_h[q, 1])).flatten())
+        del flag_rows, node_rows
+        if gravity:
+            self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes, [int(v) for v in recv_h[:, 1]])
         self.halo_send_counts = [int(t.numel()) for t in send_idx]
-        self.halo_recv_counts = self.comm.exchange_counts(self.halo_send_counts)
+        self.halo_recv_counts = [int(v) for v in recv_h[:, 0]]
         self.n_lo = sum(self.halo_recv_counts[: self.rank])
         self.n_hi = sum(self.halo_recv_counts[self.rank + 1:])
         self._halo_send_rel = send_idx  # relative to own block, converted to absolute below
@@ -338,6 +386,7 @@ class Domain:
         ext = []
         for q in range(self.size):
             bq = all_boxes[q]
+            bq = bq[bq[:, 3] >= 0]  # drop the empty slots of the fixed-size list
             if bq.shape[0] == 0:
                 ext.append(torch.full((6,), float("nan"), dtype=torch.float64, device=dev))
             else:
@@ -356,25 +405,45 @@ class Domain:
                 peers.add(q)
         return peers
 
-    def _check_halo_ownership(self, keys: torch.Tensor):
-        """every halo received from rank q must carry an SFC key inside q's assigned range, and no halo may fall into
-        this rank's own range (the push-based analog of the reference's checkHalos, halos/halos.hpp:73-105)"""
+    def _halo_ownership_bad(self, keys: torch.Tensor):
+        """number of halos (device int64 scalar) not owned by the rank that sent them, or that fall into this rank's own
+        range (the push-based analog of the reference's checkHalos, halos/halos.hpp:73-105); None without halos"""
         if self.n_lo + self.n_hi == 0:
-            return
+            return None
         dev = keys.device
         bounds = torch.tensor([k if k < 2 ** 63 else 2 ** 63 - 1 for k in self.assignment_keys[1:-1]],
-                              dtype=torch.int64, device=dev)
+                              dtype=torch.int64).to(dev, non_blocking=True)
         halo_keys = torch.cat([keys[: self.start], keys[self.end:]])
         senders = [q for q in range(self.size) if q != self.rank]
         counts = torch.tensor([self.halo_recv_counts[q] for q in senders], dtype=torch.int64)
-        expected = torch.repeat_interleave(torch.tensor(senders, dtype=torch.int64), counts).to(dev)
+        expected = torch.repeat_interleave(torch.tensor(senders, dtype=torch.int64), counts).to(dev, non_blocking=True)
         owner = torch.searchsorted(bounds, halo_keys, right=True)
-        bad = int((owner != expected).sum().item())
+        return (owner != expected).sum()
+
+    def _raise_bad_halos(self, bad: int):
         if bad:
             raise HaloOwnershipError(f"rank {self.rank}: {bad} halo particles are not owned by the rank that sent "
                                      f"them (assignment {self.assignment_keys})")
 
-    def _exchange_multipoles(self, mp_send, gcenters, gquads, prefixes):
+    def _check_halo_ownership(self, keys: torch.Tensor):
+        """immediate form of the ownership check (one host copy)"""
+        bad = self._halo_ownership_bad(keys)
+        if bad is not None:
+            self._raise_bad_halos(int(bad))
+
+    def pending_checks(self):
+        """deferred device-side checks of the last sync (float64 device tensor) for the propagator's time-step copy,
+        or None; the host values go to ``finish_checks``"""
+        if self._pending_bad is None:
+            return None
+        return self._pending_bad.to(torch.float64).reshape(1)
+
+    def finish_checks(self, vals):
+        self._pending_bad = None
+        if vals:
+            self._raise_bad_halos(int(vals[0]))
+
+    def _exchange_multipoles(self, mp_send, gcenters, gquads, prefixes, recv_counts=None):
         """one alltoallv of (center xyz f64, quadrupole 8 x f32, placeholder code) rows for the LET far field; the
         received nodes become the leaves of this rank's remote LET tree (ops.gravity.remote_let_tree)"""
         from ..ops import gravity as grav_ops
@@ -383,7 +452,7 @@ class Domain:
         rows = torch.cat([gcenters.view(-1, 4)[idx, :3], gquads.view(-1, 8)[idx].contiguous().view(torch.float64),
                           prefixes[idx].view(torch.float64).view(-1, 1)], dim=1)
         counts = [int(t.numel()) for t in mp_send]
-        recv, _ = self.comm.alltoallv(rows, counts)
+        recv, _ = self.comm.alltoallv(rows, counts, recv_counts)
         self.remote_centers = recv[:, :3].contiguous()
         self.remote_quads = recv[:, 3:7].contiguous().view(torch.float32).view(-1, 8)
         self.remote_codes = recv[:, 7].contiguous().view(torch.int64)
@@ -466,24 +535,31 @@ def _search_boxes(ot, x, y, z, h, factor: float):
 
 
 def _coarse_cut(ot, center, half, max_boxes: int) -> torch.Tensor:
-    """node indices of a tree cut with at most ~max_boxes non-empty nodes (nodes at the cut level + shallower
-    leaves): the deepest level whose cut still fits, from per-level counts gathered in one host copy"""
+    """search boxes of a tree cut with at most max_boxes non-empty nodes (the nodes at the cut level + shallower
+    leaves; the deepest level whose cut still fits) as a fixed (max_boxes, 6) tensor [center | half], empty slots with
+    half = -1. Chosen and compacted on the device: no host copy."""
+    dev = center.device
     lv = ot.node_levels().long()
     is_leaf = ot.node_to_leaf >= 0
     nonempty = half.view(-1, 3)[:, 0] >= 0
     nl = octree_ops.MAX_LEVEL + 1
-    at_level = torch.bincount(lv[nonempty], minlength=nl)[:nl]
-    leaves_at = torch.bincount(lv[nonempty & is_leaf], minlength=nl)[:nl]
+    at_level = torch.zeros(nl, dtype=torch.int64, device=dev).scatter_add_(0, lv, nonempty.long())
+    leaves_at = torch.zeros(nl, dtype=torch.int64, device=dev).scatter_add_(0, lv, (nonempty & is_leaf).long())
     # cut(c) = nonempty nodes at level c + nonempty leaves above c
-    leaves_above = torch.cumsum(leaves_at, 0) - leaves_at
-    sizes = (at_level + leaves_above).cpu().tolist()
-    best = 0
-    for c in range(0, min(nl, ot.max_depth() + 2)):
-        if sizes[c] > max_boxes and c > 0:
-            break
-        best = c
+    sizes = at_level + torch.cumsum(leaves_at, 0) - leaves_at
+    depth = min(nl, ot.max_depth() + 2)
+    ok = (sizes[:depth] <= max_boxes) | (torch.arange(depth, device=dev) == 0)  # the root always fits
+    best = torch.cumprod(ok.long(), 0).sum() - 1  # deepest level with every shallower cut fitting as well
     sel = ((lv == best) | (is_leaf & (lv < best))) & nonempty
-    return torch.nonzero(sel, as_tuple=False).flatten()
+    pos = torch.cumsum(sel.long(), 0) - 1
+    idx = torch.where(sel, pos, torch.full_like(pos, max_boxes))
+    rows = torch.cat([center.view(-1, 3), half.view(-1, 3)], dim=1)
+    out = torch.zeros((max_boxes + 1, 6), dtype=rows.dtype, device=dev)
+    out[:, 3:] = -1.0
+    out.index_copy_(0, idx, rows)
+    out = out[:max_boxes]
+    out[:, 3:] = torch.where(out[:, 3:4] >= 0, out[:, 3:], torch.full_like(out[:, 3:], -1.0))
+    return out
 
 
 def _mark_in_boxes(ot, boxes: torch.Tensor, x, y, z, box: Box, out: Optional[torch.Tensor] = None) -> torch.Tensor:

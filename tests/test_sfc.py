@@ -86,3 +86,64 @@ def test_sort_keys_permutation():
     s, p = sfc.sort_keys(keys)
     assert torch.equal(s, keys[p.long()])
     assert (s[1:] >= s[:-1]).all()
+
+
+def _stable_ref(keys):
+    """sorted keys and the stable permutation (ties by index), numpy on the host"""
+    k = keys.cpu().numpy().view(np.uint64)
+    p = np.argsort(k, kind="stable")
+    return k[p], p.astype(np.int32)
+
+
+def _nearly_sorted(n, seed, far=0):
+    rng = np.random.default_rng(seed)
+    base = np.sort(rng.integers(0, 1 << 63, n, dtype=np.uint64))
+    # small local displacements (the step-to-step SFC reordering) + a few far movers
+    jitter = rng.integers(-20, 21, n)
+    order = np.argsort(np.arange(n) + jitter, kind="stable")
+    k = base[order]
+    if far:
+        idx = rng.integers(0, n, far)
+        k[idx] = rng.integers(0, 1 << 63, far, dtype=np.uint64)
+    return torch.from_numpy(k.view(np.int64).copy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 7, 1000, 1024, 1025, 4097, 100_000, 2_000_003])
+def test_sample_sort_matches_stable_sort(gpu, n):
+    """hand-written sample sort (csrc/hip/sample_sort.hip): keys and permutation equal to a stable sort on random,
+    nearly sorted (+ far movers), and duplicate-heavy keys (buckets beyond 1024 take the global-memory path)"""
+    g = torch.Generator().manual_seed(n)
+    cases = [torch.randint(0, 1 << 63 - 1, (n,), generator=g, dtype=torch.int64),
+             _nearly_sorted(n, n, far=max(1, n // 1000)),
+             torch.randint(0, 3, (n,), generator=g, dtype=torch.int64) * (1 << 40)]
+    for keys in cases:
+        s, p = sfc.sort_keys(keys.to(gpu))
+        rs, rp = _stable_ref(keys)
+        assert np.array_equal(s.cpu().numpy().view(np.uint64), rs)
+        assert np.array_equal(p.cpu().numpy(), rp)
+
+
+@pytest.mark.gpu
+def test_sample_sort_pairs_and_scan(gpu):
+    """(key, value) pairs with arbitrary values (octree node codes) and the hand-written exclusive scan"""
+    from sphexa_amd.ops import _lib
+
+    h = _lib.hip()
+    g = torch.Generator().manual_seed(3)
+    n = 300_000
+    keys = torch.randint(0, 1 << 62, (n,), generator=g, dtype=torch.int64).to(gpu)
+    vals = torch.randperm(n, generator=g).to(torch.int32).to(gpu)
+    ko, vo = torch.empty_like(keys), torch.empty_like(vals)
+    tmp = torch.empty(h.sort_pairs_temp_bytes(n), dtype=torch.uint8, device=gpu)
+    h.sort_pairs_i64_i32(n, keys.data_ptr(), ko.data_ptr(), vals.data_ptr(), vo.data_ptr(), tmp.data_ptr(),
+                         tmp.numel(), 0, 64, torch.cuda.current_stream().cuda_stream)
+    o = torch.argsort(keys.cpu(), stable=True)
+    assert torch.equal(ko.cpu(), keys.cpu()[o]) and torch.equal(vo.cpu(), vals.cpu()[o])
+    for m in (1, 5000, 4096 * 3 + 17, 1_000_001):
+        x = torch.randint(0, 1000, (m,), generator=g, dtype=torch.int64).to(gpu)
+        ref = torch.cumsum(x.cpu(), 0) - x.cpu()
+        t = torch.empty(h.scan_temp_bytes(m), dtype=torch.uint8, device=gpu)
+        h.exclusive_scan_i64(x.data_ptr(), x.data_ptr(), m, t.data_ptr(), t.numel(),
+                             torch.cuda.current_stream().cuda_stream)
+        assert torch.equal(x.cpu(), ref)
