@@ -524,24 +524,45 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConst
     float c[6], g[6], dvi, cvi, S[3];
     iadDivvCurlvJLoop<kAvS>(unsigned(i), sc.K, box, &pl, 0, n, h[i], kx[i], coopOf(rec, tile, i, a),
                             KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, g, S);
-    if (!valid) return;
-    for (int k = 0; k < 6; ++k)
-        cij.p[k][i] = c[k];
-    divv[i]  = dvi;
-    curlv[i] = cvi;
-    if constexpr (kAvS) avS[i - a.first] = make_float4(S[0], S[1], S[2], 0.f);
-    if (doGrad)
+    if (valid)
+    {
         for (int k = 0; k < 6; ++k)
-            dV.p[k][i] = g[k];
+            cij.p[k][i] = c[k];
+        divv[i]  = dvi;
+        curlv[i] = cvi;
+        if constexpr (kAvS) avS[i - a.first] = make_float4(S[0], S[1], S[2], 0.f);
+        if (doGrad)
+            for (int k = 0; k < 6; ++k)
+                dV.p[k][i] = g[k];
+    }
     if constexpr (std::is_same_v<R, SrcIadQ>)
     {
-        // the AV loop's and the momentum loop's records of this target (as packAvVKernel / packMomQKernel; the
-        // momentum record's alpha is written by the AV loop)
-        if (avOut || momOut)
+        // the AV loop's and the momentum loop's records of this wave's targets (as packAvVKernel / packMomQKernel;
+        // the momentum record's alpha is written by the AV loop). A record is 2 / 5 dwordx4 per lane at a 32 / 80 B
+        // stride; staged through LDS, the wave writes its 64 contiguous records as whole 1-KiB rows instead.
+        if ((avOut || momOut) && ballot(valid))
         {
+            __shared__ float4 stage[kBlock / 64][64 * 5];
+            float4* w       = stage[threadIdx.x >> 6];
+            const int lane  = threadIdx.x & 63;
+            const int64_t i0 = int64_t(__builtin_amdgcn_readfirstlane(int(i - a.first))) + a.first; // lane 0 is valid
+            const int nv     = int(min(int64_t(64), int64_t(a.last) - i0));
             const SrcIadQ pi = rec[i];
             const float ci   = cs[i];
-            if (avOut) avOut[i] = SrcAvV{pi.x, pi.y, pi.z, pi.vol * dvi, pi.vx, pi.vy, pi.vz, ci};
+            auto flush = [&](float4* dst, int chunks)
+            {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int q = 0; q < chunks; ++q)
+                {
+                    const int cidx = q * 64 + lane;
+                    if (cidx < nv * chunks) dst[cidx] = w[cidx];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            };
             if (momOut)
             {
                 SrcMomQ r;
@@ -565,7 +586,19 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConst
                 r.prho  = prho[i];
                 r.alpha = 0.f;
                 r.mrho  = r.m / r.rho;
-                momOut[i] = r;
+                const float4* rp = reinterpret_cast<const float4*>(&r);
+#pragma unroll
+                for (int k = 0; k < 5; ++k)
+                    w[lane * 5 + k] = rp[k];
+                flush(reinterpret_cast<float4*>(momOut + i0), 5);
+            }
+            if (avOut)
+            {
+                const SrcAvV r{pi.x, pi.y, pi.z, pi.vol * dvi, pi.vx, pi.vy, pi.vz, ci};
+                const float4* rp = reinterpret_cast<const float4*>(&r);
+                w[lane * 2]      = rp[0];
+                w[lane * 2 + 1]  = rp[1];
+                flush(reinterpret_cast<float4*>(avOut + i0), 2);
             }
         }
     }

@@ -191,26 +191,32 @@ __global__ __launch_bounds__(256) void leafBoxesKernel(const int32_t* __restrict
                                                        double factor, double* __restrict__ center,
                                                        double* __restrict__ half)
 {
-    const int64_t i = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
-    if (i >= N || n2l[i] < 0) return; // wave-uniform
-    const int lane = threadIdx.x & 63;
+    // 16 lanes per node (4 nodes per wave): leaves hold <= bucket (~16-64) particles, so a whole wave per leaf left
+    // most lanes idle and paid six 64-lane double reductions per leaf (and a wave per internal node)
+    const int64_t i = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 4;
+    const int sub   = threadIdx.x & 15;
+    const bool leaf = i < N && n2l[i] >= 0;
     double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
-    for (int32_t p = ns[i] + lane; p < ne[i]; p += 64)
+    if (leaf)
     {
-        double r    = h ? factor * double(h[p]) : 0.0;
-        double v[3] = {x[p], y[p], z[p]};
-        for (int d = 0; d < 3; ++d)
+        for (int32_t p = ns[i] + sub; p < ne[i]; p += 16)
         {
-            mn[d] = fmin(mn[d], v[d] - r);
-            mx[d] = fmax(mx[d], v[d] + r);
+            double r    = h ? factor * double(h[p]) : 0.0;
+            double v[3] = {x[p], y[p], z[p]};
+            for (int d = 0; d < 3; ++d)
+            {
+                mn[d] = fmin(mn[d], v[d] - r);
+                mx[d] = fmax(mx[d], v[d] + r);
+            }
         }
     }
-    for (int d = 0; d < 3; ++d)
-    {
-        mn[d] = waveMin(mn[d]);
-        mx[d] = waveMax(mx[d]);
-    }
-    if (lane == 0) storeBox(center, half, i, mn, mx);
+    for (int o = 8; o > 0; o >>= 1)
+        for (int d = 0; d < 3; ++d)
+        {
+            mn[d] = fmin(mn[d], __shfl_xor(mn[d], o));
+            mx[d] = fmax(mx[d], __shfl_xor(mx[d], o));
+        }
+    if (leaf && sub == 0) storeBox(center, half, i, mn, mx);
 }
 
 void leafBoxes(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
@@ -218,7 +224,7 @@ void leafBoxes(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* 
                hipStream_t s)
 {
     if (N <= 0) return;
-    leafBoxesKernel<<<unsigned((N + 3) / 4), 256, 0, s>>>(n2l, N, ns, ne, x, y, z, h, factor, center, half);
+    leafBoxesKernel<<<unsigned((N + 15) / 16), 256, 0, s>>>(n2l, N, ns, ne, x, y, z, h, factor, center, half);
     SPHX_LAUNCH_CHECK();
 }
 

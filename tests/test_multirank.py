@@ -315,3 +315,46 @@ def test_peer_pruning_far_ranks():
     res = run_ranks(_blobs_worker, 2)
     assert [r["peers"] for r in res] == [0, 0]
     assert [r["halos"] for r in res] == [0, 0]
+
+
+def _let_cost_worker(rank, world, comm, n):
+    from sphexa_amd.app.simulation import Simulation
+    from sphexa_amd.models.gravity import MultipoleHolder
+
+    sim = Simulation("evrard", n=n, device="cpu", comm=comm)
+    d, dom, p = sim.d, sim.domain, sim.propagator
+    s, e = dom.start_index(), dom.end_index()
+    for f in ("ax", "ay", "az"):
+        d[f][s:e] = 0.0
+    mh = MultipoleHolder()
+    mh.upsweep(d, dom)
+    mh.traverse(d, dom)
+    grav_halos = dom.n_particles_with_halos() - dom.n_particles()
+    remote = int(dom.stats.get("remote_multipoles", 0))
+    rm2p, rp2p = mh.stats.get("remote_m2p", 0), mh.stats.get("remote_p2p", 0)
+    lm2p, lp2p = mh.stats.get("m2p", 0), mh.stats.get("p2p", 0)
+    # the same particles synchronized for SPH only: halos = the 2h neighborhoods alone
+    dom.sync(d, p.conserved_fields(), p.dependent, gravity=False)
+    sph_halos = dom.n_particles_with_halos() - dom.n_particles()
+    return dict(n=e - s, grav_halos=grav_halos, sph_halos=sph_halos, remote=remote, rm2p=rm2p, rp2p=rp2p, lm2p=lm2p,
+                lp2p=lp2p)
+
+
+def test_let_cost_quantified():
+    """cost of the push LET at 8 ranks (Evrard -n 64, 262 k particles, 33 k per rank, verdict r2 item 7): the
+    particles of every opened leaf travel as gravity halos on top of the SPH halos, the first unopened nodes as
+    multipoles. Reported per rank (profiles/r3_let_cost.md: gravity halos 2.05 / 1.21 / 0.89 x the owned particles
+    at 17 k / 58 k / 137 k particles per rank, i.e. ~N^-1/3: ~0.55 x at Evrard -n 200's 0.59 M per rank on 8 GPUs).
+    Bounds: SPH halos <= gravity halos <= 2.5 x owned at this size, a few thousand remote multipoles, remote M2P per
+    target below the local M2P, no remote P2P (remote nodes are always accepted)"""
+    n = 64
+    res = run_ranks(_let_cost_worker, 8, n)
+    for r in res:
+        print(f"rank particles {r['n']}: halos SPH {r['sph_halos']} (+{r['sph_halos'] / r['n']:.2f}) gravity "
+              f"{r['grav_halos']} (+{r['grav_halos'] / r['n']:.2f}), remote multipoles {r['remote']}, per target: "
+              f"local M2P {r['lm2p'] / r['n']:.0f} P2P {r['lp2p'] / r['n']:.0f}, remote M2P {r['rm2p'] / r['n']:.0f} "
+              f"P2P {r['rp2p'] / r['n']:.0f}")
+    for r in res:
+        assert r["sph_halos"] <= r["grav_halos"] <= 2.5 * r["n"]
+        assert 0 < r["remote"] < 20000
+        assert r["rm2p"] < r["lm2p"] and r["rp2p"] == 0

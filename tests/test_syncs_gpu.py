@@ -1,0 +1,31 @@
+"""Host synchronizations per time step (verdict r2 item 5): counted with torch's sync-debug mode by
+scripts/sync_inventory.py; several ranks share the GPU over gloo and the gloo bounce copies (comm._stage_host /
+_stage_dev, absent with RCCL) are not counted. Ceilings: 2 (Sedov) / 3 (Evrard: + open-box extent) on one rank,
+5 / 7 for any number of ranks (global leaf counts, send/recv counts, halo counts, + the remote LET codes with
+gravity)."""
+
+import os
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+
+
+@pytest.mark.parametrize("init,ceiling", [("sedov", 2), ("evrard", 3)])
+def test_syncs_one_rank(gpu, init, ceiling):
+    import sync_inventory as S
+
+    sites, _ = S.inventory(init, 30)
+    assert sum(sites.values()) <= ceiling, dict(sites)
+
+
+@pytest.mark.parametrize("ranks", [2, 8])
+@pytest.mark.parametrize("init,ceiling", [("sedov", 5), ("evrard", 7)])
+def test_syncs_multi_rank(gpu, ranks, init, ceiling):
+    import sync_inventory as S
+
+    for rank, sites, staged in S.multi_rank(ranks, init, 40):
+        assert sum(sites.values()) <= ceiling, (rank, sites)
