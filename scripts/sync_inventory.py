@@ -23,12 +23,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 STAGING = ("_stage_host", "_stage_dev")  # parallel/comm.py gloo bounce-buffer copies
 
 
-def inventory(init: str, n: int, steps_before: int = 2, comm=None):
-    """(counted sites, staging sites) of one step after ``steps_before`` steps"""
+def inventory(init: str, n: int, steps_before: int = 2, comm=None, steps: int = 1):
+    """(counted sites, staging sites) of one step after ``steps_before`` steps (``steps`` > 1: lists of them, one per
+    step: steps in which a per-step octree is rebalanced add the synchronous rebalance loop, octree.update_tree)"""
     from sphexa_amd.app.simulation import Simulation
 
     sim = Simulation(init, n=n, prop="ve", device=torch.device("cuda", 0), comm=comm, out=None, quiet=True)
     sim.run(steps_before)
+    per_step = []
     sites, staged = collections.Counter(), collections.Counter()
 
     def hook(message, category, filename, lineno, file=None, line=None):
@@ -44,26 +46,35 @@ def inventory(init: str, n: int, steps_before: int = 2, comm=None):
 
     warnings.showwarning = hook
     warnings.simplefilter("always")
-    torch.cuda.set_sync_debug_mode("warn")
-    sim.run(1)
-    torch.cuda.set_sync_debug_mode("default")
-    return sites, staged
+    for _ in range(steps):
+        sites.clear()
+        staged.clear()
+        torch.cuda.set_sync_debug_mode("warn")
+        sim.run(1)
+        torch.cuda.set_sync_debug_mode("default")
+        per_step.append((collections.Counter(sites), collections.Counter(staged)))
+    if steps == 1:
+        return per_step[0]
+    return [p[0] for p in per_step], [p[1] for p in per_step]
 
 
-def _worker(rank, size, port, init, n, q):
+def _worker(rank, size, port, init, n, q, steps=1):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(size))
     dist.init_process_group("gloo", rank=rank, world_size=size)
     from sphexa_amd.parallel.comm import Comm
 
-    sites, staged = inventory(init, n, comm=Comm())
-    q.put((rank, dict(sites), dict(staged)))
+    sites, staged = inventory(init, n, comm=Comm(), steps=steps)
+    if steps == 1:
+        q.put((rank, dict(sites), dict(staged)))
+    else:
+        q.put((rank, [dict(x) for x in sites], [dict(x) for x in staged]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def multi_rank(size: int, init: str, n: int):
+def multi_rank(size: int, init: str, n: int, steps: int = 1):
     import socket
 
     import torch.multiprocessing as mp
@@ -74,7 +85,7 @@ def multi_rank(size: int, init: str, n: int):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, size, port, init, n, q)) for r in range(size)]
+    procs = [ctx.Process(target=_worker, args=(r, size, port, init, n, q, steps)) for r in range(size)]
     for p in procs:
         p.start()
     out = sorted(q.get(timeout=600) for _ in procs)

@@ -580,10 +580,20 @@ def _mark_in_boxes(ot, boxes: torch.Tensor, x, y, z, box: Box, out: Optional[tor
     return flags
 
 
+ROW_FIELDS_MAX = 16  # fields per packRows launch (csrc/hip/sfc_sort.hip kMaxGatherFields)
+
+
+def _row_chunks(tensors):
+    return [list(tensors[i:i + ROW_FIELDS_MAX]) for i in range(0, len(tensors), ROW_FIELDS_MAX)]
+
+
 def _pack_rows(tensors: Sequence[torch.Tensor], idx: Optional[torch.Tensor]) -> torch.Tensor:
-    """gather rows idx of several 1-D fields into one (n, rowbytes) uint8 matrix. On the GPU one kernel packs every
-    field (8-byte fields first, rows padded to 8 bytes: csrc/hip/sfc_sort.hip packRows); the CPU path concatenates
-    the fields' bytes in the given order. All ranks use the same path, so both ends agree on the row layout."""
+    """gather rows idx of several 1-D fields into one (n, rowbytes) uint8 matrix. On the GPU one kernel packs up to 16
+    fields (8-byte fields first, rows padded to 8 bytes: csrc/hip/sfc_sort.hip packRows); more fields are packed in
+    chunks of 16 whose row blocks sit side by side. The CPU path concatenates the fields' bytes in the given order. All
+    ranks use the same path, so both ends agree on the row layout."""
+    if len(tensors) > ROW_FIELDS_MAX:
+        return torch.cat([_pack_rows(c, idx) for c in _row_chunks(tensors)], dim=1)
     if tensors and tensors[0].is_cuda:
         hp = _lib.hip()
         sizes = [t.element_size() for t in tensors]
@@ -601,9 +611,22 @@ def _pack_rows(tensors: Sequence[torch.Tensor], idx: Optional[torch.Tensor]) -> 
     return torch.cat(cols, dim=1) if cols else None
 
 
+def _row_width(tensors) -> int:
+    if tensors[0].is_cuda:
+        return _lib.hip().row_bytes([t.element_size() for t in tensors])
+    return sum(t.element_size() for t in tensors)
+
+
 def _unpack_rows(rows: torch.Tensor, tensors: Sequence[torch.Tensor], offset: int):
     n = rows.shape[0]
     if n == 0:
+        return
+    if len(tensors) > ROW_FIELDS_MAX:
+        col = 0
+        for c in _row_chunks(tensors):
+            w = _row_width(c)
+            _unpack_rows(rows[:, col:col + w], c, offset)
+            col += w
         return
     if rows.is_cuda:
         rows = rows.contiguous()

@@ -144,3 +144,21 @@ def test_async_halo_exchanges_in_flight():
         assert r["halos"] > 0
         assert r["err_v"] == 0.0 and r["err_c"] == 0.0
         assert r["kx_min"] >= 1.0
+
+
+def test_pack_rows_more_than_16_fields():
+    """migration packs keys + every conserved field; more than the 16 fields of one packRows launch are
+    packed in chunks whose row blocks sit side by side, and unpack restores every field"""
+    import torch
+
+    from sphexa_amd.parallel.domain import _pack_rows, _unpack_rows
+
+    g = torch.Generator().manual_seed(0)
+    n = 257
+    fields = [torch.randn(n, generator=g, dtype=torch.float64 if k % 3 == 0 else torch.float32) for k in range(21)]
+    idx = torch.randperm(n, generator=g)[:100]
+    rows = _pack_rows(fields, idx)
+    outs = [torch.zeros(200, dtype=f.dtype) for f in fields]
+    _unpack_rows(rows, outs, 50)
+    for f, o in zip(fields, outs):
+        assert torch.equal(o[50:150], f[idx])

@@ -172,3 +172,20 @@ def test_pack_unpack_rows_roundtrip(gpu):
     _unpack_rows(rows, outs, 5)
     for t, o in zip(fields, outs):
         assert torch.equal(o[5:3006], t[idx])
+
+
+@pytest.mark.gpu
+def test_pack_rows_more_than_16_fields_gpu(gpu):
+    """GPU row packing (packRows/unpackRows kernels) of 21 fields: chunks of 16 side by side, exact round trip"""
+    from sphexa_amd.parallel.domain import _pack_rows, _unpack_rows
+
+    g = torch.Generator().manual_seed(0)
+    n = 257
+    fields = [torch.randn(n, generator=g, dtype=torch.float64 if k % 3 == 0 else torch.float32).to(gpu)
+              for k in range(21)]
+    idx = torch.randperm(n, generator=g)[:100].to(gpu)
+    rows = _pack_rows(fields, idx)
+    outs = [torch.zeros(200, dtype=f.dtype, device=gpu) for f in fields]
+    _unpack_rows(rows, outs, 50)
+    for f, o in zip(fields, outs):
+        assert torch.equal(o[50:150], f[idx])
