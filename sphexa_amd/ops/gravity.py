@@ -123,8 +123,12 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         hp.gravity_lists(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), st_dev.data_ptr(),
                          scratch.data_ptr(), TEST_FRONT_CAP, cap_m, cap_l, s)
         pcount = _int32_view(hp.gravity_particle_counts(scratch.data_ptr(), n, cap_m, cap_l), groups, scratch)
+        # per-group offsets of the P2P particle runs: exclusive scan (hand-written tile scan, sample_sort.hip) of the
+        # counts with a trailing zero, so poff[groups] is the total
         poff = torch.zeros(groups + 1, dtype=torch.int64, device=x.device)
-        torch.cumsum(pcount, 0, out=poff[1:])
+        poff[:groups].copy_(pcount)
+        stmp = torch.empty(hp.scan_temp_bytes(groups + 1), dtype=torch.uint8, device=x.device)
+        hp.exclusive_scan_i64(poff.data_ptr(), poff.data_ptr(), groups + 1, stmp.data_ptr(), stmp.numel(), s)
         pacc = torch.empty(4 * n, dtype=torch.float32, device=x.device)  # P2P partials (phi, a) per target
         # the P2P list size goes to pinned host memory ahead of the M2P kernel: the host waits for that copy only,
         # and enqueues the P2P part while M2P runs (no idle gap on the GPU)
@@ -197,7 +201,13 @@ def let_selection_masks(tree: Octree, failed: torch.Tensor, mp: torch.Tensor, n_
     N = tree.num_nodes
     f = failed.bool()
     leaf_open = f[tree.leaf_to_node.long()]
-    pflags = torch.repeat_interleave(leaf_open.to(torch.uint8), tree.counts.long(), output_size=n_particles)
+    if n_particles is None:
+        pflags = torch.repeat_interleave(leaf_open.to(torch.uint8), tree.counts.long())
+    else:
+        # leaf of every particle from the leaf start offsets (no scan of the counts, no host copy)
+        starts = tree.node_start[tree.leaf_to_node.long()].long() - tree.offset
+        lidx = torch.searchsorted(starts, torch.arange(n_particles, device=f.device), right=True) - 1
+        pflags = leaf_open[lidx.clamp(min=0)].to(torch.uint8)
     mass = mp.view(-1, 8)[:, 0]
     send = ~f & (mass > 0)
     if N > 1:

@@ -104,3 +104,29 @@ def gather_many(perm: torch.Tensor, srcs: Sequence[torch.Tensor], outs: Sequence
         for s, o in zip(srcs, outs):
             _lib.cpu().gather(n, perm.data_ptr(), s.data_ptr(), o.data_ptr(), s.element_size())
     return outs
+
+
+def exclusive_scan(t: torch.Tensor) -> torch.Tensor:
+    """exclusive prefix sum (int64) of a 1-D tensor; on the GPU the hand-written tile scan (csrc/hip/sample_sort.hip),
+    so a time step runs no library (rocPRIM) scan"""
+    t = t.to(torch.int64).contiguous()
+    n = t.numel()
+    if not t.is_cuda or n == 0:
+        return torch.cumsum(t, 0) - t
+    h = _lib.hip()
+    out = torch.empty_like(t)
+    tmp = torch.empty(h.scan_temp_bytes(n), dtype=torch.uint8, device=t.device)
+    h.exclusive_scan_i64(t.data_ptr(), out.data_ptr(), n, tmp.data_ptr(), tmp.numel(), _stream())
+    return out
+
+
+def compact_indices(flags: torch.Tensor, count: int) -> torch.Tensor:
+    """indices of the nonzero entries of ``flags`` in order, given their number (known on the host): exclusive scan
+    + scatter, no host synchronization and no library select kernel"""
+    n = flags.numel()
+    f = flags.reshape(-1) != 0
+    pos = exclusive_scan(f)
+    out = torch.empty(count + 1, dtype=torch.int64, device=flags.device)
+    dst = torch.where(f, pos, torch.full_like(pos, count))
+    out.scatter_(0, dst, torch.arange(n, dtype=torch.int64, device=flags.device))
+    return out[:count]

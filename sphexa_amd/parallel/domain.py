@@ -23,10 +23,14 @@ MI355X-native design:
     octree_focus_mpi.hpp): a push-based locally-essential tree. Every sender walks its own-particle tree against
     each receiver's boxes (ops.gravity.mark_let): nodes whose particle box overlaps a receiver box or whose vector
     MAC the box violates are opened; particles of opened leaves become the receiver's halos (a superset of the
-    SPH halos), the first unopened node on every root-to-leaf path is sent as one quadrupole. Received
-    quadrupoles (``remote_centers``/``remote_quads``) pass the MAC for every local target by construction and
-    are applied as a flat M2P; the local octree over own + halos provides the rest, so every remote particle's
-    mass is counted exactly once.
+    SPH halos), the first unopened node on every root-to-leaf path is sent as one quadrupole. The received
+    quadrupoles (``remote_centers``/``remote_quads``) become the leaves of a remote LET tree (``remote_tree``,
+    ops.gravity.remote_let_tree) whose leaves carry the always-accept MAC sentinel and whose internal nodes combine
+    them; the local octree over own + halos provides the rest, so every remote particle's mass is counted once.
+  * host synchronizations of a multi-rank sync: the global leaf counts (host rebalance + cut search), the send and
+    receive counts of the migration, the halo/multipole counts of the discovery (all counts exchanged on the device,
+    one copy each), the remote LET codes with gravity; the halo-ownership check is deferred into the propagator's
+    time-step copy (``pending_checks``). scripts/sync_inventory.py, tests/test_syncs_gpu.py.
 """
 
 from __future__ import annotations
@@ -338,7 +342,7 @@ class Domain:
         self.stats["peers"] = len(peers - {self.rank})
         # per destination rank: particle flags (halos) and, with gravity, multipole-node flags; the counts of all
         # ranks go through one device all-to-all and come to the host with the receive counts in ONE copy, then the
-        # index lists are extracted at their known sizes (nonzero_static: no further synchronization)
+        # index lists are compacted at their known sizes (scan + scatter: no further synchronization)
         dev = skeys.device
         n_own = skeys.numel()
         flag_rows = torch.zeros((self.size, n_own), dtype=torch.uint8, device=dev)
@@ -364,9 +368,9 @@ class Domain:
         send_idx: List[torch.Tensor] = []
         mp_send: List[torch.Tensor] = []
         for q in range(self.size):
-            send_idx.append(torch.nonzero_static(flag_rows[q], size=int(send_h[q, 0])).flatten())
+            send_idx.append(sfc_ops.compact_indices(flag_rows[q], int(send_h[q, 0])))
             if gravity:
-                mp_send.append(torch.nonzero_static(node_rows[q], size=int(send_h[q, 1])).flatten())
+                mp_send.append(sfc_ops.compact_indices(node_rows[q], int(send_h[q, 1])))
         del flag_rows, node_rows
         if gravity:
             self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes, [int(v) for v in recv_h[:, 1]])
@@ -546,12 +550,12 @@ def _coarse_cut(ot, center, half, max_boxes: int) -> torch.Tensor:
     at_level = torch.zeros(nl, dtype=torch.int64, device=dev).scatter_add_(0, lv, nonempty.long())
     leaves_at = torch.zeros(nl, dtype=torch.int64, device=dev).scatter_add_(0, lv, (nonempty & is_leaf).long())
     # cut(c) = nonempty nodes at level c + nonempty leaves above c
-    sizes = at_level + torch.cumsum(leaves_at, 0) - leaves_at
+    sizes = at_level + sfc_ops.exclusive_scan(leaves_at)
     depth = min(nl, ot.max_depth() + 2)
     ok = (sizes[:depth] <= max_boxes) | (torch.arange(depth, device=dev) == 0)  # the root always fits
     best = torch.cumprod(ok.long(), 0).sum() - 1  # deepest level with every shallower cut fitting as well
     sel = ((lv == best) | (is_leaf & (lv < best))) & nonempty
-    pos = torch.cumsum(sel.long(), 0) - 1
+    pos = sfc_ops.exclusive_scan(sel.long())  # rank of each selected node among the selected
     idx = torch.where(sel, pos, torch.full_like(pos, max_boxes))
     rows = torch.cat([center.view(-1, 3), half.view(-1, 3)], dim=1)
     out = torch.zeros((max_boxes + 1, 6), dtype=rows.dtype, device=dev)
