@@ -127,6 +127,11 @@ PYBIND11_MODULE(_sphx_hip, m)
                           Ptr s) { packRows(n, P<int64_t>(idx), src, sizes, P<void>(rows), St(s)); });
     m.def("unpack_rows", [](int64_t n, Ptr rows, const std::vector<uintptr_t>& dst, const std::vector<int>& sizes,
                             int64_t off, Ptr s) { unpackRows(n, P<void>(rows), dst, sizes, off, St(s)); });
+    m.def("reduce_work_bytes", []() { return reduceWorkBytes(); });
+    m.def("multi_min_max", [](int64_t n, const std::vector<uintptr_t>& ptrs, const std::vector<int>& isDouble, Ptr out,
+                              Ptr work, Ptr s) { multiMinMax(n, ptrs, isDouble, P<double>(out), P<void>(work), St(s)); });
+    m.def("max_norm2", [](int64_t first, int64_t last, Ptr ax, Ptr ay, Ptr az, Ptr out, Ptr work, Ptr s)
+          { maxNorm2(first, last, P<float>(ax), P<float>(ay), P<float>(az), P<double>(out), P<void>(work), St(s)); });
     m.def("scan_temp_bytes", [](int64_t n) { return scanTempBytes(n); });
     m.def("exclusive_scan_i64", [](Ptr in, Ptr out, int64_t n, Ptr tmp, size_t tb, Ptr s)
           { exclusiveScanI64(P<int64_t>(in), P<int64_t>(out), n, P<void>(tmp), tb, St(s)); });
@@ -194,6 +199,8 @@ PYBIND11_MODULE(_sphx_hip, m)
           py::arg("iterateH"), py::arg("stats"), py::arg("scratch"), py::arg("testFrontCap"), py::arg("s"),
           py::arg("home") = 0, py::arg("ov_stride") = 1, py::arg("m") = 0, py::arg("ntot") = 0, py::arg("rec") = 0);
     m.def("neighbor_row_stripes", []() { return neighborRowStripes(); });
+    m.def("row_plan", [](int64_t groups, unsigned ngmax, Ptr tab, int home, Ptr over, Ptr s)
+          { rowPlan(groups, ngmax, P<int32_t>(tab), home, P<unsigned long long>(over), St(s)); });
     m.def("packed_table_ints", [](unsigned ngmax) { return packedTableInts(ngmax); });
     m.def("packed_rows_max", [](unsigned ngmax) { return packedRowsMax(ngmax); });
     m.def("list_blocks_max", [](unsigned ngmax) { return listBlocksMax(ngmax); });

@@ -67,6 +67,13 @@ size_t exclusiveScanTempBytes(int64_t n);
 void exclusiveScanI64Hip(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s);
 void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s);
 
+// reduce.hip: single-launch reductions (workspace: reduceWorkBytes(), zero-initialized once; one stream at a time)
+size_t reduceWorkBytes();
+void multiMinMax(int64_t n, const std::vector<uintptr_t>& ptrs, const std::vector<int>& isDouble, double* out,
+                 void* work, hipStream_t s);
+void maxNorm2(int64_t first, int64_t last, const float* ax, const float* ay, const float* az, double* out, void* work,
+              hipStream_t s);
+
 // octree.hip
 void nodeCounts(const KeyT* tree, int64_t L, const KeyT* keys, int64_t n, int32_t* counts, hipStream_t s);
 void rebalanceOps(const KeyT* tree, const int32_t* counts, int64_t L, uint32_t bucket, int64_t* ops, int* changed,
@@ -101,6 +108,8 @@ void packPosQ(int64_t n, const double* x, const double* y, const double* z, cons
               SrcPosQ* out, hipStream_t s);
 //! overflow-row stripes of the packed-list pool; stats must hold 8 + 32 * stripes counters
 int neighborRowStripes();
+//! list-row demand of the next search's five pool candidates per overflow stripe (zeroed over[5 * stripes], += )
+void rowPlan(int64_t groups, unsigned ngmax, const int32_t* tab, int home, unsigned long long* over, hipStream_t s);
 
 // hydro.hip
 struct MomFields

@@ -823,6 +823,44 @@ static void scratchLayout(int64_t n, int64_t& spillMemOff, int64_t& total)
 
 int neighborRowStripes() { return kRowStripes; }
 
+/*! @brief list-row demand of the next search's pool candidates: over[k][s] = sum over the groups g of stripe
+ *         s = g mod stripes of max(rows_g - cand_k, 0), cand_k = max(1, home + k - 2), rows_g = list blocks + chunk-table
+ *         rows of group g (its table). One launch instead of a torch expression per candidate (ops/neighbors.py).
+ */
+__global__ void rowPlanKernel(int64_t groups, int T, const int32_t* __restrict__ tab, int home, int stripes,
+                              unsigned long long* __restrict__ over)
+{
+    __shared__ unsigned long long acc[5][kRowStripes];
+    for (int e = threadIdx.x; e < 5 * kRowStripes; e += blockDim.x)
+        acc[e / kRowStripes][e % kRowStripes] = 0ull;
+    __syncthreads();
+    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < groups; g += int64_t(gridDim.x) * blockDim.x)
+    {
+        const int32_t* t = tab + g * T;
+        const int rows   = t[0] + (t[1] >> 16);
+        const int s      = int(g % stripes);
+        for (int k = 0; k < 5; ++k)
+        {
+            const int c = max(1, home + k - 2);
+            if (rows > c) atomicAdd(&acc[k][s], (unsigned long long)(rows - c));
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 5 * stripes; e += blockDim.x)
+    {
+        const unsigned long long v = acc[e / stripes][e % stripes];
+        if (v) atomicAdd(over + e, v);
+    }
+}
+
+void rowPlan(int64_t groups, unsigned ngmax, const int32_t* tab, int home, unsigned long long* over, hipStream_t s)
+{
+    if (groups <= 0) return;
+    const unsigned grid = unsigned(std::min<int64_t>(256, (groups + 255) / 256));
+    rowPlanKernel<<<grid, 256, 0, s>>>(groups, int(packedTableInts(ngmax)), tab, home, kRowStripes, over);
+    SPHX_LAUNCH_CHECK();
+}
+
 size_t neighborScratchBytes(int64_t n, unsigned)
 {
     int64_t a, total;

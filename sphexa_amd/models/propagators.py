@@ -116,9 +116,9 @@ class Propagator:
                 rho = torch.full((), float(d.minDtRho), **f64)
             acc = inf
             if grav:
-                a2 = (d["ax"][first:last].double() ** 2 + d["ay"][first:last].double() ** 2 +
-                      d["az"][first:last].double() ** 2).max()
-                max_acc = torch.sqrt(a2)
+                from ..ops.reduce import max_norm2
+
+                max_acc = torch.sqrt(max_norm2(d["ax"], d["ay"], d["az"], first, last))
                 acc = torch.where(max_acc > 0, d.etaAcc * torch.sqrt(d.eps / max_acc), inf)
             others = min([d.maxDtIncrease * d.minDt] + [float(e) for e in extra])
             loc = torch.minimum(torch.minimum(torch.minimum(acc, courant), rho), torch.full((), others, **f64))

@@ -184,8 +184,10 @@ def global_h_min_device(d, comm) -> torch.Tensor:
     h = d["h"][: d.size]
     m = d["m"][: d.size]
     if h.numel():
-        lo, hi = torch.aminmax(m)
-        loc = torch.stack([h.min().to(torch.float64), lo.to(torch.float64), -hi.to(torch.float64)])
+        from .reduce import min_max
+
+        mm = min_max([h, m])  # [min h, max h, min m, max m], one launch on the GPU
+        loc = torch.stack([mm[0], mm[2], -mm[3]])
     else:
         loc = torch.full((3,), math.inf, dtype=torch.float64, device=h.device)
     if comm is not None and comm.size > 1:

@@ -200,22 +200,6 @@ def _pool_plan(prev: NeighborList | None, groups: int, ng0: int, stripes: int):
     return max(1, round(ng0 / 8) + 1), max(8, -(-int(0.35 * ng0 / 8 * groups + 0.5) // stripes))
 
 
-def _next_plan(buf: torch.Tensor, groups: int, ngmax: int, home: int, stripes: int):
-    """rows per group of this search (table column 0) -> the pool plan of the next one, chosen among home +- 2 for
-    the fewest rows (home rows of every group + stripe capacity for the longest stripe's overflow, +10 %); returns
-    device tensors [5] of (home candidates, total rows)"""
-    T = packed_table_ints(ngmax)
-    nr = group_rows(buf[:groups * T].view(groups, T)).to(torch.int32)
-    pad = (-groups) % stripes
-    if pad:
-        nr = torch.cat([nr, torch.zeros(pad, dtype=torch.int32, device=nr.device)])
-    cand = (torch.arange(-2, 3, device=nr.device) + home).clamp(min=1)
-    # one candidate at a time: a (5, groups) temporary would be 40 B/particle at the search's memory high-water mark
-    over = torch.stack([(nr - cand[k]).clamp_(min=0).view(-1, stripes).sum(dim=0).amax() for k in range(5)])
-    ov = (over.double() * 1.1).long() + 8
-    return cand, ov, cand * groups + stripes * ov
-
-
 def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
                    nidx: torch.Tensor | None = None, prev: NeighborList | None = None,
                    ride_along=None) -> NeighborList:
@@ -263,34 +247,40 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               int(iterate_h) | (2 if COLLECT_STATS else 0), stats.data_ptr(),
                               scratch.data_ptr(), TEST_FRONT_CAP, _stream(), home=home, ov_stride=ov,
                               m=d["m"].data_ptr(), ntot=d.size, rec=rec.data_ptr())
-            ctr = stats[8::32][:K]
-            cand, cand_ov, cand_rows = _next_plan(buf, num_groups, ngmax, home, K)
+            # per-stripe row demand of the five pool candidates of the next search (one kernel), the stripe
+            # counters and the search statistics: one host copy
+            over = torch.zeros(5 * K, dtype=torch.int64, device=x.device)
+            hp.row_plan(num_groups, ngmax, buf.data_ptr(), home, over.data_ptr(), _stream())
             # evaluated once per call (it may issue a collective, so every rank calls it exactly once); a repeated
             # search keeps the converged h of the first one, so the first values stay valid
             first_try = _attempt == 0
             ex = (ride_along().to(torch.float64).reshape(-1).view(torch.int64)
                   if (ride_along is not None and first_try) else None)
-            parts = [stats[:8], ctr.amax().view(1), ctr.sum().view(1), cand, cand_ov, cand_rows]
+            parts = [stats[:8], stats[8::32][:K], over]
             host = torch.cat(parts + ([ex] if ex is not None else [])).cpu()
             if ex is not None:
-                ride_host = host[25:].view(torch.float64).tolist()
+                ride_host = host[8 + 6 * K:].view(torch.float64).tolist()
             st = host[:8]
-            if int(host[8]) <= ov:
+            ctr = host[8:8 + K]
+            if int(ctr.max()) <= ov:
                 break
             # an overflow stripe ran out: the search left h converged, repeat it with enough rows
             buf = nidx = None
             if prev is not None:
                 prev.nidx = None
-            buf = torch.empty(region + (num_groups * home + K * (int(int(host[8]) * 1.1) + 8)) * 256,
+            buf = torch.empty(region + (num_groups * home + K * (int(int(ctr.max()) * 1.1) + 8)) * 256,
                               dtype=torch.int32, device=x.device)
         else:
             raise NeighborSearchError("packed neighbor lists: overflow rows exhausted twice")
         # the search packed every particle's SrcPosQ record into workspace 0: the XMass loop reads them as they are
         _handoff(d).clear()
         handoff_mark(d, "posq_all")
-        used = num_groups * home + int(host[9])
-        best = int(torch.argmin(host[20:25]))
-        plan_home, plan_ov = int(host[10 + best]), int(host[15 + best])
+        cand = (torch.arange(-2, 3) + home).clamp(min=1)
+        cand_ov = (host[8 + K:8 + 6 * K].view(5, K).amax(dim=1).double() * 1.1).long() + 8
+        cand_rows = cand * num_groups + K * cand_ov
+        used = num_groups * home + int(ctr.sum())
+        best = int(torch.argmin(cand_rows))
+        plan_home, plan_ov = int(cand[best]), int(cand_ov[best])
         # size the next pool for the largest need of the last 32 searches: neighbor counts on lattices jump between
         # shells every few steps (Sedov: 12 -> 16 rows per group for one step), and a pool sized for the last step
         # alone would make those steps repeat the search

@@ -48,6 +48,7 @@ from .comm import Comm, MAX, MIN, SUM
 
 HALO_FIELDS = ("x", "y", "z", "h", "m")
 REORDER_BATCH = 3  # conserved fields reordered per gather launch in sync (bounds the transient memory)
+REORDER_ALL_BYTES = 1 << 30  # below this transient size all remaining fields are reordered together
 
 
 class HaloOwnershipError(RuntimeError):
@@ -118,13 +119,10 @@ class Domain:
         """recompute extents of non-periodic dimensions from the owned particles (global MIN/MAX allreduce)"""
         if all(b == PERIODIC for b in self.box.bc):
             return
-        coords = (x, y, z)
-        dev = x.device
-        mins = torch.stack([c.min() if c.numel() else torch.tensor(math.inf, dtype=c.dtype, device=dev)
-                            for c in coords])
-        maxs = torch.stack([c.max() if c.numel() else torch.tensor(-math.inf, dtype=c.dtype, device=dev)
-                            for c in coords])
-        ext = torch.cat([mins, -maxs])
+        from ..ops.reduce import min_max
+
+        mm = min_max([x, y, z]).view(3, 2)  # one launch on the GPU
+        ext = torch.cat([mm[:, 0], -mm[:, 1]])
         self.comm.allreduce(ext, MIN)
         ext = ext.cpu().tolist()
         for d in range(3):
@@ -179,8 +177,11 @@ class Domain:
         # which stay alive until their gather has been enqueued)
         rest = [f for f in names if f not in sorted_done]
         cap = d.capacity
-        for c in range(0, len(rest), REORDER_BATCH):
-            batch = rest[c:c + REORDER_BATCH]
+        # a few fields per gather launch bounds the transient memory of large runs; small ones (launch-bound) take
+        # all fields in one or two launches
+        per = len(rest) if cap * 8 * max(len(rest), 1) <= REORDER_ALL_BYTES else REORDER_BATCH
+        for c in range(0, len(rest), max(per, 1)):
+            batch = rest[c:c + max(per, 1)]
             bufs = [torch.empty(cap, dtype=d.buffer(f).dtype, device=d.device) for f in batch]
             sfc_ops.gather_many(perm, [own[f] for f in batch], [b[self.start:self.end] for b in bufs])
             for f, b in zip(batch, bufs):
