@@ -338,12 +338,28 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
             for (int r = 0; r < 4; ++r)
                 C[r] = sC[16 * tile + 4 * kq + r];
             const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#ifdef SPHX_M2P_PIPE
+            f32x4 Qxn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[0], zero, 0, 0, 0);
+            f32x4 Qyn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[0], zero, 0, 0, 0);
+            f32x4 Qzn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[0], zero, 0, 0, 0);
+#endif
 #pragma unroll
             for (int tb = 0; tb < 4; ++tb)
             {
+#ifdef SPHX_M2P_PIPE
+                const f32x4 Qx = Qxn, Qy = Qyn, Qz = Qzn;
+                if (tb < 3)
+                {
+                    Qxn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[tb + 1], zero, 0, 0, 0);
+                    Qyn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[tb + 1], zero, 0, 0, 0);
+                    Qzn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[tb + 1], zero, 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#else
                 const f32x4 Qx = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[tb], zero, 0, 0, 0);
                 const f32x4 Qy = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[tb], zero, 0, 0, 0);
                 const f32x4 Qz = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[tb], zero, 0, 0, 0);
+#endif
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                 {
@@ -721,11 +737,27 @@ __device__ inline void flushP2P(const int32_t* plst, int n, const GravLists& L, 
             }
             const f32x4 cR  = {Pr[0].w, Pr[1].w, Pr[2].w, Pr[3].w};
             const f32x4 c0v = {0.f, 0.f, 0.f, 0.f};
+#ifndef SPHX_P2P_NOPIPE
+            // the next target block's tiles are issued before this block's VALU work, so the ~40-cycle MFMA result
+            // latency is covered by the wave's own pair arithmetic instead of stalling it once per block
+            f32x4 R2n = __builtin_amdgcn_mfma_f32_16x16x4f32(aR, T.bR2[0], cR, 0, 0, 0);
+            f32x4 H2n = __builtin_amdgcn_mfma_f32_16x16x4f32(aH, T.bH2[0], c0v, 0, 0, 0);
+#endif
 #pragma unroll
             for (int tb = 0; tb < 4; ++tb)
             {
+#ifdef SPHX_P2P_NOPIPE
                 f32x4 R2 = __builtin_amdgcn_mfma_f32_16x16x4f32(aR, T.bR2[tb], cR, 0, 0, 0);
                 f32x4 H2 = __builtin_amdgcn_mfma_f32_16x16x4f32(aH, T.bH2[tb], c0v, 0, 0, 0);
+#else
+                const f32x4 R2 = R2n, H2 = H2n;
+                if (tb < 3)
+                {
+                    R2n = __builtin_amdgcn_mfma_f32_16x16x4f32(aR, T.bR2[tb + 1], cR, 0, 0, 0);
+                    H2n = __builtin_amdgcn_mfma_f32_16x16x4f32(aH, T.bH2[tb + 1], c0v, 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0); // keep the scheduler from sinking them back to their first use
+#endif
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                 {
@@ -1062,6 +1094,86 @@ __global__ __launch_bounds__(256) void gravityExpandKernel(int64_t first, int64_
     }
 }
 
+/* Cost-ordered dispatch of the evaluation kernels. A group's P2P (M2P) work is its particle (node) count, which
+ * varies ~7x between Evrard groups (mean 3.8 k P2P per target, max 27 k): dispatched in SFC order, the heaviest
+ * groups can start late and leave most SIMDs idle at the end of the kernel. The groups are therefore handed out
+ * heaviest first (longest-processing-time order), binned by work with 4 bins per octave: a histogram kernel and a
+ * scatter kernel (order within a bin is arbitrary; every group is evaluated independently, results are unchanged).
+ */
+constexpr int kOrdBins = 128;
+
+//! @brief bin of a group's work, heaviest bin first (0); empty and fallback groups (count <= 0) last
+__device__ __forceinline__ int costBin(int c)
+{
+    if (c <= 0) return kOrdBins - 1;
+    const unsigned u = unsigned(c);
+    const int e      = 31 - __clz(u);
+    const int sub    = e >= 2 ? int(u >> (e - 2)) & 3 : 0;
+    return kOrdBins - 2 - min(4 * e + sub, kOrdBins - 2);
+}
+
+//! @brief work of group g in evaluation kernel k (0: M2P nodes, 1: P2P particles)
+__device__ __forceinline__ int groupWork(const GravSlabs& S, int64_t g, int k)
+{
+    return k == 0 ? S.counts[2 * g] : (S.counts[2 * g] < 0 ? 0 : S.pcount[g]);
+}
+
+__global__ __launch_bounds__(256) void gravityOrderHistKernel(int64_t groups, GravSlabs S, int32_t* __restrict__ hist)
+{
+    __shared__ int32_t h[2 * kOrdBins];
+    for (int k = threadIdx.x; k < 2 * kOrdBins; k += blockDim.x)
+        h[k] = 0;
+    __syncthreads();
+    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < groups; g += int64_t(gridDim.x) * blockDim.x)
+    {
+        atomicAdd(&h[costBin(groupWork(S, g, 0))], 1);
+        atomicAdd(&h[kOrdBins + costBin(groupWork(S, g, 1))], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 2 * kOrdBins; k += blockDim.x)
+        if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+
+//! @brief order[k][pos] = group, bins in ascending order (heaviest first); hist/cursor: 2 x kOrdBins (cursor zeroed)
+__global__ __launch_bounds__(256) void gravityOrderScatterKernel(int64_t groups, GravSlabs S,
+                                                                 const int32_t* __restrict__ hist,
+                                                                 int32_t* __restrict__ cursor,
+                                                                 int32_t* __restrict__ order)
+{
+    __shared__ int32_t off[2 * kOrdBins];
+    if (threadIdx.x < 2)
+    {
+        int s = 0;
+        for (int b = 0; b < kOrdBins; ++b)
+        {
+            off[threadIdx.x * kOrdBins + b] = s;
+            s += hist[threadIdx.x * kOrdBins + b];
+        }
+    }
+    __syncthreads();
+    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < groups; g += int64_t(gridDim.x) * blockDim.x)
+    {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+        {
+            const int b = k * kOrdBins + costBin(groupWork(S, g, k));
+            order[k * groups + off[b] + atomicAdd(&cursor[b], 1)] = int32_t(g);
+        }
+    }
+}
+
+//! @brief group of a wave of the evaluation kernels: the cost order when given, else XCD-aware SFC order
+__device__ __forceinline__ int64_t evalGroup(const int32_t* order, int64_t numGroups)
+{
+    const int wave = threadIdx.x >> 6;
+    if (order)
+    {
+        const int64_t slot = int64_t(blockIdx.x) * kGWaves + wave;
+        return slot < numGroups ? int64_t(order[slot]) : numGroups;
+    }
+    return int64_t(xcdRemap(blockIdx.x, gridDim.x)) * kGWaves + wave;
+}
+
 //! @brief shared prologue of the evaluation kernels: the group's targets, fp64 box center, fp32 relative coordinates
 struct EvalTarget
 {
@@ -1094,7 +1206,8 @@ __global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t 
                                                            float G, float* __restrict__ ax, float* __restrict__ ay,
                                                            float* __restrict__ az, double* __restrict__ ugrav,
                                                            double* __restrict__ out,
-                                                           unsigned long long* __restrict__ stats, GravSlabs S)
+                                                           unsigned long long* __restrict__ stats, GravSlabs S,
+                                                           const int32_t* __restrict__ order)
 {
 #ifdef SPHX_GRAV_M2P_MFMA2
     __shared__ float4 stage[kGWaves][kM2P2Stage];
@@ -1104,7 +1217,7 @@ __global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t 
     __shared__ double red[kGWaves];
     const int wave          = threadIdx.x >> 6;
     const int64_t numGroups = (last - first + 63) / 64;
-    const int64_t g         = int64_t(xcdRemap(blockIdx.x, gridDim.x)) * kGWaves + wave;
+    const int64_t g         = evalGroup(order, numGroups);
     double upot             = 0;
     int nm                  = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[2 * g]) : -1;
     SPHX_DCHECK(nm <= S.capM, 3);
@@ -1143,14 +1256,15 @@ __global__ __launch_bounds__(256, SPHX_P2P_WAVES) void gravityP2PKernel(int64_t 
                                                            unsigned long long* __restrict__ stats, GravSlabs S,
                                                            const int64_t* __restrict__ poff,
                                                            const int32_t* __restrict__ pidx,
-                                                           float4* __restrict__ pacc)
+                                                           float4* __restrict__ pacc,
+                                                           const int32_t* __restrict__ order)
 {
     __shared__ GravLds lds[kGWaves];
     __shared__ double red[kGWaves];
     const int lane          = laneId();
     const int wave          = threadIdx.x >> 6;
     const int64_t numGroups = (last - first + 63) / 64;
-    const int64_t g         = int64_t(xcdRemap(blockIdx.x, gridDim.x)) * kGWaves + wave;
+    const int64_t g         = evalGroup(order, numGroups);
     double upot             = 0;
     const int nl            = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[2 * g + 1]) : -1;
     if (nl >= 0)
@@ -1190,7 +1304,7 @@ __global__ void gravityCombineKernel(int64_t first, int64_t last, const float4* 
     if (ugrav) ugrav[i] += double(G) * double(m[i]) * double(a.x);
 }
 
-constexpr int kGSpillWaves = 128;
+constexpr int kGSpillWaves = 512;
 constexpr int kGSpillFront = 65536;
 
 __global__ __launch_bounds__(64) void gravitySpillKernel(int64_t first, int64_t last, GravTree t,
@@ -1225,7 +1339,7 @@ size_t gravityScratchBytes(int64_t n, int capM, int capL)
 {
     int64_t groups = (n + 63) / 64;
     return size_t(padTo64(groups) + int64_t(kGSpillWaves) * kGSpillFront + padTo64(2 * groups) + padTo64(groups) +
-                  groups * int64_t(capM + capL)) *
+                  groups * int64_t(capM + capL) + padTo64(2 * groups) + 4 * kOrdBins) *
            sizeof(int32_t);
 }
 
@@ -1234,6 +1348,8 @@ struct GravScratch
     int32_t* spillList;
     int32_t* spillMem;
     GravSlabs S;
+    int32_t* order; // 2 x groups: M2P order, P2P order (heaviest first)
+    int32_t* hist;  // 2 x kOrdBins histogram + 2 x kOrdBins scatter cursors
 };
 
 static GravScratch carve(void* scratch, int64_t groups, int capM, int capL)
@@ -1246,6 +1362,8 @@ static GravScratch carve(void* scratch, int64_t groups, int capM, int capL)
     int32_t* mlist  = pcount + padTo64(groups);
     int32_t* llist  = mlist + groups * int64_t(capM);
     c.S             = GravSlabs{mlist, llist, counts, pcount, capM, capL};
+    c.order         = llist + groups * int64_t(capL);
+    c.hist          = c.order + padTo64(2 * groups);
     return c;
 }
 
@@ -1285,10 +1403,32 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
     unsigned grid  = unsigned((groups + kGWaves - 1) / kGWaves);
     // phase 1: M2P only (needs no particle index list), phase 2: the P2P part, 0: both. Split so that the host
     // reads the P2P list size while the M2P kernel runs (ops/gravity.py)
+#ifdef SPHX_GRAV_SFC_ORDER
+    const int32_t* orderM = nullptr;
+    const int32_t* orderP = nullptr;
+#else
+    // M2P keeps the SFC order by default: heaviest-first dispatch scatters the node lists of concurrently running
+    // groups over the tree (A/B on Evrard -n 200: P2P 10.14 -> 9.29 ms, M2P 8.10 -> 8.60 ms with both ordered)
+#ifdef SPHX_GRAV_M2P_ORDER
+    const int32_t* orderM = c.order;
+#else
+    const int32_t* orderM = nullptr;
+#endif
+    const int32_t* orderP = c.order + groups;
+    if (phase != 2)
+    {
+        SPHX_CHECK(hipMemsetAsync(c.hist, 0, 4 * kOrdBins * sizeof(int32_t), s));
+        const unsigned og = unsigned(std::min<int64_t>((groups + 255) / 256, 1024));
+        gravityOrderHistKernel<<<og, 256, 0, s>>>(groups, c.S, c.hist);
+        SPHX_LAUNCH_CHECK();
+        gravityOrderScatterKernel<<<og, 256, 0, s>>>(groups, c.S, c.hist, c.hist + 2 * kOrdBins, c.order);
+        SPHX_LAUNCH_CHECK();
+    }
+#endif
     if (phase == 1)
     {
         gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
-                                                       stats, c.S);
+                                                       stats, c.S, orderM);
         SPHX_LAUNCH_CHECK();
         return;
     }
@@ -1312,13 +1452,13 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
     SPHX_CHECK(hipEventRecord(fork, s));
     SPHX_CHECK(hipStreamWaitEvent(side, fork, 0));
     gravityP2PKernel<<<grid, 64 * kGWaves, 0, side>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
-                                                      stats, c.S, poff, pidx, pacc);
+                                                      stats, c.S, poff, pidx, pacc, orderP);
     SPHX_LAUNCH_CHECK();
     SPHX_CHECK(hipEventRecord(join, side));
     if (phase == 0)
     {
         gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
-                                                       stats, c.S);
+                                                       stats, c.S, orderM);
         SPHX_LAUNCH_CHECK();
     }
     SPHX_CHECK(hipStreamWaitEvent(s, join, 0));

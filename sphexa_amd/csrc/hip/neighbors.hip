@@ -782,7 +782,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) SPHX_NS_OCC void findNeighbors
 /*! spill path: persistent waves take the queued groups and redo them with frontier/leaf storage in global
  *  memory (kSpillFront / kSpillLeaves entries per wave); a group that overflows even these counts in stats[1]
  */
-constexpr int kSpillWaves  = 128;
+constexpr int kSpillWaves  = 512; // persistent waves of the spill kernel (Noh -n 300: 128 waves took 2.7 ms)
 constexpr int kSpillFront  = 16384;
 constexpr int kSpillLeaves = 65536;
 

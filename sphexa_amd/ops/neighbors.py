@@ -20,6 +20,7 @@ from __future__ import annotations
 import os
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -257,10 +258,12 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
             ex = (ride_along().to(torch.float64).reshape(-1).view(torch.int64)
                   if (ride_along is not None and first_try) else None)
             parts = [stats[:8], stats[8::32][:K], over]
-            host = torch.cat(parts + ([ex] if ex is not None else [])).cpu()
+            # (host-side bookkeeping in numpy: a torch op on a CPU tensor costs ~5-10 us of launch-path overhead,
+            # and the GPU idles until the pair loops are enqueued)
+            host = torch.cat(parts + ([ex] if ex is not None else [])).cpu().numpy()
             if ex is not None:
-                ride_host = host[8 + 6 * K:].view(torch.float64).tolist()
-            st = host[:8]
+                ride_host = host[8 + 6 * K:].view(np.float64).tolist()
+            st = host[:8].tolist()
             ctr = host[8:8 + K]
             if int(ctr.max()) <= ov:
                 break
@@ -275,11 +278,11 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         # the search packed every particle's SrcPosQ record into workspace 0: the XMass loop reads them as they are
         _handoff(d).clear()
         handoff_mark(d, "posq_all")
-        cand = (torch.arange(-2, 3) + home).clamp(min=1)
-        cand_ov = (host[8 + K:8 + 6 * K].view(5, K).amax(dim=1).double() * 1.1).long() + 8
+        cand = np.maximum(np.arange(-2, 3) + home, 1)
+        cand_ov = (host[8 + K:8 + 6 * K].reshape(5, K).max(axis=1).astype(np.float64) * 1.1).astype(np.int64) + 8
         cand_rows = cand * num_groups + K * cand_ov
         used = num_groups * home + int(ctr.sum())
-        best = int(torch.argmin(cand_rows))
+        best = int(np.argmin(cand_rows))
         plan_home, plan_ov = int(cand[best]), int(cand_ov[best])
         # size the next pool for the largest need of the last 32 searches: neighbor counts on lattices jump between
         # shells every few steps (Sedov: 12 -> 16 rows per group for one step), and a pool sized for the last step
