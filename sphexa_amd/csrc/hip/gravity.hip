@@ -1134,13 +1134,15 @@ __global__ __launch_bounds__(256) void gravityOrderHistKernel(int64_t groups, Gr
         if (h[k]) atomicAdd(&hist[k], h[k]);
 }
 
-//! @brief order[k][pos] = group, bins in ascending order (heaviest first); hist/cursor: 2 x kOrdBins (cursor zeroed)
+//! @brief order[k][pos] = group, bins in ascending order (heaviest first); hist/cursor: 2 x kOrdBins (cursor zeroed).
+//!        Ranks within a bin are taken in LDS per block and one global atomic per (block, bin) reserves their range:
+//!        one global atomic per group and kernel on a handful of hot bins took ~1 ms for 74 k groups.
 __global__ __launch_bounds__(256) void gravityOrderScatterKernel(int64_t groups, GravSlabs S,
                                                                  const int32_t* __restrict__ hist,
                                                                  int32_t* __restrict__ cursor,
                                                                  int32_t* __restrict__ order)
 {
-    __shared__ int32_t off[2 * kOrdBins];
+    __shared__ int32_t off[2 * kOrdBins], cnt[2 * kOrdBins], base[2 * kOrdBins];
     if (threadIdx.x < 2)
     {
         int s = 0;
@@ -1150,15 +1152,30 @@ __global__ __launch_bounds__(256) void gravityOrderScatterKernel(int64_t groups,
             s += hist[threadIdx.x * kOrdBins + b];
         }
     }
-    __syncthreads();
-    for (int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < groups; g += int64_t(gridDim.x) * blockDim.x)
+    for (int64_t g0 = int64_t(blockIdx.x) * blockDim.x; g0 < groups; g0 += int64_t(gridDim.x) * blockDim.x)
     {
+        for (int k = threadIdx.x; k < 2 * kOrdBins; k += blockDim.x)
+            cnt[k] = 0;
+        __syncthreads();
+        const int64_t g = g0 + threadIdx.x;
+        int b[2], r[2];
 #pragma unroll
         for (int k = 0; k < 2; ++k)
         {
-            const int b = k * kOrdBins + costBin(groupWork(S, g, k));
-            order[k * groups + off[b] + atomicAdd(&cursor[b], 1)] = int32_t(g);
+            b[k] = k * kOrdBins + (g < groups ? costBin(groupWork(S, g, k)) : 0);
+            r[k] = g < groups ? atomicAdd(&cnt[b[k]], 1) : 0;
         }
+        __syncthreads();
+        for (int k = threadIdx.x; k < 2 * kOrdBins; k += blockDim.x)
+            base[k] = cnt[k] ? atomicAdd(&cursor[k], cnt[k]) : 0;
+        __syncthreads();
+        if (g < groups)
+        {
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                order[k * groups + off[b[k]] + base[b[k]] + r[k]] = int32_t(g);
+        }
+        __syncthreads();
     }
 }
 

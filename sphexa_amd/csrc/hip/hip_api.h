@@ -166,7 +166,7 @@ void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, in
                        const float* wh, void* rec, float* ax, float* ay, float* az, double* du, float* minDt,
                        hipStream_t s);
 void updatePositions(int64_t first, int64_t last, double dt, double dt_m1, const PosArgs& p, double cv,
-                     const Box& box, hipStream_t s);
+                     const Box& box, hipStream_t s, const double* dtDev = nullptr);
 void updateH(int64_t first, int64_t last, unsigned ng0, const int32_t* nc, float* h, hipStream_t s);
 void conservedQuantities(int64_t first, int64_t last, const double* x, const double* y, const double* z,
                          const float* vx, const float* vy, const float* vz, const float* m, const double* temp,

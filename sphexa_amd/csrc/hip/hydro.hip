@@ -776,10 +776,16 @@ __global__ __launch_bounds__(kBlock) void momentumEnergyStdKernel(NbrArgs a, Sph
 }
 
 __global__ void updatePositionsKernel(int64_t first, int64_t last, double dt, double dt_m1, PosArgs p, double cv,
-                                      Box box)
+                                      Box box, const double* __restrict__ dtDev)
 {
     int64_t i = first + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= last) return;
+    if (dtDev)
+    {
+        // device-resident time step [dt, dt_m1] (the propagator's deferred host copy, propagators.py)
+        dt    = dtDev[0];
+        dt_m1 = dtDev[1];
+    }
     bool fbc[3] = {box.bc[0] == kFixed, box.bc[1] == kFixed, box.bc[2] == kFixed};
     bool frozen = false;
     if ((fbc[0] || fbc[1] || fbc[2]) && p.vx[i] == 0.f && p.vy[i] == 0.f && p.vz[i] == 0.f)
@@ -1084,10 +1090,10 @@ void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, in
 }
 
 void updatePositions(int64_t first, int64_t last, double dt, double dt_m1, const PosArgs& p, double cv,
-                     const Box& box, hipStream_t s)
+                     const Box& box, hipStream_t s, const double* dtDev)
 {
     if (last <= first) return;
-    updatePositionsKernel<<<gridFor(last - first, 256), 256, 0, s>>>(first, last, dt, dt_m1, p, cv, box);
+    updatePositionsKernel<<<gridFor(last - first, 256), 256, 0, s>>>(first, last, dt, dt_m1, p, cv, box, dtDev);
     SPHX_LAUNCH_CHECK();
 }
 

@@ -99,6 +99,7 @@ class Cooler:
 
 class HydroCoolingProp(HydroProp):
     """standard SPH on the specific internal energy u with radiative cooling (``--prop std-cooling``)"""
+    needs_host_dt = True  # the new dt is used on the host within the step (Propagator.defer_host)
 
     conserved = ["u", "vx", "vy", "vz", "x_m1", "y_m1", "z_m1", "du_m1"]
     dependent = ["rho", "p", "c", "ax", "ay", "az", "du", "c11", "c12", "c13", "c22", "c23", "c33", "nc"]

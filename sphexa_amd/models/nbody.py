@@ -15,6 +15,7 @@ from .propagators import Propagator
 
 
 class NbodyProp(Propagator):
+    needs_host_dt = True  # the new dt is used on the host within the step (Propagator.defer_host)
     conserved = ["vx", "vy", "vz", "x_m1", "y_m1", "z_m1"]
     dependent = ["ax", "ay", "az", "du", "du_m1"]
 

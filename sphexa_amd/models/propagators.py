@@ -32,6 +32,13 @@ from ..utils.timer import Timer
 class Propagator:
     conserved: List[str] = []
     dependent: List[str] = []
+    # GPU: the host copy of the new time step (with the gravity statistics and deferred domain checks riding along)
+    # may stay in flight until the next step's neighbor search, which synchronizes anyway: the position update reads
+    # dt from the device and the host keeps enqueueing, so the GPU does not idle across the step boundary. Set by
+    # drivers that read no host values between steps (bench.py); finish_host() collects the values on demand.
+    defer_host = False
+    # propagators that use the new dt on the host within the step (stirring, cooling) never defer
+    needs_host_dt = False
 
     def __init__(self, out=sys.stdout, rank: int = 0, quiet: bool = False):
         self.out = out if rank == 0 and not quiet else None
@@ -39,6 +46,7 @@ class Propagator:
         self.timer = Timer(self.out)
         self.nl = None
         self.gravity = None
+        self._host_pending = None
 
     # --------------------------------------------------------------------------------------------- interface
     def conserved_fields(self) -> List[str]:
@@ -72,16 +80,27 @@ class Propagator:
         pass
 
     # ---------------------------------------------------------------------------------------------- shared
-    def _neighbors(self, domain, d):
-        """neighbor search + h iteration"""
+    def _neighbors(self, domain, d, first_loop=None):
+        """neighbor search + h iteration. ``first_loop(d, nl, box)`` (GPU): the pair loop that follows the search; it
+        is enqueued speculatively before the host waits for the search statistics (find_neighbors ``speculate``), so
+        the GPU does not idle while the host books the search. Returns True if it ran and holds."""
         first, last = domain.start_index(), domain.end_index()
         gpu = d.device.type == "cuda"
+        spec = []
+        speculate = None
+        if gpu and first_loop is not None:
+            def speculate(nl_s):
+                spec.append(H.speculate_loop(d, domain.box, lambda: first_loop(d, nl_s, domain.box)))
         self.nl = find_neighbors(d, domain.octree, domain.box, first, last,
                                  prev=self.nl,  # (not nidx=: an argument would pin the old GPU buffer)
                                  # global h minimum + mass extremes come back with the search statistics
-                                 ride_along=(lambda: H.global_h_min_device(d, domain.comm)) if gpu else None)
+                                 ride_along=(lambda: H.global_h_min_device(d, domain.comm)) if gpu else None,
+                                 speculate=speculate)
         if gpu:
             H.apply_global_h_min(d, self.nl.ride_along)
+            # the previous step's time-step copy completed before the search statistics did (same stream)
+            self.finish_host(d)
+        return bool(spec) and self.nl.speculated and H.speculation_holds(d, domain.box, spec[0])
 
     def _gravity(self, domain, d):
         if d.g != 0.0:
@@ -99,6 +118,7 @@ class Propagator:
         the local minimum is formed on the device from the device-resident inputs (Courant minimum of the momentum
         loop, max divv, max |a|^2), reduced over ranks there, and comes to the host in ONE copy together with the
         gravity statistics/energy (GravityPending) and the domain's deferred checks (Domain.pending_checks)."""
+        self.finish_host(d)  # (a deferred copy is normally collected by the search already)
         first, last = domain.start_index(), domain.end_index()
         grav = d.g != 0.0 and last > first
         pend = list(getattr(self.gravity, "pending", None) or [])
@@ -127,14 +147,18 @@ class Propagator:
             flat = [glob, courant.reshape(1), rho.reshape(1)] + [p.dev for p in pend]
             if checks is not None:
                 flat.append(checks.to(torch.float64).reshape(-1))
-            vals = torch.cat(flat).tolist()
-            dt = vals[0]
-            d.minDtCourant, d.minDtRho = vals[1], vals[2]
-            k = 3 + 10 * len(pend)
-            if pend:
-                self.gravity.finish(d, [vals[3 + 10 * i: 3 + 10 * (i + 1)] for i in range(len(pend))])
-            if checks is not None:
-                domain.finish_checks(vals[k:])
+            packed = torch.cat(flat)
+            if self.defer_host and not self.needs_host_dt:
+                # [dt, dt_m1] for the position update on the device; the host values follow in finish_host()
+                d._dt_dev = torch.cat([glob, torch.full((1,), d.minDt, **f64)])
+                host = torch.empty(packed.numel(), dtype=torch.float64, pin_memory=True)
+                host.copy_(packed, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                self._host_pending = (host, ev, pend, checks is not None, domain)
+                return
+            self._apply_host(d, domain, packed.tolist(), pend, checks is not None)
+            return
         else:
             if pend:
                 self.gravity.finish(d, [p.dev.cpu().tolist() for p in pend])
@@ -154,6 +178,30 @@ class Propagator:
         d.ttot += dt
         d.minDt_m1 = d.minDt
         d.minDt = dt
+
+    def _apply_host(self, d, domain, vals, pend, has_checks):
+        dt = vals[0]
+        d.minDtCourant, d.minDtRho = vals[1], vals[2]
+        k = 3 + 10 * len(pend)
+        if pend:
+            self.gravity.finish(d, [vals[3 + 10 * i: 3 + 10 * (i + 1)] for i in range(len(pend))])
+        if has_checks:
+            domain.finish_checks(vals[k:])
+        d.ttot += dt
+        d.minDt_m1 = d.minDt
+        d.minDt = dt
+
+    def finish_host(self, d):
+        """collect a deferred time-step copy (defer_host): dt, ttot, the Courant/rho minima, gravity energy and
+        statistics, deferred domain checks"""
+        p = self._host_pending
+        if p is None:
+            return
+        self._host_pending = None
+        host, ev, pend, has_checks, domain = p
+        ev.synchronize()
+        d._dt_dev = None
+        self._apply_host(d, domain, host.tolist(), pend, has_checks)
 
     def rho_timestep(self, d, first, last):
         """max divv of the owned particles as a device scalar; compute_timestep turns it into Krho / |max divv|"""
@@ -208,11 +256,12 @@ class HydroVeProp(Propagator):
         first, last = domain.start_index(), domain.end_index()
         # velocity halos are not read before the IAD loop: their exchange overlaps the search, XMass and Gradh
         vel_halos = domain.exchange_halos_start(d, ["vx", "vy", "vz"])
-        self._neighbors(domain, d)
+        done = self._neighbors(domain, d, first_loop=H.compute_xmass)
         t.step("FindNeighbors")
         nl = self.nl
 
-        H.compute_xmass(d, nl, box)
+        if not done:
+            H.compute_xmass(d, nl, box)
         t.step("XMass")
         domain.exchange_halos(d, ["xm"])
         t.step("mpi::synchronizeHalos")

@@ -179,6 +179,8 @@ class TurbulenceData:
 
 
 class TurbVeProp(HydroVeProp):
+    needs_host_dt = True  # the new dt is used on the host within the step (Propagator.defer_host)
+
     def __init__(self, out=sys.stdout, rank=0, av_clean=False, quiet=False, settings=None):
         super().__init__(out, rank, av_clean, quiet)
         self.turb = TurbulenceData(settings, rank == 0 and not quiet) if settings is not None else None

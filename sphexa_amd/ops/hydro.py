@@ -204,6 +204,26 @@ def apply_global_h_min(d, vals):
     d._h_min_global = hmin
     val = mlo if (mlo == mhi and mlo > 0) else 0.0
     d._m_uniform = ((m.data_ptr(), m.numel(), m._version), val)
+    d._spec_prev = (hmin, val)  # the decisions of the next step's speculative first loop (speculate_loop)
+
+
+def speculate_loop(d, box: Box, run):
+    """run a pair loop (``run()``) before this step's global h minimum and mass extremes have reached the host, under
+    the previous step's values; returns the (fixed-point, uniform-mass) path it took, or None if there is no previous
+    step. ``speculation_holds`` tells after apply_global_h_min whether the real values take the same path (else the
+    loop is re-run). The fixed-point path changes only when h_min crosses the quantum bound."""
+    prev = getattr(d, "_spec_prev", None)
+    if prev is None:
+        return None
+    m = d["m"][: d.size]
+    d._h_min_global = prev[0]
+    d._m_uniform = ((m.data_ptr(), m.numel(), m._version), prev[1])
+    run()
+    return bool(d.fixedPoint), uniform_mass(d) > 0
+
+
+def speculation_holds(d, box: Box, spec) -> bool:
+    return spec is not None and spec == (fixed_point_ok(d, box), uniform_mass(d) > 0)
 
 
 def set_global_h_min(d, comm):
@@ -440,7 +460,8 @@ def compute_positions(d, first: int, last: int, box: Box):
             d["z_m1"].data_ptr(), d["ax"].data_ptr(), d["ay"].data_ptr(), d["az"].data_ptr(), d["h"].data_ptr(),
             _p(temp), _p(u), d["du"].data_ptr(), d["du_m1"].data_ptr(), cv, box.to_array())
     if _is_gpu(d):
-        _lib.hip().update_positions(*args, _stream())
+        dt_dev = getattr(d, "_dt_dev", None)  # [dt, dt_m1] on the device while the host copy is deferred
+        _lib.hip().update_positions(*args, _stream(), dtDev=0 if dt_dev is None else dt_dev.data_ptr())
     else:
         _lib.cpu().update_positions(*args)
 

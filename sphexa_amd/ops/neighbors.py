@@ -45,6 +45,7 @@ class NeighborList:
     plan: tuple | None = None  # HIP: (groups, home rows, overflow rows per stripe) for the next search
     hist: tuple = ()  # HIP: rows needed by recent searches (pool sizing)
     ride_along: list | None = None  # HIP: host values of find_neighbors' ride_along tensor
+    speculated: bool = False  # HIP: find_neighbors' ``speculate`` ran on these lists (no repeated search)
 
     @property
     def stride(self):
@@ -203,12 +204,15 @@ def _pool_plan(prev: NeighborList | None, groups: int, ng0: int, stripes: int):
 
 def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
                    nidx: torch.Tensor | None = None, prev: NeighborList | None = None,
-                   ride_along=None) -> NeighborList:
+                   ride_along=None, speculate=None) -> NeighborList:
     """search neighbors of particles [first, last) within 2h, adjusting h towards ng0 neighbors.
 
     ``prev``: the previous step's lists; on the GPU its buffer is reused when it has the right size.
     ``ride_along`` (GPU): a callable returning a float64 device tensor computed after the search; its values reach
     the host in the same copy as the search statistics (``NeighborList.ride_along``), saving a synchronization.
+    ``speculate`` (GPU): called with the provisional lists after the statistics copy is enqueued and before the host
+    waits for it, to enqueue work that needs the lists (the first pair loop) while the host waits and books; the
+    returned lists carry ``speculated`` = False if the search had to be repeated (the work must then be redone).
     """
     x, y, z, h, nc = d["x"], d["y"], d["z"], d["h"], d["nc"]
     n = last - first
@@ -238,6 +242,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         from .hydro import _handoff, _rec, handoff_mark
         rec = _rec(d, 0, "xmass")
         ride_host = None
+        spec_buf = None
         for _attempt in range(2):
             ov = ((buf.numel() - region) // 256 - num_groups * home) // K
             stats = torch.zeros(8 + 32 * K, dtype=torch.int64, device=x.device)
@@ -260,7 +265,20 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
             parts = [stats[:8], stats[8::32][:K], over]
             # (host-side bookkeeping in numpy: a torch op on a CPU tensor costs ~5-10 us of launch-path overhead,
             # and the GPU idles until the pair loops are enqueued)
-            host = torch.cat(parts + ([ex] if ex is not None else [])).cpu().numpy()
+            packed = torch.cat(parts + ([ex] if ex is not None else []))
+            if speculate is not None and first_try:
+                pinned = torch.empty(packed.numel(), dtype=torch.int64, pin_memory=True)
+                pinned.copy_(packed, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                _handoff(d).clear()
+                handoff_mark(d, "posq_all")
+                speculate(NeighborList(buf, first, last, ngmax, True))
+                spec_buf = buf
+                ev.synchronize()
+                host = pinned.numpy()
+            else:
+                host = packed.cpu().numpy()
             if ex is not None:
                 ride_host = host[8 + 6 * K:].view(np.float64).tolist()
             st = host[:8].tolist()
@@ -275,9 +293,13 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               dtype=torch.int32, device=x.device)
         else:
             raise NeighborSearchError("packed neighbor lists: overflow rows exhausted twice")
-        # the search packed every particle's SrcPosQ record into workspace 0: the XMass loop reads them as they are
-        _handoff(d).clear()
-        handoff_mark(d, "posq_all")
+        speculated = spec_buf is not None and spec_buf is buf
+        if not speculated:
+            # the search packed every particle's SrcPosQ record into workspace 0: the XMass loop reads them as they
+            # are (a speculative first loop has already taken them and left its own hand-offs)
+            _handoff(d).clear()
+            handoff_mark(d, "posq_all")
+        spec_buf = None
         cand = np.maximum(np.arange(-2, 3) + home, 1)
         cand_ov = (host[8 + K:8 + 6 * K].reshape(5, K).max(axis=1).astype(np.float64) * 1.1).astype(np.int64) + 8
         cand_rows = cand * num_groups + K * cand_ov
@@ -306,7 +328,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         if COLLECT_STATS:  # staged candidates and hits per group; candidates inside sub-group boxes (what-if)
             extra = stats[9:12].cpu().tolist()
             d.nc_hits, d.nc_staged, d.nc_subbox = (v / num_groups for v in extra)
-        return NeighborList(buf, first, last, ngmax, True, used, plan, hist, ride_host)
+        return NeighborList(buf, first, last, ngmax, True, used, plan, hist, ride_host, speculated)
 
     need = max(n, 1) * ngmax
     if nidx is None or nidx.numel() < need:

@@ -147,3 +147,61 @@ def test_noh_ci_accuracy(gpu):
     assert abs(err["Density"] / 10.42 - 1) < 0.15
     assert abs(err["Pressure"] / 2.88 - 1) < 0.15
     assert abs(err["Velocity"] / 0.14 - 1) < 0.20
+
+
+@pytest.mark.parametrize("case,prop,n", [("evrard", "ve", 32), ("noh", "std", 32), ("sedov", "ve", 20)])
+def test_deferred_host_timestep(gpu, small_glass, case, prop, n):
+    """Propagator.defer_host (bench.py): the position update reads dt from the device and the host values (dt,
+    ttot, energies, gravity statistics) arrive at the next search; after finish_host the run equals the synchronous
+    one step for step"""
+    ref = Simulation(case, n=n, prop=prop, device=gpu)
+    dfr = Simulation(case, n=n, prop=prop, device=gpu)
+    dfr.propagator.defer_host = True
+    for _ in range(3):
+        ref.step()
+        dfr.step()
+    assert dfr.propagator._host_pending is not None and dfr.d._dt_dev is not None
+    dfr.propagator.finish_host(dfr.d)
+    assert dfr.propagator._host_pending is None and dfr.d._dt_dev is None
+    for k in ("minDt", "minDt_m1", "ttot", "egrav"):
+        assert getattr(dfr.d, k) == pytest.approx(getattr(ref.d, k), rel=1e-6, abs=1e-300), k
+    names = ["x", "vx", "h", "temp"]
+    a, b = _sorted_state(ref, names), _sorted_state(dfr, names)
+    for k in names:
+        assert torch.allclose(a[k], b[k], rtol=1e-5, atol=1e-9), k
+
+
+def test_speculative_xmass(gpu, small_glass):
+    """the VE step enqueues XMass before the host has the search statistics (Propagator._neighbors first_loop):
+    from the second step on the speculation holds and the run equals one without it"""
+    from sphexa_amd.models import propagators as PR
+
+    ref = Simulation("evrard", n=32, prop="ve", device=gpu)
+    spc = Simulation("evrard", n=32, prop="ve", device=gpu)
+    held = []
+    orig = PR.Propagator._neighbors
+
+    def no_spec(self, domain, d, first_loop=None):
+        return orig(self, domain, d)
+
+    def watch(self, domain, d, first_loop=None):
+        r = orig(self, domain, d, first_loop)
+        held.append(r)
+        return r
+
+    for _ in range(3):
+        PR.Propagator._neighbors = no_spec
+        try:
+            ref.step()
+        finally:
+            PR.Propagator._neighbors = watch
+        try:
+            spc.step()
+        finally:
+            PR.Propagator._neighbors = orig
+    assert held == [False, True, True]
+    names = ["x", "vx", "h", "temp"]
+    a, b = _sorted_state(ref, names), _sorted_state(spc, names)
+    for k in names:
+        assert torch.allclose(a[k], b[k], rtol=1e-6, atol=1e-12), k
+    assert spc.d.minDt == pytest.approx(ref.d.minDt, rel=1e-6)
