@@ -132,6 +132,15 @@ PYBIND11_MODULE(_sphx_hip, m)
                               Ptr work, Ptr s) { multiMinMax(n, ptrs, isDouble, P<double>(out), P<void>(work), St(s)); });
     m.def("max_norm2", [](int64_t first, int64_t last, Ptr ax, Ptr ay, Ptr az, Ptr out, Ptr work, Ptr s)
           { maxNorm2(first, last, P<float>(ax), P<float>(ay), P<float>(az), P<double>(out), P<void>(work), St(s)); });
+    m.def("timestep_reduce",
+          [](int64_t first, int64_t last, Ptr ax, Ptr ay, Ptr az, Ptr courantDev, double courantHost, Ptr divvMax,
+             double rhoHost, double Krho, double etaAcc, double eps, double others, double prevDt, Ptr out, Ptr work,
+             Ptr s)
+          {
+              timestepReduce(first, last, P<float>(ax), P<float>(ay), P<float>(az), P<float>(courantDev), courantHost,
+                             P<float>(divvMax), rhoHost, Krho, etaAcc, eps, others, prevDt, P<double>(out),
+                             P<void>(work), St(s));
+          });
     m.def("scan_temp_bytes", [](int64_t n) { return scanTempBytes(n); });
     m.def("exclusive_scan_i64", [](Ptr in, Ptr out, int64_t n, Ptr tmp, size_t tb, Ptr s)
           { exclusiveScanI64(P<int64_t>(in), P<int64_t>(out), n, P<void>(tmp), tb, St(s)); });
@@ -164,6 +173,14 @@ PYBIND11_MODULE(_sphx_hip, m)
           {
               leafBoxes(P<int32_t>(n2l), N, P<int32_t>(ns), P<int32_t>(ne), P<double>(x), P<double>(y), P<double>(z),
                         P<float>(h), factor, P<double>(c), P<double>(hf), St(s));
+          });
+    m.def("leaf_boxes_fused",
+          [](Ptr n2l, int64_t N, Ptr ns, Ptr ne, Ptr x, Ptr y, Ptr z, Ptr child, Ptr parents, Ptr c, Ptr hf, Ptr cnt,
+             Ptr s)
+          {
+              leafBoxesFused(P<int32_t>(n2l), N, P<int32_t>(ns), P<int32_t>(ne), P<double>(x), P<double>(y),
+                             P<double>(z), P<int32_t>(child), P<int32_t>(parents), P<double>(c), P<double>(hf),
+                             P<unsigned>(cnt), St(s));
           });
     m.def("upsweep_boxes", [](int64_t a, int64_t b, Ptr n2l, Ptr child, Ptr c, Ptr hf, Ptr s)
           { upsweepBoxes(a, b, P<int32_t>(n2l), P<int32_t>(child), P<double>(c), P<double>(hf), St(s)); });
@@ -393,6 +410,15 @@ PYBIND11_MODULE(_sphx_hip, m)
           {
               gravityLeaves(P<int32_t>(n2l), N, P<int32_t>(ns), P<int32_t>(ne), P<double>(x), P<double>(y),
                             P<double>(z), P<float>(mm), P<double>(centers), P<void>(mp), St(s));
+          });
+    m.def("gravity_upsweep_fused",
+          [](Ptr n2l, int64_t N, Ptr ns, Ptr ne, Ptr x, Ptr y, Ptr z, Ptr mm, Ptr child, Ptr parents, Ptr prefixes,
+             const BoxArr& box, int kind, double invTheta, Ptr centers, Ptr mp, Ptr cnt, Ptr s)
+          {
+              gravityUpsweepFused(P<int32_t>(n2l), N, P<int32_t>(ns), P<int32_t>(ne), P<double>(x), P<double>(y),
+                                  P<double>(z), P<float>(mm), P<int32_t>(child), P<int32_t>(parents),
+                                  P<KeyT>(prefixes), toBox(box), kind, invTheta, P<double>(centers), P<void>(mp),
+                                  P<unsigned>(cnt), St(s));
           });
     m.def("gravity_upsweep_level", [](int64_t a, int64_t b, Ptr n2l, Ptr child, Ptr centers, Ptr mp, Ptr s)
           {

@@ -127,6 +127,147 @@ __global__ void gravitySetMacKernel(int64_t N, const KeyT* __restrict__ prefixes
     else { c[3] = vecMacR2(c, gc, gs, invTheta); }
 }
 
+/*! @brief the whole upsweep in one launch (leaves, every internal level, vector-MAC radii): a wave per leaf computes
+ *         its multipole like gravityLeavesKernel; then lane 0 climbs: it counts itself into the parent's arrival
+ *         counter (release fence first) and the eighth sibling to arrive (acquire fence) forms the parent from its
+ *         children (agent-scope loads: the children were written by waves on other XCDs), sets the children's MAC
+ *         radii (they are not read again) and climbs on. The counter is re-armed to 0 by its eighth arrival. Replaces
+ *         2 + depth launches (the level loop of ops/gravity.py) that at small per-rank sizes cost more host time than
+ *         GPU time.
+ */
+__device__ __forceinline__ double ldAgent(const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ldAgent(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__device__ __forceinline__ void setMacOf(int64_t i, const double c[4], const KeyT* prefixes, const Box& box, int kind,
+                                         double invTheta, double* centers)
+{
+    double gc[3], gs[3];
+    nodeGeometry(kind, prefixes[i], box, gc, gs);
+    double* o = centers + 4 * i;
+    if (c[3] == 0)
+    {
+        o[0] = gc[0], o[1] = gc[1], o[2] = gc[2], o[3] = 0;
+    }
+    else { o[3] = vecMacR2(c, gc, gs, invTheta); }
+}
+
+__global__ __launch_bounds__(256) void gravityUpsweepFusedKernel(const int32_t* __restrict__ n2l, int64_t N,
+                                                                 const int32_t* __restrict__ ns,
+                                                                 const int32_t* __restrict__ ne,
+                                                                 const double* __restrict__ x,
+                                                                 const double* __restrict__ y,
+                                                                 const double* __restrict__ z,
+                                                                 const float* __restrict__ m,
+                                                                 const int32_t* __restrict__ child,
+                                                                 const int32_t* __restrict__ parents,
+                                                                 const KeyT* __restrict__ prefixes, Box box, int kind,
+                                                                 double invTheta, double* centers, Quadrupole* mp,
+                                                                 unsigned* cnt)
+{
+    const int64_t i = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (i >= N || n2l[i] < 0) return; // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int32_t a = ns[i], b = ne[i];
+    double c[4] = {0, 0, 0, 0};
+    for (int32_t p = a + lane; p < b; p += 64)
+    {
+        double mi = m[p];
+        c[0] += mi * x[p];
+        c[1] += mi * y[p];
+        c[2] += mi * z[p];
+        c[3] += mi;
+    }
+    for (int k = 0; k < 4; ++k)
+        c[k] = waveSum(c[k]);
+    const double inv    = c[3] != 0 ? 1.0 / c[3] : 0.0;
+    const double com[3] = {c[0] * inv, c[1] * inv, c[2] * inv};
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int32_t p = a + lane; p < b; p += 64)
+    {
+        double rx = x[p] - com[0], ry = y[p] - com[1], rz = z[p] - com[2], mi = m[p];
+        acc[0] += rx * rx * mi;
+        acc[1] += rx * ry * mi;
+        acc[2] += rx * rz * mi;
+        acc[3] += ry * ry * mi;
+        acc[4] += ry * rz * mi;
+        acc[5] += rz * rz * mi;
+    }
+    for (int k = 0; k < 6; ++k)
+        acc[k] = waveSum(acc[k]);
+    if (lane != 0) return;
+    const double tr = acc[0] + acc[3] + acc[5];
+    Quadrupole q;
+    q.q[qMass]         = MT(c[3]);
+    q.q[qXX]           = MT(3 * acc[0] - tr);
+    q.q[qYY]           = MT(3 * acc[3] - tr);
+    q.q[qZZ]           = MT(3 * acc[5] - tr);
+    q.q[qXY]           = MT(3 * acc[1]);
+    q.q[qXZ]           = MT(3 * acc[2]);
+    q.q[qYZ]           = MT(3 * acc[4]);
+    q.q[qTrace]        = MT(tr);
+    mp[i]              = q;
+    double own[4]      = {com[0], com[1], com[2], c[3]};
+    centers[4 * i + 0] = own[0];
+    centers[4 * i + 1] = own[1];
+    centers[4 * i + 2] = own[2];
+    centers[4 * i + 3] = own[3];
+
+    int64_t node = i;
+    while (node > 0)
+    {
+        const int32_t pn = parents[(node - 1) / 8];
+        __threadfence(); // release: this node's multipole before the arrival
+        if (atomicAdd(&cnt[pn], 1u) != 7u) return;
+        cnt[pn] = 0u;    // every sibling has arrived: re-armed for the next launch
+        __threadfence(); // acquire: the siblings' multipoles
+        const int32_t co = child[pn];
+        double ch[8][4];
+        double s[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 8; ++k)
+        {
+            for (int d = 0; d < 4; ++d)
+                ch[k][d] = ldAgent(centers + 4 * (co + k) + d);
+            s[0] += ch[k][3] * ch[k][0];
+            s[1] += ch[k][3] * ch[k][1];
+            s[2] += ch[k][3] * ch[k][2];
+            s[3] += ch[k][3];
+        }
+        const double iv = s[3] != 0 ? 1.0 / s[3] : 0.0;
+        const double pc[3] = {s[0] * iv, s[1] * iv, s[2] * iv};
+        Quadrupole pq{};
+        for (int k = 0; k < 8; ++k)
+        {
+            Quadrupole cq;
+            const float* src = reinterpret_cast<const float*>(mp + co + k);
+            for (int e = 0; e < 8; ++e)
+                cq.q[e] = ldAgent(src + e);
+            addQuadrupole(pq, pc[0] - ch[k][0], pc[1] - ch[k][1], pc[2] - ch[k][2], cq);
+        }
+        mp[pn]              = pq;
+        centers[4 * pn + 0] = pc[0];
+        centers[4 * pn + 1] = pc[1];
+        centers[4 * pn + 2] = pc[2];
+        centers[4 * pn + 3] = s[3];
+        for (int k = 0; k < 8; ++k)
+            setMacOf(co + k, ch[k], prefixes, box, kind, invTheta, centers);
+        own[0] = pc[0], own[1] = pc[1], own[2] = pc[2], own[3] = s[3];
+        node = pn;
+    }
+    setMacOf(0, own, prefixes, box, kind, invTheta, centers); // the root (reached by exactly one climber)
+}
+
+void gravityUpsweepFused(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
+                         const double* y, const double* z, const float* m, const int32_t* child,
+                         const int32_t* parents, const KeyT* prefixes, const Box& box, int kind, double invTheta,
+                         double* centers, void* mp, unsigned* cnt, hipStream_t s)
+{
+    if (N <= 0) return;
+    gravityUpsweepFusedKernel<<<unsigned((N + 3) / 4), 256, 0, s>>>(n2l, N, ns, ne, x, y, z, m, child, parents,
+                                                                    prefixes, box, kind, invTheta, centers,
+                                                                    (Quadrupole*)mp, cnt);
+    SPHX_LAUNCH_CHECK();
+}
+
 void gravityLeaves(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
                    const double* y, const double* z, const float* m, double* centers, void* mp, hipStream_t s)
 {

@@ -73,6 +73,9 @@ void multiMinMax(int64_t n, const std::vector<uintptr_t>& ptrs, const std::vecto
                  void* work, hipStream_t s);
 void maxNorm2(int64_t first, int64_t last, const float* ax, const float* ay, const float* az, double* out, void* work,
               hipStream_t s);
+void timestepReduce(int64_t first, int64_t last, const float* ax, const float* ay, const float* az,
+                    const float* courantDev, double courantHost, const float* divvMax, double rhoHost, double Krho,
+                    double etaAcc, double eps, double others, double prevDt, double* out, void* work, hipStream_t s);
 
 // octree.hip
 void nodeCounts(const KeyT* tree, int64_t L, const KeyT* keys, int64_t n, int32_t* counts, hipStream_t s);
@@ -86,6 +89,9 @@ void linkNodes(const KeyT* codes, const int32_t* vals, int64_t N, int32_t* child
                int32_t* leafToNode, int64_t* levelRange, hipStream_t s);
 void nodeRanges(const KeyT* codes, int64_t N, const KeyT* keys, int64_t n, int64_t offset, int32_t* ns, int32_t* ne,
                 hipStream_t s);
+void leafBoxesFused(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
+                    const double* y, const double* z, const int32_t* child, const int32_t* parents, double* center,
+                    double* half, unsigned* cnt, hipStream_t s);
 void leafBoxes(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
                const double* y, const double* z, const float* h, double factor, double* center, double* half,
                hipStream_t s);
@@ -191,6 +197,10 @@ void computeGravityMultipole(int order, int64_t first, int64_t last, const int32
                              hipStream_t s);
 
 // gravity.hip
+void gravityUpsweepFused(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
+                         const double* y, const double* z, const float* m, const int32_t* child,
+                         const int32_t* parents, const KeyT* prefixes, const Box& box, int kind, double invTheta,
+                         double* centers, void* mp, unsigned* cnt, hipStream_t s);
 void gravityLeaves(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
                    const double* y, const double* z, const float* m, double* centers, void* mp, hipStream_t s);
 void gravityUpsweepLevel(int64_t a, int64_t b, const int32_t* n2l, const int32_t* child, double* centers, void* mp,

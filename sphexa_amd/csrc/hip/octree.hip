@@ -219,6 +219,78 @@ __global__ __launch_bounds__(256) void leafBoxesKernel(const int32_t* __restrict
     if (leaf && sub == 0) storeBox(center, half, i, mn, mx);
 }
 
+/*! @brief leaf boxes and every internal box in one launch: the leaf's first lane counts itself into the parent's
+ *         arrival counter (release fence first); the eighth sibling to arrive (acquire fence) forms the parent's box
+ *         from its children (agent-scope loads: written by other XCDs) and climbs on; counters re-arm to 0. Replaces
+ *         the per-level upsweepBoxes launches (ops/octree.py refit/build: 1 + depth launches). */
+__global__ __launch_bounds__(256) void leafBoxesFusedKernel(const int32_t* __restrict__ n2l, int64_t N,
+                                                            const int32_t* __restrict__ ns,
+                                                            const int32_t* __restrict__ ne,
+                                                            const double* __restrict__ x, const double* __restrict__ y,
+                                                            const double* __restrict__ z,
+                                                            const int32_t* __restrict__ child,
+                                                            const int32_t* __restrict__ parents, double* center,
+                                                            double* half, unsigned* cnt)
+{
+    const int64_t i = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 4;
+    const int sub   = threadIdx.x & 15;
+    const bool leaf = i < N && n2l[i] >= 0;
+    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
+    if (leaf)
+    {
+        for (int32_t p = ns[i] + sub; p < ne[i]; p += 16)
+        {
+            double v[3] = {x[p], y[p], z[p]};
+            for (int d = 0; d < 3; ++d)
+            {
+                mn[d] = fmin(mn[d], v[d]);
+                mx[d] = fmax(mx[d], v[d]);
+            }
+        }
+    }
+    for (int o = 8; o > 0; o >>= 1)
+        for (int d = 0; d < 3; ++d)
+        {
+            mn[d] = fmin(mn[d], __shfl_xor(mn[d], o));
+            mx[d] = fmax(mx[d], __shfl_xor(mx[d], o));
+        }
+    if (!leaf || sub != 0) return;
+    storeBox(center, half, i, mn, mx);
+    int64_t node = i;
+    while (node > 0)
+    {
+        const int32_t pn = parents[(node - 1) / 8];
+        __threadfence(); // release: this node's box before the arrival
+        if (atomicAdd(&cnt[pn], 1u) != 7u) return;
+        cnt[pn] = 0u;    // re-armed for the next launch
+        __threadfence(); // acquire: the siblings' boxes
+        const int32_t c = child[pn];
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        for (int k = 0; k < 8; ++k)
+            for (int d = 0; d < 3; ++d)
+            {
+                const double hh = __hip_atomic_load(half + 3 * (c + k) + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (hh < 0) continue;
+                const double cc = __hip_atomic_load(center + 3 * (c + k) + d, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+                lo[d] = fmin(lo[d], cc - hh);
+                hi[d] = fmax(hi[d], cc + hh);
+            }
+        storeBox(center, half, pn, lo, hi);
+        node = pn;
+    }
+}
+
+void leafBoxesFused(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
+                    const double* y, const double* z, const int32_t* child, const int32_t* parents, double* center,
+                    double* half, unsigned* cnt, hipStream_t s)
+{
+    if (N <= 0) return;
+    leafBoxesFusedKernel<<<unsigned((N + 15) / 16), 256, 0, s>>>(n2l, N, ns, ne, x, y, z, child, parents, center,
+                                                                 half, cnt);
+    SPHX_LAUNCH_CHECK();
+}
+
 void leafBoxes(const int32_t* n2l, int64_t N, const int32_t* ns, const int32_t* ne, const double* x,
                const double* y, const double* z, const float* h, double factor, double* center, double* half,
                hipStream_t s)

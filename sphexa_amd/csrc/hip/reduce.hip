@@ -128,6 +128,55 @@ __global__ __launch_bounds__(kRedBlock) void maxNorm2Kernel(int64_t first, int64
     if (threadIdx.x == 0) out[0] = v;
 }
 
+/*! @brief the local time step in one launch (reference sph/timestep.hpp: min of the Courant, density and acceleration
+ *         criteria and maxDtIncrease x the previous dt): max |a|^2 over [first, last) reduced like maxNorm2Kernel, then
+ *         the last block forms out = [dt, dt_m1, courant, rho] (dt_m1: the previous dt, for the position update).
+ *         courant / divvMax: device scalars (nullptr: the host values) */
+__global__ __launch_bounds__(kRedBlock) void timestepKernel(int64_t first, int64_t last, const float* __restrict__ ax,
+                                                            const float* __restrict__ ay,
+                                                            const float* __restrict__ az,
+                                                            const float* __restrict__ courantDev, double courantHost,
+                                                            const float* __restrict__ divvMax, double rhoHost,
+                                                            double Krho, double etaAcc, double eps, double others,
+                                                            double prevDt, double* __restrict__ partials,
+                                                            double* __restrict__ out, unsigned* ticket)
+{
+    __shared__ double red[kRedBlock / 64];
+    auto mx  = [](double a, double b) { return fmax(a, b); };
+    double m = 0.0;
+    if (ax)
+        for (int64_t i = first + int64_t(blockIdx.x) * kRedBlock + threadIdx.x; i < last;
+             i += int64_t(gridDim.x) * kRedBlock)
+        {
+            const double x = ax[i], y = ay[i], z = az[i];
+            m              = fmax(m, x * x + y * y + z * z);
+        }
+    m = blockReduce(m, red, mx);
+    if (threadIdx.x == 0) partials[blockIdx.x] = m;
+    if (!lastBlock(ticket)) return;
+    double v = 0.0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += kRedBlock)
+        v = fmax(v, __hip_atomic_load(partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    v = blockReduce(v, red, mx);
+    if (threadIdx.x == 0)
+    {
+        const double inf     = __builtin_inf();
+        const double maxAcc  = sqrt(v);
+        const double acc     = (ax && maxAcc > 0.0) ? etaAcc * sqrt(eps / maxAcc) : inf;
+        const double courant = courantDev ? double(courantDev[0]) : courantHost;
+        double rho           = rhoHost;
+        if (divvMax)
+        {
+            const double d = fabs(double(divvMax[0]));
+            rho            = d != 0.0 ? Krho / d : inf;
+        }
+        out[0] = fmin(fmin(fmin(acc, courant), rho), others);
+        out[1] = prevDt;
+        out[2] = courant;
+        out[3] = rho;
+    }
+}
+
 unsigned blocksFor(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>(kRedBlocks, (n + 1023) / 1024))); }
 
 } // namespace
@@ -159,6 +208,18 @@ void maxNorm2(int64_t first, int64_t last, const float* ax, const float* ay, con
     unsigned* ticket = static_cast<unsigned*>(work);
     double* partials = reinterpret_cast<double*>(static_cast<char*>(work) + 256);
     maxNorm2Kernel<<<blocksFor(last - first), kRedBlock, 0, s>>>(first, last, ax, ay, az, partials, out, ticket);
+    SPHX_LAUNCH_CHECK();
+}
+
+void timestepReduce(int64_t first, int64_t last, const float* ax, const float* ay, const float* az,
+                    const float* courantDev, double courantHost, const float* divvMax, double rhoHost, double Krho,
+                    double etaAcc, double eps, double others, double prevDt, double* out, void* work, hipStream_t s)
+{
+    unsigned* ticket = static_cast<unsigned*>(work);
+    double* partials = reinterpret_cast<double*>(static_cast<char*>(work) + 256);
+    timestepKernel<<<ax ? blocksFor(last - first) : 1u, kRedBlock, 0, s>>>(first, last, ax, ay, az, courantDev,
+                                                                        courantHost, divvMax, rhoHost, Krho, etaAcc,
+                                                                        eps, others, prevDt, partials, out, ticket);
     SPHX_LAUNCH_CHECK();
 }
 

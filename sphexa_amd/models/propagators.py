@@ -124,33 +124,22 @@ class Propagator:
         pend = list(getattr(self.gravity, "pending", None) or [])
         checks = domain.pending_checks() if hasattr(domain, "pending_checks") else None
         if d.device.type == "cuda":
-            # (scalars enter as fills: torch.tensor(value, device=...) would be a synchronizing host-to-device copy)
-            f64 = dict(dtype=torch.float64, device=d.device)
-            inf = torch.full((), math.inf, **f64)
-            courant = (d.minDtCourant_dev.reshape(()).to(torch.float64) if d.minDtCourant is None
-                       else torch.full((), float(d.minDtCourant), **f64))
-            if torch.is_tensor(d.minDtRho):
-                mx = d.minDtRho.reshape(()).to(torch.float64).abs()  # max divv of the owned particles
-                rho = torch.where(mx != 0, d.Krho / mx, inf)
-            else:
-                rho = torch.full((), float(d.minDtRho), **f64)
-            acc = inf
-            if grav:
-                from ..ops.reduce import max_norm2
+            from ..ops.reduce import timestep_reduce
 
-                max_acc = torch.sqrt(max_norm2(d["ax"], d["ay"], d["az"], first, last))
-                acc = torch.where(max_acc > 0, d.etaAcc * torch.sqrt(d.eps / max_acc), inf)
+            # one launch (csrc/hip/reduce.hip timestepKernel): max |a|^2, the Courant minimum of the momentum loop and
+            # the max divv of the IAD loop -> out = [dt, dt_m1, courant, rho] on the device
             others = min([d.maxDtIncrease * d.minDt] + [float(e) for e in extra])
-            loc = torch.minimum(torch.minimum(torch.minimum(acc, courant), rho), torch.full((), others, **f64))
-            glob = loc.reshape(1).clone()
-            domain.comm.allreduce(glob, MIN)
-            flat = [glob, courant.reshape(1), rho.reshape(1)] + [p.dev for p in pend]
+            courant = d.minDtCourant_dev if d.minDtCourant is None else float(d.minDtCourant)
+            out = timestep_reduce(d["ax"], d["ay"], d["az"], first, last, grav, courant, d.minDtRho, d.Krho,
+                                  d.etaAcc, d.eps, others, d.minDt)
+            domain.comm.allreduce(out[:1], MIN)
+            flat = [out[0:1], out[2:4]] + [p.dev for p in pend]
             if checks is not None:
                 flat.append(checks.to(torch.float64).reshape(-1))
             packed = torch.cat(flat)
             if self.defer_host and not self.needs_host_dt:
                 # [dt, dt_m1] for the position update on the device; the host values follow in finish_host()
-                d._dt_dev = torch.cat([glob, torch.full((1,), d.minDt, **f64)])
+                d._dt_dev = out[0:2]
                 host = torch.empty(packed.numel(), dtype=torch.float64, pin_memory=True)
                 host.copy_(packed, non_blocking=True)
                 ev = torch.cuda.Event()

@@ -38,12 +38,34 @@ def _int32_view(ptr: int, count: int, base: torch.Tensor) -> torch.Tensor:
     return base.view(torch.uint8)[off:off + 4 * count].view(torch.int32)
 
 
+# GPU upsweep in one launch (arrival counters) instead of leaves + one launch per level + MAC. Off: measured 8x slower
+# (Evrard -n 100: 1.17 ms vs ~0.15 ms; the per-node agent-scope fences write back / invalidate the XCD L2s), kept for
+# A/B and covered by tests/test_gravity.py::test_fused_upsweep_matches_levels
+UPSWEEP_FUSED = False
+
+
+def _arrival_counters(n: int, device) -> torch.Tensor:
+    from .octree import arrival_counters
+
+    return arrival_counters(n, device)
+
+
 def upsweep(tree: Octree, x, y, z, m, box: Box, theta: float, sfc_kind: int = 0):
     """mass centers + squared vector-MAC radii (N x 4 f64) and quadrupoles (N x 8 f32) of every node"""
     N = tree.num_nodes
     centers = torch.empty(4 * N, dtype=torch.float64, device=x.device)
-    mp = torch.zeros(8 * N, dtype=torch.float32, device=x.device)
     inv_theta = 1.0 / theta
+    if x.is_cuda and UPSWEEP_FUSED:
+        # one launch: leaves, every level (arrival counters), MAC radii (gravity.hip gravityUpsweepFusedKernel)
+        mp = torch.empty(8 * N, dtype=torch.float32, device=x.device)
+        _lib.hip().gravity_upsweep_fused(tree.node_to_leaf.data_ptr(), N, tree.node_start.data_ptr(),
+                                         tree.node_end.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(),
+                                         m.data_ptr(), tree.child_offsets.data_ptr(), tree.parents.data_ptr(),
+                                         tree.prefixes.data_ptr(), box.to_array(), sfc_kind, inv_theta,
+                                         centers.data_ptr(), mp.data_ptr(), _arrival_counters(N, x.device).data_ptr(),
+                                         _stream())
+        return centers, mp
+    mp = torch.zeros(8 * N, dtype=torch.float32, device=x.device)
     if x.is_cuda:
         h = _lib.hip()
         s = _stream()

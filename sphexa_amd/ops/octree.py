@@ -166,6 +166,36 @@ class TreeState:
         return ot
 
 
+# GPU tight boxes in one launch (leaves + arrival-counter climb, octree.hip leafBoxesFusedKernel) instead of one launch
+# per level. Off: the per-node agent-scope fences make it slower than the launches it saves (Sedov -n 100: 0.51 ms vs
+# ~0.06 ms per step); kept for A/B, covered by tests/test_octree.py::test_fused_boxes_match_levels
+BOXES_FUSED = False
+_COUNTERS: dict = {}
+
+
+def arrival_counters(n: int, device) -> torch.Tensor:
+    """grow-only zeroed per-node arrival counters of the one-launch upsweeps (boxes here, multipoles in
+    ops/gravity.py): every launch leaves the counters it used at 0, so the kernels can share them on one stream"""
+    t = _COUNTERS.get(device)
+    if t is None or t.numel() < n:
+        t = _COUNTERS[device] = torch.zeros(max(n, 1024) * 5 // 4, dtype=torch.int32, device=device)
+    return t
+
+
+def _boxes_hip(h, n2l, child, parents, lr, N, ns, ne, x, y, z, center, half, s):
+    if BOXES_FUSED:
+        h.leaf_boxes_fused(n2l.data_ptr(), N, ns.data_ptr(), ne.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(),
+                           child.data_ptr(), parents.data_ptr(), center.data_ptr(), half.data_ptr(),
+                           arrival_counters(N, x.device).data_ptr(), s)
+        return
+    h.leaf_boxes(n2l.data_ptr(), N, ns.data_ptr(), ne.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(),
+                 center.data_ptr(), half.data_ptr(), s)
+    for l in range(MAX_LEVEL, -1, -1):
+        a, b = lr[l], lr[l + 1]
+        if b > a:
+            h.upsweep_boxes(a, b, n2l.data_ptr(), child.data_ptr(), center.data_ptr(), half.data_ptr(), s)
+
+
 def _refit_octree_hip(prev: "Octree", counts, keys, x, y, z, offset) -> "Octree":
     """the linked structure of ``prev`` (same leaves) with new particle ranges and tight boxes"""
     h = _lib.hip()
@@ -177,14 +207,8 @@ def _refit_octree_hip(prev: "Octree", counts, keys, x, y, z, offset) -> "Octree"
     center = torch.empty(3 * N, dtype=torch.float64, device=dev)
     half = torch.empty(3 * N, dtype=torch.float64, device=dev)
     h.node_ranges(prev.prefixes.data_ptr(), N, keys.data_ptr(), n, offset, ns.data_ptr(), ne.data_ptr(), s)
-    h.leaf_boxes(prev.node_to_leaf.data_ptr(), N, ns.data_ptr(), ne.data_ptr(), x.data_ptr(), y.data_ptr(),
-                 z.data_ptr(), center.data_ptr(), half.data_ptr(), s)
-    lr = prev.level_range
-    for l in range(MAX_LEVEL, -1, -1):
-        a, b = lr[l], lr[l + 1]
-        if b > a:
-            h.upsweep_boxes(a, b, prev.node_to_leaf.data_ptr(), prev.child_offsets.data_ptr(), center.data_ptr(),
-                            half.data_ptr(), s)
+    _boxes_hip(h, prev.node_to_leaf, prev.child_offsets, prev.parents, prev.level_range, N, ns, ne, x, y, z, center,
+               half, s)
     import dataclasses
     return dataclasses.replace(prev, counts=counts, node_start=ns, node_end=ne, center=center, half=half,
                                offset=offset)
@@ -267,14 +291,12 @@ def _build_octree_hip(tree, counts, keys, x, y, z, offset) -> Octree:
     center = torch.empty(3 * N, dtype=torch.float64, device=dev)
     half = torch.empty(3 * N, dtype=torch.float64, device=dev)
     h.node_ranges(codes_s.data_ptr(), N, keys.data_ptr(), n, offset, ns.data_ptr(), ne.data_ptr(), s)
-    h.leaf_boxes(vals_s.data_ptr(), N, ns.data_ptr(), ne.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(),
-                 center.data_ptr(), half.data_ptr(), s)
-    # the level ranges (host copy) are read while the node-range and leaf-box kernels run
+    if BOXES_FUSED:
+        _boxes_hip(h, vals_s, child, parents, None, N, ns, ne, x, y, z, center, half, s)
+    # the level ranges (host copy) are read while the node-range and box kernels run
     lr = [int(v) for v in level_range.cpu().tolist()]
-    for l in range(MAX_LEVEL, -1, -1):
-        a, b = lr[l], lr[l + 1]
-        if b > a:
-            h.upsweep_boxes(a, b, vals_s.data_ptr(), child.data_ptr(), center.data_ptr(), half.data_ptr(), s)
+    if not BOXES_FUSED:
+        _boxes_hip(h, vals_s, child, parents, lr, N, ns, ne, x, y, z, center, half, s)
     return Octree(tree=tree, counts=counts, num_nodes=N, num_leaves=L, prefixes=codes_s, child_offsets=child,
                   parents=parents, node_to_leaf=vals_s, leaf_to_node=leaf_to_node, level_range=lr, node_start=ns,
                   node_end=ne, center=center, half=half, offset=offset)

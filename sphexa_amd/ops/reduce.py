@@ -53,3 +53,22 @@ def max_norm2(ax: torch.Tensor, ay: torch.Tensor, az: torch.Tensor, first: int, 
                              _work(dev).data_ptr(), torch.cuda.current_stream().cuda_stream)
         return out.reshape(())
     return (ax[first:last].double() ** 2 + ay[first:last].double() ** 2 + az[first:last].double() ** 2).max()
+
+
+def timestep_reduce(ax, ay, az, first: int, last: int, grav: bool, courant, divv_max, Krho: float, eta_acc: float,
+                    eps: float, others: float, prev_dt: float) -> torch.Tensor:
+    """GPU: float64 device tensor [dt, dt_m1, courant, rho] of the local time step in one launch (reference
+    sph/timestep.hpp): dt = min(etaAcc sqrt(eps / max|a|) if ``grav``, courant, Krho / |divv_max|, others); ``courant``
+    and ``divv_max`` are float32 device scalars or host floats (``divv_max`` host: the rho criterion itself)"""
+    dev = ax.device
+    out = torch.empty(4, dtype=torch.float64, device=dev)
+    c_dev = courant.data_ptr() if torch.is_tensor(courant) else 0
+    c_host = 0.0 if torch.is_tensor(courant) else float(courant)
+    r_dev = divv_max.data_ptr() if torch.is_tensor(divv_max) else 0
+    r_host = 0.0 if torch.is_tensor(divv_max) else float(divv_max)
+    if torch.is_tensor(divv_max) and divv_max.dtype != torch.float32:
+        raise TypeError("divv_max must be a float32 device scalar")
+    _lib.hip().timestep_reduce(first, last, ax.data_ptr() if grav else 0, ay.data_ptr(), az.data_ptr(), c_dev, c_host,
+                               r_dev, r_host, float(Krho), float(eta_acc), float(eps), float(others), float(prev_dt),
+                               out.data_ptr(), _work(dev).data_ptr(), torch.cuda.current_stream().cuda_stream)
+    return out

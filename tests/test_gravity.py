@@ -172,3 +172,21 @@ def test_remote_leaves_always_applied_cpu():
 @pytest.mark.gpu
 def test_remote_leaves_always_applied_gpu(gpu):
     _remote_leaf_case(gpu)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [50, 20000, 150000])
+def test_fused_upsweep_matches_levels(gpu, monkeypatch, n):
+    """the one-launch upsweep (arrival counters, gravity.hip gravityUpsweepFusedKernel) equals the level-by-level
+    launches; repeated and interleaved launches on trees of different sizes (the counters re-arm themselves)"""
+    box, ot, x, y, z, m, h = _setup(n, gpu)
+    monkeypatch.setattr(G, "UPSWEEP_FUSED", False)
+    cl, ml = G.upsweep(ot, x, y, z, m, box, 0.5)
+    monkeypatch.setattr(G, "UPSWEEP_FUSED", True)
+    for _ in range(3):
+        cf, mf = G.upsweep(ot, x, y, z, m, box, 0.5)
+        assert torch.allclose(cf, cl, rtol=1e-12, atol=1e-14)
+        assert torch.allclose(mf, ml, rtol=1e-5, atol=1e-9)
+        small = _setup(40, gpu)
+        G.upsweep(small[1], *small[2:6], small[0], 0.5)
+    assert int(G._arrival_counters(1, x.device).abs().sum()) == 0

@@ -103,3 +103,30 @@ def test_single_leaf_tree():
     assert tree.numel() == 2
     o = O.build_octree(tree, counts, keys, x, y, z)
     assert o.num_nodes == 1 and o.node_to_leaf[0] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,bucket", [(30, 64), (5000, 16), (200_000, 64)])
+def test_fused_boxes_match_levels(gpu, monkeypatch, n, bucket):
+    """the one-launch box upsweep (arrival counters, O.hip leafBoxesFusedKernel) equals the per-level launches
+    and the CPU node boxes, for a fresh build and a refit; counters are left at 0"""
+    g = torch.Generator().manual_seed(n)
+    x, y, z = (torch.rand(n, generator=g, dtype=torch.float64) ** 2 for _ in range(3))
+    box = Box([0.0] * 3, [1.0] * 3)
+    keys = sfc.compute_keys(x, y, z, box)
+    s, p = sfc.sort_keys(keys)
+    x, y, z = x[p.long()], y[p.long()], z[p.long()]
+    tree, counts = O.update_tree(None, s, bucket)
+    ref = O.build_octree(tree, counts, s, x, y, z)
+    dx, dy, dz, ds = (t.to(gpu) for t in (x, y, z, s))
+    tg, cg = tree.to(gpu), counts.to(gpu)
+    monkeypatch.setattr(O, "BOXES_FUSED", False)
+    lv = O.build_octree(tg, cg, ds, dx, dy, dz)
+    monkeypatch.setattr(O, "BOXES_FUSED", True)
+    fu = O.build_octree(tg, cg, ds, dx, dy, dz)
+    for a in (lv, fu):
+        assert torch.allclose(a.center.cpu(), ref.center, rtol=0, atol=1e-15)
+        assert torch.allclose(a.half.cpu(), ref.half, rtol=0, atol=1e-15)
+    re = O._refit_octree_hip(fu, cg, ds, dx, dy, dz, 0)
+    assert torch.equal(re.center, lv.center) and torch.equal(re.half, lv.half)
+    assert int(O.arrival_counters(1, dx.device).abs().sum()) == 0
