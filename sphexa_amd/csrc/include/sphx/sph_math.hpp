@@ -317,8 +317,10 @@ SPHX_HD void pairDelta(CT xi, CT yi, CT zi, CT xj, CT yj, CT zj, HT hi, const Bo
 
 /*! @brief fixed-point coordinate frame of the gfx950 source records: coordinates become 32-bit offsets in the box.
  *         Periodic dimensions span the full 2^32 range, so the wrapping int32 difference of two offsets IS the
- *         minimum image (no fold); open dimensions use 2^30 per box length (|dx| < 2L stays in range). Quantizing
- *         the positions costs at most one quantum q (L/2^32 periodic, L/2^30 open) per separation component; the
+ *         minimum image (no fold); open dimensions use 2^31 per box length: the box is the bounding box of the
+ *         particles (Domain.update_box), so offsets lie in [0, 2^31] and a difference of two of them never wraps to a
+ *         small value (|dx| <= L -> |int32 difference| <= 2^31; only a difference of exactly 2^31 flips its sign and
+ *         stays far). Quantizing the positions costs at most one quantum q (L/2^32 periodic, L/2^31 open) per separation component; the
  *         integer difference is then exact and rounds once to fp32. The host admits this path only while
  *         q <= 2^-22 h_min (ops/hydro.py FIXED_POINT_REL_QUANTUM), i.e. within 2-4x of the reference's fp32 rounding
  *         of its fp64 difference at the kernel support of the smallest particle, and below it for h >= 4 h_min;
@@ -338,7 +340,7 @@ inline QFrame qframeOf(const Box& b)
     {
         const double L = b.len(d) > 0 ? b.len(d) : 1.0;
         q.lo[d]        = b.lo[d];
-        q.s[d]         = (b.periodic(d) ? 4294967296.0 : 1073741824.0) / L;
+        q.s[d]         = (b.periodic(d) ? 4294967296.0 : 2147483648.0) / L;
         q.inv[d]       = float(1.0 / q.s[d]);
     }
     return q;

@@ -164,7 +164,7 @@ def compute_density(d, nl: NeighborList, box: Box):
     compute_xmass(d, nl, box, out_field="rho")
 
 
-# fixed-point records: the coordinate quantum (box length / 2^32 periodic, / 2^30 open) must stay below this
+# fixed-point records: the coordinate quantum (box length / 2^32 periodic, / 2^31 open) must stay below this
 # fraction of the SMALLEST h. The wrapping int32 difference of two records is exact up to one quantum per component,
 # then rounded once to fp32, so a separation carries <= 2^-22 h_min of error: within 2-4x of the reference's fp32
 # rounding of its fp64 difference at the kernel support of the smallest particle (2^-24 |dx|, |dx| < 2h) and below
@@ -237,7 +237,7 @@ def quantum(box: Box) -> float:
     q = 0.0
     for L, bc in zip(box.lengths(), box.bc):
         L = L if L > 0 else 1.0
-        q = max(q, L / (2.0 ** 32 if bc == PERIODIC else 2.0 ** 30))
+        q = max(q, L / (2.0 ** 32 if bc == PERIODIC else 2.0 ** 31))
     return q
 
 

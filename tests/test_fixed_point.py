@@ -20,9 +20,9 @@ def test_fixed_point_guard():
     d = _D(torch.full((4,), 4e-3, dtype=torch.float32))
     assert H.FIXED_POINT_REL_QUANTUM <= 2.0 ** -22
     assert H.fixed_point_ok(d, Box([0.0] * 3, [1.0] * 3, [PERIODIC] * 3))
-    # open dimensions use 2^30 steps: 1 / 2^30 = 9.3e-10 <= 2^-22 * 4e-3 = 9.5e-10
-    assert H.fixed_point_ok(d, Box([0.0] * 3, [1.0] * 3, [OPEN] * 3))
-    assert not H.fixed_point_ok(d, Box([0.0] * 3, [1.1] * 3, [OPEN] * 3))
+    # open dimensions use 2^31 steps (the box is the particles' bounding box): 2 / 2^31 = 9.3e-10 <= 2^-22 * 4e-3
+    assert H.fixed_point_ok(d, Box([0.0] * 3, [2.0] * 3, [OPEN] * 3))
+    assert not H.fixed_point_ok(d, Box([0.0] * 3, [2.1] * 3, [OPEN] * 3))
     # periodic dimensions use the full 2^32 range
     assert H.fixed_point_ok(d, Box([0.0] * 3, [4.0] * 3, [PERIODIC] * 3))
     assert not H.fixed_point_ok(d, Box([0.0] * 3, [4.2] * 3, [PERIODIC] * 3))
