@@ -1320,16 +1320,114 @@ __global__ __launch_bounds__(256) void gravityOrderScatterKernel(int64_t groups,
     }
 }
 
-//! @brief group of a wave of the evaluation kernels: the cost order when given, else XCD-aware SFC order
-__device__ __forceinline__ int64_t evalGroup(const int32_t* order, int64_t numGroups)
+//! @brief group of a wave of the evaluation kernels: the cost order when given (one entry per wave slot of the grid,
+//!        numGroups = no group), else XCD-aware SFC order
+__device__ __forceinline__ int64_t evalGroup(const int32_t* order, int64_t numSlots, int64_t numGroups)
 {
     const int wave = threadIdx.x >> 6;
     if (order)
     {
         const int64_t slot = int64_t(blockIdx.x) * kGWaves + wave;
-        return slot < numGroups ? int64_t(order[slot]) : numGroups;
+        return slot < numSlots ? int64_t(order[slot]) : numGroups;
     }
     return int64_t(xcdRemap(blockIdx.x, gridDim.x)) * kGWaves + wave;
+}
+
+/* XCD-coherent cost order of the P2P kernel (variant -DSPHX_GRAV_SG_ORDER): the heaviest-first order of single groups
+ * scatters the groups that run at the same time on one XCD over the whole domain, and their source particles miss in
+ * its L2 (TCC hit rate 36 % on Evrard -n 200). Here the unit is a super-group of kSG = 16 SFC-consecutive groups (4 blocks, which share
+ * most of their sources): super-groups are ranked by total work (same bins), rank r goes to XCD r % 8 as its
+ * (r / 8)-th run of 4 consecutive blocks on that XCD (the dispatcher deals block b to XCD b % 8), so every XCD works
+ * heaviest first through a balanced share while the 4 blocks of a super-group run side by side in one L2.
+ * Measured (Evrard -n 200, gpurun_out/go4): L2 hit rate 36 -> 66 %, but P2P 9.07 -> 9.43 ms: the coarser unit balances
+ * worse, and the misses were not what bounds the loop (profiles/r3_grav_pmc.md). Not the default.
+ */
+constexpr int kSG = 16;
+
+__device__ __forceinline__ int sgWork(const GravSlabs& S, int64_t sg, int64_t groups)
+{
+    long long w = 0;
+    for (int64_t g = sg * kSG; g < min(groups, (sg + 1) * kSG); ++g)
+        w += groupWork(S, g, 1);
+    return int(min(w, (long long)INT32_MAX));
+}
+
+//! @brief grid (blocks) of the P2P kernel under the super-group order: whole runs of 4 blocks on all 8 XCDs
+__host__ __device__ inline int64_t sgGridBlocks(int64_t groups)
+{
+    const int64_t nsg = (groups + kSG - 1) / kSG;
+    return 8 * (kSG / kGWaves) * ((nsg + 7) / 8);
+}
+
+__global__ __launch_bounds__(256) void gravitySgHistKernel(int64_t groups, GravSlabs S, int32_t* __restrict__ hist)
+{
+    __shared__ int32_t h[kOrdBins];
+    for (int k = threadIdx.x; k < kOrdBins; k += blockDim.x)
+        h[k] = 0;
+    __syncthreads();
+    const int64_t nsg = (groups + kSG - 1) / kSG;
+    for (int64_t sg = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; sg < nsg; sg += int64_t(gridDim.x) * blockDim.x)
+        atomicAdd(&h[costBin(sgWork(S, sg, groups))], 1);
+    __syncthreads();
+    for (int k = threadIdx.x; k < kOrdBins; k += blockDim.x)
+        if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+
+__global__ __launch_bounds__(256) void gravitySgScatterKernel(int64_t groups, GravSlabs S,
+                                                              const int32_t* __restrict__ hist,
+                                                              int32_t* __restrict__ cursor,
+                                                              int32_t* __restrict__ order)
+{
+    __shared__ int32_t off[kOrdBins], cnt[kOrdBins], base[kOrdBins];
+    if (threadIdx.x == 0)
+    {
+        int s = 0;
+        for (int b = 0; b < kOrdBins; ++b)
+        {
+            off[b] = s;
+            s += hist[b];
+        }
+    }
+    const int64_t nsg   = (groups + kSG - 1) / kSG;
+    const int64_t slots = sgGridBlocks(groups) * kGWaves;
+    for (int64_t s0 = int64_t(blockIdx.x) * blockDim.x; s0 < (nsg + 7) / 8 * 8; s0 += int64_t(gridDim.x) * blockDim.x)
+    {
+        for (int k = threadIdx.x; k < kOrdBins; k += blockDim.x)
+            cnt[k] = 0;
+        __syncthreads();
+        const int64_t sg = s0 + threadIdx.x;
+        const int b      = sg < nsg ? costBin(sgWork(S, sg, groups)) : 0;
+        const int r0     = sg < nsg ? atomicAdd(&cnt[b], 1) : 0;
+        __syncthreads();
+        for (int k = threadIdx.x; k < kOrdBins; k += blockDim.x)
+            base[k] = cnt[k] ? atomicAdd(&cursor[k], cnt[k]) : 0;
+        __syncthreads();
+        if (sg < nsg)
+        {
+            const int64_t r = off[b] + base[b] + r0;
+            for (int t = 0; t < kSG / kGWaves; ++t)
+            {
+                const int64_t blk = 8 * ((kSG / kGWaves) * (r >> 3) + t) + (r & 7);
+                for (int w = 0; w < kGWaves; ++w)
+                {
+                    const int64_t g = sg * kSG + t * kGWaves + w;
+                    order[blk * kGWaves + w] = int32_t(g < groups ? g : groups);
+                }
+            }
+        }
+        else if (sg < (nsg + 7) / 8 * 8)
+        {
+            // the slots of the padding ranks (nsg .. multiple of 8) hold no group
+            const int64_t r = sg;
+            for (int t = 0; t < kSG / kGWaves; ++t)
+            {
+                const int64_t blk = 8 * ((kSG / kGWaves) * (r >> 3) + t) + (r & 7);
+                for (int w = 0; w < kGWaves; ++w)
+                    if (blk * kGWaves + w < slots) order[blk * kGWaves + w] = int32_t(groups);
+            }
+        }
+        __syncthreads();
+    }
 }
 
 //! @brief shared prologue of the evaluation kernels: the group's targets, fp64 box center, fp32 relative coordinates
@@ -1365,7 +1463,7 @@ __global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t 
                                                            float* __restrict__ az, double* __restrict__ ugrav,
                                                            double* __restrict__ out,
                                                            unsigned long long* __restrict__ stats, GravSlabs S,
-                                                           const int32_t* __restrict__ order)
+                                                           const int32_t* __restrict__ order, int64_t numSlots)
 {
 #ifdef SPHX_GRAV_M2P_MFMA2
     __shared__ float4 stage[kGWaves][kM2P2Stage];
@@ -1375,7 +1473,7 @@ __global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t 
     __shared__ double red[kGWaves];
     const int wave          = threadIdx.x >> 6;
     const int64_t numGroups = (last - first + 63) / 64;
-    const int64_t g         = evalGroup(order, numGroups);
+    const int64_t g         = evalGroup(order, numSlots, numGroups);
     double upot             = 0;
     int nm                  = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[2 * g]) : -1;
     SPHX_DCHECK(nm <= S.capM, 3);
@@ -1415,14 +1513,14 @@ __global__ __launch_bounds__(256, SPHX_P2P_WAVES) void gravityP2PKernel(int64_t 
                                                            const int64_t* __restrict__ poff,
                                                            const int32_t* __restrict__ pidx,
                                                            float4* __restrict__ pacc,
-                                                           const int32_t* __restrict__ order)
+                                                           const int32_t* __restrict__ order, int64_t numSlots)
 {
     __shared__ GravLds lds[kGWaves];
     __shared__ double red[kGWaves];
     const int lane          = laneId();
     const int wave          = threadIdx.x >> 6;
     const int64_t numGroups = (last - first + 63) / 64;
-    const int64_t g         = evalGroup(order, numGroups);
+    const int64_t g         = evalGroup(order, numSlots, numGroups);
     double upot             = 0;
     const int nl            = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[2 * g + 1]) : -1;
     if (nl >= 0)
@@ -1497,7 +1595,8 @@ size_t gravityScratchBytes(int64_t n, int capM, int capL)
 {
     int64_t groups = (n + 63) / 64;
     return size_t(padTo64(groups) + int64_t(kGSpillWaves) * kGSpillFront + padTo64(2 * groups) + padTo64(groups) +
-                  groups * int64_t(capM + capL) + padTo64(2 * groups) + 4 * kOrdBins) *
+                  groups * int64_t(capM + capL) + padTo64(2 * groups) + padTo64(4 * sgGridBlocks(groups)) +
+                  4 * kOrdBins) *
            sizeof(int32_t);
 }
 
@@ -1506,7 +1605,8 @@ struct GravScratch
     int32_t* spillList;
     int32_t* spillMem;
     GravSlabs S;
-    int32_t* order; // 2 x groups: M2P order, P2P order (heaviest first)
+    int32_t* order;   // 2 x groups: M2P order, P2P order (heaviest first, single groups)
+    int32_t* orderSG; // P2P wave slots under the super-group order (sgGridBlocks x kGWaves)
     int32_t* hist;  // 2 x kOrdBins histogram + 2 x kOrdBins scatter cursors
 };
 
@@ -1521,7 +1621,8 @@ static GravScratch carve(void* scratch, int64_t groups, int capM, int capL)
     int32_t* llist  = mlist + groups * int64_t(capM);
     c.S             = GravSlabs{mlist, llist, counts, pcount, capM, capL};
     c.order         = llist + groups * int64_t(capL);
-    c.hist          = c.order + padTo64(2 * groups);
+    c.orderSG       = c.order + padTo64(2 * groups);
+    c.hist          = c.orderSG + padTo64(4 * sgGridBlocks(groups));
     return c;
 }
 
@@ -1559,6 +1660,8 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
     int64_t groups = (n + 63) / 64;
     GravScratch c  = carve(scratch, groups, capM, capL);
     unsigned grid  = unsigned((groups + kGWaves - 1) / kGWaves);
+    unsigned gridP = grid; // P2P grid (the super-group order pads it to whole runs on all XCDs)
+    int64_t slotsP = groups; // valid entries of the P2P order
     // phase 1: M2P only (needs no particle index list), phase 2: the P2P part, 0: both. Split so that the host
     // reads the P2P list size while the M2P kernel runs (ops/gravity.py)
 #ifdef SPHX_GRAV_SFC_ORDER
@@ -1572,21 +1675,35 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
 #else
     const int32_t* orderM = nullptr;
 #endif
-    const int32_t* orderP = c.order + groups;
     if (phase != 2)
     {
         SPHX_CHECK(hipMemsetAsync(c.hist, 0, 4 * kOrdBins * sizeof(int32_t), s));
         const unsigned og = unsigned(std::min<int64_t>((groups + 255) / 256, 1024));
+#ifndef SPHX_GRAV_SG_ORDER
         gravityOrderHistKernel<<<og, 256, 0, s>>>(groups, c.S, c.hist);
         SPHX_LAUNCH_CHECK();
         gravityOrderScatterKernel<<<og, 256, 0, s>>>(groups, c.S, c.hist, c.hist + 2 * kOrdBins, c.order);
         SPHX_LAUNCH_CHECK();
+#else
+        const unsigned sgb = unsigned(std::min<int64_t>(((groups + kSG - 1) / kSG + 255) / 256 + 1, 1024));
+        gravitySgHistKernel<<<sgb, 256, 0, s>>>(groups, c.S, c.hist + kOrdBins);
+        SPHX_LAUNCH_CHECK();
+        gravitySgScatterKernel<<<sgb, 256, 0, s>>>(groups, c.S, c.hist + kOrdBins, c.hist + 3 * kOrdBins, c.orderSG);
+        SPHX_LAUNCH_CHECK();
+#endif
     }
+#ifndef SPHX_GRAV_SG_ORDER
+    const int32_t* orderP = c.order + groups;
+#else
+    const int32_t* orderP = c.orderSG;
+    gridP                 = unsigned(sgGridBlocks(groups));
+    slotsP                = int64_t(gridP) * kGWaves;
+#endif
 #endif
     if (phase == 1)
     {
         gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
-                                                       stats, c.S, orderM);
+                                                       stats, c.S, orderM, groups);
         SPHX_LAUNCH_CHECK();
         return;
     }
@@ -1609,14 +1726,14 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
 #endif
     SPHX_CHECK(hipEventRecord(fork, s));
     SPHX_CHECK(hipStreamWaitEvent(side, fork, 0));
-    gravityP2PKernel<<<grid, 64 * kGWaves, 0, side>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
-                                                      stats, c.S, poff, pidx, pacc, orderP);
+    gravityP2PKernel<<<gridP, 64 * kGWaves, 0, side>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
+                                                      stats, c.S, poff, pidx, pacc, orderP, slotsP);
     SPHX_LAUNCH_CHECK();
     SPHX_CHECK(hipEventRecord(join, side));
     if (phase == 0)
     {
         gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
-                                                       stats, c.S, orderM);
+                                                       stats, c.S, orderM, groups);
         SPHX_LAUNCH_CHECK();
     }
     SPHX_CHECK(hipStreamWaitEvent(s, join, 0));
