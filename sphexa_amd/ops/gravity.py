@@ -130,8 +130,8 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         return 0.0
     if x.is_cuda:
         hp = _lib.hip()
-        out = torch.zeros(2, dtype=torch.float64, device=x.device)
-        st_dev = torch.zeros(8, dtype=torch.int64, device=x.device)
+        zb = torch.zeros(10, dtype=torch.int64, device=x.device)  # one fill: statistics (int64) + energy (float64)
+        st_dev, out = zb[:8], zb[8:].view(torch.float64)
         from .neighbors import _scratch
 
         cap_m, cap_l = TEST_CAPS if TEST_CAPS is not None else (_CAPS["m"], _CAPS["l"])

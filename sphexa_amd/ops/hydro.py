@@ -180,13 +180,16 @@ def invalidate_h_cache(d):
 
 
 def global_h_min_device(d, comm) -> torch.Tensor:
-    """[min h, min m, -max m] over all ranks as a float64 device tensor (no host copy; see set_global_h_min)"""
+    """[min h, min m, -max m] over all ranks as a float64 device tensor (no host copy; see set_global_h_min); on one
+    rank the reduction's own [min h, max h, min m, max m] (no further launches)"""
     h = d["h"][: d.size]
     m = d["m"][: d.size]
     if h.numel():
         from .reduce import min_max
 
         mm = min_max([h, m])  # [min h, max h, min m, max m], one launch on the GPU
+        if comm is None or comm.size == 1:
+            return mm
         loc = torch.stack([mm[0], mm[2], -mm[3]])
     else:
         loc = torch.full((3,), math.inf, dtype=torch.float64, device=h.device)
@@ -198,8 +201,11 @@ def global_h_min_device(d, comm) -> torch.Tensor:
 def apply_global_h_min(d, vals):
     """store the host values of global_h_min_device: the per-step h minimum of the fixed-point guard and the
     uniform-mass cache keyed on the current mass tensor"""
-    hmin, mlo, mhi = (float(v) for v in vals)
-    mhi = -mhi
+    vals = [float(v) for v in vals]
+    if len(vals) == 4:  # one rank: [min h, max h, min m, max m]
+        hmin, mlo, mhi = vals[0], vals[2], vals[3]
+    else:
+        hmin, mlo, mhi = vals[0], vals[1], -vals[2]
     m = d["m"][: d.size]
     d._h_min_global = hmin
     val = mlo if (mlo == mhi and mlo > 0) else 0.0
