@@ -783,8 +783,37 @@ __device__ __forceinline__ void p2pFinish(const P2PTarget& T, float acc[4])
     acc[3] += v[3] - T.zr * v[4] + T.v[3];
 }
 
+//! @brief source index at offset o of a plain index list
+struct ListIdx
+{
+    const int32_t* p;
+    __device__ __forceinline__ int32_t operator()(int o) const { return p[o]; }
+};
+
+/*! @brief source index at offset o of a window of opened leaves: pre = exclusive prefix of the leaf sizes (+ total),
+ *         st = first particle of each leaf, both in LDS; binary search for the leaf (the P2P kernel generates its
+ *         source indices from the leaf list instead of reading an expanded per-group index list) */
+struct LeafIdx
+{
+    const int32_t* pre;
+    const int32_t* st;
+    int nw;
+    __device__ __forceinline__ int32_t operator()(int o) const
+    {
+        int lo = 0, hi = nw; // pre[lo] <= o < pre[hi]
+        while (hi - lo > 1)
+        {
+            const int mid = (lo + hi) >> 1;
+            if (pre[mid] <= o) lo = mid;
+            else hi = mid;
+        }
+        return st[lo] + (o - pre[lo]);
+    }
+};
+
 //! @brief all queued P2P particles against the group's 64 targets, 64 sources per staged LDS tile
-__device__ inline void flushP2P(const int32_t* plst, int n, const GravLists& L, const double* x, const double* y,
+template<class Idx>
+__device__ inline void flushP2P(const Idx& plst, int n, const GravLists& L, const double* x, const double* y,
                                 const double* z, const float* h, const float* m, const double gc[3], P2PTarget& T)
 {
     n = __builtin_amdgcn_readfirstlane(n);
@@ -799,8 +828,8 @@ __device__ inline void flushP2P(const int32_t* plst, int n, const GravLists& L, 
         rx = x[j], ry = y[j], rz = z[j];
         rh = h[j], rm = m[j];
     };
-    int32_t jN  = lane < n ? plst[lane] : plst[0];
-    int32_t jNN = 64 + lane < n ? plst[64 + lane] : plst[0];
+    int32_t jN  = lane < n ? plst(lane) : plst(0);
+    int32_t jNN = 64 + lane < n ? plst(64 + lane) : plst(0);
     gather(jN);
     for (int c0 = 0; c0 < n; c0 += 64)
     {
@@ -831,7 +860,7 @@ __device__ inline void flushP2P(const int32_t* plst, int n, const GravLists& L, 
             reinterpret_cast<float*>(L.sxm + 64)[lane] = Qn.y;
         }
         jN = jNN;
-        jNN = c0 + 128 + lane < n ? plst[c0 + 128 + lane] : plst[0];
+        jNN = c0 + 128 + lane < n ? plst(c0 + 128 + lane) : plst(0);
         gather(jN); // unconditional (past the end: clamped index) so the loads land in the loop registers directly
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (!mfma)
@@ -928,7 +957,7 @@ __device__ __forceinline__ void queueLeaf(int a0, int n0, int& np, const GravLis
         if (np + c > kGP2P)
         {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            flushP2P(L.plst, np, L, x, y, z, h, m, tc, T);
+            flushP2P(ListIdx{L.plst}, np, L, x, y, z, h, m, tc, T);
             np = 0;
         }
         if (lane < c) L.plst[np + lane] = a0 + off + lane;
@@ -1092,7 +1121,7 @@ __device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t l
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     evalM2P(L.mlst, nm, t, tc, xr, yr, zr, L.spos, acc);
-    flushP2P(L.plst, np, L, x, y, z, h, m, tc, T);
+    flushP2P(ListIdx{L.plst}, np, L, x, y, z, h, m, tc, T);
     p2pFinish(T, acc);
     gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, totP2P, totM2P, upot);
     return true;
@@ -1530,9 +1559,51 @@ __global__ __launch_bounds__(256, SPHX_P2P_WAVES) void gravityP2PKernel(int64_t 
         float acc[4] = {0, 0, 0, 0};
         P2PTarget T;
         p2pInit(T, e.xr, e.yr, e.zr, e.hi);
-        const int64_t p0 = poff[g];
-        const int np     = int(poff[g + 1] - p0);
-        flushP2P(pidx + p0, np, L, x, y, z, h, m, e.tc, T);
+        int np = 0;
+        if (pidx)
+        {
+            const int64_t p0 = poff[g];
+            np               = int(poff[g + 1] - p0);
+            flushP2P(ListIdx{pidx + p0}, np, L, x, y, z, h, m, e.tc, T);
+        }
+        else
+        {
+            // windows of up to 255 opened leaves: sizes prefix-summed into LDS (plst holds the prefix (256) | the
+            // starts (255)), the source indices generated per chunk (no expanded index list, no host-sized buffer)
+            static_assert(kGP2P >= 2 * 256, "leaf window of the P2P kernel");
+            const int32_t* ll = S.llist + g * S.capL;
+            int32_t* pre      = L.plst;
+            int32_t* st       = L.plst + 256;
+            for (int w0 = 0; w0 < nl; w0 += 255)
+            {
+                const int nw = min(255, nl - w0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the previous window's reads are done
+                int run = 0;
+                for (int b = 0; b < nw; b += 64)
+                {
+                    const int k      = b + lane;
+                    const int32_t lf = k < nw ? ll[w0 + k] : -1;
+                    const int32_t a0 = lf >= 0 ? t.ns[lf] : 0;
+                    const int sz     = lf >= 0 ? t.ne[lf] - a0 : 0;
+                    int inc          = sz; // inclusive wave scan of the sizes
+                    for (int o = 1; o < 64; o <<= 1)
+                    {
+                        const int v = __shfl_up(inc, o);
+                        if (lane >= o) inc += v;
+                    }
+                    if (k < nw)
+                    {
+                        pre[k] = run + inc - sz;
+                        st[k]  = a0;
+                    }
+                    run += __shfl(inc, 63);
+                }
+                if (lane == 0) pre[nw] = run;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                flushP2P(LeafIdx{pre, st, nw}, run, L, x, y, z, h, m, e.tc, T);
+                np += run;
+            }
+        }
         p2pFinish(T, acc);
         unsigned long long totP2P = (unsigned long long)np;
         gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, totP2P, 0ull, upot, pacc);
@@ -1707,8 +1778,11 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
         SPHX_LAUNCH_CHECK();
         return;
     }
-    gravityExpandKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, c.S, poff, pidx);
-    SPHX_LAUNCH_CHECK();
+    if (pidx)
+    {
+        gravityExpandKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, c.S, poff, pidx);
+        SPHX_LAUNCH_CHECK();
+    }
     // P2P partials land in pacc and are added by gravityCombineKernel. The two evaluation kernels run one after the
     // other on s: run concurrently (P2P on a side stream, SPHX_GRAV_CONCURRENT) they compete for the same SIMDs and
     // the step is ~1 ms slower on Evrard -n 200 (37.4 vs 38.4 ms, profiles/r2_perf_log.md)

@@ -38,6 +38,10 @@ def _int32_view(ptr: int, count: int, base: torch.Tensor) -> torch.Tensor:
     return base.view(torch.uint8)[off:off + 4 * count].view(torch.int32)
 
 
+# P2P sources through an expanded per-group particle index list (the host reads its size: one wait per evaluation)
+# instead of indices generated from the opened-leaf lists inside the P2P kernel (default)
+P2P_EXPAND = False
+
 # GPU upsweep in one launch (arrival counters) instead of leaves + one launch per level + MAC. Off: measured 8x slower
 # (Evrard -n 100: 1.17 ms vs ~0.15 ms; the per-node agent-scope fences write back / invalidate the XCD L2s), kept for
 # A/B and covered by tests/test_gravity.py::test_fused_upsweep_matches_levels
@@ -144,6 +148,16 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         # phase 1: interaction lists + per-group P2P particle counts
         hp.gravity_lists(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), st_dev.data_ptr(),
                          scratch.data_ptr(), TEST_FRONT_CAP, cap_m, cap_l, s)
+        pacc = torch.empty(4 * n, dtype=torch.float32, device=x.device)  # P2P partials (phi, a) per target
+        if not P2P_EXPAND:
+            # the P2P kernel generates its source indices from the opened-leaf lists: no index list, no host wait
+            hp.gravity_eval(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
+                            m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
+                            0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), st_dev.data_ptr(),
+                            scratch.data_ptr(), cap_m, cap_l, 0, 0, pacc.data_ptr(), s, phase=0)
+            pending = GravityPending(torch.cat([st_dev.to(torch.float64), out]), groups, (cap_m, cap_l), stats,
+                                     x.device)
+            return pending if defer else pending.finish(pending.dev.cpu().tolist())
         pcount = _int32_view(hp.gravity_particle_counts(scratch.data_ptr(), n, cap_m, cap_l), groups, scratch)
         # per-group offsets of the P2P particle runs: exclusive scan (hand-written tile scan, sample_sort.hip) of the
         # counts with a trailing zero, so poff[groups] is the total
@@ -151,7 +165,6 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         poff[:groups].copy_(pcount)
         stmp = torch.empty(hp.scan_temp_bytes(groups + 1), dtype=torch.uint8, device=x.device)
         hp.exclusive_scan_i64(poff.data_ptr(), poff.data_ptr(), groups + 1, stmp.data_ptr(), stmp.numel(), s)
-        pacc = torch.empty(4 * n, dtype=torch.float32, device=x.device)  # P2P partials (phi, a) per target
         # the P2P list size goes to pinned host memory ahead of the M2P kernel: the host waits for that copy only,
         # and enqueues the P2P part while M2P runs (no idle gap on the GPU)
         total_h = _pinned_total()
