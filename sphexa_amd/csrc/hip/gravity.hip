@@ -1734,7 +1734,8 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
     unsigned gridP = grid; // P2P grid (the super-group order pads it to whole runs on all XCDs)
     int64_t slotsP = groups; // valid entries of the P2P order
     // phase 1: M2P only (needs no particle index list), phase 2: the P2P part, 0: both. Split so that the host
-    // reads the P2P list size while the M2P kernel runs (ops/gravity.py)
+    // reads the P2P list size while the M2P kernel runs (ops/gravity.py P2P_EXPAND; by default phase 0 runs everything
+    // with pidx == nullptr: the P2P kernel generates its sources from the leaf lists and nothing waits on the host)
 #ifdef SPHX_GRAV_SFC_ORDER
     const int32_t* orderM = nullptr;
     const int32_t* orderP = nullptr;
