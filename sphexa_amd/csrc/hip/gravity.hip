@@ -340,9 +340,14 @@ struct GravLists
     int32_t* mlst; // MAC-accepted nodes (M2P), fused path only
     int32_t* plst; // particle indices of opened leaves (P2P)
     float4* spos;  // staged P2P tile: {x, y, z, |x|^2} relative to the group center; M2P: 3 x 64 records
-    float4* smh;   // staged P2P tile: {m, h, h^2, 0}
+    float2* sab;   // staged P2P tile: MFMA A operands {aR_k, aH_k} of source s at [k * kAbRow + s] (see flushP2P)
+    float* sm;     // staged P2P tile: source masses
     float4* sxm;   // staged P2P tile for the VALU path: {x, y, z, m}, then the 64 h values as 16 float4
 };
+
+//! row stride (float2) of the k-major MFMA operand rows: 80 = 16 mod 32, so the lanes of kq and kq + 1 (one
+//! 32-lane group of ds_read_b64) read opposite halves of the 64 banks
+constexpr int kAbRow = 80;
 
 /*! @brief M2P of a list of nodes, 64 per batch: lane k gathers node k's expansion center (fp32, relative to the
  *         group center tc) and quadrupole, the batch is staged in LDS as 3 float4 per node and every lane applies
@@ -411,7 +416,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
  * components for nodes 4 (l >> 4) + r, r < 4, and target 16 tb + (l & 15). The VALU finishes the pair (separation,
  * rsqrt, r.Qr, monopole, accumulation): 25 instead of 34 VALU per pair, the 9 multiply-adds of Q r move to the
  * matrix pipe (8 issue cycles per 1024 products). Node batches of 64 are staged in LDS as the MFMA A operands
- * (per node and k one float4 {A_x[k], A_y[k], A_z[k], 0}) plus {c, M}; the next batch's gathers are in flight meanwhile.
+ * (per node and k one float4 {A_x[k], A_y[k], A_z[k], 0}, stored k-major: sA[64 k + node]) plus {c, M}; the next
+ * batch's gathers are in flight meanwhile. k-major rows make the staging stores contiguous per k and put the 16
+ * lanes of a ds_read lane group on 16 distinct 16-B slots (node-major [node][k] rows were 4-way conflicted on the
+ * stores and 2-way on the reads: SQ_LDS_BANK_CONFLICT 2650 per wave, profiles/r3_grav_pmc.md).
  * No precision guard is needed (unlike the P2P tile): Q t - Q c carries rounding ~eps |Q| |c| against |Q r| with
  * |c| <= |r| + R_group, and R2 is formed on the VALU from r.
  */
@@ -422,7 +430,7 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
     if (n <= 0) return;
     const int lane = laneId(), kq = lane >> 4, col = lane & 15;
     float4* sC = stage;      // 64 x {cx, cy, cz, M}
-    float4* sA = stage + 64; // 64 x 4 (k) x {A_x[k], A_y[k], A_z[k], 0}
+    float4* sA = stage + 64; // 4 (k) x 64 x {A_x[k], A_y[k], A_z[k], 0}
     // target side: B operand [x, y, z, 1]_k of target 16 tb + col, and the four targets' coordinates
     float bT[4], tx[4], ty[4], tz[4];
 #pragma unroll
@@ -460,11 +468,11 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
             const float Qcx = Qxx * cx + Qxy * cy + Qxz * cz;
             const float Qcy = Qxy * cx + Qyy * cy + Qyz * cz;
             const float Qcz = Qxz * cx + Qyz * cy + Qzz * cz;
-            sC[lane]             = make_float4(cx, cy, cz, M);
-            sA[4 * lane + 0]     = make_float4(Qxx, Qxy, Qxz, 0.f);
-            sA[4 * lane + 1]     = make_float4(Qxy, Qyy, Qyz, 0.f);
-            sA[4 * lane + 2]     = make_float4(Qxz, Qyz, Qzz, 0.f);
-            sA[4 * lane + 3]     = make_float4(-Qcx, -Qcy, -Qcz, 0.f);
+            sC[lane]        = make_float4(cx, cy, cz, M);
+            sA[lane]        = make_float4(Qxx, Qxy, Qxz, 0.f);
+            sA[64 + lane]   = make_float4(Qxy, Qyy, Qyz, 0.f);
+            sA[128 + lane]  = make_float4(Qxz, Qyz, Qzz, 0.f);
+            sA[192 + lane]  = make_float4(-Qcx, -Qcy, -Qcz, 0.f);
         }
         idxN  = idxNN;
         idxNN = b0 + 128 + lane < n ? list[b0 + 128 + lane] : 0;
@@ -473,7 +481,7 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
         const int ntile = (min(64, n - b0) + 15) >> 4;
         for (int tile = 0; tile < ntile; ++tile)
         {
-            const float4 A = sA[4 * (16 * tile + col) + kq];
+            const float4 A = sA[64 * kq + 16 * tile + col];
             float4 C[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -552,7 +560,7 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
 }
 
 //! float4 slots of the per-wave staging area used by evalM2PMfma2 (64 nodes per batch)
-constexpr int kM2P2Stage = 64 + 16 + 256 + 128;
+constexpr int kM2P2Stage = 64 + 16 + 256 + 160;
 
 /*! @brief M2P with every bilinear part of the pair on the matrix cores: separation, quadrupole-vector product and the
  *         quadratic form, leaving the VALU the radial factors and the accumulation.
@@ -585,7 +593,7 @@ __device__ inline void evalM2PMfma2(const int32_t* list, int n, const GravTree& 
     float4* sC = stage;                                      // 64 x {-c_x, -c_y, -c_z, M}
     float* sD  = reinterpret_cast<float*>(stage + 64);       // 64 x c.Qc
     float4* sA = stage + 80;                                 // (node, k) -> {Qr_x, Qr_y, Qr_z, R2} A operands
-    float2* sB = reinterpret_cast<float2*>(stage + 336);     // (node, k) -> the two rQr A operands
+    float2* sB = reinterpret_cast<float2*>(stage + 336);     // (k, node) -> the two rQr A operands (rows of 80)
     float bT[4], b2a[4], b2b[4], tt[4];
 #pragma unroll
     for (int tb = 0; tb < 4; ++tb)
@@ -627,14 +635,14 @@ __device__ inline void evalM2PMfma2(const int32_t* list, int n, const GravTree& 
             const float Qcz = Qxz * cx + Qyz * cy + Qzz * cz;
             sC[lane]         = make_float4(-cx, -cy, -cz, M);
             sD[lane]         = cx * Qcx + cy * Qcy + cz * Qcz;
-            sA[4 * lane + 0] = make_float4(Qxx, Qxy, Qxz, -2.f * cx);
-            sA[4 * lane + 1] = make_float4(Qxy, Qyy, Qyz, -2.f * cy);
-            sA[4 * lane + 2] = make_float4(Qxz, Qyz, Qzz, -2.f * cz);
-            sA[4 * lane + 3] = make_float4(-Qcx, -Qcy, -Qcz, cx * cx + cy * cy + cz * cz);
-            sB[4 * lane + 0] = make_float2(Qxx, 2.f * Qyz);
-            sB[4 * lane + 1] = make_float2(Qyy, -2.f * Qcx);
-            sB[4 * lane + 2] = make_float2(2.f * Qxy, -2.f * Qcy);
-            sB[4 * lane + 3] = make_float2(2.f * Qxz, -2.f * Qcz);
+            sA[lane]         = make_float4(Qxx, Qxy, Qxz, -2.f * cx);
+            sA[64 + lane]    = make_float4(Qxy, Qyy, Qyz, -2.f * cy);
+            sA[128 + lane]   = make_float4(Qxz, Qyz, Qzz, -2.f * cz);
+            sA[192 + lane]   = make_float4(-Qcx, -Qcy, -Qcz, cx * cx + cy * cy + cz * cz);
+            sB[lane]         = make_float2(Qxx, 2.f * Qyz);
+            sB[80 + lane]    = make_float2(Qyy, -2.f * Qcx);
+            sB[160 + lane]   = make_float2(2.f * Qxy, -2.f * Qcy);
+            sB[240 + lane]   = make_float2(2.f * Qxz, -2.f * Qcz);
         }
         idxN  = idxNN;
         idxNN = b0 + 128 + lane < n ? list[b0 + 128 + lane] : 0;
@@ -643,8 +651,8 @@ __device__ inline void evalM2PMfma2(const int32_t* list, int n, const GravTree& 
         const int ntile = (min(64, n - b0) + 15) >> 4;
         for (int tile = 0; tile < ntile; ++tile)
         {
-            const float4 A  = sA[4 * (16 * tile + col) + kq];
-            const float2 A2 = sB[4 * (16 * tile + col) + kq];
+            const float4 A  = sA[64 * kq + 16 * tile + col];
+            const float2 A2 = sB[80 * kq + 16 * tile + col];
             const float4 D  = reinterpret_cast<const float4*>(sD)[4 * tile + kq]; // c.Qc of rows 4 kq + r
             float4 C[4];
 #pragma unroll
@@ -734,6 +742,7 @@ struct P2PTarget
     float sx[4], sy[4], sz[4], sw[4], phi[4];
     float xr, yr, zr, hi, v[4]; // VALU path: own target, own accumulators
     float maxT2, hminT;         // group extent for the accuracy test
+    int nMfma, nValu;           // 64-source chunks evaluated on the MFMA tile / the VALU fallback (wave-uniform)
 };
 
 constexpr float kMfmaP2PTol = 4e-6f / 6e-8f; // tolerated (|x_s|^2 + |x_t|^2) / (h_s + h_t)^2_min
@@ -756,6 +765,7 @@ __device__ __forceinline__ void p2pInit(P2PTarget& T, float xr, float yr, float 
     T.v[0] = T.v[1] = T.v[2] = T.v[3] = 0.f;
     T.maxT2 = waveMax(r2);
     T.hminT = waveMin(hi);
+    T.nMfma = T.nValu = 0;
 }
 
 //! @brief sum the per-lane partials of P2PTarget over the four source lane groups; returns {phi, ax, ay, az} of the
@@ -849,8 +859,16 @@ __device__ inline void flushP2P(const Idx& plst, int n, const GravLists& L, cons
 #endif
         if (mfma)
         {
-            L.spos[lane] = Pn;
-            L.smh[lane]  = Qn;
+            // A operands of the R2 / H2 tiles stored k-major, so lane (kq, col) fetches its {aR, aH} pair with one
+            // conflict-free ds_read_b64 (a per-lane component select of source-major records became divergent
+            // 8-way conflicted ds_read_b32s: SQ_LDS_BANK_CONFLICT 2044 per wave, profiles/r3_grav_pmc.md)
+            L.spos[lane]             = Pn;
+            L.sab[lane]              = make_float2(Pn.x, Qn.z);
+            L.sab[kAbRow + lane]     = make_float2(Pn.y, Qn.y);
+            L.sab[2 * kAbRow + lane] = make_float2(Pn.z, 1.f);
+            L.sab[3 * kAbRow + lane] = make_float2(1.f, 0.f);
+            L.sm[lane]               = Qn.x;
+            ++T.nMfma;
         }
         else
         {
@@ -858,6 +876,7 @@ __device__ inline void flushP2P(const Idx& plst, int n, const GravLists& L, cons
             // + {m,h,h^2,0} pair is read as b96 + half a read2_b64: 8-cycle instructions on a shared LDS)
             L.sxm[lane]                            = make_float4(Pn.x, Pn.y, Pn.z, Qn.x);
             reinterpret_cast<float*>(L.sxm + 64)[lane] = Qn.y;
+            ++T.nValu;
         }
         jN = jNN;
         jNN = c0 + 128 + lane < n ? plst(c0 + 128 + lane) : plst(0);
@@ -893,18 +912,14 @@ __device__ inline void flushP2P(const Idx& plst, int n, const GravLists& L, cons
         const int nsb = (cnt + 15) >> 4;
         for (int sb = 0; sb < nsb; ++sb)
         {
-            float4 Pa = L.spos[sb * 16 + (lane & 15)];
-            float4 Qa = L.smh[sb * 16 + (lane & 15)];
-            float aR  = kq == 0 ? Pa.x : (kq == 1 ? Pa.y : (kq == 2 ? Pa.z : 1.f));
-            float aH  = kq == 0 ? Qa.z : (kq == 1 ? Qa.y : (kq == 2 ? 1.f : 0.f));
+            const float2 ab = L.sab[kq * kAbRow + sb * 16 + (lane & 15)];
+            const float aR  = ab.x, aH = ab.y;
             float4 Pr[4];
-            float mr[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-            {
                 Pr[r] = L.spos[sb * 16 + 4 * kq + r];
-                mr[r] = L.smh[sb * 16 + 4 * kq + r].x;
-            }
+            const float4 m4   = reinterpret_cast<const float4*>(L.sm)[sb * 4 + kq];
+            const float mr[4] = {m4.x, m4.y, m4.z, m4.w};
             const f32x4 cR  = {Pr[0].w, Pr[1].w, Pr[2].w, Pr[3].w};
             const f32x4 c0v = {0.f, 0.f, 0.f, 0.f};
 #ifndef SPHX_P2P_NOPIPE
@@ -1055,7 +1070,8 @@ __device__ __forceinline__ void gravityStore(int64_t g, int64_t first, int64_t l
     if (laneId() == 0)
     {
         // stats: [0] sum of P2P per target, [1] failed groups, [2] sum of M2P, [3] max P2P, [4] max M2P,
-        //        [5] groups queued for the fused global-stack kernel, [6]/[7] slab demand (leaves / M2P nodes)
+        //        [5] groups queued for the fused global-stack kernel, [6]/[7] slab demand (leaves / M2P nodes),
+        //        [8] P2P chunks on MFMA | VALU tiles << 32 (P2P kernel)
         auto nv = (unsigned long long)(min(int64_t(64), last - (first + g * 64)));
         atomicAdd(&stats[0], totP2P * nv);
         atomicAdd(&stats[2], totM2P * nv);
@@ -1145,12 +1161,14 @@ struct GravLds
 {
     int32_t mlst[kGM2P];
     int32_t plst[kGP2P];
-    float4 stage[3 * 64]; // P2P tile (2 x 64) or M2P batch (3 x 64)
+    float4 stage[64 + 2 * kAbRow + 16]; // P2P tile (positions | k-major A operands | masses) or M2P batch (3 x 64)
 };
 
 __device__ __forceinline__ GravLists listsOf(GravLds& s)
 {
-    return GravLists{s.mlst, s.plst, s.stage, s.stage + 64, s.stage}; // VALU tile aliases the MFMA tile
+    // the VALU tile aliases the MFMA tile
+    return GravLists{s.mlst, s.plst, s.stage, reinterpret_cast<float2*>(s.stage + 64),
+                     reinterpret_cast<float*>(s.stage + 64 + 2 * kAbRow), s.stage};
 }
 
 //! @brief global-memory interaction list slabs: per group capM node ids and capL leaf ids + 2 counts (-1: fallback)
@@ -1605,6 +1623,8 @@ __global__ __launch_bounds__(256, SPHX_P2P_WAVES) void gravityP2PKernel(int64_t 
             }
         }
         p2pFinish(T, acc);
+        // [8]: chunks on the MFMA tile (low 32 bits) / on the VALU fallback (high 32 bits)
+        if (lane == 0) atomicAdd(&stats[8], (unsigned long long)T.nMfma | ((unsigned long long)T.nValu << 32));
         unsigned long long totP2P = (unsigned long long)np;
         gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, totP2P, 0ull, upot, pacc);
     }

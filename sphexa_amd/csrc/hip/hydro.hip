@@ -906,7 +906,7 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
     }
     else
     {
-        const QFrame q = qframeOf(box);
+        const QFrame q = qframeOf(box, sc.fixedPoint);
         packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    { packPosQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, m, q, (SrcPosQ*)rec); });
         xmassQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec, wh, xm,
@@ -923,7 +923,7 @@ void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
     if (a.last <= a.first) return;
     if (mUniform > 0.f && sc.fixedPoint)
     {
-        const QFrame q = qframeOf(box);
+        const QFrame q = qframeOf(box, sc.fixedPoint);
         packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    { packXmQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, xm, q, (SrcXmQ*)rec); });
         veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcXmQ*)rec, wh, whd, kx,
@@ -991,7 +991,7 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
     }
     else
     {
-        const QFrame q = qframeOf(box);
+        const QFrame q = qframeOf(box, sc.fixedPoint);
         packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    {
                        packIadQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, kx, vx, vy, vz, xm, q,
@@ -1028,7 +1028,7 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
     }
     else if (avS)
     {
-        const QFrame q = qframeOf(box);
+        const QFrame q = qframeOf(box, sc.fixedPoint);
         packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    {
                        packAvVKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, kx, vx, vy, vz, xm, c, divv,
@@ -1039,7 +1039,7 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
     }
     else
     {
-        const QFrame q = qframeOf(box);
+        const QFrame q = qframeOf(box, sc.fixedPoint);
         packAvQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, c, q, (SrcAvQ*)rec);
         avSwitchesQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, cc, (const SrcAvQ*)rec, divv, wh, dt,
                                                       alpha);
@@ -1065,7 +1065,7 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
     }
     else
     {
-        const QFrame q = qframeOf(box);
+        const QFrame q = qframeOf(box, sc.fixedPoint);
         // (the gradient records of AV cleaning are packed here: no hand-off then)
         packRanges(gv ? 0 : inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    { packMomQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, f, q, (SrcMomQ*)rec, gv); });

@@ -18,6 +18,7 @@
  */
 #pragma once
 
+#include <cmath>
 #include <cstddef>
 #include <cstdint>
 
@@ -56,8 +57,9 @@ struct SphConsts
     unsigned ngmax;
     float sincIndex;  // exponent n of the sinc^n kernel
     int kernelChoice; // 0: sinc^n, 1: 0.9 sinc^4 + 0.1 sinc^9
-    int fixedPoint;   // GPU pair loops may read fixed-point (QFrame) records: set when the coordinate quantum is
-                      // <= 2^-18 of the smallest h (ops/hydro.py: fixed_point_ok), else fp64-coordinate records
+    int fixedPoint;   // GPU pair loops may read fixed-point (QFrame) records: nonzero when the coordinate quantum
+                      // is <= 2^-22 of the smallest h; bits 1.. hold the frame shifts (qframeOf, ops/hydro.py:
+                      // fixed_point_code), else fp64-coordinate records
 };
 
 //! @brief linear interpolation in a table sampled on [0, 2]
@@ -333,19 +335,30 @@ struct QFrame
     float inv[3];       // separation = int32(offset_i - offset_j) * inv
 };
 
-inline QFrame qframeOf(const Box& b)
+/*! @brief frame of the pair loops: SphConsts::fixedPoint = 1 | shift_x << 1 | shift_y << 6 | shift_z << 11 (0: fp64
+ *         records). A shift of k multiplies the scale by 2^k: offsets then wrap with period P = L / 2^k (periodic) or
+ *         2L / 2^k (open). The wrapping int32 difference is still the exact separation of every pair closer than P/2,
+ *         and the pair loops only evaluate pairs within 2 h_i: the host picks the largest shifts with P/2 > 2 h_max
+ *         (ops/hydro.py fixed_point_code), so a box whose smallest h is far below its extent (a collapsing cloud)
+ *         keeps 32-bit records with quanta of P/2^32 instead of L/2^31. Periodic images move an offset by a multiple
+ *         of 2^32 (L is 2^k periods), so the wrapped difference stays the minimum image. The neighbor search needs
+ *         the unwrapped box frame (candidates lie farther than 2h) and always uses shift 0 (code 1).
+ */
+inline QFrame qframeOf(const Box& b, int code = 1)
 {
     QFrame q;
     for (int d = 0; d < 3; ++d)
     {
-        const double L = b.len(d) > 0 ? b.len(d) : 1.0;
-        q.lo[d]        = b.lo[d];
-        q.s[d]         = (b.periodic(d) ? 4294967296.0 : 2147483648.0) / L;
-        q.inv[d]       = float(1.0 / q.s[d]);
+        const double L   = b.len(d) > 0 ? b.len(d) : 1.0;
+        const int shift  = (code >> (1 + 5 * d)) & 31;
+        q.lo[d]          = b.lo[d];
+        q.s[d]           = std::ldexp(1.0, (b.periodic(d) ? 32 : 31) + shift) / L;
+        q.inv[d]         = float(1.0 / q.s[d]);
     }
     return q;
 }
 
+//! offset modulo 2^32 ((v - lo) * s stays below 2^52 for shifts <= 20, ops/hydro.py MAX_FRAME_SHIFT)
 SPHX_HD uint32_t quantize(double v, double lo, double s)
 {
     return uint32_t((unsigned long long)(long long)rint((v - lo) * s));

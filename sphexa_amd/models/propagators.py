@@ -171,9 +171,10 @@ class Propagator:
     def _apply_host(self, d, domain, vals, pend, has_checks):
         dt = vals[0]
         d.minDtCourant, d.minDtRho = vals[1], vals[2]
-        k = 3 + 10 * len(pend)
+        nv = pend[0].NVALS if pend else 0
+        k = 3 + nv * len(pend)
         if pend:
-            self.gravity.finish(d, [vals[3 + 10 * i: 3 + 10 * (i + 1)] for i in range(len(pend))])
+            self.gravity.finish(d, [vals[3 + nv * i: 3 + nv * (i + 1)] for i in range(len(pend))])
         if has_checks:
             domain.finish_checks(vals[k:])
         d.ttot += dt

@@ -102,14 +102,17 @@ def _pinned_total() -> torch.Tensor:
 
 class GravityPending:
     """statistics and energy of a GPU gravity evaluation still on the device (compute_gravity(defer=True)): the
-    caller brings ``dev`` (float64 [10]) to the host with other per-step values and calls ``finish``"""
+    caller brings ``dev`` (float64 [NVALS]) to the host with other per-step values and calls ``finish``"""
+
+    NSTATS = 9   # int64 statistics of the kernels (gravity.hip gravityStore)
+    NVALS = 11   # statistics + energy
 
     def __init__(self, dev, groups: int, caps, stats, device):
         self.dev, self.groups, self.caps, self.stats, self.device = dev, groups, caps, stats, device
 
     def finish(self, vals) -> float:
-        st = [int(v) for v in vals[:8]]  # exact: counts below 2^53
-        energy = float(vals[8])
+        st = [int(v) for v in vals[:self.NSTATS]]  # exact: counts below 2^53
+        energy = float(vals[self.NSTATS])
         if TEST_CAPS is None and st[5] > 0:
             # groups fell back to the (slow, serial) fused kernel: grow the slabs to the observed demand while the
             # slab memory stays below ~6% of the device (it is 4 B x groups x (capM + capL))
@@ -119,7 +122,8 @@ class GravityPending:
             if 4 * self.groups * (cm + cl) <= budget:
                 _CAPS["m"], _CAPS["l"] = cm, cl
         if self.stats is not None:
-            self.stats.update(p2p=st[0], m2p=st[2], max_p2p=st[3], max_m2p=st[4], fallback=st[5], caps=self.caps)
+            self.stats.update(p2p=st[0], m2p=st[2], max_p2p=st[3], max_m2p=st[4], fallback=st[5], caps=self.caps,
+                              p2p_mfma_chunks=st[8] & 0xFFFFFFFF, p2p_valu_chunks=st[8] >> 32)
         if st[1] > 0:
             raise RuntimeError(f"gravity traversal stack overflow in {st[1]} groups")
         return energy
@@ -134,8 +138,9 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         return 0.0
     if x.is_cuda:
         hp = _lib.hip()
-        zb = torch.zeros(10, dtype=torch.int64, device=x.device)  # one fill: statistics (int64) + energy (float64)
-        st_dev, out = zb[:8], zb[8:].view(torch.float64)
+        # one fill: statistics (int64) + energy (float64)
+        zb = torch.zeros(GravityPending.NVALS, dtype=torch.int64, device=x.device)
+        st_dev, out = zb[:GravityPending.NSTATS], zb[GravityPending.NSTATS:].view(torch.float64)
         from .neighbors import _scratch
 
         cap_m, cap_l = TEST_CAPS if TEST_CAPS is not None else (_CAPS["m"], _CAPS["l"])

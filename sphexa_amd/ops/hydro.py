@@ -148,7 +148,8 @@ def compute_xmass(d, nl: NeighborList, box: Box, out_field: str = "xm"):
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d[out_field].data_ptr())
     if _is_gpu(d):
         ho = _handoff(d)
-        posq = handoff_take(d, "posq_all") and bool(d.fixedPoint)
+        # the search's SrcPosQ records are in the unshifted box frame (code 1)
+        posq = handoff_take(d, "posq_all") and d.fixedPoint == 1
         # the VE chain: XMass writes Gradh's fixed-point records of its targets (uniform mass: the SrcXmQ path)
         out = _recB(d).data_ptr() if (out_field == "xm" and d.fixedPoint and uniform_mass(d) > 0) else 0
         ho.clear()
@@ -164,53 +165,65 @@ def compute_density(d, nl: NeighborList, box: Box):
     compute_xmass(d, nl, box, out_field="rho")
 
 
-# fixed-point records: the coordinate quantum (box length / 2^32 periodic, / 2^31 open) must stay below this
+# fixed-point records: the coordinate quantum (wrap period / 2^32, sph_math.hpp qframeOf) must stay below this
 # fraction of the SMALLEST h. The wrapping int32 difference of two records is exact up to one quantum per component,
 # then rounded once to fp32, so a separation carries <= 2^-22 h_min of error: within 2-4x of the reference's fp32
 # rounding of its fp64 difference at the kernel support of the smallest particle (2^-24 |dx|, |dx| < 2h) and below
-# it for every particle with h >= 4 h_min (sph_math.hpp QFrame). Boxes/h that fail the bound switch the loops to
-# fp64-coordinate records: Evrard's open, collapsing cloud does; periodic lattices down to h ~ 1e-3 L do not.
+# it for every particle with h >= 4 h_min (sph_math.hpp QFrame). The wrap period of each dimension is the box length
+# divided by the largest power of two (the frame shift) that keeps every pair within 2 h_max unambiguous: half a
+# period must exceed FRAME_PAIR_MARGIN * 2 h_max. A collapsing cloud (Evrard: h_min ~ 1e-3 of the box) thus keeps
+# the 32-bit records; boxes/h that fail even then use fp64-coordinate records.
 FIXED_POINT_REL_QUANTUM = 2.0 ** -22
+FRAME_PAIR_MARGIN = 1.125
+MAX_FRAME_SHIFT = 20
 
 
 def invalidate_h_cache(d):
     """h was rewritten by a native kernel (h iteration, h update) or replaced by the domain sync"""
     d._h_min = None
     d._h_min_global = None
+    d._h_max_global = None
+
+
+_SIGNS = {}
 
 
 def global_h_min_device(d, comm) -> torch.Tensor:
-    """[min h, min m, -max m] over all ranks as a float64 device tensor (no host copy; see set_global_h_min); on one
-    rank the reduction's own [min h, max h, min m, max m] (no further launches)"""
+    """[min h, max h, min m, max m] over all ranks as a float64 device tensor (no host copy; see set_global_h_min); on
+    one rank the reduction's own output (no further launches), on several one MIN allreduce of [min h, -max h, min m,
+    -max m] and a sign flip"""
     h = d["h"][: d.size]
     m = d["m"][: d.size]
+    multi = comm is not None and comm.size > 1
     if h.numel():
         from .reduce import min_max
 
         mm = min_max([h, m])  # [min h, max h, min m, max m], one launch on the GPU
-        if comm is None or comm.size == 1:
+        if not multi:
             return mm
-        loc = torch.stack([mm[0], mm[2], -mm[3]])
+        sg = _SIGNS.get(h.device)
+        if sg is None:
+            sg = _SIGNS[h.device] = torch.tensor([1.0, -1.0, 1.0, -1.0], dtype=torch.float64, device=h.device)
+        loc = mm * sg
     else:
-        loc = torch.full((3,), math.inf, dtype=torch.float64, device=h.device)
-    if comm is not None and comm.size > 1:
+        loc = torch.full((4,), math.inf, dtype=torch.float64, device=h.device)
+        sg = torch.tensor([1.0, -1.0, 1.0, -1.0], dtype=torch.float64, device=h.device)
+    if multi:
         comm.allreduce(loc, "min")
+        loc = loc * sg
     return loc
 
 
 def apply_global_h_min(d, vals):
-    """store the host values of global_h_min_device: the per-step h minimum of the fixed-point guard and the
-    uniform-mass cache keyed on the current mass tensor"""
-    vals = [float(v) for v in vals]
-    if len(vals) == 4:  # one rank: [min h, max h, min m, max m]
-        hmin, mlo, mhi = vals[0], vals[2], vals[3]
-    else:
-        hmin, mlo, mhi = vals[0], vals[1], -vals[2]
+    """store the host values of global_h_min_device ([min h, max h, min m, max m]): the per-step h extremes of the
+    fixed-point guard and frame, and the uniform-mass cache keyed on the current mass tensor"""
+    hmin, hmax, mlo, mhi = (float(v) for v in vals)
     m = d["m"][: d.size]
     d._h_min_global = hmin
+    d._h_max_global = hmax
     val = mlo if (mlo == mhi and mlo > 0) else 0.0
     d._m_uniform = ((m.data_ptr(), m.numel(), m._version), val)
-    d._spec_prev = (hmin, val)  # the decisions of the next step's speculative first loop (speculate_loop)
+    d._spec_prev = (hmin, hmax, val)  # the decisions of the next step's speculative first loop (speculate_loop)
 
 
 def speculate_loop(d, box: Box, run):
@@ -222,14 +235,14 @@ def speculate_loop(d, box: Box, run):
     if prev is None:
         return None
     m = d["m"][: d.size]
-    d._h_min_global = prev[0]
-    d._m_uniform = ((m.data_ptr(), m.numel(), m._version), prev[1])
+    d._h_min_global, d._h_max_global = prev[0], prev[1]
+    d._m_uniform = ((m.data_ptr(), m.numel(), m._version), prev[2])
     run()
-    return bool(d.fixedPoint), uniform_mass(d) > 0
+    return d.fixedPoint, uniform_mass(d) > 0
 
 
 def speculation_holds(d, box: Box, spec) -> bool:
-    return spec is not None and spec == (fixed_point_ok(d, box), uniform_mass(d) > 0)
+    return spec is not None and spec == (fixed_point_code(d, box), uniform_mass(d) > 0)
 
 
 def set_global_h_min(d, comm):
@@ -239,39 +252,78 @@ def set_global_h_min(d, comm):
     apply_global_h_min(d, global_h_min_device(d, comm).tolist())
 
 
-def quantum(box: Box) -> float:
-    q = 0.0
-    for L, bc in zip(box.lengths(), box.bc):
+def frame_code(box: Box, hmin: float, hmax: float) -> int:
+    """SphConsts::fixedPoint of the pair loops for these h extremes (sph_math.hpp qframeOf): 0 for fp64 records,
+    else 1 | shift_x << 1 | shift_y << 6 | shift_z << 11 with, per dimension, the largest shift whose wrap period
+    P = L / 2^k (periodic) or 2L / 2^k (open) keeps P / 2 > FRAME_PAIR_MARGIN * 2 h_max, provided the quantum P / 2^32
+    is <= FIXED_POINT_REL_QUANTUM * h_min. Also rejects boxes too small for an unambiguous wrap at shift 0 (open
+    extent L <= 2 h_max * margin: the pair at lo and hi would wrap)."""
+    if not (hmin > 0) or not math.isfinite(hmax):
+        return 0
+    need = FRAME_PAIR_MARGIN * 2.0 * max(hmax, hmin)  # half a period must exceed this
+    code = 1
+    for k, (L, bc) in enumerate(zip(box.lengths(), box.bc)):
         L = L if L > 0 else 1.0
-        q = max(q, L / (2.0 ** 32 if bc == PERIODIC else 2.0 ** 31))
+        P0 = L if bc == PERIODIC else 2.0 * L
+        if P0 / 2.0 <= need:
+            return 0
+        shift = min(MAX_FRAME_SHIFT, int(math.floor(math.log2(P0 / (2.0 * need)))))
+        while shift > 0 and P0 / 2.0 ** (shift + 1) <= need:
+            shift -= 1
+        if P0 / 2.0 ** shift / 2.0 ** 32 > FIXED_POINT_REL_QUANTUM * hmin:
+            return 0
+        code |= shift << (1 + 5 * k)
+    return code
+
+
+def quantum(box: Box, code: int = 1) -> float:
+    """largest coordinate quantum of the fixed-point frame ``code`` (sph_math.hpp qframeOf)"""
+    q = 0.0
+    for k, (L, bc) in enumerate(zip(box.lengths(), box.bc)):
+        L = L if L > 0 else 1.0
+        shift = (code >> (1 + 5 * k)) & 31
+        q = max(q, L / 2.0 ** ((32 if bc == PERIODIC else 31) + shift))
     return q
 
 
-def fixed_point_ok(d, box: Box) -> bool:
-    """Whether the GPU pair loops may read fixed-point coordinate records (QFrame, sph_math.hpp) for this box and
-    these smoothing lengths; otherwise they read fp64-coordinate records. Uses the per-step global minimum of h when
-    the propagator has set one (set_global_h_min), else the local minimum cached on the identity and version of h."""
+def _h_extremes(d):
     hmin = getattr(d, "_h_min_global", None)
-    if hmin is None:
+    hmax = getattr(d, "_h_max_global", None)
+    if hmin is None or hmax is None:
         h = d["h"][: d.size]
         key = (h.data_ptr(), h.numel(), h._version)
         hit = getattr(d, "_h_min", None)
         if hit is None or hit[0] != key:
-            hit = (key, float(h.min()) if h.numel() else 0.0)
+            ext = torch.stack(torch.aminmax(h)).tolist() if h.numel() else [0.0, 0.0]
+            hit = (key, float(ext[0]), float(ext[1]))
             d._h_min = hit
-        hmin = hit[1]
-    ok = hmin > 0 and quantum(box) <= FIXED_POINT_REL_QUANTUM * hmin
+        hmin, hmax = hit[1], hit[2]
+    return hmin, hmax
+
+
+def fixed_point_code(d, box: Box) -> int:
+    """The frame code of the GPU pair loops (frame_code) for this box and these smoothing lengths: 0 = fp64-coordinate
+    records. Uses the per-step global h extremes when the propagator has set them (set_global_h_min), else the local
+    ones cached on the identity and version of h."""
+    hmin, hmax = _h_extremes(d)
+    code = frame_code(box, hmin, hmax)
+    ok = code != 0
     prev = getattr(d, "fixedPointPath", None)
     if prev is not None and prev != ok:
         d.fixedPointSwitches = getattr(d, "fixedPointSwitches", 0) + 1
     d.fixedPointPath = ok
-    return ok
+    return code
+
+
+def fixed_point_ok(d, box: Box) -> bool:
+    """Whether the GPU pair loops may read fixed-point coordinate records (QFrame, sph_math.hpp)"""
+    return fixed_point_code(d, box) != 0
 
 
 def _consts(d, box: Box):
-    """SphConsts array of a pair loop, with the fixed-point switch of the GPU path decided for this box"""
+    """SphConsts array of a pair loop, with the fixed-point frame of the GPU path decided for this box"""
     if _is_gpu(d):
-        d.fixedPoint = 1 if fixed_point_ok(d, box) else 0
+        d.fixedPoint = fixed_point_code(d, box)
     return d.consts_array()
 
 

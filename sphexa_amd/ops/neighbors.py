@@ -178,6 +178,7 @@ ALLOW_NC_FAIL = os.environ.get("SPHX_ALLOW_NC_FAIL") == "1"
 def _check_convergence(d, fails: int):
     d._h_min = None  # the h iteration rewrote h in place (ops/hydro.py caches its minimum)
     d._h_min_global = None
+    d._h_max_global = None
     d.nc_fail = int(fails)
     if fails > 0 and not ALLOW_NC_FAIL:
         raise NeighborSearchError(f"coupled nc/h iteration failed to converge ({fails} particles on the CPU path, target groups on the GPU) "

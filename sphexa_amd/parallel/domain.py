@@ -211,6 +211,7 @@ class Domain:
         # cached per-step reductions of h and m so the pair loops re-derive them for the new particle set
         d._h_min = None
         d._h_min_global = None
+        d._h_max_global = None
         d._m_uniform = None
 
         all_keys = d["keys"]

@@ -149,7 +149,7 @@ def test_two_ranks_one_gpu_let_gravity_vs_direct():
     np.fill_diagonal(w, 0.0)
     ref = (w[:, :, None] * d).sum(1)
     err = np.sort(np.linalg.norm(acc - ref, axis=1) / np.linalg.norm(ref, axis=1))
-    assert err[int(0.01 * n)] < 1e-3 and err[-1] < 3e-2
+    assert err[int(0.99 * n)] < 1e-3 and err[-1] < 3e-2, (err[int(0.99 * n)], err[-1])
     assert sorted(map(tuple, np.round(pos, 12))) == sorted(map(tuple, np.round(X, 12)))
 
 

@@ -1,5 +1,7 @@
 """CPU tier: the switch between fixed-point and fp64-coordinate records of the GPU pair loops (ops/hydro.py)."""
 
+import numpy as np
+import pytest
 import torch
 
 from sphexa_amd.ops import hydro as H
@@ -16,16 +18,66 @@ class _D:
         return self._h
 
 
+def _shifts(code):
+    return [(code >> (1 + 5 * k)) & 31 for k in range(3)]
+
+
 def test_fixed_point_guard():
     d = _D(torch.full((4,), 4e-3, dtype=torch.float32))
     assert H.FIXED_POINT_REL_QUANTUM <= 2.0 ** -22
     assert H.fixed_point_ok(d, Box([0.0] * 3, [1.0] * 3, [PERIODIC] * 3))
-    # open dimensions use 2^31 steps (the box is the particles' bounding box): 2 / 2^31 = 9.3e-10 <= 2^-22 * 4e-3
-    assert H.fixed_point_ok(d, Box([0.0] * 3, [2.0] * 3, [OPEN] * 3))
-    assert not H.fixed_point_ok(d, Box([0.0] * 3, [2.1] * 3, [OPEN] * 3))
-    # periodic dimensions use the full 2^32 range
-    assert H.fixed_point_ok(d, Box([0.0] * 3, [4.0] * 3, [PERIODIC] * 3))
-    assert not H.fixed_point_ok(d, Box([0.0] * 3, [4.2] * 3, [PERIODIC] * 3))
+    # the wrap period shrinks by powers of two while half of it exceeds 1.125 * 2 h_max = 9e-3:
+    # periodic L = 1 -> 1/32 (shift 5), open L = 1 -> 2/64 (shift 6), open L = 2.1 -> 4.2/128 (shift 7)
+    assert _shifts(H.fixed_point_code(d, Box([0.0] * 3, [1.0] * 3, [PERIODIC] * 3))) == [5] * 3
+    assert _shifts(H.fixed_point_code(d, Box([0.0] * 3, [1.0] * 3, [OPEN] * 3))) == [6] * 3
+    assert _shifts(H.fixed_point_code(d, Box([0.0] * 3, [2.1] * 3, [OPEN] * 3))) == [7] * 3
+    assert _shifts(H.fixed_point_code(d, Box([0.0, 0.0, 0.0], [1.0, 2.1, 0.5], [PERIODIC, OPEN, OPEN]))) == [5, 7, 5]
+    # boxes too small for an unambiguous wrap at shift 0 (an open pair at lo and hi would flip sign)
+    assert H.fixed_point_code(d, Box([0.0] * 3, [0.008] * 3, [OPEN] * 3)) == 0
+    assert H.fixed_point_code(d, Box([0.0] * 3, [0.017] * 3, [PERIODIC] * 3)) == 0
+    # a small h_min against a large h_max: the quantum of the period that h_max needs is too coarse -> fp64
+    assert H.frame_code(Box([0.0] * 3, [1.0] * 3, [OPEN] * 3), 1e-6, 1e-2) == 0
+    assert H.frame_code(Box([0.0] * 3, [1.0] * 3, [OPEN] * 3), 1e-4, 1e-2) != 0
+
+
+def _wrap_sep(code, box, xi, xj):
+    """the GPU pair separation of two fixed-point records (sph_math.hpp quantize + pairSep), emulated in int64"""
+    out = []
+    for k, (lo, L, bc) in enumerate(zip(box.lo, box.lengths(), box.bc)):
+        sh = (code >> (1 + 5 * k)) & 31
+        sc = 2.0 ** ((32 if bc == PERIODIC else 31) + sh) / L
+        oi = np.rint((xi[:, k] - lo) * sc).astype(np.int64) & 0xFFFFFFFF
+        oj = np.rint((xj[:, k] - lo) * sc).astype(np.int64) & 0xFFFFFFFF
+        d = (oi - oj) & 0xFFFFFFFF
+        d = np.where(d >= 2 ** 31, d - 2 ** 32, d)
+        out.append(d / sc)
+    return np.stack(out, 1)
+
+
+@pytest.mark.parametrize("bc", [OPEN, PERIODIC])
+def test_shifted_frame_separations_are_exact_minimum_images(bc):
+    """every pair within 2 h_max: the wrapped 32-bit difference in the shifted frame is the (minimum-image)
+    separation up to one quantum per component, for pairs anywhere in the box, across the periodic seam included"""
+    rng = np.random.default_rng(3)
+    box = Box([-1.0, -0.5, 0.25], [1.0, 0.7, 0.6], [bc] * 3)
+    hmax = 0.01
+    code = H.frame_code(box, 2e-3, hmax)
+    assert code != 0 and min(_shifts(code)) > 0
+    n = 200000
+    lo, L = np.array(box.lo), np.array(box.lengths())
+    xi = lo + rng.random((n, 3)) * L
+    dx = rng.normal(size=(n, 3))
+    dx *= (2 * hmax * rng.random(n) ** (1 / 3) / np.linalg.norm(dx, axis=1))[:, None]
+    xj = xi - dx
+    if bc == PERIODIC:
+        xj = lo + np.mod(xj - lo, L)  # sources wrapped into the box: the pair crosses the seam
+    else:
+        keep = np.all((xj >= lo) & (xj <= lo + L), axis=1)
+        xi, xj, dx = xi[keep], xj[keep], dx[keep]
+    sep = _wrap_sep(code, box, xi, xj)
+    q = H.quantum(box, code)
+    assert np.abs(sep - dx).max() <= 1.01 * q
+    assert q <= H.FIXED_POINT_REL_QUANTUM * 2e-3
 
 
 def test_fixed_point_guard_tracks_h_updates():

@@ -45,38 +45,52 @@ def test_gpu_h_iteration_failure_raises(gpu, monkeypatch):
 
 
 def _evrard_step(gpu, force):
+    """one Evrard step; ``force``: None (natural frame), or the frame code every pair loop takes (0: fp64 records,
+    1: unshifted 32-bit box frame)"""
     from sphexa_amd.app.simulation import Simulation
 
     sim = Simulation("evrard", n=40, device=gpu)
-    hmin = float(sim.d["h"][: sim.d.size].min())
-    natural = (H.fixed_point_ok(sim.d, sim.domain.box), H.quantum(sim.domain.box) / hmin)
+    h = sim.d["h"][: sim.d.size]
+    natural = H.frame_code(sim.domain.box, float(h.min()), float(h.max()))
     if force is not None:
-        H_orig = H.fixed_point_ok
-        H.fixed_point_ok = lambda d, box: force
+        orig = H.fixed_point_code
+        H.fixed_point_code = lambda d, box: force
     try:
         sim.step()
+        code = sim.d.fixedPoint
     finally:
         if force is not None:
-            H.fixed_point_ok = H_orig
+            H.fixed_point_code = orig
     s, e = sim.domain.start_index(), sim.domain.end_index()
-    return natural, {f: sim.d[f][s:e].double().cpu() for f in ("ax", "ay", "du", "alpha", "h")}
+    return natural, code, {f: sim.d[f][s:e].double().cpu() for f in ("ax", "ay", "az", "du", "alpha", "h")}
 
 
-def test_evrard_takes_fp64_records_and_fixed_point_stays_close(gpu):
-    (natural, ratio), ref = _evrard_step(gpu, None)
-    print(f"Evrard n=40: quantum / hmin = {ratio:.3e} (2^{__import__('math').log2(ratio):.1f}), "
-          f"natural path {'fixed-point' if natural else 'fp64'}")
-    assert natural == (ratio <= H.FIXED_POINT_REL_QUANTUM)
-    _, fx = _evrard_step(gpu, True)
-    _, f64 = _evrard_step(gpu, False)
-    for f in ref:
-        # the natural path is one of the two (equal up to atomics ordering in the gravity sums)
-        other = fx if natural else f64
-        assert (ref[f] - other[f]).abs().max().item() <= 1e-6 * ref[f].abs().max().item(), f
-    for f, tol in (("ax", 2e-4), ("ay", 2e-4), ("du", 2e-4), ("alpha", 1e-5)):
+def test_evrard_frame_shift_keeps_fixed_point_records(gpu):
+    """Evrard's collapsing cloud: the unshifted box frame (quanta of L/2^31) is too coarse for its smallest h, the
+    shifted frame (wrap period L/2^k > 4.5 h_max, sph_math.hpp qframeOf) is not: the pair loops keep the 32-bit
+    records, and their forces match the fp64-coordinate records"""
+    natural, code, ref = _evrard_step(gpu, None)
+    shifts = [(natural >> (1 + 5 * k)) & 31 for k in range(3)]
+    print(f"Evrard n=40: frame code {natural:#x}, shifts {shifts}")
+    assert natural != 0 and code == natural and min(shifts) > 0
+    _, c64, f64 = _evrard_step(gpu, 0)
+    assert c64 == 0
+    for f, tol in (("ax", 2e-6), ("ay", 2e-6), ("az", 2e-6), ("du", 2e-6), ("alpha", 1e-6)):
         scale = max(f64[f].abs().max().item(), 1e-30)  # du is 0 on the first step of the cloud at rest
+        err = (ref[f] - f64[f]).abs().max().item() / scale
+        print(f"shifted fixed-point vs fp64 records, {f}: max |diff| / max |fp64| = {err:.3e}")
+        assert err < tol, (f, err)
+
+
+def test_evrard_unshifted_frame_stays_close(gpu):
+    """the unshifted box frame, forced below its quantum bound, is still within fp32-level distance of fp64"""
+    _, c1, fx = _evrard_step(gpu, 1)
+    _, _, f64 = _evrard_step(gpu, 0)
+    assert c1 == 1
+    for f, tol in (("ax", 2e-4), ("ay", 2e-4), ("du", 2e-4), ("alpha", 1e-5)):
+        scale = max(f64[f].abs().max().item(), 1e-30)
         err = (fx[f] - f64[f]).abs().max().item() / scale
-        print(f"fixed-point vs fp64 records, {f}: max rel err {err:.3e}")
+        print(f"unshifted fixed-point vs fp64 records, {f}: max rel err {err:.3e}")
         assert err < tol, (f, err)
 
 

@@ -258,8 +258,8 @@ def test_uniform_mass_detection(gpu):
 
 def test_ve_step_fp64_records_matches_cpu(gpu, monkeypatch):
     """fp64-coordinate record path of the GPU pair loops (taken when the fixed-point quantum is too coarse for the
-    smallest h, ops/hydro.py: fixed_point_ok)"""
-    monkeypatch.setattr(H, "fixed_point_ok", lambda d, box: False)
+    smallest h, ops/hydro.py: fixed_point_code)"""
+    monkeypatch.setattr(H, "fixed_point_code", lambda d, box: 0)
     results = {}
     for dev in ("cpu", gpu):
         d = P.ParticlesData(dev)

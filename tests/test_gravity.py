@@ -1,5 +1,7 @@
 """Barnes-Hut gravity vs direct sum (reference ryoanji/test: traversal_cpu.cpp, interface/global_forces_gpu.cpp
-thresholds: 1st-percentile relative acceleration error < 1e-3, max < 3e-2, potential relative error < 1e-2)."""
+thresholds: the 99th percentile of the ascending relative acceleration errors, errors[size * 0.99], < 1e-3 at
+theta 0.5 (interface/global_forces_gpu.cpp:171,181) and < 3e-3 at theta 0.6 (nbody/traversal_cpu.cpp:150), max < 3e-2,
+potential relative error < 1e-2)."""
 
 import numpy as np
 import pytest
@@ -43,8 +45,9 @@ def _errors(a_bh, a_ref):
     return np.sort(num / den)
 
 
-@pytest.mark.parametrize("theta", [0.5, 0.75])
-def test_bh_vs_direct_cpu(theta):
+# (theta, p99 gate): the reference's two gates; theta 0.75 is not gated by the reference (measured p99 3.0e-3)
+@pytest.mark.parametrize("theta,p99", [(0.5, 1e-3), (0.6, 3e-3), (0.75, 5e-3)])
+def test_bh_vs_direct_cpu(theta, p99):
     n = 6000
     box, ot, x, y, z, m, h = _setup(n)
     centers, mp = G.upsweep(ot, x, y, z, m, box, theta)
@@ -57,7 +60,7 @@ def test_bh_vs_direct_cpu(theta):
     a = np.stack([ax.numpy(), ay.numpy(), az.numpy()], 1).astype(np.float64)
     r = np.stack([rx.numpy(), ry.numpy(), rz.numpy()], 1).astype(np.float64)
     err = _errors(a, r)
-    assert err[int(0.01 * n)] < 1e-3
+    assert err[int(0.99 * n)] < p99, err[int(0.99 * n)]
     assert err[-1] < 3e-2
     assert abs(eg - egd) / abs(egd) < 1e-2
 
@@ -98,7 +101,7 @@ def test_gravity_gpu_matches_cpu(gpu):
     G.direct_sum(0, n, xg, yg, zg, hg, mg, 1.0, rx, ry, rz)
     d = np.stack([rx.cpu().numpy(), ry.cpu().numpy(), rz.cpu().numpy()], 1).astype(np.float64)
     err = _errors(a.astype(np.float64), d)
-    assert err[int(0.01 * n)] < 1e-3 and err[-1] < 3e-2
+    assert err[int(0.99 * n)] < 1e-3 and err[-1] < 3e-2, (err[int(0.99 * n)], err[-1])
 
 
 @pytest.mark.gpu

@@ -107,7 +107,7 @@ def test_let_gravity_vs_direct(world):
     egd = G.direct_sum(0, N, xt, yt, zt, h, m, 1.0, rx, ry, rz)
     ref = np.stack([rx.numpy(), ry.numpy(), rz.numpy()], 1).astype(np.float64)
     err = np.sort(np.linalg.norm(a - ref, axis=1) / np.linalg.norm(ref, axis=1))
-    assert err[int(0.01 * N)] < 1e-3
+    assert err[int(0.99 * N)] < 1e-3, err[int(0.99 * N)]
     assert err[-1] < 3e-2
     eg = sum(r["egrav"] for r in res)
     assert abs(eg - egd) / abs(egd) < 1e-2
