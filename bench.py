@@ -10,7 +10,9 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
 GPU with torch.distributed.run. W untimed steps, then exactly K timed steps bracketed by barrier + device sync,
 max over ranks, rank 0 prints one JSON line. The whole time step is inside the timed region: domain sync (SFC keys,
 sort, octree, migration, halo discovery + LET), neighbor search with h iteration, the five VE loops, EOS, four halo
-exchanges, gravity (upsweep, traversal, remote multipoles), global dt reduction and the position/energy/h update.
+exchanges, gravity (upsweep, traversal, remote multipoles), global dt reduction, the position/energy/h update and the
+per-iteration conserved quantities of the reference's time loop (sphexa.cpp:150: energies, momenta, neighbor sum,
+globally reduced on the device; their host copy is collected at the next step's first synchronization).
 
 Scaling: the problem size is fixed as N grows -> strong scaling.
 
@@ -152,6 +154,9 @@ def _run_case(init: str, n: int, args, comm, device) -> dict:
     dt = time.perf_counter() - t0
 
     prop.finish_host(d)  # (outside the timed region: the last step's dt, energies and statistics)
+    if rank == 0 and args.verbose:
+        print(f"# conserved after the last step: etot {d.etot:.10g} (ecin {d.ecin:.6g}, eint {d.eint:.6g}, egrav "
+              f"{d.egrav:.6g}), neighbors {d.totalNeighbors}", file=sys.stderr)
     dt = comm.allreduce_scalar(dt, "max", device=device)
     ms = 1000.0 * dt / max(args.steps, 1)
     value = d.numParticlesGlobal * args.steps / dt

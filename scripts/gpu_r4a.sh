@@ -27,3 +27,10 @@ for k, a in agg.items():
           "LDS/wave %.0f" % (a["SQ_INSTS_LDS"] / w), "wait-inst %.2f" % (a["SQ_WAIT_INST_ANY"] / c),
           "valu-active %.2f" % (a["SQ_ACTIVE_INST_VALU"] / c))
 PY
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/e100 -o run -- \
+    python3 bench.py --init evrard -n 100 --steps 5 --warmup 3 > $O/e100.log 2>&1 || { tail -5 $O/e100.log; exit 1; }
+python3 scripts/gpu_busy.py $O/e100/run_kernel_trace.csv 4 > $O/e100_busy.txt; head -3 $O/e100_busy.txt
+python3 scripts/step_sequence.py $O/e100/run_kernel_trace.csv -2 > $O/e100_seq.txt; tail -12 $O/e100_seq.txt
+timeout -k 10 200 python3 scripts/host_profile.py --init evrard -n 100 --steps 20 --top 60 > $O/e100_host.txt 2>&1 \
+    || { tail -5 $O/e100_host.txt; exit 1; }
+grep "ms/step" $O/e100_host.txt

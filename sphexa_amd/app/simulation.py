@@ -46,9 +46,14 @@ class Simulation:
         self.domain = Domain(self.comm, box, bucket_size_focus=bucket_size_focus, bucket_size=bucket, theta=theta)
         self.propagator.sync(self.domain, self.d)
 
-    def step(self):
+    def step(self, observe: bool = True):
+        """one iteration of the reference's time loop (sphexa.cpp:145-174): the propagator step, then the globally
+        reduced conserved quantities (deferred to the next step's first synchronization when the propagator defers
+        its host copies, Propagator.observe)"""
         self.propagator.step(self.domain, self.d)
         _lib.raise_on_device_check(f"iteration {self.d.iteration}")  # SPHX_DEVICE_CHECKS=1 builds only
+        if observe:
+            self.propagator.observe(self.domain, self.d)
         self.d.iteration += 1
 
     def run(self, steps: int):

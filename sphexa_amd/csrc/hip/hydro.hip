@@ -1108,6 +1108,7 @@ void conservedQuantities(int64_t first, int64_t last, const double* x, const dou
                          const float* vx, const float* vy, const float* vz, const float* m, const double* temp,
                          const double* u, const int32_t* nc, double cv, double* out, hipStream_t s)
 {
+    SPHX_CHECK(hipMemsetAsync(out, 0, 10 * sizeof(double), s)); // the sums accumulate atomically
     if (last <= first) return;
     unsigned grid = std::min<unsigned>(gridFor(last - first, 256), 2048);
     conservedKernel<<<grid, 256, 0, s>>>(first, last, x, y, z, vx, vy, vz, m, temp, u, nc, cv, out);

@@ -27,7 +27,8 @@ def local_conserved(d, first: int, last: int) -> torch.Tensor:
     temp = d["temp"] if d.is_allocated("temp") else None
     u = d["u"] if d.is_allocated("u") else None
     nc = d["nc"] if d.is_allocated("nc") else None
-    out = torch.zeros(10, dtype=torch.float64, device=d.device)
+    # (zeroed by the native launchers: no separate fill kernel)
+    out = torch.empty(10, dtype=torch.float64, device=d.device)
     args = (first, last, d["x"].data_ptr(), d["y"].data_ptr(), d["z"].data_ptr(), d["vx"].data_ptr(),
             d["vy"].data_ptr(), d["vz"].data_ptr(), d["m"].data_ptr(), 0 if temp is None else temp.data_ptr(),
             0 if u is None else u.data_ptr(), 0 if nc is None else nc.data_ptr(), cv, out.data_ptr())
@@ -38,16 +39,49 @@ def local_conserved(d, first: int, last: int) -> torch.Tensor:
     return out
 
 
-def compute_conserved_quantities(d, first: int, last: int, comm):
-    q = local_conserved(d, first, last)
-    q[2] = d.egrav
-    comm.allreduce(q, SUM)
-    q = q.cpu().tolist()
-    d.ecin, d.eint, d.egrav = q[0], q[1], q[2]
+def apply_conserved(d, q):
+    """host values of the reduced 10-vector (slot 2 unused: egrav comes from the gravity evaluation)"""
+    d.ecin, d.eint = q[0], q[1]
     d.etot = d.ecin + d.eint + d.egrav
     d.linmom = math.sqrt(q[3] ** 2 + q[4] ** 2 + q[5] ** 2)
     d.angmom = math.sqrt(q[6] ** 2 + q[7] ** 2 + q[8] ** 2)
     d.totalNeighbors = int(q[9])
+
+
+def compute_conserved_quantities(d, first: int, last: int, comm):
+    q = local_conserved(d, first, last)
+    comm.allreduce(q, SUM)
+    apply_conserved(d, q.cpu().tolist())
+
+
+class DeferredConserved:
+    """the per-iteration conserved quantities of the time loop (reference sphexa.cpp:150, conserved_gpu.cu:53-107)
+    without a host synchronization: the device sums and their allreduce are enqueued after the step, the 10-vector
+    goes to pinned host memory asynchronously and is applied when the next step's first synchronization (the neighbor
+    search statistics) has passed, or on demand (``finish``)"""
+
+    def __init__(self):
+        self._host = None
+        self._ev = None
+        self.pending = False
+
+    def enqueue(self, d, first: int, last: int, comm):
+        q = local_conserved(d, first, last)
+        comm.allreduce(q, SUM)
+        if self._host is None:
+            self._host = torch.empty(10, dtype=torch.float64, pin_memory=True)
+            self._ev = torch.cuda.Event()
+        self.finish(d)  # (a previous copy is collected before its buffer is reused)
+        self._host.copy_(q, non_blocking=True)
+        self._ev.record()
+        self.pending = True
+
+    def finish(self, d):
+        if not self.pending:
+            return
+        self._ev.synchronize()
+        self.pending = False
+        apply_conserved(d, self._host.tolist())
 
 
 class TimeAndEnergy:

@@ -47,6 +47,7 @@ class Propagator:
         self.nl = None
         self.gravity = None
         self._host_pending = None
+        self._observed = None
 
     # --------------------------------------------------------------------------------------------- interface
     def conserved_fields(self) -> List[str]:
@@ -183,15 +184,30 @@ class Propagator:
 
     def finish_host(self, d):
         """collect a deferred time-step copy (defer_host): dt, ttot, the Courant/rho minima, gravity energy and
-        statistics, deferred domain checks"""
+        statistics, deferred domain checks; then the deferred conserved quantities of the previous step (observe)"""
         p = self._host_pending
-        if p is None:
-            return
-        self._host_pending = None
-        host, ev, pend, has_checks, domain = p
-        ev.synchronize()
-        d._dt_dev = None
-        self._apply_host(d, domain, host.tolist(), pend, has_checks)
+        if p is not None:
+            self._host_pending = None
+            host, ev, pend, has_checks, domain = p
+            ev.synchronize()
+            d._dt_dev = None
+            self._apply_host(d, domain, host.tolist(), pend, has_checks)
+        if self._observed is not None:
+            self._observed.finish(d)
+
+    def observe(self, domain, d):
+        """the per-iteration conserved quantities of the time loop (reference sphexa.cpp:150: energies, momenta and
+        the neighbor sum, globally reduced). With defer_host on the GPU the reduction is enqueued and its host copy is
+        collected by finish_host (models/observables.py DeferredConserved); otherwise it completes here."""
+        from .observables import DeferredConserved, compute_conserved_quantities
+
+        first, last = domain.start_index(), domain.end_index()
+        if d.device.type == "cuda" and self.defer_host:
+            if self._observed is None:
+                self._observed = DeferredConserved()
+            self._observed.enqueue(d, first, last, domain.comm)
+        else:
+            compute_conserved_quantities(d, first, last, domain.comm)
 
     def rho_timestep(self, d, first, last):
         """max divv of the owned particles as a device scalar; compute_timestep turns it into Krho / |max divv|"""

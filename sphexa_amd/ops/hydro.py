@@ -252,24 +252,46 @@ def set_global_h_min(d, comm):
     apply_global_h_min(d, global_h_min_device(d, comm).tolist())
 
 
-def frame_code(box: Box, hmin: float, hmax: float) -> int:
+def _frame_dims(box: Box):
+    for k, (L, bc) in enumerate(zip(box.lengths(), box.bc)):
+        L = L if L > 0 else 1.0
+        yield k, (L if bc == PERIODIC else 2.0 * L)  # wrap period at shift 0
+
+
+def frame_valid(box: Box, code: int, hmin: float, hmax: float) -> bool:
+    """whether frame ``code`` (nonzero) is unambiguous for pairs within 2 h_max (half a period > FRAME_PAIR_MARGIN
+    * 2 h_max) and fine enough for h_min (quantum <= FIXED_POINT_REL_QUANTUM * h_min) in this box"""
+    if not code or not (hmin > 0) or not math.isfinite(hmax):
+        return False
+    need = FRAME_PAIR_MARGIN * 2.0 * max(hmax, hmin)
+    for k, P0 in _frame_dims(box):
+        P = P0 / 2.0 ** ((code >> (1 + 5 * k)) & 31)
+        if P / 2.0 <= need or P / 2.0 ** 32 > FIXED_POINT_REL_QUANTUM * hmin:
+            return False
+    return True
+
+
+def frame_code(box: Box, hmin: float, hmax: float, prev: int = 0) -> int:
     """SphConsts::fixedPoint of the pair loops for these h extremes (sph_math.hpp qframeOf): 0 for fp64 records,
-    else 1 | shift_x << 1 | shift_y << 6 | shift_z << 11 with, per dimension, the largest shift whose wrap period
-    P = L / 2^k (periodic) or 2L / 2^k (open) keeps P / 2 > FRAME_PAIR_MARGIN * 2 h_max, provided the quantum P / 2^32
-    is <= FIXED_POINT_REL_QUANTUM * h_min. Also rejects boxes too small for an unambiguous wrap at shift 0 (open
-    extent L <= 2 h_max * margin: the pair at lo and hi would wrap)."""
+    else 1 | shift_x << 1 | shift_y << 6 | shift_z << 11. The previous step's code is kept while it stays valid
+    (frame_valid), so the choice does not flicker with h (the speculative first loop of a step runs under the previous
+    step's code, ops/hydro.py speculate_loop). A fresh choice takes, per dimension, one shift less than the largest
+    valid one when the quantum bound allows it (a factor 2 of headroom for h_max to grow). Boxes too small for an
+    unambiguous wrap at shift 0 (open extent L <= 2 h_max * margin: the pair at lo and hi would wrap) get 0."""
+    if frame_valid(box, prev, hmin, hmax):
+        return prev
     if not (hmin > 0) or not math.isfinite(hmax):
         return 0
     need = FRAME_PAIR_MARGIN * 2.0 * max(hmax, hmin)  # half a period must exceed this
     code = 1
-    for k, (L, bc) in enumerate(zip(box.lengths(), box.bc)):
-        L = L if L > 0 else 1.0
-        P0 = L if bc == PERIODIC else 2.0 * L
+    for k, P0 in _frame_dims(box):
         if P0 / 2.0 <= need:
             return 0
         shift = min(MAX_FRAME_SHIFT, int(math.floor(math.log2(P0 / (2.0 * need)))))
         while shift > 0 and P0 / 2.0 ** (shift + 1) <= need:
             shift -= 1
+        if shift > 0 and P0 / 2.0 ** (shift - 1) / 2.0 ** 32 <= FIXED_POINT_REL_QUANTUM * hmin:
+            shift -= 1  # headroom
         if P0 / 2.0 ** shift / 2.0 ** 32 > FIXED_POINT_REL_QUANTUM * hmin:
             return 0
         code |= shift << (1 + 5 * k)
@@ -306,7 +328,8 @@ def fixed_point_code(d, box: Box) -> int:
     records. Uses the per-step global h extremes when the propagator has set them (set_global_h_min), else the local
     ones cached on the identity and version of h."""
     hmin, hmax = _h_extremes(d)
-    code = frame_code(box, hmin, hmax)
+    code = frame_code(box, hmin, hmax, getattr(d, "_frame_prev", 0))
+    d._frame_prev = code
     ok = code != 0
     prev = getattr(d, "fixedPointPath", None)
     if prev is not None and prev != ok:

@@ -26,15 +26,22 @@ def test_fixed_point_guard():
     d = _D(torch.full((4,), 4e-3, dtype=torch.float32))
     assert H.FIXED_POINT_REL_QUANTUM <= 2.0 ** -22
     assert H.fixed_point_ok(d, Box([0.0] * 3, [1.0] * 3, [PERIODIC] * 3))
-    # the wrap period shrinks by powers of two while half of it exceeds 1.125 * 2 h_max = 9e-3:
-    # periodic L = 1 -> 1/32 (shift 5), open L = 1 -> 2/64 (shift 6), open L = 2.1 -> 4.2/128 (shift 7)
-    assert _shifts(H.fixed_point_code(d, Box([0.0] * 3, [1.0] * 3, [PERIODIC] * 3))) == [5] * 3
-    assert _shifts(H.fixed_point_code(d, Box([0.0] * 3, [1.0] * 3, [OPEN] * 3))) == [6] * 3
-    assert _shifts(H.fixed_point_code(d, Box([0.0] * 3, [2.1] * 3, [OPEN] * 3))) == [7] * 3
-    assert _shifts(H.fixed_point_code(d, Box([0.0, 0.0, 0.0], [1.0, 2.1, 0.5], [PERIODIC, OPEN, OPEN]))) == [5, 7, 5]
+    # the wrap period shrinks by powers of two while half of it exceeds 1.125 * 2 h_max = 9e-3, less one shift of
+    # headroom: periodic L = 1 -> 1/16 (shift 4), open L = 1 -> 2/32 (shift 5), open L = 2.1 -> 4.2/64 (shift 6)
+    fresh = lambda b: H.frame_code(b, 4e-3, 4e-3)  # noqa: E731
+    assert _shifts(fresh(Box([0.0] * 3, [1.0] * 3, [PERIODIC] * 3))) == [4] * 3
+    assert _shifts(fresh(Box([0.0] * 3, [1.0] * 3, [OPEN] * 3))) == [5] * 3
+    assert _shifts(fresh(Box([0.0] * 3, [2.1] * 3, [OPEN] * 3))) == [6] * 3
+    assert _shifts(fresh(Box([0.0, 0.0, 0.0], [1.0, 2.1, 0.5], [PERIODIC, OPEN, OPEN]))) == [4, 6, 4]
+    # a valid previous code is kept (no flicker between steps); an invalid one is replaced
+    b = Box([0.0] * 3, [1.0] * 3, [OPEN] * 3)
+    c5 = fresh(b)
+    assert H.frame_code(b, 4e-3, 1.3e-2, c5) == c5  # h_max grew within the headroom
+    assert H.frame_code(b, 4e-3, 1.5e-2, c5) != c5 and H.frame_valid(b, H.frame_code(b, 4e-3, 1.5e-2, c5), 4e-3, 1.5e-2)
+    assert all(not H.frame_valid(b, c5 + (2 << (1 + 5 * k)), 4e-3, 4e-3) for k in range(3))
     # boxes too small for an unambiguous wrap at shift 0 (an open pair at lo and hi would flip sign)
-    assert H.fixed_point_code(d, Box([0.0] * 3, [0.008] * 3, [OPEN] * 3)) == 0
-    assert H.fixed_point_code(d, Box([0.0] * 3, [0.017] * 3, [PERIODIC] * 3)) == 0
+    assert H.frame_code(Box([0.0] * 3, [0.008] * 3, [OPEN] * 3), 4e-3, 4e-3) == 0
+    assert H.frame_code(Box([0.0] * 3, [0.017] * 3, [PERIODIC] * 3), 4e-3, 4e-3) == 0
     # a small h_min against a large h_max: the quantum of the period that h_max needs is too coarse -> fp64
     assert H.frame_code(Box([0.0] * 3, [1.0] * 3, [OPEN] * 3), 1e-6, 1e-2) == 0
     assert H.frame_code(Box([0.0] * 3, [1.0] * 3, [OPEN] * 3), 1e-4, 1e-2) != 0
