@@ -483,12 +483,15 @@ PYBIND11_MODULE(_sphx_hip, m)
           { updateH(first, last, ng0, P<int32_t>(nc), P<float>(h), St(s)); });
     m.def("conserved_quantities",
           [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr vx, Ptr vy, Ptr vz, Ptr mm, Ptr temp, Ptr u, Ptr nc,
-             double cv, Ptr out, Ptr s)
+             double cv, Ptr out, Ptr s, Ptr eg0, Ptr eg1)
           {
               conservedQuantities(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(vx), P<float>(vy),
                                   P<float>(vz), P<float>(mm), P<double>(temp), P<double>(u), P<int32_t>(nc), cv,
-                                  P<double>(out), St(s));
-          });
+                                  P<double>(out), St(s), P<double>(eg0), P<double>(eg1));
+          },
+          py::arg("first"), py::arg("last"), py::arg("x"), py::arg("y"), py::arg("z"), py::arg("vx"), py::arg("vy"),
+          py::arg("vz"), py::arg("m"), py::arg("temp"), py::arg("u"), py::arg("nc"), py::arg("cv"), py::arg("out"),
+          py::arg("stream"), py::arg("eg0") = 0, py::arg("eg1") = 0);
 
     m.def("compute_stirring",
           [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr ax, Ptr ay, Ptr az, int numModes, Ptr modes,

@@ -176,7 +176,8 @@ void updatePositions(int64_t first, int64_t last, double dt, double dt_m1, const
 void updateH(int64_t first, int64_t last, unsigned ng0, const int32_t* nc, float* h, hipStream_t s);
 void conservedQuantities(int64_t first, int64_t last, const double* x, const double* y, const double* z,
                          const float* vx, const float* vy, const float* vz, const float* m, const double* temp,
-                         const double* u, const int32_t* nc, double cv, double* out, hipStream_t s);
+                         const double* u, const int32_t* nc, double cv, double* out, hipStream_t s,
+                         const double* eg0 = nullptr, const double* eg1 = nullptr);
 
 // cooling.hip (physics: sphx/cooling.hpp); coolingTimestep min-reduces into *out (initialize to 1e300)
 void coolParticles(int64_t first, int64_t last, double dt, const float* rho, const double* u, double* du,

@@ -847,9 +847,12 @@ __global__ void conservedKernel(int64_t first, int64_t last, const double* __res
                                 const float* __restrict__ vx, const float* __restrict__ vy,
                                 const float* __restrict__ vz, const float* __restrict__ m,
                                 const double* __restrict__ temp, const double* __restrict__ u,
-                                const int32_t* __restrict__ nc, double cv, double* __restrict__ out)
+                                const int32_t* __restrict__ nc, double cv, double* __restrict__ out,
+                                const double* __restrict__ eg0, const double* __restrict__ eg1)
 {
     double q[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // the rank's gravitational energy (device values of the gravity evaluations) rides in slot 2
+    if (blockIdx.x == 0 && threadIdx.x == 0) q[2] = (eg0 ? *eg0 : 0.0) + (eg1 ? *eg1 : 0.0);
     for (int64_t i = first + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < last;
          i += int64_t(gridDim.x) * blockDim.x)
     {
@@ -1106,12 +1109,12 @@ void updateH(int64_t first, int64_t last, unsigned ng0, const int32_t* nc, float
 
 void conservedQuantities(int64_t first, int64_t last, const double* x, const double* y, const double* z,
                          const float* vx, const float* vy, const float* vz, const float* m, const double* temp,
-                         const double* u, const int32_t* nc, double cv, double* out, hipStream_t s)
+                         const double* u, const int32_t* nc, double cv, double* out, hipStream_t s,
+                         const double* eg0, const double* eg1)
 {
     SPHX_CHECK(hipMemsetAsync(out, 0, 10 * sizeof(double), s)); // the sums accumulate atomically
-    if (last <= first) return;
-    unsigned grid = std::min<unsigned>(gridFor(last - first, 256), 2048);
-    conservedKernel<<<grid, 256, 0, s>>>(first, last, x, y, z, vx, vy, vz, m, temp, u, nc, cv, out);
+    unsigned grid = std::max<unsigned>(1, std::min<unsigned>(gridFor(std::max<int64_t>(last - first, 1), 256), 2048));
+    conservedKernel<<<grid, 256, 0, s>>>(first, last, x, y, z, vx, vy, vz, m, temp, u, nc, cv, out, eg0, eg1);
     SPHX_LAUNCH_CHECK();
 }
 

@@ -66,5 +66,7 @@ class MultipoleHolder:
         if self._rstats is not None:
             self.stats["remote_m2p"] = self._rstats.get("m2p", 0)
             self.stats["remote_p2p"] = self._rstats.get("p2p", 0)
-        # rank-local share; the observables reduction sums it over ranks (as the reference's MPI_Reduce does)
-        d.egrav = self._host_energy + sum(energies)
+        # rank-local share (egrav_local); the observables reduction sums it over ranks into d.egrav (as the
+        # reference's MPI_Reduce does)
+        d.egrav_local = self._host_energy + sum(energies)
+        d.egrav = d.egrav_local

@@ -21,8 +21,10 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-def local_conserved(d, first: int, last: int) -> torch.Tensor:
-    """returns float64 tensor [eKin, eInt, 0, linmom(3), angmom(3), ncsum] on the data device"""
+def local_conserved(d, first: int, last: int, egrav=None) -> torch.Tensor:
+    """returns float64 tensor [eKin, eInt, egrav, linmom(3), angmom(3), ncsum] on the data device. ``egrav``: the
+    rank's gravitational energy as a host float, or (GPU) a list of <= 2 float64 device scalars (the energies of
+    pending gravity evaluations, read by the kernel); default: the rank's last gravity energy (d.egrav_local)"""
     cv = ideal_gas_cv(d.muiConst, d.gamma)
     temp = d["temp"] if d.is_allocated("temp") else None
     u = d["u"] if d.is_allocated("u") else None
@@ -32,16 +34,23 @@ def local_conserved(d, first: int, last: int) -> torch.Tensor:
     args = (first, last, d["x"].data_ptr(), d["y"].data_ptr(), d["z"].data_ptr(), d["vx"].data_ptr(),
             d["vy"].data_ptr(), d["vz"].data_ptr(), d["m"].data_ptr(), 0 if temp is None else temp.data_ptr(),
             0 if u is None else u.data_ptr(), 0 if nc is None else nc.data_ptr(), cv, out.data_ptr())
+    if egrav is None:
+        egrav = float(getattr(d, "egrav_local", 0.0))
+    dev = [] if isinstance(egrav, (int, float)) else list(egrav)
     if d.device.type == "cuda":
-        _lib.hip().conserved_quantities(*args, _stream())
+        if not dev and egrav != 0.0:
+            dev = [torch.tensor([float(egrav)], dtype=torch.float64).pin_memory().to(d.device, non_blocking=True)]
+        ptr = [t.data_ptr() for t in dev] + [0, 0]
+        _lib.hip().conserved_quantities(*args, _stream(), eg0=ptr[0], eg1=ptr[1])
     else:
         _lib.cpu().conserved_quantities(*args)
+        out[2] = float(egrav) if not dev else float(sum(float(t) for t in dev))
     return out
 
 
 def apply_conserved(d, q):
-    """host values of the reduced 10-vector (slot 2 unused: egrav comes from the gravity evaluation)"""
-    d.ecin, d.eint = q[0], q[1]
+    """host values of the globally reduced 10-vector"""
+    d.ecin, d.eint, d.egrav = q[0], q[1], q[2]
     d.etot = d.ecin + d.eint + d.egrav
     d.linmom = math.sqrt(q[3] ** 2 + q[4] ** 2 + q[5] ** 2)
     d.angmom = math.sqrt(q[6] ** 2 + q[7] ** 2 + q[8] ** 2)
@@ -65,8 +74,8 @@ class DeferredConserved:
         self._ev = None
         self.pending = False
 
-    def enqueue(self, d, first: int, last: int, comm):
-        q = local_conserved(d, first, last)
+    def enqueue(self, d, first: int, last: int, comm, egrav=None):
+        q = local_conserved(d, first, last, egrav)
         comm.allreduce(q, SUM)
         if self._host is None:
             self._host = torch.empty(10, dtype=torch.float64, pin_memory=True)

@@ -205,7 +205,15 @@ class Propagator:
         if d.device.type == "cuda" and self.defer_host:
             if self._observed is None:
                 self._observed = DeferredConserved()
-            self._observed.enqueue(d, first, last, domain.comm)
+            # the gravity energy of this step is still on the device (GravityPending): the kernel reads it there
+            grav = self.gravity
+            pend = list(getattr(grav, "pending", None) or [])
+            eg = None
+            if pend and not grav._host_energy:
+                eg = [p.energy_dev() for p in pend]
+            elif grav is not None and pend:
+                grav.finish_sync(d)  # (mixed host/device energies: collect them now)
+            self._observed.enqueue(d, first, last, domain.comm, eg)
         else:
             compute_conserved_quantities(d, first, last, domain.comm)
 

@@ -110,6 +110,10 @@ class GravityPending:
     def __init__(self, dev, groups: int, caps, stats, device):
         self.dev, self.groups, self.caps, self.stats, self.device = dev, groups, caps, stats, device
 
+    def energy_dev(self):
+        """the evaluation's energy as a float64 device scalar (a view of ``dev``)"""
+        return self.dev[self.NSTATS:self.NSTATS + 1]
+
     def finish(self, vals) -> float:
         st = [int(v) for v in vals[:self.NSTATS]]  # exact: counts below 2^53
         energy = float(vals[self.NSTATS])

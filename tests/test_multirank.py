@@ -358,3 +358,67 @@ def test_let_cost_quantified():
         assert r["sph_halos"] <= r["grav_halos"] <= 2.5 * r["n"]
         assert 0 < r["remote"] < 20000
         assert r["rm2p"] < r["lm2p"] and r["rp2p"] == 0
+
+
+# ------------------------------------------------------------------------ multi-step equivalence per test case
+def _case_worker(rank, world, comm, init, n, steps, prop):
+    """``steps`` iterations of a test case (Simulation: propagator step + per-iteration conserved quantities) on
+    ``world`` ranks; returns the owned particles' keys and state"""
+    from sphexa_amd.app.simulation import Simulation
+
+    sim = Simulation(init, n=n, prop=prop, device="cpu", comm=comm)
+    for _ in range(steps):
+        sim.step()
+    d, dom = sim.d, sim.domain
+    s, e = dom.start_index(), dom.end_index()
+    out = dict(etot=d.etot, ecin=d.ecin, nsum=d.totalNeighbors, dt=d.minDt, ttot=d.ttot,
+               keys=d["keys"][s:e].numpy().copy())
+    for f in ("x", "y", "z", "vx", "vy", "vz", "h", "temp", "alpha"):
+        if d.is_allocated(f):
+            out[f] = d[f][s:e].numpy().copy()
+    return out
+
+
+def _compare_case(ref, res, fields, rtol, dt_rtol):
+    r0 = res[0]
+    assert r0["nsum"] == ref["nsum"]
+    assert r0["dt"] == pytest.approx(ref["dt"], rel=dt_rtol)
+    assert r0["ttot"] == pytest.approx(ref["ttot"], rel=dt_rtol)
+    assert r0["etot"] == pytest.approx(ref["etot"], rel=rtol)
+    keys = np.concatenate([r["keys"] for r in res])
+    order = np.argsort(keys, kind="stable")
+    ro = np.argsort(ref["keys"], kind="stable")
+    assert np.array_equal(keys[order], ref["keys"][ro])
+    errs = {}
+    for f in fields:
+        got = np.concatenate([r[f] for r in res])[order].astype(np.float64)
+        want = ref[f][ro].astype(np.float64)
+        scale = max(np.abs(want).max(), 1e-30)
+        errs[f] = np.abs(got - want).max() / scale
+    print("max |N ranks - 1 rank| / max |1 rank|:", {k: f"{v:.2e}" for k, v in errs.items()})
+    for f, e in errs.items():
+        assert e <= rtol, (f, e)
+
+
+@pytest.mark.parametrize("init,world,n,steps,prop", [
+    ("turbulence", 8, 12, 5, "turbulence"),  # stirring: replicated mt19937 phases + per-rank mode sums
+    ("noh", 8, 12, 5, "ve"),
+])
+def test_case_steps_nranks_match_single(init, world, n, steps, prop):
+    """8 ranks of a glass-based case over 5 steps equal one rank up to fp32 summation order (neighbor lists are
+    traversed in different orders by the per-rank octrees): identical neighbor sums, keys and time steps"""
+    ref = run_ranks(_case_worker, 1, init, n, steps, prop)[0]
+    res = run_ranks(_case_worker, world, init, n, steps, prop)
+    _compare_case(ref, res, ("x", "y", "z", "vx", "vy", "vz", "h", "temp", "alpha"), 1e-5, 1e-6)
+
+
+def test_evrard_steps_4_ranks_match_single():
+    """Evrard with self-gravity on 4 ranks over 3 steps: the SPH part is exact up to summation order, the far field
+    differs by the per-rank LET trees (same MAC, different node sets: accuracy-class differences of ~1e-3 in the
+    gravitational accelerations, of which a few steps leave ~dt^2 a in the positions)"""
+    ref = run_ranks(_case_worker, 1, "evrard", 24, 3, "ve")[0]
+    res = run_ranks(_case_worker, 4, "evrard", 24, 3, "ve")
+    _compare_case(ref, res, ("x", "y", "z", "h", "temp"), 1e-4, 1e-4)
+    got = np.concatenate([r["vx"] for r in res])[np.argsort(np.concatenate([r["keys"] for r in res]), kind="stable")]
+    want = ref["vx"][np.argsort(ref["keys"], kind="stable")]
+    assert np.abs(got - want).max() <= 5e-3 * np.abs(want).max()
