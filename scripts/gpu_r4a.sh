@@ -3,9 +3,9 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r4a; mkdir -p $O; export TMPDIR=/tmp
-timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > $O/tests.log 2>&1 \
-    || { tail -40 $O/tests.log; exit 1; }
-tail -1 $O/tests.log
+timeout -k 10 700 python3 -u -m pytest tests -m gpu -q --maxfail=15 --timeout 150 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; grep -E "passed|failed" $O/tests.log | tail -2; grep FAILED $O/tests.log | head -15
+[ $rc -gt 1 ] && { echo "pytest rc $rc: stopping"; tail -30 $O/tests.log; exit 1; }
 timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 grep -o '"ms_per_step": [0-9.]*\|"evrard_ms_per_step": [0-9.]*' $O/bench.json
 timeout -k 10 200 python3 scripts/grav_stats.py > $O/grav_stats.txt 2>&1 || { tail -20 $O/grav_stats.txt; exit 1; }

@@ -111,6 +111,12 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("sort_pairs_temp_bytes", [](int64_t n) { return sortPairsTempBytes(n); });
     m.def("sort_keys", [](int64_t n, Ptr kin, Ptr kout, Ptr perm, Ptr tmp, size_t tmpBytes, Ptr s)
           { sortKeys(n, P<KeyT>(kin), P<KeyT>(kout), P<int32_t>(perm), P<void>(tmp), tmpBytes, St(s)); });
+    m.def("merge_sorted_runs", [](int64_t n, Ptr keys, const std::vector<int64_t>& offsets, Ptr out, Ptr perm, Ptr s)
+          {
+              mergeSortedRuns(n, P<KeyT>(keys), offsets.data(), int(offsets.size()) - 1, P<KeyT>(out), P<int32_t>(perm),
+                              St(s));
+          });
+    m.def("merge_runs_max", []() { return kMergeRuns; });
     m.def("sort_pairs_i64_i32",
           [](int64_t n, Ptr kin, Ptr kout, Ptr vin, Ptr vout, Ptr tmp, size_t tmpBytes, int b0, int b1, Ptr s)
           {

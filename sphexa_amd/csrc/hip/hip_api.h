@@ -49,6 +49,12 @@ size_t sortPairsTempBytes(int64_t n);
 void sortPairs(int64_t n, const KeyT* keysIn, KeyT* keysOut, const int32_t* valsIn, int32_t* valsOut, void* tmp,
                size_t tmpBytes, int beginBit, int endBit, hipStream_t s);
 void sortKeys(int64_t n, const KeyT* keysIn, KeyT* keysOut, int32_t* perm, void* tmp, size_t tmpBytes, hipStream_t s);
+//! non-empty sorted runs a merge handles (mergeSortedRuns); more runs: sort
+constexpr int kMergeRuns = 16;
+//! stable merge of the sorted runs [runOffsets[b], runOffsets[b + 1]) of keys (host offsets): out = merged keys,
+//! perm = source index of each output position
+void mergeSortedRuns(int64_t n, const KeyT* keys, const int64_t* runOffsets, int numRuns, KeyT* out, int32_t* perm,
+                     hipStream_t s);
 void gather(int64_t n, const int32_t* perm, const void* src, void* dst, int elemSize, hipStream_t s);
 void gatherMulti(int64_t n, const int32_t* perm, const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,
                  int elemSize, hipStream_t s);

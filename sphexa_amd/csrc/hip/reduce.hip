@@ -26,6 +26,11 @@ struct Fields4
     int count;
 };
 
+//! min / max that propagate NaN (fmin/fmax drop a NaN operand: a NaN coordinate or h would vanish from the box and
+//! the h extremes instead of showing up in them)
+__device__ __forceinline__ double nanMin(double a, double b) { return a != a ? a : (b != b ? b : fmin(a, b)); }
+__device__ __forceinline__ double nanMax(double a, double b) { return a != a ? a : (b != b ? b : fmax(a, b)); }
+
 __device__ __forceinline__ double loadAs(const void* p, int isD, int64_t i)
 {
     return isD ? static_cast<const double*>(p)[i] : double(static_cast<const float*>(p)[i]);
@@ -69,16 +74,16 @@ __global__ __launch_bounds__(kRedBlock) void multiMinMaxKernel(int64_t n, Fields
                                                                double* __restrict__ out, unsigned* ticket)
 {
     __shared__ double red[kRedBlock / 64];
-    auto mn = [](double a, double b) { return fmin(a, b); };
-    auto mx = [](double a, double b) { return fmax(a, b); };
+    auto mn = [](double a, double b) { return nanMin(a, b); };
+    auto mx = [](double a, double b) { return nanMax(a, b); };
     for (int k = 0; k < f.count; ++k)
     {
         double lo = DBL_MAX, hi = -DBL_MAX;
         for (int64_t i = int64_t(blockIdx.x) * kRedBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kRedBlock)
         {
             const double v = loadAs(f.p[k], f.isDouble[k], i);
-            lo             = fmin(lo, v);
-            hi             = fmax(hi, v);
+            lo             = nanMin(lo, v);
+            hi             = nanMax(hi, v);
         }
         lo = blockReduce(lo, red, mn);
         hi = blockReduce(hi, red, mx);
@@ -96,7 +101,7 @@ __global__ __launch_bounds__(kRedBlock) void multiMinMaxKernel(int64_t n, Fields
         for (unsigned b = threadIdx.x; b < gridDim.x; b += kRedBlock)
         {
             const double p = __hip_atomic_load(partials + k * gridDim.x + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v              = isMin ? fmin(v, p) : fmax(v, p);
+            v              = isMin ? nanMin(v, p) : nanMax(v, p);
         }
         v = isMin ? blockReduce(v, red, mn) : blockReduce(v, red, mx);
         if (threadIdx.x == 0) out[k] = v;
@@ -110,20 +115,20 @@ __global__ __launch_bounds__(kRedBlock) void maxNorm2Kernel(int64_t first, int64
                                                             unsigned* ticket)
 {
     __shared__ double red[kRedBlock / 64];
-    auto mx = [](double a, double b) { return fmax(a, b); };
+    auto mx = [](double a, double b) { return nanMax(a, b); };
     double m = 0.0;
     for (int64_t i = first + int64_t(blockIdx.x) * kRedBlock + threadIdx.x; i < last;
          i += int64_t(gridDim.x) * kRedBlock)
     {
         const double x = ax[i], y = ay[i], z = az[i];
-        m              = fmax(m, x * x + y * y + z * z);
+        m              = nanMax(m, x * x + y * y + z * z);
     }
     m = blockReduce(m, red, mx);
     if (threadIdx.x == 0) partials[blockIdx.x] = m;
     if (!lastBlock(ticket)) return;
     double v = 0.0;
     for (unsigned b = threadIdx.x; b < gridDim.x; b += kRedBlock)
-        v = fmax(v, __hip_atomic_load(partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        v = nanMax(v, __hip_atomic_load(partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     v = blockReduce(v, red, mx);
     if (threadIdx.x == 0) out[0] = v;
 }
@@ -142,21 +147,21 @@ __global__ __launch_bounds__(kRedBlock) void timestepKernel(int64_t first, int64
                                                             double* __restrict__ out, unsigned* ticket)
 {
     __shared__ double red[kRedBlock / 64];
-    auto mx  = [](double a, double b) { return fmax(a, b); };
+    auto mx  = [](double a, double b) { return nanMax(a, b); };
     double m = 0.0;
     if (ax)
         for (int64_t i = first + int64_t(blockIdx.x) * kRedBlock + threadIdx.x; i < last;
              i += int64_t(gridDim.x) * kRedBlock)
         {
             const double x = ax[i], y = ay[i], z = az[i];
-            m              = fmax(m, x * x + y * y + z * z);
+            m              = nanMax(m, x * x + y * y + z * z);
         }
     m = blockReduce(m, red, mx);
     if (threadIdx.x == 0) partials[blockIdx.x] = m;
     if (!lastBlock(ticket)) return;
     double v = 0.0;
     for (unsigned b = threadIdx.x; b < gridDim.x; b += kRedBlock)
-        v = fmax(v, __hip_atomic_load(partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        v = nanMax(v, __hip_atomic_load(partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     v = blockReduce(v, red, mx);
     if (threadIdx.x == 0)
     {
@@ -170,7 +175,7 @@ __global__ __launch_bounds__(kRedBlock) void timestepKernel(int64_t first, int64
             const double d = fabs(double(divvMax[0]));
             rho            = d != 0.0 ? Krho / d : inf;
         }
-        out[0] = fmin(fmin(fmin(acc, courant), rho), others);
+        out[0] = nanMin(nanMin(nanMin(acc, courant), rho), others);
         out[1] = prevDt;
         out[2] = courant;
         out[3] = rho;

@@ -85,6 +85,66 @@ void sortKeys(int64_t n, const KeyT* keysIn, KeyT* keysOut, int32_t* perm, void*
 }
 #endif
 
+/*! @brief stable merge of k sorted runs (the particles received from k ranks after a migration, each source's
+ *         part already SFC-sorted by the sender): element i of run a lands at
+ *             rank(i) = (i - off[a]) + sum_{b < a} upper_bound(run b, key) + sum_{b > a} lower_bound(run b, key),
+ *         the position a stable sort of the concatenation gives it (ties keep the run order). One thread per element,
+ *         k - 1 binary searches each (k <= kMergeRuns non-empty runs; the host sorts when there are more). Replaces the
+ *         second full sort of a multi-rank sync (reference assignment_gpu.cuh:157-181 merges the same way).
+ */
+struct MergeRuns
+{
+    int64_t off[kMergeRuns + 1];
+    int k;
+};
+
+__device__ __forceinline__ int64_t boundIn(const KeyT* __restrict__ keys, int64_t lo, int64_t hi, KeyT v, bool upper)
+{
+    while (lo < hi)
+    {
+        const int64_t mid = (lo + hi) >> 1;
+        const KeyT km     = keys[mid];
+        if (upper ? km <= v : km < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void mergeRunsKernel(int64_t n, const KeyT* __restrict__ keys, MergeRuns R, KeyT* __restrict__ out,
+                                int32_t* __restrict__ perm)
+{
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int a = 0;
+    while (a + 1 < R.k && R.off[a + 1] <= i)
+        ++a;
+    const KeyT v = keys[i];
+    int64_t r    = i - R.off[a];
+    for (int b = 0; b < R.k; ++b)
+        if (b != a) r += boundIn(keys, R.off[b], R.off[b + 1], v, b < a) - R.off[b];
+    out[r]  = v;
+    perm[r] = int32_t(i);
+}
+
+void mergeSortedRuns(int64_t n, const KeyT* keys, const int64_t* runOffsets, int numRuns, KeyT* out, int32_t* perm,
+                     hipStream_t s)
+{
+    if (n <= 0) return;
+    MergeRuns R{};
+    R.k = 0;
+    R.off[0] = 0;
+    for (int b = 0; b < numRuns; ++b) // empty runs are dropped
+        if (runOffsets[b + 1] > runOffsets[b])
+        {
+            SPHX_CHECK(R.k < kMergeRuns ? hipSuccess : hipErrorInvalidValue);
+            R.off[R.k]     = runOffsets[b];
+            R.off[R.k + 1] = runOffsets[b + 1];
+            ++R.k;
+        }
+    mergeRunsKernel<<<gridFor(n, 256), 256, 0, s>>>(n, keys, R, out, perm);
+    SPHX_LAUNCH_CHECK();
+}
+
 template<class T>
 __global__ void gatherKernel(int64_t n, const int32_t* __restrict__ perm, const T* __restrict__ src,
                              T* __restrict__ dst)

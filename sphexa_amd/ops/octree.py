@@ -6,8 +6,8 @@ node order, childOffsets, parents, levelRange, internal<->leaf maps), focus/sour
 geometric data. Tight (particle) bounding boxes per node replace the reference's geometric centers/sizes in the
 neighbor search: same results, better pruning.
 
-HIP path: per-leaf binary-search counts, rebalance op kernel, hipCUB exclusive scan, emit kernel; linking via
-per-leaf internal-node counts (no radix tree), one radix sort of the placeholder codes, per-node child search;
+HIP path: per-leaf binary-search counts, rebalance op kernel, hand-written tile scan (sample_sort.hip), emit kernel; linking via
+per-leaf internal-node counts (no radix tree), one sample sort of the placeholder codes, per-node child search;
 leaf boxes from particles and a per-level box upsweep.
 """
 

@@ -2,8 +2,10 @@
 
 Parity: reference sfc/sfc.hpp:282 + sfc/sfc_gpu.cu:38-54 (computeSfcKeys), primitives/gather.hpp:132-162 and
 primitives/gather.cuh:44-113 (SfcSorter / GpuSfcSorter: sort keys, keep the permutation, gather fields).
-HIP path: one thread per particle key kernel; hipCUB (rocPRIM onesweep) radix sort of (key, index) over the 63 used
-key bits; a multi-array gather kernel that reorders all fields of one dtype in a single launch.
+HIP path: one thread per particle key kernel; the hand-written sample sort of (key, index) (csrc/hip/sample_sort.hip,
+no library sort in a time step); a stable k-way merge of sorted runs for the particles received in a migration
+(merge_sorted_runs, reference domain/assignment_gpu.cuh:157-181); a multi-array gather kernel that reorders all
+fields of one dtype in a single launch.
 """
 
 from __future__ import annotations
@@ -65,6 +67,25 @@ def sort_keys(keys: torch.Tensor):
     out = keys.clone()
     _lib.cpu().sort_keys(n, out.data_ptr(), perm.data_ptr())
     return out, perm
+
+
+def merge_sorted_runs(keys: torch.Tensor, counts: Sequence[int]):
+    """(sorted keys, permutation int32) of keys made of len(counts) consecutive sorted runs (counts[b] keys each),
+    equal to sort_keys(keys) (a stable sort): on the GPU one merge kernel when there are at most merge_runs_max()
+    non-empty runs, else (and on the CPU) the sort"""
+    n = keys.numel()
+    if keys.is_cuda and n:
+        h = _lib.hip()
+        if sum(1 for c in counts if c) <= h.merge_runs_max():
+            offs = [0]
+            for c in counts:
+                offs.append(offs[-1] + int(c))
+            assert offs[-1] == n, (offs[-1], n)
+            out = torch.empty_like(keys)
+            perm = torch.empty(n, dtype=torch.int32, device=keys.device)
+            h.merge_sorted_runs(n, keys.data_ptr(), offs, out.data_ptr(), perm.data_ptr(), _stream())
+            return out, perm
+    return sort_keys(keys)
 
 
 def gather(perm: torch.Tensor, src: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -62,7 +62,7 @@ def _stream():
 class Domain:
     def __init__(self, comm: Comm, box: Box, bucket_size_focus: int = 64, bucket_size: Optional[int] = None,
                  theta: float = 1.0, sfc_kind: int = sfc_ops.HILBERT, halo_cut_boxes: int = 4096,
-                 check_halos: bool = True):
+                 check_halos: bool | str = True):
         self.comm = comm
         self.rank, self.size = comm.rank, comm.size
         self.box = box.copy()
@@ -152,8 +152,10 @@ class Domain:
 
         if self.size > 1:
             keys, own = self._distribute(keys, own, conserved)
-
-        skeys, perm = sfc_ops.sort_keys(keys)
+            # the received particles are one SFC-sorted run per source rank: merged, not sorted again
+            skeys, perm = sfc_ops.merge_sorted_runs(keys, self._recv_run_counts)
+        else:
+            skeys, perm = sfc_ops.sort_keys(keys)
         names = list(own.keys())
         n_own = skeys.numel()
 
@@ -202,8 +204,10 @@ class Domain:
             if self.check_halos:
                 bad = self._halo_ownership_bad(d["keys"])
                 if bad is not None:
-                    if bad.is_cuda:
-                        # deferred: the count reaches the host with the propagator's time-step copy (pending_checks)
+                    if bad.is_cuda and self.check_halos != "immediate":
+                        # deferred: the count reaches the host with the propagator's time-step copy (pending_checks),
+                        # i.e. the raise comes after the step's physics ran on the bad halos (the state is advanced
+                        # when it fires); check_halos="immediate" checks here, before any physics (one host copy)
                         self._pending_bad = bad if self._pending_bad is None else self._pending_bad + bad
                     else:
                         self._raise_bad_halos(int(bad))
@@ -299,6 +303,7 @@ class Domain:
         recv_dev = self.comm.exchange_counts_dev(send_dev)
         counts = torch.cat([send_dev, recv_dev]).view(-1).cpu().tolist()
         send_counts, recv_counts = counts[: self.size], counts[self.size:]
+        self._recv_run_counts = recv_counts
 
         names = list(own.keys())
         sorted_fields = sfc_ops.gather_many(perm, [own[f] for f in names])

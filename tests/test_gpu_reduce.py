@@ -3,6 +3,8 @@ fields, max |a|^2, and the time-step kernel (reference sph/timestep.hpp)."""
 
 import math
 
+import numpy as np
+
 import pytest
 import torch
 
@@ -49,3 +51,37 @@ def test_timestep_kernel(gpu, grav, dev_inputs, n):
     # repeated launches re-arm the ticket
     again = R.timestep_reduce(ax, ay, az, 0, n, grav, courant, divv, Krho, eta, eps, others, prev).cpu().tolist()
     assert again == out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("counts", [[1000, 0, 2500, 7], [0, 0, 0, 5000], [3000], [40] * 16, [1, 1, 1],
+                                    [20000, 20000]])
+def test_merge_sorted_runs_equals_stable_sort(gpu, counts):
+    """the migration merge (sfc_sort.hip mergeRunsKernel) of per-source sorted runs is the stable sort of their
+    concatenation: overlapping key ranges, duplicates within and across runs, empty runs"""
+    from sphexa_amd.ops import sfc
+
+    rng = np.random.default_rng(sum(counts))
+    runs = [np.sort(rng.integers(0, 5000 if i % 2 else 1 << 62, c)).astype(np.int64) for i, c in enumerate(counts)]
+    keys = torch.from_numpy(np.concatenate(runs)).to(gpu)
+    mk, mp = sfc.merge_sorted_runs(keys, counts)
+    ref = np.argsort(keys.cpu().numpy(), kind="stable")
+    assert np.array_equal(mp.cpu().numpy(), ref)
+    assert np.array_equal(mk.cpu().numpy(), keys.cpu().numpy()[ref])
+    sk, sp = sfc.sort_keys(keys)
+    assert torch.equal(sk, mk) and torch.equal(sp, mp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("where", [0, 777, 99999])
+def test_min_max_propagates_nan(gpu, where):
+    """a NaN coordinate or h shows up in the extremes (torch semantics) instead of vanishing"""
+    a = torch.rand(100000, dtype=torch.float64, device=gpu)
+    b = torch.rand(100000, dtype=torch.float32, device=gpu)
+    b[where] = float("nan")
+    out = R.min_max([a, b]).cpu().tolist()
+    assert math.isfinite(out[0]) and math.isfinite(out[1])
+    assert math.isnan(out[2]) and math.isnan(out[3])
+    ax = torch.zeros(100000, dtype=torch.float32, device=gpu)
+    ax[where] = float("nan")
+    assert math.isnan(R.max_norm2(ax, ax, ax, 0, 100000).item())
