@@ -305,20 +305,21 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("av_switches",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr cs, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
-             double dt, Ptr alpha, int64_t ntot, Ptr rec, Ptr s, Ptr avS, int inDone, Ptr momOut)
+             double dt, Ptr alpha, int64_t ntot, Ptr rec, Ptr s, Ptr avS, int inDone, Ptr momOut, Ptr alphaOut,
+             Ptr dtDev)
           {
               auto sc = toConsts(c);
               auto cp = six(cij);
               avSwitches(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
                          P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(cs), cp.data(),
                          P<float>(wh), P<float>(kx), P<float>(xm), P<float>(divv), dt, P<void>(rec), P<void>(avS),
-                         P<float>(alpha), St(s), inDone, P<void>(momOut));
+                         P<float>(alpha), St(s), inDone, P<void>(momOut), P<float>(alphaOut), P<double>(dtDev));
           },
           py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
           py::arg("x"), py::arg("y"), py::arg("z"), py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("h"),
           py::arg("cs"), py::arg("cij"), py::arg("wh"), py::arg("kx"), py::arg("xm"), py::arg("divv"), py::arg("dt"),
           py::arg("alpha"), py::arg("ntot"), py::arg("rec"), py::arg("s"), py::arg("avS") = 0, py::arg("inDone") = 0,
-          py::arg("momOut") = 0);
+          py::arg("momOut") = 0, py::arg("alphaOut") = 0, py::arg("dtDev") = 0);
     m.def("momentum_energy_ve",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr prho, Ptr cs, const std::array<Ptr, 6>& cij, Ptr kx, Ptr xm,

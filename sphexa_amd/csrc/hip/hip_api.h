@@ -170,7 +170,7 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                 const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                 const float* c, float* const cij[6], const float* wh, const float* kx, const float* xm,
                 const float* divv, double dt, void* rec, const void* avS, float* alpha, hipStream_t s, int inDone = 0,
-                void* momOut = nullptr);
+                void* momOut = nullptr, float* alphaOut = nullptr, const double* dtDev = nullptr);
 void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const MomFields& f,
                       bool avClean, const float* wh, void* rec, void* recGradV, float* ax, float* ay, float* az,
                       double* du, float* minDt, hipStream_t s, int inDone = 0);

@@ -608,18 +608,20 @@ __global__ __launch_bounds__(kBlock) void avSwitchesKernel(NbrArgs a, SphConsts 
                                                            const float* __restrict__ h, Six cij,
                                                            const SrcIad* __restrict__ rec,
                                                            const float* __restrict__ wh, double dt,
-                                                           float* __restrict__ alpha)
+                                                           const float* __restrict__ alpha,
+                                                           float* __restrict__ alphaOut, const double* dtDev)
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcIad>::S];
     int64_t i;
     PackedLane pl;
     unsigned n;
     const bool valid = targetOf(a, i, pl, n);
+    if (dtDev) dt = *dtDev;
     float ci[6] = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
     float al    = avSwitchesJLoop(unsigned(i), sc.K, box, &pl, 0, n, h[i], ci, coopOf(rec, tile, i, a),
                                   KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt, sc.alphamin, sc.alphamax,
                                   sc.decayConstant, alpha[i]);
-    if (valid) alpha[i] = al;
+    if (valid) alphaOut[i] = al;
 }
 
 //! @brief AV switches on fixed-point records (SrcAvQ + divv field): same loop as avSwitchesKernel
@@ -628,17 +630,19 @@ __global__ __launch_bounds__(kBlock) void avSwitchesQKernel(NbrArgs a, SphConsts
                                                             const SrcAvQ* __restrict__ rec,
                                                             const float* __restrict__ divv,
                                                             const float* __restrict__ wh, double dt,
-                                                            float* __restrict__ alpha)
+                                                            const float* __restrict__ alpha,
+                                                            float* __restrict__ alphaOut, const double* dtDev)
 {
     int64_t i;
     PackedLane pl;
     unsigned n;
     const bool valid = targetOf(a, i, pl, n);
+    if (dtDev) dt = *dtDev;
     float ci[6] = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
     float al    = avSwitchesJLoop(unsigned(i), sc.K, q, &pl, 0, n, h[i], ci, AvQLoader{rec, divv},
                                   KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt, sc.alphamin, sc.alphamax,
                                   sc.decayConstant, alpha[i]);
-    if (valid) alpha[i] = al;
+    if (valid) alphaOut[i] = al;
 }
 
 //! @brief AV switches on SrcAvV records (vd = vol divv) with the IAD loop's S_i (avSwitchesVJLoop, sph_math.hpp)
@@ -648,13 +652,16 @@ __global__ __launch_bounds__(kBlock) void avSwitchesVKernel(NbrArgs a, SphConsts
                                                             const float* __restrict__ divv,
                                                             const float4* __restrict__ avS,
                                                             const float* __restrict__ wh, double dt,
-                                                            float* __restrict__ alpha, SrcMomQ* __restrict__ momOut)
+                                                            const float* __restrict__ alpha,
+                                                            float* __restrict__ alphaOut, const double* dtDev,
+                                                            SrcMomQ* __restrict__ momOut)
 {
     __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcAvV>::S];
     int64_t i;
     PackedLane pl;
     unsigned n;
     const bool valid = targetOf(a, i, pl, n);
+    if (dtDev) dt = *dtDev;
     float ci[6]    = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
     const float4 s = avS[i - a.first];
     const float S[3] = {s.x, s.y, s.z};
@@ -662,7 +669,7 @@ __global__ __launch_bounds__(kBlock) void avSwitchesVKernel(NbrArgs a, SphConsts
                                 coopOf(rec, tile, i, a), KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt,
                                 sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
     if (!valid) return;
-    alpha[i] = al;
+    alphaOut[i] = al;
     if (momOut) momOut[i].alpha = al;
 }
 
@@ -1018,8 +1025,11 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                 const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                 const float* c, float* const cij[6], const float* wh, const float* kx, const float* xm,
                 const float* divv, double dt, void* rec, const void* avS, float* alpha, hipStream_t s, int inDone,
-                void* momOut)
+                void* momOut, float* alphaOut, const double* dtDev)
 {
+    // alpha_i is read by its own target only: the new values may go to another buffer (alphaOut), so that a step
+    // enqueued speculatively can be redone from the old ones (models/propagators.py)
+    if (!alphaOut) alphaOut = alpha;
     if (a.last <= a.first) return;
     Six cc;
     for (int k = 0; k < 6; ++k)
@@ -1027,7 +1037,8 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
     if (!sc.fixedPoint)
     {
         packIadKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, xm, kx, vx, vy, vz, xm, c, divv, (SrcIad*)rec);
-        avSwitchesKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, cc, (const SrcIad*)rec, wh, dt, alpha);
+        avSwitchesKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, cc, (const SrcIad*)rec, wh, dt, alpha,
+                                                      alphaOut, dtDev);
     }
     else if (avS)
     {
@@ -1038,14 +1049,15 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                                                                            q, (SrcAvV*)rec);
                    });
         avSwitchesVKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, cc, (const SrcAvV*)rec, divv,
-                                                      (const float4*)avS, wh, dt, alpha, (SrcMomQ*)momOut);
+                                                      (const float4*)avS, wh, dt, alpha, alphaOut, dtDev,
+                                                      (SrcMomQ*)momOut);
     }
     else
     {
         const QFrame q = qframeOf(box, sc.fixedPoint);
         packAvQKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, kx, vx, vy, vz, xm, c, q, (SrcAvQ*)rec);
         avSwitchesQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, cc, (const SrcAvQ*)rec, divv, wh, dt,
-                                                      alpha);
+                                                      alpha, alphaOut, dtDev);
     }
     SPHX_LAUNCH_CHECK();
 }

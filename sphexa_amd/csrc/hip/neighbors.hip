@@ -68,6 +68,11 @@ constexpr int kCbase         = 128; // chunk bases of the most recent slots (ban
 constexpr int kRingWords     = kRing * 64;
 constexpr int kStageWords    = kStagePairs * 10; // per 2 pairs {x0 x1 y0 y1} {z0 z1 cc0 cc1} x2 + 4 codes
 constexpr int kCandWords     = kRingWords + kStageWords + kCbase;
+//! frontier capacity of the sub-group passes (both frontiers inside the staging area, clear of the chunk bases)
+constexpr int kSubFront = 256;
+static_assert(2 * kSubFront <= kStageWords, "sub-pass frontiers fit the staging area");
+//! smallest lane range of a sub-group pass; a range this small that still overflows goes to the spill kernel
+constexpr int kMinSub = 4;
 //! per-wave LDS work area: the traversal frontiers, then (candidate phase) ring + staging + chunk bases
 constexpr int kWorkWords = 2 * kFrontCap > kCandWords ? 2 * kFrontCap : kCandWords;
 
@@ -222,6 +227,10 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     uint32_t* ring     = reinterpret_cast<uint32_t*>(work);
     float* stage       = reinterpret_cast<float*>(work + kRingWords);
     int32_t* cbase     = work + kRingWords + kStageWords;
+    // frontiers of the sub-group passes: the staging area (free between passes), or the spill kernel's global ones
+    int32_t* subA      = kSpill ? frontA : work + kRingWords;
+    int32_t* subB      = kSpill ? frontB : work + kRingWords + kSubFront;
+    const int subCap   = kSpill ? frontCap : min(frontCap, kSubFront);
     int32_t* rowsInt   = reinterpret_cast<int32_t*>(po.rows);
     const unsigned cap = ngmax + 1; // stored entries per lane, the target included
     const unsigned blocksMax = listBlocksMax(ngmax);
@@ -231,181 +240,29 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     const uint32_t padCode = chunkCode(0, valid ? lane : unsigned(last - 1 - (first + g * 64)));
 
     RowAlloc ra;
-    unsigned ncSph = 1, cnt = 0, fb = 0, T = 0, slot = 1, nT = 0;
+    unsigned ncSph = 1, cnt = 0, fb = 0, T = 0, slot = 1, nT = 0, nTall = 0;
     unsigned long long nStagedLast = 0, nSubLast = 0;
     uint32_t selfCode = padCode;
     int round = 0;
-    bool chunkOvf = false;
+    bool chunkOvf = false, didSplit = false;
+    // Sub-group passes (target-group splitting, reference traversal/groups.cuh:188-303): a group whose frontier or
+    // candidate-leaf list overflows is searched as consecutive lane ranges of 32, 16, ... targets, each with its own
+    // tight search box (a group straddling an SFC jump has one box over both regions: hundreds of candidate leaves).
+    // Lanes outside the range neither touch leaves nor hit; the ranges share the group's chunk table (reserved at its
+    // capacity then) and every lane's hit ring, so the lists come out as one group's. The ring holds earlier passes'
+    // pending hits, so later passes traverse in the staging area past it (kSubFront per frontier; the spill kernel's
+    // global frontiers otherwise). Only a range of kMinSub lanes that still overflows goes to the spill kernel.
+    // range length the round starts with: the previous round's split level (iterateH bit 2, tests: passes of 16)
+    int len0 = (iterateH & 4) ? 16 : 64;
     for (;; ++round)
     {
-        // 1. group search box
-        double r     = 2.0 * double(hi);
-        double lo[3] = {valid ? xi - r : 1e300, valid ? yi - r : 1e300, valid ? zi - r : 1e300};
-        double hh[3] = {valid ? xi + r : -1e300, valid ? yi + r : -1e300, valid ? zi + r : -1e300};
-        double gc[3], gs[3];
-        for (int d = 0; d < 3; ++d)
-        {
-            double a = waveMin(lo[d]);
-            double b = waveMax(hh[d]);
-            gc[d]    = 0.5 * (a + b);
-            gs[d]    = 0.5 * (b - a);
-        }
-
-        // 2. breadth-first traversal
-        int32_t* cur = frontA;
-        int32_t* nxt = frontB;
-        int nf       = 1;
-        int nLeaves  = 0;
-        if (lane == 0) cur[0] = 0;
-        waveSync<kSpill>();
-        while (nf > 0)
-        {
-            int nn = 0;
-            for (int base = 0; base < nf; base += 64)
-            {
-                int idx     = base + int(lane);
-                int32_t nd  = idx < nf ? ldList<kSpill>(cur + idx) : -1;
-                bool hit    = nd >= 0 && boxesOverlapF(gc, gs, t.center + 3 * nd, t.half + 3 * nd, fold);
-                bool isLeaf = hit && t.n2l[nd] >= 0;
-                bool isInt  = hit && !isLeaf;
-                uint64_t ml = ballot(isLeaf);
-                uint64_t mi = ballot(isInt);
-                int pl      = __popcll(ml & lanemaskLt());
-                int pi      = __popcll(mi & lanemaskLt());
-                if (isLeaf)
-                {
-                    int pos = nLeaves + pl;
-                    if (pos < leafCap) leaves[pos] = nd;
-                }
-                if (isInt)
-                {
-                    int pos    = nn + 8 * pi;
-                    int32_t co = t.child[nd];
-                    if (pos + 8 <= frontCap)
-                        for (int k = 0; k < 8; ++k)
-                            nxt[pos + k] = co + k;
-                }
-                nLeaves += __popcll(ml);
-                nn += 8 * __popcll(mi);
-            }
-            waveSync<kSpill>();
-            if (nn > frontCap || nLeaves > leafCap) { return false; }
-            int32_t* tmp = cur;
-            cur          = nxt;
-            nxt          = tmp;
-            nf           = nn;
-        }
-
-        // the fp32 group frame is valid if the folded group neighborhood cannot alias across a periodic boundary
-        bool relOk = true;
-        double R   = 0;
-        for (int d = 0; d < 3; ++d)
-        {
-            R = fmax(R, gs[d]);
-            if (box.bc[d] == kPeriodic && 2.0 * gs[d] > 0.45 * box.len(d)) relOk = false;
-        }
-        // group frame from the fixed-point positions (QFrame): int32 difference to the quantized group center (in
-        // periodic dimensions the wrapping difference is the minimum image), one fp32 rounding
-        uint32_t gq[3];
-        for (int d = 0; d < 3; ++d)
-            gq[d] = uint32_t(__builtin_amdgcn_readfirstlane(int(quantize(gc[d], qf.lo[d], qf.s[d]))));
-        const float xir = float(int32_t(qi[0] - gq[0])) * qf.inv[0];
-        const float yir = float(int32_t(qi[1] - gq[1])) * qf.inv[1];
-        const float zir = float(int32_t(qi[2] - gq[2])) * qf.inv[2];
-        const float r2f = 4.0f * hi * hi;
-        // rounding of the fp32 distance^2 around the radius: coordinates carry |err| <= delta each (quantization of
-        // the positions + fp32 rounding of the separation)
-        const float delta = float(R) * 6.0e-7f + qmax + 1e-30f;
-        // (without a valid fp32 frame every candidate takes the fp64 test; the bound stays finite so that the +inf
-        // staging sentinels never do)
-        const float band  = relOk ? 8.0f * hi * delta + 4.0f * delta * delta : 1.0e37f;
-        const double radiusSq = double(r2f);
-        // thresholds: d2 < lo is a hit, lo <= d2 <= hi goes to the fp64 re-test; lanes past the group never hit
-        const float thLo = valid ? r2f - band : -1.0f;
-        const float thHi = valid ? r2f + band : -1.0f;
-        const double ip[3] = {xi, yi, zi};
-        // group search box half sizes in the relative fp32 frame, widened by the coordinate rounding
-        const float gsf[3] = {float(gs[0]) + 2.0f * delta, float(gs[1]) + 2.0f * delta, float(gs[2]) + 2.0f * delta};
-        // rounded core box: the box of the group's particles (relative frame) grown by the largest search radius with
-        // rounded edges and corners. Any neighbor of any lane lies inside it; it excludes the corners of the group
-        // search box that no sphere reaches (~23 % of the candidates of a compact lattice group), at a few VALU per
-        // 64 sources in the staging instead of a full test step per candidate
-        float ccr[3], csr[3];
-        {
-            const float pr[3] = {xir, yir, zir};
-            for (int d = 0; d < 3; ++d)
-            {
-                const float a = waveMin(valid ? pr[d] : 3.4e38f), b = waveMax(valid ? pr[d] : -3.4e38f);
-                ccr[d]        = 0.5f * (a + b);
-                csr[d]        = 0.5f * (b - a) + 2.0f * delta;
-            }
-        }
-        const float rcore  = 2.0f * waveMax(valid ? hi : 0.0f) + 4.0f * delta;
-        const float rcore2 = rcore * rcore;
-        // statistics (opt-in): rounded boxes of the eight 8-lane sub-groups (what-if filter, counted only)
-        float sbc[3] = {0, 0, 0}, sbh[3] = {0, 0, 0}, sbr = 0;
-        unsigned long long nStaged = 0, nSub = 0;
-#ifdef SPHX_NS_STATS
-        if (iterateH & 2)
-        {
-            const float pr[3] = {xir, yir, zir};
-            for (int d = 0; d < 3; ++d)
-            {
-                float a = valid ? pr[d] : 3.4e38f, b = valid ? pr[d] : -3.4e38f;
-                for (int o = 1; o < 8; o <<= 1)
-                {
-                    a = fminf(a, __shfl_xor(a, o));
-                    b = fmaxf(b, __shfl_xor(b, o));
-                }
-                sbc[d] = 0.5f * (a + b);
-                sbh[d] = 0.5f * (b - a) + 2.0f * delta;
-            }
-            float hm = valid ? hi : 0.0f;
-            for (int o = 1; o < 8; o <<= 1)
-                hm = fmaxf(hm, __shfl_xor(hm, o));
-            sbr = 2.0f * hm + 4.0f * delta;
-        }
-#endif
-
-        // 3. touched leaves, compacted in place; chunk count -> rows of the chunk table
-        {
-            const float rt  = 2.0f * hi + 4.0f * delta;
-            const float rt2 = valid ? rt * rt : -1.0f;
-            unsigned nch = 1;
-            nT           = 0;
-            for (int l = 0; l < nLeaves; ++l)
-            {
-                const int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + l));
-                const double lc[3] = {ldConst(t.center + 3 * nd), ldConst(t.center + 3 * nd + 1),
-                                      ldConst(t.center + 3 * nd + 2)};
-                const double lh[3] = {ldConst(t.half + 3 * nd), ldConst(t.half + 3 * nd + 1),
-                                      ldConst(t.half + 3 * nd + 2)};
-                bool touch;
-                if (relOk)
-                {
-                    // leaf box in the group frame (uniform), point-box distance per lane in fp32
-                    const float ax = fmaxf(fabsf(xir - float(fold(lc[0] - gc[0], 0))) - float(lh[0]), 0.0f);
-                    const float ay = fmaxf(fabsf(yir - float(fold(lc[1] - gc[1], 1))) - float(lh[1]), 0.0f);
-                    const float az = fmaxf(fabsf(zir - float(fold(lc[2] - gc[2], 2))) - float(lh[2]), 0.0f);
-                    touch = ax * ax + ay * ay + az * az < rt2;
-                }
-                else { touch = valid && pointBoxDistSq(ip, lc, lh, box) < radiusSq; }
-                if (!ballot(touch)) continue;
-                if (lane == 0) leaves[nT] = nd;
-                nT++;
-                nch += unsigned(ldConst(t.ne + nd) - ldConst(t.ns + nd) + 63) >> 6;
-            }
-            waveSync<kSpill>();
-            chunkOvf = nch > kChunkCap;
-            if (chunkOvf) nT = 0; // reported below; the host raises
-            T = chunkTabRows(min(nch, kChunkCap));
-            ra.ensure(T, g, po);
-        }
-
-        // 4. candidates
-        fb       = 0;
-        slot     = 1;
-        selfCode = padCode;
+        fb        = 0;
+        slot      = 1;
+        selfCode  = padCode;
+        T         = 0;
+        nTall     = 0;
+        chunkOvf  = false;
+        didSplit  = len0 < 64;
         // Hit ring: linear, [slot][lane] (a store's bank is its lane whatever the slot). wp = this lane's byte address
         // of its next free slot, so an append is one ds_write + one v_add. A flush stores slots 0..7 as one list
         // block and moves slots 8..15 down.
@@ -415,9 +272,6 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         const uint32_t wFlush   = laneBase + 12u * 256u; // a lane at 12 pending entries triggers a flush
         unsigned fbDrop = 0; // blocks of a lane past its list capacity (a round that repeats): counted, not stored
         unsigned extra  = 0; // capped lists (no h iteration): hits past the cap, counted, not stored
-        // rows: home rows exist without atomics; more only when a flush might need them
-        ra.ensure(min(po.home, po.rowsMax), g, po);
-        ra.ensure(T, g, po);
         unsigned flushes = 0; // flush events of this round (a lane's block count is at most this)
         // store one block (ring slots 0..7, slots k >= nv replaced by the padding code) for every lane in `who` and
         // shift its remaining entries down
@@ -449,207 +303,416 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                 else fbDrop += 1;
             }
         };
-        // staging: groups of four candidates (two pairs) as five float4 {x0 x1 y0 y1} {z0 z1 cc0 cc1} x2 + {codes},
-        // so one pointer walks a test with immediate offsets
-        auto stagePut = [&](unsigned p, float xr, float yr, float zr, uint32_t code)
+
+        int pos = 0, len = len0, lenMin = len0;
+        while (pos < 64)
         {
-            const unsigned q = (p >> 2) & (kStagePairs / 2 - 1), r = p & 3;
-            float* e         = stage + q * 20 + (r >> 1) * 8 + (r & 1);
-            e[0]             = xr;
-            e[2]             = yr;
-            e[4]             = zr;
-            e[6]             = xr * xr + yr * yr + zr * zr;
-            reinterpret_cast<uint32_t*>(stage)[q * 20 + 16 + r] = code;
-        };
-        unsigned sHead = 0, sTail = 0; // wave-uniform candidate positions in the staging ring
-        // dot-product form of the distance test: d2 = cc_j - 2 c_j.x_i + |x_i|^2 with cc_j = |c_j|^2 staged per
-        // candidate, so a pair of candidates costs three v_pk_fma_f32 and |x_i|^2 moves into the thresholds. The
-        // cancellation (terms up to the squared group extent Rg^2) widens the rounding band by 8 ulp of 4 Rg^2; the fp64
-        // re-test keeps the sets exact
-        const f2 mx2 = {-2.0f * xir, -2.0f * xir}, my2 = {-2.0f * yir, -2.0f * yir}, mz2 = {-2.0f * zir, -2.0f * zir};
-        const float ii  = xir * xir + yir * yir + zir * zir;
-        const float rg2 = float(gs[0] * gs[0] + gs[1] * gs[1] + gs[2] * gs[2]) + 3.0f * delta;
-        const float bandDot = relOk ? 2.0e-6f * rg2 : 0.0f;
-        const float thLoI = valid ? thLo - bandDot - ii : -3.4e38f;
-        const float thHiI = valid ? thHi + bandDot - ii : -3.4e38f;
-        // fp64 re-test of a candidate in the rounding band of some lane (rare): returns the corrected hit mask
-        auto bandRetest = [&](float d2, uint32_t code, uint64_t hm) -> uint64_t
-        {
-            bool hit = (hm >> lane) & 1;
-            const uint32_t cu = uint32_t(__builtin_amdgcn_readfirstlane(int(code)));
-            const int32_t ju  = __builtin_amdgcn_readfirstlane(cbase[(cu & kChunkSlotMask) & (kCbase - 1)]) +
-                               int32_t(cu >> kChunkSlotBits);
-            SPHX_DCHECK(uint32_t(ju) < ntot, 5);
-            if (uint32_t(ju) < ntot) // (always, for staged sources; a guard against wild scalar loads)
+            // ---- one pass: the targets of lanes [pos, pos + len)
+            const bool act = valid && int(lane) >= pos && int(lane) < pos + len;
+            if (!ballot(act))
             {
-                const double d64 = distanceSqPbc(ldConst(x + ju), ldConst(y + ju), ldConst(z + ju), xi, yi, zi, box);
-                hit              = hit || (d2 <= thHiI && d64 < radiusSq);
+                pos += len;
+                continue;
             }
-            return ballot(hit);
-        };
-        // append `code` for the lanes in `hm`: exec-masked and branch-free (the compiler placed the store blocks out of
-        // line behind a taken branch per candidate). The LDS store is not counted by the compiler's lgkmcnt waits; the
-        // ring is only read by later LDS loads of this wave, which the in-order LDS queue orders after it.
-        auto append = [&](uint64_t hm, uint32_t code)
-        {
-            uint64_t save;
-            if constexpr (kCapped)
+            // 1. search box of the pass
+            double r     = 2.0 * double(hi);
+            double lo[3] = {act ? xi - r : 1e300, act ? yi - r : 1e300, act ? zi - r : 1e300};
+            double hh[3] = {act ? xi + r : -1e300, act ? yi + r : -1e300, act ? zi + r : -1e300};
+            double gc[3], gs[3];
+            for (int d = 0; d < 3; ++d)
             {
-                // (no h iteration: test and tool runs) keep the first cap entries, count the rest
-                if ((hm >> lane) & 1)
+                double a = waveMin(lo[d]);
+                double b = waveMax(hh[d]);
+                gc[d]    = 0.5 * (a + b);
+                gs[d]    = 0.5 * (b - a);
+            }
+
+            // 2. breadth-first traversal (the first pass of a round may use the ring's area: nothing is pending yet)
+            const bool mainArea = pos == 0;
+            int32_t* cur        = mainArea ? frontA : subA;
+            int32_t* nxt        = mainArea ? frontB : subB;
+            const int fcap      = mainArea ? frontCap : subCap;
+            int nf              = 1;
+            int nLeaves         = 0;
+            bool overflow       = false;
+            if (lane == 0) cur[0] = 0;
+            waveSync<kSpill>();
+            while (nf > 0)
+            {
+                int nn = 0;
+                for (int base = 0; base < nf; base += 64)
                 {
-                    if (8 * fb + ((wp - laneBase) >> 8) < cap)
+                    int idx     = base + int(lane);
+                    int32_t nd  = idx < nf ? ldList<kSpill>(cur + idx) : -1;
+                    bool hit    = nd >= 0 && boxesOverlapF(gc, gs, t.center + 3 * nd, t.half + 3 * nd, fold);
+                    bool isLeaf = hit && t.n2l[nd] >= 0;
+                    bool isInt  = hit && !isLeaf;
+                    uint64_t ml = ballot(isLeaf);
+                    uint64_t mi = ballot(isInt);
+                    int pl      = __popcll(ml & lanemaskLt());
+                    int pi      = __popcll(mi & lanemaskLt());
+                    if (isLeaf)
                     {
-                        *reinterpret_cast<LdsU32*>(uintptr_t(wp)) = code;
-                        wp += 256u;
+                        int pos2 = nLeaves + pl;
+                        if (pos2 < leafCap) leaves[pos2] = nd;
                     }
-                    else extra += 1;
+                    if (isInt)
+                    {
+                        int pos2   = nn + 8 * pi;
+                        int32_t co = t.child[nd];
+                        if (pos2 + 8 <= fcap)
+                            for (int k = 0; k < 8; ++k)
+                                nxt[pos2 + k] = co + k;
+                    }
+                    nLeaves += __popcll(ml);
+                    nn += 8 * __popcll(mi);
+                }
+                waveSync<kSpill>();
+                if (nn > fcap || nLeaves > leafCap)
+                {
+                    overflow = true;
+                    break;
+                }
+                int32_t* tmp = cur;
+                cur          = nxt;
+                nxt          = tmp;
+                nf           = nn;
+            }
+            if (overflow)
+            {
+                if (len <= kMinSub) return false; // the spill kernel redoes the whole group
+                len >>= 1;
+                lenMin   = min(lenMin, len);
+                didSplit = true;
+                continue;
+            }
+
+            // the fp32 group frame is valid if the folded group neighborhood cannot alias across a periodic boundary
+            bool relOk = true;
+            double R   = 0;
+            for (int d = 0; d < 3; ++d)
+            {
+                R = fmax(R, gs[d]);
+                if (box.bc[d] == kPeriodic && 2.0 * gs[d] > 0.45 * box.len(d)) relOk = false;
+            }
+            // group frame from the fixed-point positions (QFrame): int32 difference to the quantized group center (in
+            // periodic dimensions the wrapping difference is the minimum image), one fp32 rounding
+            uint32_t gq[3];
+            for (int d = 0; d < 3; ++d)
+                gq[d] = uint32_t(__builtin_amdgcn_readfirstlane(int(quantize(gc[d], qf.lo[d], qf.s[d]))));
+            const float xir = float(int32_t(qi[0] - gq[0])) * qf.inv[0];
+            const float yir = float(int32_t(qi[1] - gq[1])) * qf.inv[1];
+            const float zir = float(int32_t(qi[2] - gq[2])) * qf.inv[2];
+            const float r2f = 4.0f * hi * hi;
+            // rounding of the fp32 distance^2 around the radius: coordinates carry |err| <= delta each (quantization
+            // of the positions + fp32 rounding of the separation)
+            const float delta = float(R) * 6.0e-7f + qmax + 1e-30f;
+            // (without a valid fp32 frame every candidate takes the fp64 test; the bound stays finite so that the +inf
+            // staging sentinels never do)
+            const float band      = relOk ? 8.0f * hi * delta + 4.0f * delta * delta : 1.0e37f;
+            const double radiusSq = double(r2f);
+            // thresholds: d2 < lo is a hit, lo <= d2 <= hi goes to the fp64 re-test; lanes outside the pass never hit
+            const float thLo   = act ? r2f - band : -1.0f;
+            const float thHi   = act ? r2f + band : -1.0f;
+            const double ip[3] = {xi, yi, zi};
+            // pass search box half sizes in the relative fp32 frame, widened by the coordinate rounding
+            const float gsf[3] = {float(gs[0]) + 2.0f * delta, float(gs[1]) + 2.0f * delta,
+                                  float(gs[2]) + 2.0f * delta};
+            // rounded core box: the box of the pass's particles (relative frame) grown by the largest search radius
+            // with rounded edges and corners. Any neighbor of any lane lies inside it; it excludes the corners of the
+            // search box that no sphere reaches (~23 % of the candidates of a compact lattice group), at a few VALU per
+            // 64 sources in the staging instead of a full test step per candidate
+            float ccr[3], csr[3];
+            {
+                const float pr[3] = {xir, yir, zir};
+                for (int d = 0; d < 3; ++d)
+                {
+                    const float a = waveMin(act ? pr[d] : 3.4e38f), b = waveMax(act ? pr[d] : -3.4e38f);
+                    ccr[d]        = 0.5f * (a + b);
+                    csr[d]        = 0.5f * (b - a) + 2.0f * delta;
                 }
             }
-            else
+            const float rcore  = 2.0f * waveMax(act ? hi : 0.0f) + 4.0f * delta;
+            const float rcore2 = rcore * rcore;
+            // statistics (opt-in): rounded boxes of the eight 8-lane sub-groups (what-if filter, counted only)
+            float sbc[3] = {0, 0, 0}, sbh[3] = {0, 0, 0}, sbr = 0;
+            unsigned long long nStaged = 0, nSub = 0;
+#ifdef SPHX_NS_STATS
+            if (iterateH & 2)
             {
-                // with the h iteration a lane past the cap repeats the round, and only the final round's lists are
-                // kept: its blocks past the capacity are dropped (storeBlock), so the ring never overflows
-                asm volatile("s_and_saveexec_b64 %[sv], %[m]\n"
-                             "ds_write_b32 %[wp], %[code]\n"
-                             "v_add_u32_e32 %[wp], 0x100, %[wp]\n"
-                             "s_or_b64 exec, exec, %[sv]"
-                             : [wp] "+v"(wp), [sv] "=&s"(save)
-                             : [m] "s"(hm), [code] "v"(code)
-                             : "memory");
+                const float pr[3] = {xir, yir, zir};
+                for (int d = 0; d < 3; ++d)
+                {
+                    float a = act ? pr[d] : 3.4e38f, b = act ? pr[d] : -3.4e38f;
+                    for (int o = 1; o < 8; o <<= 1)
+                    {
+                        a = fminf(a, __shfl_xor(a, o));
+                        b = fmaxf(b, __shfl_xor(b, o));
+                    }
+                    sbc[d] = 0.5f * (a + b);
+                    sbh[d] = 0.5f * (b - a) + 2.0f * delta;
+                }
+                float hm = act ? hi : 0.0f;
+                for (int o = 1; o < 8; o <<= 1)
+                    hm = fmaxf(hm, __shfl_xor(hm, o));
+                sbr = 2.0f * hm + 4.0f * delta;
             }
-        };
-        /* Test `count` (a multiple of 4, <= 64) staged candidates against every lane: four candidates (five broadcast
-         * ds_read_b128) per step, one ring check per step. A test always starts at a half of the staging ring (sHead
-         * is a multiple of 64) and never wraps. Measured alternative (profiles/r3_perf_log.md): per-lane hit masks
-         * built with one v_addc per candidate and appended in batches of 32 made the loop VALU-bound in the append
-         * (+18 % VALU, search 31.9 -> 37.9 ms). */
-        auto testStaged = [&](unsigned count)
-        {
-#ifdef SPHX_NS_TIMING_NOTEST // timing experiments only (no usable lists)
-            sHead += count;
-            return;
 #endif
-            const float4* sp = reinterpret_cast<const float4*>(stage) + ((sHead >> 2) & (kStagePairs / 2 - 1)) * 5;
-#pragma nounroll
-            for (unsigned k = 0; k < count; k += 4)
+
+            // 3. touched leaves, compacted in place; chunk count -> rows of the chunk table
             {
-                float4 C[5];
-#pragma unroll
-                for (int u = 0; u < 5; ++u)
-                    C[u] = sp[u];
-                sp += 5;
-                float dd[4];
-#pragma unroll
-                for (int p = 0; p < 2; ++p)
+                const float rt  = 2.0f * hi + 4.0f * delta;
+                const float rt2 = act ? rt * rt : -1.0f;
+                unsigned nch    = 0;
+                nT              = 0;
+                for (int l = 0; l < nLeaves; ++l)
                 {
-                    const float4 A = C[2 * p], B = C[2 * p + 1];
-                    f2 t = f2{B.z, B.w};
-                    t    = __builtin_elementwise_fma(f2{A.x, A.y}, mx2, t);
-                    t    = __builtin_elementwise_fma(f2{A.z, A.w}, my2, t);
-                    t    = __builtin_elementwise_fma(f2{B.x, B.y}, mz2, t);
-                    dd[2 * p]     = t.x;
-                    dd[2 * p + 1] = t.y;
+                    const int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + l));
+                    const double lc[3] = {ldConst(t.center + 3 * nd), ldConst(t.center + 3 * nd + 1),
+                                          ldConst(t.center + 3 * nd + 2)};
+                    const double lh[3] = {ldConst(t.half + 3 * nd), ldConst(t.half + 3 * nd + 1),
+                                          ldConst(t.half + 3 * nd + 2)};
+                    bool touch;
+                    if (relOk)
+                    {
+                        // leaf box in the group frame (uniform), point-box distance per lane in fp32
+                        const float ax = fmaxf(fabsf(xir - float(fold(lc[0] - gc[0], 0))) - float(lh[0]), 0.0f);
+                        const float ay = fmaxf(fabsf(yir - float(fold(lc[1] - gc[1], 1))) - float(lh[1]), 0.0f);
+                        const float az = fmaxf(fabsf(zir - float(fold(lc[2] - gc[2], 2))) - float(lh[2]), 0.0f);
+                        touch = ax * ax + ay * ay + az * az < rt2;
+                    }
+                    else { touch = act && pointBoxDistSq(ip, lc, lh, box) < radiusSq; }
+                    if (!ballot(touch)) continue;
+                    if (lane == 0) leaves[nT] = nd;
+                    nT++;
+                    nch += unsigned(ldConst(t.ne + nd) - ldConst(t.ns + nd) + 63) >> 6;
                 }
-                const uint32_t code[4] = {__float_as_uint(C[4].x), __float_as_uint(C[4].y), __float_as_uint(C[4].z),
-                                          __float_as_uint(C[4].w)};
-                // hit masks (SGPRs) of the four candidates; one rarely taken branch covers their band re-tests, so the
-                // common path runs straight through (a taken branch per candidate cost more)
-                uint64_t hm[4];
-                uint64_t anyBand = 0;
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
+                waveSync<kSpill>();
+                if (T == 0)
                 {
-                    hm[u] = ballot(dd[u] < thLoI);
-                    anyBand |= ballot(dd[u] <= thHiI) ^ hm[u]; // (lane masks: SALU only)
+                    // table rows: exact for a single pass, the capacity once the group is split (later passes add
+                    // slots after list blocks have been stored at ordinals T + b)
+                    const bool single = pos == 0 && len == 64;
+                    T = single ? chunkTabRows(min(1 + nch, kChunkCap)) : kChunkTabRowsMax;
+                    ra.ensure(min(po.home, po.rowsMax), g, po);
+                    ra.ensure(T, g, po);
                 }
-                if (__builtin_expect(anyBand != 0, 0))
+                chunkOvf = slot + nch > kChunkCap;
+                if (chunkOvf) nT = 0; // reported below; the host raises
+                nTall += nT;
+            }
+
+            // 4. candidates
+            // staging: groups of four candidates (two pairs) as five float4 {x0 x1 y0 y1} {z0 z1 cc0 cc1} x2 + {codes},
+            // so one pointer walks a test with immediate offsets
+            auto stagePut = [&](unsigned p, float xr, float yr, float zr, uint32_t code)
+            {
+                const unsigned q = (p >> 2) & (kStagePairs / 2 - 1), rr = p & 3;
+                float* e         = stage + q * 20 + (rr >> 1) * 8 + (rr & 1);
+                e[0]             = xr;
+                e[2]             = yr;
+                e[4]             = zr;
+                e[6]             = xr * xr + yr * yr + zr * zr;
+                reinterpret_cast<uint32_t*>(stage)[q * 20 + 16 + rr] = code;
+            };
+            unsigned sHead = 0, sTail = 0; // wave-uniform candidate positions in the staging ring
+            // dot-product form of the distance test: d2 = cc_j - 2 c_j.x_i + |x_i|^2 with cc_j = |c_j|^2 staged per
+            // candidate, so a pair of candidates costs three v_pk_fma_f32 and |x_i|^2 moves into the thresholds. The
+            // cancellation (terms up to the squared group extent Rg^2) widens the rounding band by 8 ulp of 4 Rg^2;
+            // the fp64 re-test keeps the sets exact
+            const f2 mx2 = {-2.0f * xir, -2.0f * xir}, my2 = {-2.0f * yir, -2.0f * yir},
+                     mz2 = {-2.0f * zir, -2.0f * zir};
+            const float ii      = xir * xir + yir * yir + zir * zir;
+            const float rg2     = float(gs[0] * gs[0] + gs[1] * gs[1] + gs[2] * gs[2]) + 3.0f * delta;
+            const float bandDot = relOk ? 2.0e-6f * rg2 : 0.0f;
+            const float thLoI   = act ? thLo - bandDot - ii : -3.4e38f;
+            const float thHiI   = act ? thHi + bandDot - ii : -3.4e38f;
+            // fp64 re-test of a candidate in the rounding band of some lane (rare): returns the corrected hit mask
+            auto bandRetest = [&](float d2, uint32_t code, uint64_t hm) -> uint64_t
+            {
+                bool hit = (hm >> lane) & 1;
+                const uint32_t cu = uint32_t(__builtin_amdgcn_readfirstlane(int(code)));
+                const int32_t ju  = __builtin_amdgcn_readfirstlane(cbase[(cu & kChunkSlotMask) & (kCbase - 1)]) +
+                                   int32_t(cu >> kChunkSlotBits);
+                SPHX_DCHECK(uint32_t(ju) < ntot, 5);
+                if (uint32_t(ju) < ntot) // (always, for staged sources; a guard against wild scalar loads)
                 {
+                    const double d64 = distanceSqPbc(ldConst(x + ju), ldConst(y + ju), ldConst(z + ju), xi, yi, zi, box);
+                    hit              = hit || (d2 <= thHiI && d64 < radiusSq);
+                }
+                return ballot(hit);
+            };
+            // append `code` for the lanes in `hm`: exec-masked and branch-free (the compiler placed the store blocks
+            // out of line behind a taken branch per candidate). The LDS store is not counted by the compiler's lgkmcnt
+            // waits; the ring is only read by later LDS loads of this wave, which the in-order LDS queue orders after it.
+            auto append = [&](uint64_t hm, uint32_t code)
+            {
+                uint64_t save;
+                if constexpr (kCapped)
+                {
+                    // (no h iteration: test and tool runs) keep the first cap entries, count the rest
+                    if ((hm >> lane) & 1)
+                    {
+                        if (8 * fb + ((wp - laneBase) >> 8) < cap)
+                        {
+                            *reinterpret_cast<LdsU32*>(uintptr_t(wp)) = code;
+                            wp += 256u;
+                        }
+                        else extra += 1;
+                    }
+                }
+                else
+                {
+                    // with the h iteration a lane past the cap repeats the round, and only the final round's lists are
+                    // kept: its blocks past the capacity are dropped (storeBlock), so the ring never overflows
+                    asm volatile("s_and_saveexec_b64 %[sv], %[m]\n"
+                                 "ds_write_b32 %[wp], %[code]\n"
+                                 "v_add_u32_e32 %[wp], 0x100, %[wp]\n"
+                                 "s_or_b64 exec, exec, %[sv]"
+                                 : [wp] "+v"(wp), [sv] "=&s"(save)
+                                 : [m] "s"(hm), [code] "v"(code)
+                                 : "memory");
+                }
+            };
+            /* Test `count` (a multiple of 4, <= 64) staged candidates against every lane: four candidates (five
+             * broadcast ds_read_b128) per step, one ring check per step. A test always starts at a half of the staging
+             * ring (sHead is a multiple of 64) and never wraps. Measured alternative (profiles/r3_perf_log.md): per-lane
+             * hit masks built with one v_addc per candidate and appended in batches of 32 made the loop VALU-bound in
+             * the append (+18 % VALU, search 31.9 -> 37.9 ms). */
+            auto testStaged = [&](unsigned count)
+            {
+#ifdef SPHX_NS_TIMING_NOTEST // timing experiments only (no usable lists)
+                sHead += count;
+                return;
+#endif
+                const float4* sp = reinterpret_cast<const float4*>(stage) + ((sHead >> 2) & (kStagePairs / 2 - 1)) * 5;
+#pragma nounroll
+                for (unsigned k = 0; k < count; k += 4)
+                {
+                    float4 C[5];
+#pragma unroll
+                    for (int u = 0; u < 5; ++u)
+                        C[u] = sp[u];
+                    sp += 5;
+                    float dd[4];
+#pragma unroll
+                    for (int p = 0; p < 2; ++p)
+                    {
+                        const float4 A = C[2 * p], B = C[2 * p + 1];
+                        f2 tt = f2{B.z, B.w};
+                        tt    = __builtin_elementwise_fma(f2{A.x, A.y}, mx2, tt);
+                        tt    = __builtin_elementwise_fma(f2{A.z, A.w}, my2, tt);
+                        tt    = __builtin_elementwise_fma(f2{B.x, B.y}, mz2, tt);
+                        dd[2 * p]     = tt.x;
+                        dd[2 * p + 1] = tt.y;
+                    }
+                    const uint32_t code[4] = {__float_as_uint(C[4].x), __float_as_uint(C[4].y),
+                                              __float_as_uint(C[4].z), __float_as_uint(C[4].w)};
+                    // hit masks (SGPRs) of the four candidates; one rarely taken branch covers their band re-tests, so
+                    // the common path runs straight through (a taken branch per candidate cost more)
+                    uint64_t hm[4];
+                    uint64_t anyBand = 0;
 #pragma unroll
                     for (int u = 0; u < 4; ++u)
-                        if (ballot(dd[u] <= thHiI) != hm[u]) hm[u] = bandRetest(dd[u], code[u], hm[u]);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    append(hm[u], code[u]);
-                if (ballot(wp >= wFlush)) storeBlock(wp >= laneBase + 8u * 256u, 8);
-            }
-            sHead += count;
-        };
-#ifdef SPHX_NS_TIMING_NOCAND // timing experiments only (no usable lists)
-        nT = 0;
-#endif
-        for (unsigned l = 0; l < nT; ++l)
-        {
-            const int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + l));
-            const int32_t a  = ldConst(t.ns + nd);
-            const int32_t b  = ldConst(t.ne + nd);
-            for (int32_t c0 = a; c0 < b; c0 += 64)
-            {
-                const int32_t j = c0 + int32_t(lane);
-                float xr = 0, yr = 0, zr = 0;
-                bool inBox = false;
-                if (j < b)
-                {
-                    const SrcPosQ rj = xq[j];
-                    xr               = float(int32_t(rj.x - gq[0])) * qf.inv[0];
-                    yr               = float(int32_t(rj.y - gq[1])) * qf.inv[1];
-                    zr               = float(int32_t(rj.z - gq[2])) * qf.inv[2];
-                    // only sources inside the group search box can be a neighbor of any lane
-                    const float ax = fmaxf(fabsf(xr - ccr[0]) - csr[0], 0.0f);
-                    const float ay = fmaxf(fabsf(yr - ccr[1]) - csr[1], 0.0f);
-                    const float az = fmaxf(fabsf(zr - ccr[2]) - csr[2], 0.0f);
-#if SPHX_NS_ROUNDED
-                    inBox = !relOk || (fabsf(xr) <= gsf[0] && fabsf(yr) <= gsf[1] && fabsf(zr) <= gsf[2] &&
-                                       ax * ax + ay * ay + az * az <= rcore2);
-#else
-                    inBox = !relOk || (fabsf(xr) <= gsf[0] && fabsf(yr) <= gsf[1] && fabsf(zr) <= gsf[2]);
-                    (void)ax, (void)ay, (void)az;
-#endif
-                }
-                const uint64_t m = ballot(inBox);
-                if (!m) continue;
-#ifdef SPHX_NS_STATS
-                if (iterateH & 2) // statistics: staged candidates, and those inside some sub-group rounded box
-                {
-                    bool inSub = false;
-                    for (int q = 0; q < 8; ++q)
                     {
-                        const float ax = fmaxf(fabsf(xr - readLaneF(sbc[0], 8 * q)) - readLaneF(sbh[0], 8 * q), 0.f);
-                        const float ay = fmaxf(fabsf(yr - readLaneF(sbc[1], 8 * q)) - readLaneF(sbh[1], 8 * q), 0.f);
-                        const float az = fmaxf(fabsf(zr - readLaneF(sbc[2], 8 * q)) - readLaneF(sbh[2], 8 * q), 0.f);
-                        const float rq = readLaneF(sbr, 8 * q);
-                        inSub = inSub || ax * ax + ay * ay + az * az <= rq * rq;
+                        hm[u] = ballot(dd[u] < thLoI);
+                        anyBand |= ballot(dd[u] <= thHiI) ^ hm[u]; // (lane masks: SALU only)
                     }
-                    nStaged += __popcll(m);
-                    nSub += __popcll(ballot(inBox && inSub));
+                    if (__builtin_expect(anyBand != 0, 0))
+                    {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (ballot(dd[u] <= thHiI) != hm[u]) hm[u] = bandRetest(dd[u], code[u], hm[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        append(hm[u], code[u]);
+                    if (ballot(wp >= wFlush)) storeBlock(wp >= laneBase + 8u * 256u, 8);
                 }
+                sHead += count;
+            };
+#ifdef SPHX_NS_TIMING_NOCAND // timing experiments only (no usable lists)
+            nT = 0;
 #endif
-                const unsigned s = slot++;
-                if (lane == 0)
+            for (unsigned l = 0; l < nT; ++l)
+            {
+                const int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + l));
+                const int32_t a  = ldConst(t.ns + nd);
+                const int32_t b  = ldConst(t.ne + nd);
+                for (int32_t c0 = a; c0 < b; c0 += 64)
                 {
-                    const unsigned rw = ra.rowU(s >> 8);
-                    if (rw < po.poolRows) rowsInt[size_t(rw) * 256 + (s & 255)] = c0;
-                    cbase[s & (kCbase - 1)] = c0;
-                }
-                if (int64_t(c0) <= i && i < int64_t(c0) + 64) selfCode = chunkCode(s, unsigned(i - c0));
-                // compact the in-box sources into the staging pairs (source order kept: deterministic lists)
-                if (inBox) stagePut(sTail + unsigned(__popcll(m & lanemaskLt())), xr, yr, zr, chunkCode(s, lane));
-                sTail += unsigned(__popcll(m));
-                if (sTail - sHead >= 64)
-                {
-                    waveSync<false>();
-                    testStaged(64);
+                    const int32_t j = c0 + int32_t(lane);
+                    float xr = 0, yr = 0, zr = 0;
+                    bool inBox = false;
+                    if (j < b)
+                    {
+                        const SrcPosQ rj = xq[j];
+                        xr               = float(int32_t(rj.x - gq[0])) * qf.inv[0];
+                        yr               = float(int32_t(rj.y - gq[1])) * qf.inv[1];
+                        zr               = float(int32_t(rj.z - gq[2])) * qf.inv[2];
+                        // only sources inside the pass's search box can be a neighbor of any of its lanes
+                        const float ax = fmaxf(fabsf(xr - ccr[0]) - csr[0], 0.0f);
+                        const float ay = fmaxf(fabsf(yr - ccr[1]) - csr[1], 0.0f);
+                        const float az = fmaxf(fabsf(zr - ccr[2]) - csr[2], 0.0f);
+#if SPHX_NS_ROUNDED
+                        inBox = !relOk || (fabsf(xr) <= gsf[0] && fabsf(yr) <= gsf[1] && fabsf(zr) <= gsf[2] &&
+                                           ax * ax + ay * ay + az * az <= rcore2);
+#else
+                        inBox = !relOk || (fabsf(xr) <= gsf[0] && fabsf(yr) <= gsf[1] && fabsf(zr) <= gsf[2]);
+                        (void)ax, (void)ay, (void)az;
+#endif
+                    }
+                    const uint64_t m = ballot(inBox);
+                    if (!m) continue;
+#ifdef SPHX_NS_STATS
+                    if (iterateH & 2) // statistics: staged candidates, and those inside some sub-group rounded box
+                    {
+                        bool inSub = false;
+                        for (int q = 0; q < 8; ++q)
+                        {
+                            const float ax = fmaxf(fabsf(xr - readLaneF(sbc[0], 8 * q)) - readLaneF(sbh[0], 8 * q), 0.f);
+                            const float ay = fmaxf(fabsf(yr - readLaneF(sbc[1], 8 * q)) - readLaneF(sbh[1], 8 * q), 0.f);
+                            const float az = fmaxf(fabsf(zr - readLaneF(sbc[2], 8 * q)) - readLaneF(sbh[2], 8 * q), 0.f);
+                            const float rq = readLaneF(sbr, 8 * q);
+                            inSub = inSub || ax * ax + ay * ay + az * az <= rq * rq;
+                        }
+                        nStaged += __popcll(m);
+                        nSub += __popcll(ballot(inBox && inSub));
+                    }
+#endif
+                    const unsigned s = slot++;
+                    if (lane == 0)
+                    {
+                        const unsigned rw = ra.rowU(s >> 8);
+                        if (rw < po.poolRows) rowsInt[size_t(rw) * 256 + (s & 255)] = c0;
+                        cbase[s & (kCbase - 1)] = c0;
+                    }
+                    if (int64_t(c0) <= i && i < int64_t(c0) + 64) selfCode = chunkCode(s, unsigned(i - c0));
+                    // compact the in-box sources into the staging pairs (source order kept: deterministic lists)
+                    if (inBox) stagePut(sTail + unsigned(__popcll(m & lanemaskLt())), xr, yr, zr, chunkCode(s, lane));
+                    sTail += unsigned(__popcll(m));
+                    if (sTail - sHead >= 64)
+                    {
+                        waveSync<false>();
+                        testStaged(64);
+                    }
                 }
             }
-        }
-        {
-            // pad the tail to a multiple of 4 with far-away sentinels (d2 = inf: never a hit, never in the band)
-            const unsigned rem = sTail - sHead;
-            const unsigned pad = (4 - (rem & 3)) & 3;
-            if (lane < pad) stagePut(sTail + lane, 0.0f, 0.0f, __builtin_inff(), padCode);
-            waveSync<false>();
-            testStaged(rem + pad);
+            {
+                // pad the tail to a multiple of 4 with far-away sentinels (d2 = inf: never a hit, never in the band)
+                const unsigned rem = sTail - sHead;
+                const unsigned pad = (4 - (rem & 3)) & 3;
+                if (lane < pad) stagePut(sTail + lane, 0.0f, 0.0f, __builtin_inff(), padCode);
+                waveSync<false>();
+                testStaged(rem + pad);
+            }
+            nStagedLast = nStaged;
+            nSubLast    = nSub;
+            if (chunkOvf) break;
+            // next range: back to the largest aligned length the round started with
+            pos += len;
+            while (len < len0 && (pos & (2 * len - 1)) == 0)
+                len <<= 1;
         }
         {
             // entries: 8 per stored block + the pending ones (at most 15: up to two more blocks, the last one padded)
@@ -659,6 +722,8 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
             storeBlock(pend > 0, min(pend, 8u));
             storeBlock(pend > 8, pend - 8);
         }
+        nT   = nTall;
+        len0 = lenMin; // a group that had to split starts the next round split
 
         // 5. smoothing length iteration
         bool repeat = (iterateH & 1) && valid && (ncSph < ngmin || (ncSph - 1) > ngmax);
@@ -722,6 +787,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     {
         if (round >= 10) atomicAdd(&stats[0], 1ull);
         if (chunkOvf) atomicAdd(&stats[6], 1ull);
+        if (didSplit) atomicAdd(&stats[5], 1ull); // groups searched in sub-group passes (final round)
         if (iterateH & 2) // statistics (opt-in): search rounds and touched leaves, summed over groups
         {
             atomicAdd(&stats[3], (unsigned long long)(round + 1));

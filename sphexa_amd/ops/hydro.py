@@ -464,7 +464,10 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
         _lib.cpu().iad_divv_curlv(*args)
 
 
-def compute_av_switches(d, nl: NeighborList, box: Box):
+def compute_av_switches(d, nl: NeighborList, box: Box, alpha_out: torch.Tensor | None = None):
+    """AV switches: new alpha from the old one (read per target only). GPU: ``alpha_out`` receives the new values
+    (default: in place), and the time step comes from the device while the propagator's host copy of it is deferred
+    (d._dt_dev)"""
     nidx, nc = _nl_args(nl, d)
     args = (nl.first, nl.last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(), d["h"].data_ptr(),
@@ -472,21 +475,26 @@ def compute_av_switches(d, nl: NeighborList, box: Box):
             d["xm"].data_ptr(), d["divv"].data_ptr(), float(d.minDt), d["alpha"].data_ptr())
     if _is_gpu(d):
         avs = _rec(d, 1, "av").data_ptr() if (getattr(d, "_av_s_valid", False) and d.fixedPoint) else 0
+        dt_dev = getattr(d, "_dt_dev", None)
+        extra = dict(alphaOut=_p(alpha_out), dtDev=_p(dt_dev))
         if avs:
             # SrcAvV records in workspace B (own range from the IAD loop); alpha also into the momentum records
             ho = _handoff(d)
             done = 1 if handoff_take(d, "avv_own") else 0
             mom = _recM(d).data_ptr() if handoff_take(d, "momq_iad") else 0
             ho.clear()
-            _lib.hip().av_switches(*args, d.size, _recB(d).data_ptr(), _stream(), avs, inDone=done, momOut=mom)
+            _lib.hip().av_switches(*args, d.size, _recB(d).data_ptr(), _stream(), avs, inDone=done, momOut=mom,
+                                   **extra)
             if mom:
                 handoff_mark(d, "momq_own")
         else:
-            _lib.hip().av_switches(*args, *_gpu_tail(d, "av"), avs)
+            _lib.hip().av_switches(*args, *_gpu_tail(d, "av"), avs, **extra)
         d._av_s_valid = False
         d._rec1 = None  # S_i consumed (stream-ordered reuse): not held through the momentum loop
     else:
         _lib.cpu().av_switches(*args)
+        if alpha_out is not None:
+            alpha_out.copy_(d["alpha"])
 
 
 def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = False):

@@ -167,6 +167,8 @@ class NeighborSearchError(RuntimeError):
 _SCRATCH: dict = {}
 # test hook: >0 shrinks the LDS frontier of the GPU search so that groups take the global-memory spill path
 TEST_FRONT_CAP = 0
+# tests: search every target group in sub-group passes of 16 lanes (neighbors.hip searchGroup)
+TEST_FORCE_SPLIT = False
 # collect per-step search statistics on the GPU (rounds, candidate leaves; a few atomics per group)
 COLLECT_STATS = os.environ.get("SPHX_SEARCH_STATS") == "1"
 # the reference throws when the coupled nc/h iteration has not converged after 10 rounds
@@ -251,7 +253,8 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
                               tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
                               d.ng0, ngmax, buf.data_ptr(), nc.data_ptr(),
-                              int(iterate_h) | (2 if COLLECT_STATS else 0), stats.data_ptr(),
+                              int(iterate_h) | (2 if COLLECT_STATS else 0) | (4 if TEST_FORCE_SPLIT else 0),
+                              stats.data_ptr(),
                               scratch.data_ptr(), TEST_FRONT_CAP, _stream(), home=home, ov_stride=ov,
                               m=d["m"].data_ptr(), ntot=d.size, rec=rec.data_ptr())
             # per-stripe row demand of the five pool candidates of the next search (one kernel), the stripe
@@ -324,6 +327,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                                       f"(chunk-table capacity of the GPU lists)")
         _check_convergence(d, int(st[0]))
         d.nc_spilled = int(st[2])
+        d.nc_split = int(st[5])  # groups searched in sub-group passes (neighbors.hip searchGroup)
         d.nc_rounds = int(st[3]) / num_groups  # mean search rounds per group (h iteration)
         d.nc_leaves = int(st[4]) / num_groups  # mean candidate leaves per group and step
         if COLLECT_STATS:  # staged candidates and hits per group; candidates inside sub-group boxes (what-if)

@@ -197,6 +197,33 @@ def test_neighbor_spill_path(gpu, monkeypatch):
     assert neighbor_lists_as_sets(nl, dg["nc"]) == sets_ref
 
 
+@pytest.mark.parametrize("case", ["lattice", "glass_evrard"])
+def test_neighbor_subgroup_passes(gpu, monkeypatch, case):
+    """target-group splitting: groups searched as sub-group passes of 16 lanes (each with its own search box, one
+    shared chunk table) give the same h iteration, counts and neighbor sets as whole-group passes"""
+    from sphexa_amd.app.simulation import Simulation
+    from sphexa_amd.ops import neighbors as N
+
+    if case == "lattice":
+        dg, pg, domg = _setup(gpu, 16, jitter=0.01)
+        pg.sync(domg, dg)
+        tree, box, n = domg.octree, domg.box, dg.size
+    else:
+        sim = Simulation("evrard", n=30, device=gpu)
+        dg, tree, box, n = sim.d, sim.domain.octree, sim.domain.box, sim.d.size
+    h0 = dg["h"].clone()
+    nl_ref = find_neighbors(dg, tree, box, 0, n)
+    nc_ref, h_ref = dg["nc"].clone(), dg["h"].clone()
+    sets_ref = neighbor_lists_as_sets(nl_ref, nc_ref)
+    assert dg.nc_split == 0 or case != "lattice"
+    dg["h"].copy_(h0)
+    monkeypatch.setattr(N, "TEST_FORCE_SPLIT", True)
+    nl = find_neighbors(dg, tree, box, 0, n)
+    assert dg.nc_split == (n + 63) // 64
+    assert torch.equal(dg["nc"], nc_ref) and torch.equal(dg["h"], h_ref)
+    assert neighbor_lists_as_sets(nl, dg["nc"]) == sets_ref
+
+
 @pytest.mark.parametrize("hook", ["front", "caps"])
 def test_gravity_spill_path(gpu, monkeypatch, hook):
     """groups overflowing the LDS stack (front) or the interaction-list slabs (caps) are evaluated by the fused
