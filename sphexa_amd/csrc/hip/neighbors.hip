@@ -497,6 +497,8 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     ra.ensure(min(po.home, po.rowsMax), g, po);
                     ra.ensure(T, g, po);
                 }
+                if (slot + nch > kChunkCap && !(pos == 0 && len == 64))
+                    return false; // passes re-staging shared chunks outgrow the table: the spill kernel (one pass)
                 chunkOvf = slot + nch > kChunkCap;
                 if (chunkOvf) nT = 0; // reported below; the host raises
                 nTall += nT;
