@@ -139,8 +139,12 @@ def build_hip(verbose=False, variant=None, defines=()):
             jobs.append(([hipcc, *flags, *lang, "-c", s, "-o", o], o))
     _compile_all(jobs, verbose)
     if jobs or _newer(target, objs):
-        _run([hipcc, "-shared", f"--offload-arch={ARCH}", *objs, "-o", target,
+        # link to a temporary name and rename: a concurrent reader (a repository snapshot, a running test) sees the
+        # old or the new module, never a partial one
+        tmp = target + ".tmp"
+        _run([hipcc, "-shared", f"--offload-arch={ARCH}", *objs, "-o", tmp,
               f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"])
+        os.replace(tmp, target)
     return target
 
 

@@ -147,6 +147,10 @@ PYBIND11_MODULE(_sphx_hip, m)
                              P<float>(divvMax), rhoHost, Krho, etaAcc, eps, others, prevDt, P<double>(out),
                              P<void>(work), St(s));
           });
+    m.def("field_max", [](int64_t first, int64_t last, Ptr f, Ptr out, Ptr work, Ptr s)
+          { fieldMax(first, last, P<float>(f), P<float>(out), P<void>(work), St(s)); });
+    m.def("fill32", [](Ptr p, uint32_t value, int64_t n, Ptr s) { fill32(P<void>(p), value, n, St(s)); });
+    m.def("memset", [](Ptr p, int value, size_t bytes, Ptr s) { memsetAsync(P<void>(p), value, bytes, St(s)); });
     m.def("scan_temp_bytes", [](int64_t n) { return scanTempBytes(n); });
     m.def("exclusive_scan_i64", [](Ptr in, Ptr out, int64_t n, Ptr tmp, size_t tb, Ptr s)
           { exclusiveScanI64(P<int64_t>(in), P<int64_t>(out), n, P<void>(tmp), tb, St(s)); });

@@ -305,9 +305,24 @@ void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, do
 // Groups whose stack or lists overflow are evaluated by the fused spill kernel (traversal + evaluation with a
 // global-memory stack).
 
+// inner-loop forms of the MFMA P2P / M2P kernels: all tiles of a 16-source (node) block issued up front, then the
+// pair arithmetic source-outer / target-block-inner (four independent accumulator chains per step). A/B on Evrard -n
+// 200 (profiles/r4/gravity_variants.txt): P2P 9.71 -> 9.45 ms, M2P 8.33 -> 7.76 ms (at 3 waves per SIMD: the twelve
+// M2P result tiles need 48 VGPRs; at 4 waves it spills). Undefine with -DSPHX_GRAV_V1 for the pipelined forms.
+#ifndef SPHX_GRAV_V1
+#ifndef SPHX_P2P_V2
+#define SPHX_P2P_V2
+#endif
+#ifndef SPHX_M2P_V2
+#define SPHX_M2P_V2
+#endif
+#endif
+
 #ifndef SPHX_M2P_WAVES
 #ifdef SPHX_GRAV_VALU_M2P
 #define SPHX_M2P_WAVES 6 // launch bound (waves per SIMD) of the M2P kernel
+#elif defined(SPHX_M2P_V2)
+#define SPHX_M2P_WAVES 3 // twelve MFMA result tiles in flight per 16-node block (4 waves spill)
 #else
 #define SPHX_M2P_WAVES 4 // the MFMA M2P holds 16 accumulators + the 4 targets' data per lane (6 waves spill)
 #endif
@@ -487,6 +502,41 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
             for (int r = 0; r < 4; ++r)
                 C[r] = sC[16 * tile + 4 * kq + r];
             const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#ifdef SPHX_M2P_V2
+            // all twelve tiles of the 16-node block issued up front, pair arithmetic node-outer / target-block-inner
+            // (four independent accumulator chains per step)
+            f32x4 Qx[4], Qy[4], Qz[4];
+#pragma unroll
+            for (int tb = 0; tb < 4; ++tb)
+            {
+                Qx[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[tb], zero, 0, 0, 0);
+                Qy[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[tb], zero, 0, 0, 0);
+                Qz[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[tb], zero, 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+#pragma unroll
+                for (int tb = 0; tb < 4; ++tb)
+                {
+                    const float rx  = tx[tb] - C[r].x, ry = ty[tb] - C[r].y, rz = tz[tb] - C[r].z;
+                    const float r2  = rx * rx + ry * ry + rz * rz;
+                    const float ir  = __builtin_amdgcn_rsqf(r2);
+                    const float ir2 = ir * ir;
+                    const float ir5 = ir2 * ir2 * ir;
+                    const float rQr = rx * Qx[tb][r] + ry * Qy[tb][r] + rz * Qz[tb][r];
+                    const float Mir = C[r].w * ir;
+                    const float t1  = rQr * ir5;
+                    const float cmb = __builtin_fmaf(-2.5f, t1, -Mir) * ir2;
+                    ph[tb]          = __builtin_fmaf(-0.5f, t1, ph[tb] - Mir);
+                    ax[tb]          = __builtin_fmaf(cmb, rx, __builtin_fmaf(ir5, Qx[tb][r], ax[tb]));
+                    ay[tb]          = __builtin_fmaf(cmb, ry, __builtin_fmaf(ir5, Qy[tb][r], ay[tb]));
+                    az[tb]          = __builtin_fmaf(cmb, rz, __builtin_fmaf(ir5, Qz[tb][r], az[tb]));
+                }
+            }
+            continue;
+#endif
 #ifdef SPHX_M2P_PIPE
             f32x4 Qxn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[0], zero, 0, 0, 0);
             f32x4 Qyn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[0], zero, 0, 0, 0);
@@ -862,12 +912,17 @@ __device__ inline void flushP2P(const Idx& plst, int n, const GravLists& L, cons
             // A operands of the R2 / H2 tiles stored k-major, so lane (kq, col) fetches its {aR, aH} pair with one
             // conflict-free ds_read_b64 (a per-lane component select of source-major records became divergent
             // 8-way conflicted ds_read_b32s: SQ_LDS_BANK_CONFLICT 2044 per wave, profiles/r3_grav_pmc.md)
+#ifdef SPHX_P2P_V2
+            L.spos[lane] = make_float4(Pn.x, Pn.y, Pn.z, Qn.x);
+            L.sm[lane]   = Pn.w; // |x|^2: the C input of the R2 tiles, 4 consecutive sources per b128 read
+#else
             L.spos[lane]             = Pn;
+            L.sm[lane]               = Qn.x;
+#endif
             L.sab[lane]              = make_float2(Pn.x, Qn.z);
             L.sab[kAbRow + lane]     = make_float2(Pn.y, Qn.y);
             L.sab[2 * kAbRow + lane] = make_float2(Pn.z, 1.f);
             L.sab[3 * kAbRow + lane] = make_float2(1.f, 0.f);
-            L.sm[lane]               = Qn.x;
             ++T.nMfma;
         }
         else
@@ -910,6 +965,48 @@ __device__ inline void flushP2P(const Idx& plst, int n, const GravLists& L, cons
             continue;
         }
         const int nsb = (cnt + 15) >> 4;
+#ifdef SPHX_P2P_V2
+        // all eight tiles of a 16-source block (4 target blocks x R2, H2) issued up front, then the pair arithmetic
+        // source-outer / target-block-inner: four independent accumulator chains per step instead of one chain of
+        // four dependent updates per target block (issue stalls on the accumulations and the MFMA results were ~40 %
+        // of the cycles, profiles/r3_grav_pmc.md)
+        for (int sb = 0; sb < nsb; ++sb)
+        {
+            const float2 ab = L.sab[kq * kAbRow + sb * 16 + (lane & 15)];
+            const float4 c4 = reinterpret_cast<const float4*>(L.sm)[sb * 4 + kq]; // |x_s|^2 of the lane's 4 sources
+            const f32x4 cR  = {c4.x, c4.y, c4.z, c4.w};
+            const f32x4 c0v = {0.f, 0.f, 0.f, 0.f};
+            f32x4 R2[4], H2[4];
+#pragma unroll
+            for (int tb = 0; tb < 4; ++tb)
+            {
+                R2[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ab.x, T.bR2[tb], cR, 0, 0, 0);
+                H2[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ab.y, T.bH2[tb], c0v, 0, 0, 0);
+            }
+            float4 Pr[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                Pr[r] = L.spos[sb * 16 + 4 * kq + r]; // {x, y, z, m}
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+#pragma unroll
+                for (int tb = 0; tb < 4; ++tb)
+                {
+                    float re = maxNoCanon(R2[tb][r], H2[tb][r]);
+                    float ir = __builtin_amdgcn_rsqf(re);
+                    float w  = Pr[r].w * ir * (ir * ir);
+                    T.phi[tb] -= w * R2[tb][r];
+                    T.sx[tb] += w * Pr[r].x;
+                    T.sy[tb] += w * Pr[r].y;
+                    T.sz[tb] += w * Pr[r].z;
+                    T.sw[tb] += w;
+                }
+            }
+        }
+        continue;
+#endif
         for (int sb = 0; sb < nsb; ++sb)
         {
             const float2 ab = L.sab[kq * kAbRow + sb * 16 + (lane & 15)];

@@ -82,6 +82,12 @@ void maxNorm2(int64_t first, int64_t last, const float* ax, const float* ay, con
 void timestepReduce(int64_t first, int64_t last, const float* ax, const float* ay, const float* az,
                     const float* courantDev, double courantHost, const float* divvMax, double rhoHost, double Krho,
                     double etaAcc, double eps, double others, double prevDt, double* out, void* work, hipStream_t s);
+//! *out = max of f over [first, last) (float32 device scalar; two launches)
+void fieldMax(int64_t first, int64_t last, const float* f, float* out, void* work, hipStream_t s);
+//! n 32-bit words at p set to value (hipMemsetD32Async: e.g. +inf for a min-reduced scalar), stream-ordered
+void fill32(void* p, uint32_t value, int64_t n, hipStream_t s);
+//! bytes at p set to value (hipMemsetAsync), stream-ordered
+void memsetAsync(void* p, int value, size_t bytes, hipStream_t s);
 
 // octree.hip
 void nodeCounts(const KeyT* tree, int64_t L, const KeyT* keys, int64_t n, int32_t* counts, hipStream_t s);

@@ -192,7 +192,7 @@ __device__ __forceinline__ bool boxesOverlapF(const double c1[3], const double s
 /*! @brief search of one target group (one wave). Returns false if the frontier or the leaf list overflowed the
  *         given capacities (nothing is written then, the group is retried by the spill kernel).
  */
-template<bool kSpill, bool kCapped>
+template<bool kSpill, bool kCapped, bool kSplit>
 __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t last, const double* __restrict__ x,
                                             const double* __restrict__ y, const double* __restrict__ z,
                                             const SrcPosQ* __restrict__ xq, const QFrame& qf, uint32_t ntot,
@@ -253,7 +253,9 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     // pending hits, so later passes traverse in the staging area past it (kSubFront per frontier; the spill kernel's
     // global frontiers otherwise). Only a range of kMinSub lanes that still overflows goes to the spill kernel.
     // range length the round starts with: the previous round's split level (iterateH bit 2, tests: passes of 16)
-    int len0 = (iterateH & 4) ? 16 : 64;
+    // (kSplit = false: the main kernel's single whole-group pass; an overflow queues the group for the split kernel)
+    int len0 = (kSplit && (iterateH & 4)) ? 16 : 64;
+    if (!kSplit && !kSpill && (iterateH & 4)) return false; // (tests: every group through the split kernel)
     for (;; ++round)
     {
         fb        = 0;
@@ -308,11 +310,14 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         while (pos < 64)
         {
             // ---- one pass: the targets of lanes [pos, pos + len)
-            const bool act = valid && int(lane) >= pos && int(lane) < pos + len;
-            if (!ballot(act))
+            const bool act = kSplit ? valid && int(lane) >= pos && int(lane) < pos + len : valid;
+            if constexpr (kSplit)
             {
-                pos += len;
-                continue;
+                if (!ballot(act))
+                {
+                    pos += len;
+                    continue;
+                }
             }
             // 1. search box of the pass
             double r     = 2.0 * double(hi);
@@ -328,7 +333,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
             }
 
             // 2. breadth-first traversal (the first pass of a round may use the ring's area: nothing is pending yet)
-            const bool mainArea = pos == 0;
+            const bool mainArea = !kSplit || pos == 0;
             int32_t* cur        = mainArea ? frontA : subA;
             int32_t* nxt        = mainArea ? frontB : subB;
             const int fcap      = mainArea ? frontCap : subCap;
@@ -380,7 +385,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
             }
             if (overflow)
             {
-                if (len <= kMinSub) return false; // the spill kernel redoes the whole group
+                if (!kSplit || len <= kMinSub) return false; // queued: split kernel, then the spill kernel
                 len >>= 1;
                 lenMin   = min(lenMin, len);
                 didSplit = true;
@@ -492,12 +497,12 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                 {
                     // table rows: exact for a single pass, the capacity once the group is split (later passes add
                     // slots after list blocks have been stored at ordinals T + b)
-                    const bool single = pos == 0 && len == 64;
+                    const bool single = !kSplit || (pos == 0 && len == 64);
                     T = single ? chunkTabRows(min(1 + nch, kChunkCap)) : kChunkTabRowsMax;
                     ra.ensure(min(po.home, po.rowsMax), g, po);
                     ra.ensure(T, g, po);
                 }
-                if (slot + nch > kChunkCap && !(pos == 0 && len == 64))
+                if (kSplit && slot + nch > kChunkCap && !(pos == 0 && len == 64))
                     return false; // passes re-staging shared chunks outgrow the table: the spill kernel (one pass)
                 chunkOvf = slot + nch > kChunkCap;
                 if (chunkOvf) nT = 0; // reported below; the host raises
@@ -710,7 +715,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
             }
             nStagedLast = nStaged;
             nSubLast    = nSub;
-            if (chunkOvf) break;
+            if (!kSplit || chunkOvf) break;
             // next range: back to the largest aligned length the round started with
             pos += len;
             while (len < len0 && (pos & (2 * len - 1)) == 0)
@@ -838,12 +843,44 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) SPHX_NS_OCC void findNeighbors
     const unsigned lb = xcdRemap(blockIdx.x, gridDim.x);
     const int64_t g   = int64_t(lb) * kWavesPerBlock + wave;
     if (g >= groups) return;
-    bool ok = searchGroup<false, kCapped>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po, nc, iterateH, stats,
-                                 work[wave], work[wave] + kFrontCap, leaves[wave], frontCap, kLeafCap, work[wave]);
+    bool ok = searchGroup<false, kCapped, false>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po, nc,
+                                                 iterateH, stats, work[wave], work[wave] + kFrontCap, leaves[wave],
+                                                 frontCap, kLeafCap, work[wave]);
     if (!ok && (threadIdx.x & 63) == 0)
     {
         unsigned long long k = atomicAdd(&stats[2], 1ull);
         spillList[k]         = int32_t(g);
+    }
+}
+
+/*! split path: persistent one-wave blocks take the groups the main kernel queued and search them in sub-group passes
+ *  (LDS frontiers, searchGroup<kSplit>); groups that overflow even in passes of kMinSub lanes are queued again for the
+ *  spill kernel (stats[7]). Kept out of the main kernel, whose registers and code stay those of the single pass. */
+constexpr int kSplitWaves = 1024;
+
+template<bool kCapped>
+__global__ __launch_bounds__(64) SPHX_NS_OCC void findNeighborsSplitKernel(int64_t first, int64_t last,
+                                                               const double* __restrict__ x,
+                                                               const double* __restrict__ y,
+                                                               const double* __restrict__ z,
+                                                               const SrcPosQ* __restrict__ xq, QFrame qf,
+                                                               uint32_t ntot, float* __restrict__ h, NsTree t, Box box,
+                                                               unsigned ng0, unsigned ngmax, PackedOut po,
+                                                               int32_t* __restrict__ nc, int iterateH,
+                                                               unsigned long long* __restrict__ stats,
+                                                               const int32_t* __restrict__ splitList,
+                                                               int32_t* __restrict__ spillList, int frontCap)
+{
+    __shared__ __attribute__((aligned(4096))) int32_t work[kWorkWords];
+    __shared__ int32_t leaves[kLeafCap];
+    const int64_t numSplit = int64_t(__hip_atomic_load(&stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int64_t k = blockIdx.x; k < numSplit; k += gridDim.x)
+    {
+        const int64_t g = splitList[k];
+        bool ok = searchGroup<false, kCapped, true>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po,
+                                                    nc, iterateH, stats, work, work + kFrontCap, leaves, frontCap,
+                                                    kLeafCap, work);
+        if (!ok && threadIdx.x == 0) spillList[atomicAdd(&stats[7], 1ull)] = int32_t(g);
     }
 }
 
@@ -868,24 +905,24 @@ __global__ __launch_bounds__(64) void findNeighborsSpillKernel(int64_t first, in
                                                                int32_t* __restrict__ scratch)
 {
     __shared__ __attribute__((aligned(4096))) int32_t work[kCandWords];
-    const int64_t numSpill = int64_t(__hip_atomic_load(&stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const int64_t numSpill = int64_t(__hip_atomic_load(&stats[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     int32_t* frontA = scratch + int64_t(blockIdx.x) * (2 * kSpillFront + kSpillLeaves);
     int32_t* frontB = frontA + kSpillFront;
     int32_t* leaves = frontB + kSpillFront;
     for (int64_t k = blockIdx.x; k < numSpill; k += gridDim.x)
     {
         int64_t g = spillList[k];
-        bool ok   = searchGroup<true, kCapped>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po, nc, iterateH, stats,
+        bool ok   = searchGroup<true, kCapped, false>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po, nc, iterateH, stats,
                                       frontA, frontB, leaves, kSpillFront, kSpillLeaves, work);
         if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
     }
 }
 
-//! scratch layout (ints): spill list | spill frontiers
+//! scratch layout (ints): split list | spill list | spill frontiers
 static void scratchLayout(int64_t n, int64_t& spillMemOff, int64_t& total)
 {
     const int64_t groups = (n + 63) / 64;
-    spillMemOff          = (groups + 63) / 64 * 64;
+    spillMemOff          = 2 * ((groups + 63) / 64 * 64);
     total                = spillMemOff + int64_t(kSpillWaves) * (2 * kSpillFront + kSpillLeaves);
 }
 
@@ -958,8 +995,9 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
                        stats + 8};
     int64_t spillMemOff, total;
     scratchLayout(n, spillMemOff, total);
-    int32_t* spillList = static_cast<int32_t*>(scratch);
-    int32_t* spillMem  = spillList + spillMemOff;
+    int32_t* splitList = static_cast<int32_t*>(scratch);
+    int32_t* spillList = splitList + spillMemOff / 2;
+    int32_t* spillMem  = splitList + spillMemOff;
     const int fc       = testFrontCap > 0 ? min(testFrontCap, kFrontCap) : kFrontCap;
     const unsigned grid = unsigned((groups + kWavesPerBlock - 1) / kWavesPerBlock);
     // fixed-point source records {x, y, z, m} of every particle the tree covers (the XMass loop reads the same)
@@ -971,7 +1009,11 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
         constexpr bool kC = decltype(capped)::value;
         findNeighborsKernel<kC><<<grid, 64 * kWavesPerBlock, 0, s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h, t,
                                                                      box, ng0, ngmax,
-                                                                     groups, po, nc, iterateH, stats, spillList, fc);
+                                                                     groups, po, nc, iterateH, stats, splitList, fc);
+        SPHX_LAUNCH_CHECK();
+        findNeighborsSplitKernel<kC><<<kSplitWaves, 64, 0, s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h, t,
+                                                                box, ng0, ngmax, po, nc, iterateH, stats, splitList,
+                                                                spillList, fc);
         SPHX_LAUNCH_CHECK();
         findNeighborsSpillKernel<kC><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h, t, box, ng0, ngmax, po, nc,
                                                                 iterateH, stats, spillList, spillMem);

@@ -2,9 +2,11 @@
  *
  * Parity: the reference's per-step global extrema (sfc/box_mpi.hpp:83-118 bounding box, the minimum h of the
  * time step and mass checks) are std::minmax / thrust::reduce + MPI_Allreduce. Here one launch reduces all fields of
- * a query: every block reduces its share (wave64 shuffles + LDS), writes a partial, and the last block to finish
- * (one atomic ticket, agent-scope fences) folds the partials and re-arms the ticket. At small per-rank sizes a step
- * is bound by launches, and torch's per-field min/max/aminmax/stack/cat cost ~15 launches per query.
+ * a query: every block reduces its share (wave64 shuffles + LDS) and writes a partial, and a one-block fold kernel
+ * reduces the partials (two launches). The previous single launch with a last-block ticket needed an agent-scope
+ * release fence per block, which on gfx950 writes back the XCD's L2: 40-45 us per reduction at 0.6 M particles
+ * (profiles/r4_*), where the two launches take ~10 us. At small per-rank sizes a step is bound by launches, and
+ * torch's per-field min/max/aminmax/stack/cat cost ~15 launches per query.
  */
 #include <cfloat>
 
@@ -52,26 +54,7 @@ __device__ __forceinline__ double blockReduce(double v, double* red, Op op)
     return r;
 }
 
-/*! @brief last-block-done: returns true in the one block that runs after every block has published its partials
- *         (the ticket is re-armed to 0 for the next launch) */
-__device__ __forceinline__ bool lastBlock(unsigned* ticket)
-{
-    __shared__ bool last;
-    __threadfence(); // this block's partials are visible device-wide before its ticket
-    __syncthreads();
-    if (threadIdx.x == 0)
-    {
-        unsigned t = atomicAdd(ticket, 1u);
-        last       = t == gridDim.x - 1;
-        if (last) *ticket = 0u;
-    }
-    __syncthreads();
-    if (last) __threadfence(); // acquire side: the partials of the other blocks
-    return last;
-}
-
-__global__ __launch_bounds__(kRedBlock) void multiMinMaxKernel(int64_t n, Fields4 f, double* __restrict__ partials,
-                                                               double* __restrict__ out, unsigned* ticket)
+__global__ __launch_bounds__(kRedBlock) void multiMinMaxKernel(int64_t n, Fields4 f, double* __restrict__ partials)
 {
     __shared__ double red[kRedBlock / 64];
     auto mn = [](double a, double b) { return nanMin(a, b); };
@@ -93,87 +76,110 @@ __global__ __launch_bounds__(kRedBlock) void multiMinMaxKernel(int64_t n, Fields
             partials[(2 * k + 1) * gridDim.x + blockIdx.x] = hi;
         }
     }
-    if (!lastBlock(ticket)) return;
-    for (int k = 0; k < 2 * f.count; ++k)
+}
+
+//! one block: out[k] = min (k even) / max (k odd) over the `blocks` partials of value k
+__global__ __launch_bounds__(kRedBlock) void foldMinMaxKernel(int nvals, unsigned blocks,
+                                                              const double* __restrict__ partials,
+                                                              double* __restrict__ out)
+{
+    __shared__ double red[kRedBlock / 64];
+    auto mn = [](double a, double b) { return nanMin(a, b); };
+    auto mx = [](double a, double b) { return nanMax(a, b); };
+    for (int k = 0; k < nvals; ++k)
     {
         const bool isMin = (k & 1) == 0;
         double v         = isMin ? DBL_MAX : -DBL_MAX;
-        for (unsigned b = threadIdx.x; b < gridDim.x; b += kRedBlock)
-        {
-            const double p = __hip_atomic_load(partials + k * gridDim.x + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v              = isMin ? nanMin(v, p) : nanMax(v, p);
-        }
+        for (unsigned b = threadIdx.x; b < blocks; b += kRedBlock)
+            v = isMin ? nanMin(v, partials[k * blocks + b]) : nanMax(v, partials[k * blocks + b]);
         v = isMin ? blockReduce(v, red, mn) : blockReduce(v, red, mx);
         if (threadIdx.x == 0) out[k] = v;
     }
 }
 
+//! per-block max |a|^2 (if ax) -> partials[b], and (if f) the max of the field f -> partials[gridDim + b]
 __global__ __launch_bounds__(kRedBlock) void maxNorm2Kernel(int64_t first, int64_t last, const float* __restrict__ ax,
                                                             const float* __restrict__ ay,
                                                             const float* __restrict__ az,
-                                                            double* __restrict__ partials, double* __restrict__ out,
-                                                            unsigned* ticket)
+                                                            double* __restrict__ partials,
+                                                            const float* __restrict__ f = nullptr)
 {
     __shared__ double red[kRedBlock / 64];
     auto mx = [](double a, double b) { return nanMax(a, b); };
-    double m = 0.0;
+    double m = 0.0, fm = -DBL_MAX;
     for (int64_t i = first + int64_t(blockIdx.x) * kRedBlock + threadIdx.x; i < last;
          i += int64_t(gridDim.x) * kRedBlock)
     {
-        const double x = ax[i], y = ay[i], z = az[i];
-        m              = nanMax(m, x * x + y * y + z * z);
-    }
-    m = blockReduce(m, red, mx);
-    if (threadIdx.x == 0) partials[blockIdx.x] = m;
-    if (!lastBlock(ticket)) return;
-    double v = 0.0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += kRedBlock)
-        v = nanMax(v, __hip_atomic_load(partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    v = blockReduce(v, red, mx);
-    if (threadIdx.x == 0) out[0] = v;
-}
-
-/*! @brief the local time step in one launch (reference sph/timestep.hpp: min of the Courant, density and acceleration
- *         criteria and maxDtIncrease x the previous dt): max |a|^2 over [first, last) reduced like maxNorm2Kernel, then
- *         the last block forms out = [dt, dt_m1, courant, rho] (dt_m1: the previous dt, for the position update).
- *         courant / divvMax: device scalars (nullptr: the host values) */
-__global__ __launch_bounds__(kRedBlock) void timestepKernel(int64_t first, int64_t last, const float* __restrict__ ax,
-                                                            const float* __restrict__ ay,
-                                                            const float* __restrict__ az,
-                                                            const float* __restrict__ courantDev, double courantHost,
-                                                            const float* __restrict__ divvMax, double rhoHost,
-                                                            double Krho, double etaAcc, double eps, double others,
-                                                            double prevDt, double* __restrict__ partials,
-                                                            double* __restrict__ out, unsigned* ticket)
-{
-    __shared__ double red[kRedBlock / 64];
-    auto mx  = [](double a, double b) { return nanMax(a, b); };
-    double m = 0.0;
-    if (ax)
-        for (int64_t i = first + int64_t(blockIdx.x) * kRedBlock + threadIdx.x; i < last;
-             i += int64_t(gridDim.x) * kRedBlock)
+        if (ax)
         {
             const double x = ax[i], y = ay[i], z = az[i];
             m              = nanMax(m, x * x + y * y + z * z);
         }
-    m = blockReduce(m, red, mx);
-    if (threadIdx.x == 0) partials[blockIdx.x] = m;
-    if (!lastBlock(ticket)) return;
-    double v = 0.0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += kRedBlock)
-        v = nanMax(v, __hip_atomic_load(partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    v = blockReduce(v, red, mx);
+        if (f) fm = nanMax(fm, double(f[i]));
+    }
+    if (ax)
+    {
+        m = blockReduce(m, red, mx);
+        if (threadIdx.x == 0) partials[blockIdx.x] = m;
+    }
+    if (f)
+    {
+        fm = blockReduce(fm, red, mx);
+        if (threadIdx.x == 0) partials[gridDim.x + blockIdx.x] = fm;
+    }
+}
+
+//! one block: max over the partials
+__device__ __forceinline__ double foldMax(unsigned blocks, const double* __restrict__ partials, double* red,
+                                          double v = 0.0)
+{
+    auto mx  = [](double a, double b) { return nanMax(a, b); };
+    for (unsigned b = threadIdx.x; b < blocks; b += kRedBlock)
+        v = nanMax(v, partials[b]);
+    return blockReduce(v, red, mx);
+}
+
+__global__ __launch_bounds__(kRedBlock) void foldMaxKernel(unsigned blocks, const double* __restrict__ partials,
+                                                           double* __restrict__ out)
+{
+    __shared__ double red[kRedBlock / 64];
+    const double v = foldMax(blocks, partials, red);
+    if (threadIdx.x == 0) out[0] = v;
+}
+
+/*! @brief the local time step (reference sph/timestep.hpp: min of the Courant, density and acceleration criteria and
+ *         maxDtIncrease x the previous dt): max |a|^2 over [first, last) as maxNorm2Kernel partials, then this one-block
+ *         kernel forms out = [dt, dt_m1, courant, rho] (dt_m1: the previous dt, for the position update).
+ *         courant / divvMax: device scalars (nullptr: the host values) */
+//! one block: out = float(max over the field partials partials[blocks .. 2 blocks))
+__global__ __launch_bounds__(kRedBlock) void foldFieldMaxKernel(unsigned blocks, const double* __restrict__ partials,
+                                                                float* __restrict__ out)
+{
+    __shared__ double red[kRedBlock / 64];
+    const double v = foldMax(blocks, partials + blocks, red, -DBL_MAX);
+    if (threadIdx.x == 0) out[0] = float(v);
+}
+
+__global__ __launch_bounds__(kRedBlock) void timestepKernel(bool grav, unsigned blocks,
+                                                            const double* __restrict__ partials,
+                                                            const float* __restrict__ courantDev, double courantHost,
+                                                            const float* __restrict__ divvMax, double rhoHost,
+                                                            double Krho, double etaAcc, double eps, double others,
+                                                            double prevDt, double* __restrict__ out)
+{
+    __shared__ double red[kRedBlock / 64];
+    const double v = grav ? foldMax(blocks, partials, red) : 0.0;
     if (threadIdx.x == 0)
     {
         const double inf     = __builtin_inf();
         const double maxAcc  = sqrt(v);
-        const double acc     = (ax && maxAcc > 0.0) ? etaAcc * sqrt(eps / maxAcc) : inf;
+        const double acc     = (grav && maxAcc > 0.0) ? etaAcc * sqrt(eps / maxAcc) : (grav && v != v ? v : inf);
         const double courant = courantDev ? double(courantDev[0]) : courantHost;
         double rho           = rhoHost;
         if (divvMax)
         {
             const double d = fabs(double(divvMax[0]));
-            rho            = d != 0.0 ? Krho / d : inf;
+            rho            = d != 0.0 ? Krho / d : (d != d ? d : inf);
         }
         out[0] = nanMin(nanMin(nanMin(acc, courant), rho), others);
         out[1] = prevDt;
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(kRedBlock) void timestepKernel(int64_t first, int64
     }
 }
 
-unsigned blocksFor(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>(kRedBlocks, (n + 1023) / 1024))); }
+unsigned blocksFor(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>(kRedBlocks, (n + 4095) / 4096))); }
 
 } // namespace
 
@@ -200,19 +206,23 @@ void multiMinMax(int64_t n, const std::vector<uintptr_t>& ptrs, const std::vecto
         f.p[k]        = reinterpret_cast<const void*>(ptrs[k]);
         f.isDouble[k] = isDouble[k];
     }
-    // workspace: [ticket (256 B, zero-initialized once by the caller) | partials]
-    unsigned* ticket = static_cast<unsigned*>(work);
+    // workspace: [256 B (unused) | partials]
     double* partials = reinterpret_cast<double*>(static_cast<char*>(work) + 256);
-    multiMinMaxKernel<<<blocksFor(n), kRedBlock, 0, s>>>(n, f, partials, out, ticket);
+    const unsigned blocks = blocksFor(n);
+    multiMinMaxKernel<<<blocks, kRedBlock, 0, s>>>(n, f, partials);
+    SPHX_LAUNCH_CHECK();
+    foldMinMaxKernel<<<1, kRedBlock, 0, s>>>(2 * f.count, blocks, partials, out);
     SPHX_LAUNCH_CHECK();
 }
 
 void maxNorm2(int64_t first, int64_t last, const float* ax, const float* ay, const float* az, double* out, void* work,
               hipStream_t s)
 {
-    unsigned* ticket = static_cast<unsigned*>(work);
-    double* partials = reinterpret_cast<double*>(static_cast<char*>(work) + 256);
-    maxNorm2Kernel<<<blocksFor(last - first), kRedBlock, 0, s>>>(first, last, ax, ay, az, partials, out, ticket);
+    double* partials      = reinterpret_cast<double*>(static_cast<char*>(work) + 256);
+    const unsigned blocks = blocksFor(last - first);
+    maxNorm2Kernel<<<blocks, kRedBlock, 0, s>>>(first, last, ax, ay, az, partials);
+    SPHX_LAUNCH_CHECK();
+    foldMaxKernel<<<1, kRedBlock, 0, s>>>(blocks, partials, out);
     SPHX_LAUNCH_CHECK();
 }
 
@@ -220,12 +230,36 @@ void timestepReduce(int64_t first, int64_t last, const float* ax, const float* a
                     const float* courantDev, double courantHost, const float* divvMax, double rhoHost, double Krho,
                     double etaAcc, double eps, double others, double prevDt, double* out, void* work, hipStream_t s)
 {
-    unsigned* ticket = static_cast<unsigned*>(work);
-    double* partials = reinterpret_cast<double*>(static_cast<char*>(work) + 256);
-    timestepKernel<<<ax ? blocksFor(last - first) : 1u, kRedBlock, 0, s>>>(first, last, ax, ay, az, courantDev,
-                                                                        courantHost, divvMax, rhoHost, Krho, etaAcc,
-                                                                        eps, others, prevDt, partials, out, ticket);
+    double* partials      = reinterpret_cast<double*>(static_cast<char*>(work) + 256);
+    const unsigned blocks = ax ? blocksFor(last - first) : 0u;
+    if (ax)
+    {
+        maxNorm2Kernel<<<blocks, kRedBlock, 0, s>>>(first, last, ax, ay, az, partials);
+        SPHX_LAUNCH_CHECK();
+    }
+    timestepKernel<<<1, kRedBlock, 0, s>>>(ax != nullptr, blocks, partials, courantDev, courantHost, divvMax, rhoHost,
+                                           Krho, etaAcc, eps, others, prevDt, out);
     SPHX_LAUNCH_CHECK();
+}
+
+void fieldMax(int64_t first, int64_t last, const float* f, float* out, void* work, hipStream_t s)
+{
+    double* partials      = reinterpret_cast<double*>(static_cast<char*>(work) + 256);
+    const unsigned blocks = blocksFor(last - first);
+    maxNorm2Kernel<<<blocks, kRedBlock, 0, s>>>(first, last, nullptr, nullptr, nullptr, partials, f);
+    SPHX_LAUNCH_CHECK();
+    foldFieldMaxKernel<<<1, kRedBlock, 0, s>>>(blocks, partials, out);
+    SPHX_LAUNCH_CHECK();
+}
+
+void memsetAsync(void* p, int value, size_t bytes, hipStream_t s)
+{
+    if (bytes > 0) SPHX_CHECK(hipMemsetAsync(p, value, bytes, s));
+}
+
+void fill32(void* p, uint32_t value, int64_t n, hipStream_t s)
+{
+    if (n > 0) SPHX_CHECK(hipMemsetD32Async(static_cast<hipDeviceptr_t>(p), int(value), size_t(n), s));
 }
 
 } // namespace sphx::hip

@@ -218,9 +218,15 @@ class Propagator:
             compute_conserved_quantities(d, first, last, domain.comm)
 
     def rho_timestep(self, d, first, last):
-        """max divv of the owned particles as a device scalar; compute_timestep turns it into Krho / |max divv|"""
+        """max divv of the owned particles as a 0-d tensor (GPU: float32 device scalar of the native reduction);
+        compute_timestep turns it into Krho / |max divv|. Reduced right after the IAD loop: the divv storage is
+        handed to other fields before the time step (field state machine)"""
         if last <= first:
             return math.inf
+        if d.device.type == "cuda":
+            from ..ops.reduce import field_max
+
+            return field_max(d["divv"], first, last)
         return d["divv"][first:last].max()
 
     def print_iteration_timings(self, domain, d):

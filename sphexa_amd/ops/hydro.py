@@ -507,7 +507,9 @@ def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = F
               d["kx"].data_ptr(), d["xm"].data_ptr(), d["alpha"].data_ptr(), dv, d.wh.data_ptr(), bool(av_clean),
               d["ax"].data_ptr(), d["ay"].data_ptr(), d["az"].data_ptr(), d["du"].data_ptr())
     if _is_gpu(d):
-        dt = torch.full((1,), math.inf, dtype=torch.float32, device=d.device)
+        from .reduce import fill_f32
+
+        dt = fill_f32(torch.empty(1, dtype=torch.float32, device=d.device), math.inf)  # (native fill)
         gv = _rec(d, 1, "gradv").data_ptr() if av_clean else 0  # SrcGradV records (AV cleaning only)
         ho = _handoff(d)
         done = 1 if handoff_take(d, "momq_own") else 0
@@ -529,7 +531,9 @@ def compute_momentum_energy_std(d, nl: NeighborList, box: Box):
               [d[c].data_ptr() for c in CIJ], d.wh.data_ptr(), d["ax"].data_ptr(), d["ay"].data_ptr(),
               d["az"].data_ptr(), d["du"].data_ptr())
     if _is_gpu(d):
-        dt = torch.full((1,), math.inf, dtype=torch.float32, device=d.device)
+        from .reduce import fill_f32
+
+        dt = fill_f32(torch.empty(1, dtype=torch.float32, device=d.device), math.inf)
         _lib.hip().momentum_energy_std(*common, dt.data_ptr(), *_gpu_tail(d, "std"))
         d.minDtCourant_dev = dt
         d.minDtCourant = None

@@ -56,12 +56,14 @@ def max_norm2(ax: torch.Tensor, ay: torch.Tensor, az: torch.Tensor, first: int, 
 
 
 def timestep_reduce(ax, ay, az, first: int, last: int, grav: bool, courant, divv_max, Krho: float, eta_acc: float,
-                    eps: float, others: float, prev_dt: float) -> torch.Tensor:
-    """GPU: float64 device tensor [dt, dt_m1, courant, rho] of the local time step in one launch (reference
+                    eps: float, others: float, prev_dt: float, out: torch.Tensor | None = None) -> torch.Tensor:
+    """GPU: float64 device tensor [dt, dt_m1, courant, rho] of the local time step in two launches (reference
     sph/timestep.hpp): dt = min(etaAcc sqrt(eps / max|a|) if ``grav``, courant, Krho / |divv_max|, others); ``courant``
-    and ``divv_max`` are float32 device scalars or host floats (``divv_max`` host: the rho criterion itself)"""
+    and ``divv_max`` are float32 device scalars or host floats (``divv_max`` host: the rho criterion itself).
+    ``out``: destination (4 float64 on the device)"""
     dev = ax.device
-    out = torch.empty(4, dtype=torch.float64, device=dev)
+    if out is None:
+        out = torch.empty(4, dtype=torch.float64, device=dev)
     c_dev = courant.data_ptr() if torch.is_tensor(courant) else 0
     c_host = 0.0 if torch.is_tensor(courant) else float(courant)
     r_dev = divv_max.data_ptr() if torch.is_tensor(divv_max) else 0
@@ -72,3 +74,27 @@ def timestep_reduce(ax, ay, az, first: int, last: int, grav: bool, courant, divv
                                r_dev, r_host, float(Krho), float(eta_acc), float(eps), float(others), float(prev_dt),
                                out.data_ptr(), _work(dev).data_ptr(), torch.cuda.current_stream().cuda_stream)
     return out
+
+
+def field_max(f: torch.Tensor, first: int, last: int) -> torch.Tensor:
+    """max of a float32 field over [first, last) as a float32 device scalar (two native launches, no torch reduce)"""
+    out = torch.empty(1, dtype=torch.float32, device=f.device)
+    _lib.hip().field_max(first, last, f.data_ptr(), out.data_ptr(), _work(f.device).data_ptr(),
+                         torch.cuda.current_stream().cuda_stream)
+    return out.reshape(())
+
+
+def fill_f32(t: torch.Tensor, value: float):
+    """stream-ordered native fill of a float32 device tensor (no torch fill kernel)"""
+    import struct
+
+    bits = struct.unpack("<I", struct.pack("<f", value))[0]
+    _lib.hip().fill32(t.data_ptr(), bits, t.numel(), torch.cuda.current_stream().cuda_stream)
+    return t
+
+
+def zero_(t: torch.Tensor):
+    """stream-ordered native zeroing of a device tensor (hipMemsetAsync: no torch fill kernel)"""
+    if t.numel():
+        _lib.hip().memset(t.data_ptr(), 0, t.numel() * t.element_size(), torch.cuda.current_stream().cuda_stream)
+    return t
