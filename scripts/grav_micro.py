@@ -39,6 +39,17 @@ def main():
     ms = t0.elapsed_time(t1) / a.k
     print(f"variant {os.environ.get('SPHX_HIP_VARIANT', 'default')}: evrard -n {a.n} ({e - s} particles) gravity "
           f"evaluation {ms:.3f} ms")
+    # consistency: two more evaluations with statistics (identical inputs: identical results)
+    res = []
+    for _ in range(2):
+        acc2 = [torch.zeros_like(v) for v in acc]
+        st = {}
+        eg = G.compute_gravity(*args[:-3], *acc2, stats=st)
+        res.append((acc2, eg, st))
+    (a0, e0, s0), (a1, e1, s1) = res
+    same = all(torch.equal(u, v) for u, v in zip(a0, a1))
+    print(f"  stats {s0}\n  egrav {e0:.9e} / {e1:.9e}, repeat identical: {same}, "
+          f"|a| max {float(torch.sqrt(a0[0]**2 + a0[1]**2 + a0[2]**2).max()):.6e}")
 
 
 if __name__ == "__main__":

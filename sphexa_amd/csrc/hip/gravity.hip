@@ -305,31 +305,30 @@ void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, do
 // Groups whose stack or lists overflow are evaluated by the fused spill kernel (traversal + evaluation with a
 // global-memory stack).
 
-// inner-loop forms of the MFMA P2P / M2P kernels: all tiles of a 16-source (node) block issued up front, then the
-// pair arithmetic source-outer / target-block-inner (four independent accumulator chains per step). A/B on Evrard -n
-// 200 (profiles/r4/gravity_variants.txt): P2P 9.71 -> 9.45 ms, M2P 8.33 -> 7.76 ms (at 3 waves per SIMD: the twelve
-// M2P result tiles need 48 VGPRs; at 4 waves it spills). Undefine with -DSPHX_GRAV_V1 for the pipelined forms.
-#ifndef SPHX_GRAV_V1
-#ifndef SPHX_P2P_V2
-#define SPHX_P2P_V2
-#endif
-#ifndef SPHX_M2P_V2
-#define SPHX_M2P_V2
-#endif
-#endif
-
 #ifndef SPHX_M2P_WAVES
-#ifdef SPHX_GRAV_VALU_M2P
-#define SPHX_M2P_WAVES 6 // launch bound (waves per SIMD) of the M2P kernel
-#elif defined(SPHX_M2P_V2)
 #define SPHX_M2P_WAVES 3 // twelve MFMA result tiles in flight per 16-node block (4 waves spill)
-#else
-#define SPHX_M2P_WAVES 4 // the MFMA M2P holds 16 accumulators + the 4 targets' data per lane (6 waves spill)
-#endif
 #endif
 #ifndef SPHX_M2P_UNROLL
 #define SPHX_M2P_UNROLL 2 // unroll of the per-node M2P loop
 #endif
+
+/* Target sub-boxes of the interaction lists (the two 32-target halves of a group, lanes 0-31 = half A, 32-63 = B).
+ * The list kernel walks the tree once per group with both half boxes: a node accepted by the MAC of one half only is
+ * an M2P interaction of that half, and the other half descends into its children; an opened leaf is a P2P interaction
+ * of the halves whose MAC it fails. Entries carry their half mask in bits 30-31 (kHalfA | kHalfB; node ids and
+ * particle indices stay below 2^30). The evaluation kernels apply an entry to the target blocks of its halves only
+ * (P2P: per-half source masses, target blocks of absent halves skipped; M2P: a per-half factor in 1/r). Half boxes
+ * remove 19 % of the P2P and 6 % of the M2P pair interactions on Evrard -n 200 (profiles/r3_perf_log.md, "Gravity
+ * target groups smaller than a wave"). Untagged entries (0, the fused fallback kernel's lists) mean both halves.
+ */
+constexpr unsigned kHalfA = 1u, kHalfB = 2u, kTagShift = 30;
+constexpr int32_t kIdMask = (1 << kTagShift) - 1;
+
+__device__ __forceinline__ unsigned tagOf(int32_t e)
+{
+    const unsigned t = unsigned(e) >> kTagShift;
+    return t ? t : (kHalfA | kHalfB);
+}
 
 constexpr int kGWaves = 4;
 #ifndef SPHX_GSTACK
@@ -354,10 +353,11 @@ struct GravLists
 {
     int32_t* mlst; // MAC-accepted nodes (M2P), fused path only
     int32_t* plst; // particle indices of opened leaves (P2P)
-    float4* spos;  // staged P2P tile: {x, y, z, |x|^2} relative to the group center; M2P: 3 x 64 records
+    float4* spos;  // staged P2P tile: x | y | z | m_A (64 floats each, relative to the group center); M2P: 3 x 64 records
     float2* sab;   // staged P2P tile: MFMA A operands {aR_k, aH_k} of source s at [k * kAbRow + s] (see flushP2P)
-    float* sm;     // staged P2P tile: source masses
-    float4* sxm;   // staged P2P tile for the VALU path: {x, y, z, m}, then the 64 h values as 16 float4
+    float* sm;     // staged P2P tile: |x_s|^2 (the C input of the R2 tiles)
+    float* smB;    // staged P2P tile: source masses for the targets of half B (spos.w: half A)
+    float4* sxm;   // staged P2P tile for the VALU path: {x, y, z, m_A}, the 64 h values, the 64 m_B (16 float4 each)
 };
 
 //! row stride (float2) of the k-major MFMA operand rows: 80 = 16 mod 32, so the lanes of kq and kq + 1 (one
@@ -380,13 +380,15 @@ __device__ inline void evalM2P(const int32_t* list, int n, const GravTree& t, co
     // so no wait on the loads is needed before the arithmetic of the current batch
     double rc[3];
     float4 q0, q1;
-    auto gather = [&](int32_t nd)
+    auto gather = [&](int32_t e)
     {
-        const double* c = t.centers + 4 * nd;
-        const float4* q = reinterpret_cast<const float4*>(t.mp + nd);
+        const int32_t nd = e & kIdMask;
+        const double* c  = t.centers + 4 * nd;
+        const float4* q  = reinterpret_cast<const float4*>(t.mp + nd);
         rc[0] = c[0], rc[1] = c[1], rc[2] = c[2];
         q0 = q[0], q1 = q[1];
     };
+    const unsigned myHalf = lane < 32 ? kHalfA : kHalfB;
     // node indices are read two batches ahead, node data one batch ahead of the arithmetic
     int32_t idxN  = lane < n ? list[lane] : 0;
     int32_t idxNN = 64 + lane < n ? list[64 + lane] : 0;
@@ -395,8 +397,8 @@ __device__ inline void evalM2P(const int32_t* list, int n, const GravTree& t, co
     {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         stage[lane] = make_float4(float(rc[0] - tc[0]), float(rc[1] - tc[1]), float(rc[2] - tc[2]), q0.x);
-        stage[64 + lane]  = make_float4(q0.y, q0.z, q0.w, q1.x); // qxx qxy qxz qyy
-        stage[128 + lane] = make_float4(q1.y, q1.z, 0.f, 0.f);   // qyz qzz
+        stage[64 + lane]  = make_float4(q0.y, q0.z, q0.w, q1.x);                 // qxx qxy qxz qyy
+        stage[128 + lane] = make_float4(q1.y, q1.z, __int_as_float(int(tagOf(idxN))), 0.f); // qyz qzz halves
         idxN              = idxNN;
         idxNN             = b0 + 128 + lane < n ? list[b0 + 128 + lane] : 0;
         gather(idxN); // unconditional (past the end: clamped index) so the loads land in the loop registers directly
@@ -406,6 +408,7 @@ __device__ inline void evalM2P(const int32_t* list, int n, const GravTree& t, co
         for (int k = 0; k < cnt; ++k)
         {
             float4 a = stage[k], b = stage[64 + k], c = stage[128 + k];
+            if (!(unsigned(__float_as_int(c.z)) & myHalf)) continue; // a node of the other half only
             Quadrupole q;
             q.q[qMass]  = a.w;
             q.q[qXX]    = b.x;
@@ -422,7 +425,152 @@ __device__ inline void evalM2P(const int32_t* list, int n, const GravTree& t, co
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-/*! @brief M2P with the quadrupole-vector products on the matrix cores (v_mfma_f32_16x16x4_f32).
+/* P2P source records: {qx, qy, qz, h} per particle (16 B, plus the 4-B mass), coordinates in a 31-bit fixed-point
+ * frame over 1.5x the particles' extent. The P2P loops form the source-to-group-center offsets by an exact integer
+ * subtraction and one conversion (the rounding of fp32 (x_s - c) as before), from 20 instead of 32 gathered bytes per
+ * source: the gathers of the P2P kernel miss the L2 (hit rate 37 %, heaviest-first group order) and keep its texture
+ * data path busy (TD_BUSY ~94 % of the kernel, profiles/r4/pmc_grav.txt).
+ */
+struct GravFrame
+{
+    double org[3], scale[3];
+    float inv[3];
+};
+
+//! @brief the frame from the particles' [min, max] per dimension (mm, 6 doubles on the device)
+__device__ __forceinline__ GravFrame gravFrame(const double* mm)
+{
+    GravFrame f;
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+    {
+        const double lo = mm[2 * d], hi = mm[2 * d + 1];
+        const double L  = fmax(1.5 * (hi - lo), 1e-12 * fmax(fabs(lo), fabs(hi)) + 1e-300);
+        f.org[d]        = lo - 0.25 * (hi - lo);
+        f.scale[d]      = 2147483648.0 / L;
+        f.inv[d]        = float(L / 2147483648.0);
+    }
+    return f;
+}
+
+__device__ __forceinline__ uint32_t gravQuant(double v, const GravFrame& f, int d)
+{
+    return uint32_t(fmin(fmax((v - f.org[d]) * f.scale[d] + 0.5, 0.0), 2147483647.0));
+}
+
+__global__ void gravityRecordsKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                                     const double* __restrict__ z, const float* __restrict__ h,
+                                     const double* __restrict__ mm, int4* __restrict__ rec)
+{
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const GravFrame f = gravFrame(mm);
+    rec[i] = make_int4(int(gravQuant(x[i], f, 0)), int(gravQuant(y[i], f, 1)), int(gravQuant(z[i], f, 2)),
+                       __float_as_int(h[i]));
+}
+
+//! @brief source side of a group's P2P passes: records, masses, the quantized group center and the quantum
+struct P2PSrc
+{
+    const int4* rec;
+    const float* m;
+    uint32_t qc[3];
+    float inv[3];
+    float dc[3]; // group center minus the quantized one (added to the targets' offsets)
+    float co[3]; // quantized group center minus the frame origin (M2P node offsets)
+};
+
+__device__ __forceinline__ P2PSrc p2pSrc(const int4* rec, const float* m, const double* mm, const double gc[3])
+{
+    const GravFrame f = gravFrame(mm);
+    P2PSrc S;
+    S.rec = rec;
+    S.m   = m;
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+    {
+        S.qc[d]  = __builtin_amdgcn_readfirstlane(gravQuant(gc[d], f, d));
+        S.inv[d] = f.inv[d];
+        S.dc[d]  = float(gc[d] - (f.org[d] + double(S.qc[d]) / f.scale[d]));
+        S.co[d]  = float(double(S.qc[d]) / f.scale[d]);
+    }
+    return S;
+}
+
+/* M2P node records: {c - o, M} | {Qxx, Qxy, Qxz, Qyy} | {Qyz, Qzz} with o the frame origin, 40 B per node gathered
+ * instead of 64 (fp64 center line + two quadrupole float4). Centers are fp32 offsets, not fixed point: the nodes of
+ * a remote (LET) tree lie anywhere in the global box, outside the local particles' frame. An accepted node is at
+ * least its MAC radius away, so the absolute rounding (~6e-8 of the frame extent) stays far below the expansion's
+ * own error. */
+struct NodeRecs
+{
+    const float4* a;
+    const float4* b;
+    const float2* c;
+};
+
+__global__ void gravityNodeRecordsKernel(int64_t N, const double* __restrict__ centers,
+                                         const Quadrupole* __restrict__ mp, const double* __restrict__ mm,
+                                         float4* __restrict__ a, float4* __restrict__ b, float2* __restrict__ c)
+{
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const GravFrame f = gravFrame(mm);
+    const double* cc  = centers + 4 * i;
+    const float4* q   = reinterpret_cast<const float4*>(mp + i);
+    const float4 q0 = q[0], q1 = q[1]; // M, qxx, qxy, qxz | qyy, qyz, qzz, (trace)
+    a[i] = make_float4(float(cc[0] - f.org[0]), float(cc[1] - f.org[1]), float(cc[2] - f.org[2]), q0.x);
+    b[i] = make_float4(q0.y, q0.z, q0.w, q1.x);
+    c[i] = make_float2(q1.y, q1.z);
+}
+
+//! @brief target side of the MFMA M2P: B operand [x, y, z, 1]_k of target 16 tb + col and the four targets' coordinates,
+//!        accumulators per target block (lane group kq holds partial sums over its node rows)
+struct M2PTarget
+{
+    float bT[4], tx[4], ty[4], tz[4];
+    float ph[4], ax[4], ay[4], az[4];
+};
+
+__device__ __forceinline__ void m2pInit(M2PTarget& T, float xr, float yr, float zr)
+{
+    const int lane = laneId(), kq = lane >> 4, col = lane & 15;
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+    {
+        const int src = tb * 16 + col;
+        T.tx[tb] = __shfl(xr, src), T.ty[tb] = __shfl(yr, src), T.tz[tb] = __shfl(zr, src);
+        T.bT[tb] = kq == 0 ? T.tx[tb] : (kq == 1 ? T.ty[tb] : (kq == 2 ? T.tz[tb] : 1.f));
+        T.ph[tb] = T.ax[tb] = T.ay[tb] = T.az[tb] = 0.f;
+    }
+}
+
+//! @brief the partials of target 16 tb + col sit in the four lane groups kq: sum them, lane L adds target L's
+__device__ __forceinline__ void m2pFinish(const M2PTarget& T, float acc[4])
+{
+    const int myTb = laneId() >> 4;
+    float v[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+    {
+        float p[4] = {T.ph[tb], T.ax[tb], T.ay[tb], T.az[tb]};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            float s = p[q];
+            s += __shfl_xor(s, 16);
+            s += __shfl_xor(s, 32);
+            v[q] = (tb == myTb) ? s : v[q];
+        }
+    }
+    acc[0] += v[0];
+    acc[1] += v[1];
+    acc[2] += v[2];
+    acc[3] += v[3];
+}
+
+/*! @brief M2P with the quadrupole-vector products on the matrix cores (v_mfma_f32_16x16x4_f32), for the target blocks
+ *         [kTb0, kTb1) (0-4: the whole group; 0-2 / 2-4: the nodes accepted by half A / B only, see kHalfA).
  *
  * Per pair (target t, node n, r = t - c_n) the quadrupole term needs Q_n r, a 3x4 by 4-vector product that is
  * bilinear in node and target data: (Q r)_a = sum_k A_a[n][k] T[k][t] with A_a = [Q_ax, Q_ay, Q_az, -(Q c)_a] per node
@@ -434,37 +582,27 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
  * (per node and k one float4 {A_x[k], A_y[k], A_z[k], 0}, stored k-major: sA[64 k + node]) plus {c, M}; the next
  * batch's gathers are in flight meanwhile. k-major rows make the staging stores contiguous per k and put the 16
  * lanes of a ds_read lane group on 16 distinct 16-B slots (node-major [node][k] rows were 4-way conflicted on the
- * stores and 2-way on the reads: SQ_LDS_BANK_CONFLICT 2650 per wave, profiles/r3_grav_pmc.md).
+ * stores and 2-way on the reads: SQ_LDS_BANK_CONFLICT 2650 per wave, profiles/r3_grav_pmc.md). Per 16-node block all
+ * tiles are issued up front and the pair arithmetic runs node-outer / target-block-inner (independent accumulator
+ * chains; A/B on Evrard -n 200: 8.33 -> 7.76 ms, profiles/r4/gravity_variants.txt).
  * No precision guard is needed (unlike the P2P tile): Q t - Q c carries rounding ~eps |Q| |c| against |Q r| with
  * |c| <= |r| + R_group, and R2 is formed on the VALU from r.
  */
-__device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t, const double tc[3], float xr,
-                                   float yr, float zr, float4* stage, float acc[4])
+template<int kTb0, int kTb1>
+__device__ inline void evalM2PMfma(const int32_t* list, int n, const NodeRecs& R, const P2PSrc& S, float4* stage,
+                                   M2PTarget& T)
 {
     n = __builtin_amdgcn_readfirstlane(n);
     if (n <= 0) return;
     const int lane = laneId(), kq = lane >> 4, col = lane & 15;
     float4* sC = stage;      // 64 x {cx, cy, cz, M}
     float4* sA = stage + 64; // 4 (k) x 64 x {A_x[k], A_y[k], A_z[k], 0}
-    // target side: B operand [x, y, z, 1]_k of target 16 tb + col, and the four targets' coordinates
-    float bT[4], tx[4], ty[4], tz[4];
-#pragma unroll
-    for (int tb = 0; tb < 4; ++tb)
+    float4 ra, rb;
+    float2 rq;
+    auto gather = [&](int32_t e)
     {
-        const int src = tb * 16 + col;
-        tx[tb] = __shfl(xr, src), ty[tb] = __shfl(yr, src), tz[tb] = __shfl(zr, src);
-        bT[tb] = kq == 0 ? tx[tb] : (kq == 1 ? ty[tb] : (kq == 2 ? tz[tb] : 1.f));
-    }
-    float ph[4] = {0, 0, 0, 0}, ax[4] = {0, 0, 0, 0}, ay[4] = {0, 0, 0, 0}, az[4] = {0, 0, 0, 0};
-
-    double rc[3];
-    float4 q0, q1;
-    auto gather = [&](int32_t nd)
-    {
-        const double* c = t.centers + 4 * nd;
-        const float4* q = reinterpret_cast<const float4*>(t.mp + nd);
-        rc[0] = c[0], rc[1] = c[1], rc[2] = c[2];
-        q0 = q[0], q1 = q[1];
+        const int32_t nd = e & kIdMask;
+        ra = R.a[nd], rb = R.b[nd], rq = R.c[nd];
     };
     int32_t idxN  = lane < n ? list[lane] : 0;
     int32_t idxNN = 64 + lane < n ? list[64 + lane] : 0;
@@ -475,11 +613,12 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
         {
             // node b0 + lane: padding nodes (past n) are massless, quadrupole-free and far away (zero contribution)
             const bool live = b0 + lane < n;
-            const float cx = live ? float(rc[0] - tc[0]) : 1e10f, cy = live ? float(rc[1] - tc[1]) : 1e10f,
-                        cz = live ? float(rc[2] - tc[2]) : 1e10f;
-            const float M   = live ? q0.x : 0.f;
-            const float Qxx = live ? q0.y : 0.f, Qxy = live ? q0.z : 0.f, Qxz = live ? q0.w : 0.f;
-            const float Qyy = live ? q1.x : 0.f, Qyz = live ? q1.y : 0.f, Qzz = live ? q1.z : 0.f;
+            const float cx  = live ? ra.x - S.co[0] : 1e10f;
+            const float cy  = live ? ra.y - S.co[1] : 1e10f;
+            const float cz  = live ? ra.z - S.co[2] : 1e10f;
+            const float M   = live ? ra.w : 0.f;
+            const float Qxx = live ? rb.x : 0.f, Qxy = live ? rb.y : 0.f, Qxz = live ? rb.z : 0.f;
+            const float Qyy = live ? rb.w : 0.f, Qyz = live ? rq.x : 0.f, Qzz = live ? rq.y : 0.f;
             const float Qcx = Qxx * cx + Qxy * cy + Qxz * cz;
             const float Qcy = Qxy * cx + Qyy * cy + Qyz * cz;
             const float Qcz = Qxz * cx + Qyz * cy + Qzz * cz;
@@ -502,25 +641,22 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
             for (int r = 0; r < 4; ++r)
                 C[r] = sC[16 * tile + 4 * kq + r];
             const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-#ifdef SPHX_M2P_V2
-            // all twelve tiles of the 16-node block issued up front, pair arithmetic node-outer / target-block-inner
-            // (four independent accumulator chains per step)
             f32x4 Qx[4], Qy[4], Qz[4];
 #pragma unroll
-            for (int tb = 0; tb < 4; ++tb)
+            for (int tb = kTb0; tb < kTb1; ++tb)
             {
-                Qx[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[tb], zero, 0, 0, 0);
-                Qy[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[tb], zero, 0, 0, 0);
-                Qz[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[tb], zero, 0, 0, 0);
+                Qx[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, T.bT[tb], zero, 0, 0, 0);
+                Qy[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, T.bT[tb], zero, 0, 0, 0);
+                Qz[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, T.bT[tb], zero, 0, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int r = 0; r < 4; ++r)
             {
 #pragma unroll
-                for (int tb = 0; tb < 4; ++tb)
+                for (int tb = kTb0; tb < kTb1; ++tb)
                 {
-                    const float rx  = tx[tb] - C[r].x, ry = ty[tb] - C[r].y, rz = tz[tb] - C[r].z;
+                    const float rx  = T.tx[tb] - C[r].x, ry = T.ty[tb] - C[r].y, rz = T.tz[tb] - C[r].z;
                     const float r2  = rx * rx + ry * ry + rz * rz;
                     const float ir  = __builtin_amdgcn_rsqf(r2);
                     const float ir2 = ir * ir;
@@ -529,241 +665,15 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const GravTree& t
                     const float Mir = C[r].w * ir;
                     const float t1  = rQr * ir5;
                     const float cmb = __builtin_fmaf(-2.5f, t1, -Mir) * ir2;
-                    ph[tb]          = __builtin_fmaf(-0.5f, t1, ph[tb] - Mir);
-                    ax[tb]          = __builtin_fmaf(cmb, rx, __builtin_fmaf(ir5, Qx[tb][r], ax[tb]));
-                    ay[tb]          = __builtin_fmaf(cmb, ry, __builtin_fmaf(ir5, Qy[tb][r], ay[tb]));
-                    az[tb]          = __builtin_fmaf(cmb, rz, __builtin_fmaf(ir5, Qz[tb][r], az[tb]));
-                }
-            }
-            continue;
-#endif
-#ifdef SPHX_M2P_PIPE
-            f32x4 Qxn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[0], zero, 0, 0, 0);
-            f32x4 Qyn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[0], zero, 0, 0, 0);
-            f32x4 Qzn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[0], zero, 0, 0, 0);
-#endif
-#pragma unroll
-            for (int tb = 0; tb < 4; ++tb)
-            {
-#ifdef SPHX_M2P_PIPE
-                const f32x4 Qx = Qxn, Qy = Qyn, Qz = Qzn;
-                if (tb < 3)
-                {
-                    Qxn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[tb + 1], zero, 0, 0, 0);
-                    Qyn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[tb + 1], zero, 0, 0, 0);
-                    Qzn = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[tb + 1], zero, 0, 0, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#else
-                const f32x4 Qx = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[tb], zero, 0, 0, 0);
-                const f32x4 Qy = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[tb], zero, 0, 0, 0);
-                const f32x4 Qz = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[tb], zero, 0, 0, 0);
-#endif
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    const float rx  = tx[tb] - C[r].x, ry = ty[tb] - C[r].y, rz = tz[tb] - C[r].z;
-                    const float r2  = rx * rx + ry * ry + rz * rz;
-                    const float ir  = __builtin_amdgcn_rsqf(r2);
-                    const float ir2 = ir * ir;
-                    const float ir5 = ir2 * ir2 * ir;
-                    const float rQr = rx * Qx[r] + ry * Qy[r] + rz * Qz[r];
-                    const float Mir = C[r].w * ir;
-                    const float t1  = rQr * ir5;
-#ifdef SPHX_M2P_FMA
-                    const float cmb = __builtin_fmaf(-2.5f, t1, -Mir) * ir2;
-                    ph[tb]          = __builtin_fmaf(-0.5f, t1, ph[tb] - Mir);
-                    ax[tb]          = __builtin_fmaf(cmb, rx, __builtin_fmaf(ir5, Qx[r], ax[tb]));
-                    ay[tb]          = __builtin_fmaf(cmb, ry, __builtin_fmaf(ir5, Qy[r], ay[tb]));
-                    az[tb]          = __builtin_fmaf(cmb, rz, __builtin_fmaf(ir5, Qz[r], az[tb]));
-#else
-                    const float cmb = (-2.5f * t1 - Mir) * ir2;
-                    ph[tb] -= Mir + 0.5f * t1;
-                    ax[tb] += ir5 * Qx[r] + cmb * rx;
-                    ay[tb] += ir5 * Qy[r] + cmb * ry;
-                    az[tb] += ir5 * Qz[r] + cmb * rz;
-#endif
+                    T.ph[tb]        = __builtin_fmaf(-0.5f, t1, T.ph[tb] - Mir);
+                    T.ax[tb]        = __builtin_fmaf(cmb, rx, __builtin_fmaf(ir5, Qx[tb][r], T.ax[tb]));
+                    T.ay[tb]        = __builtin_fmaf(cmb, ry, __builtin_fmaf(ir5, Qy[tb][r], T.ay[tb]));
+                    T.az[tb]        = __builtin_fmaf(cmb, rz, __builtin_fmaf(ir5, Qz[tb][r], T.az[tb]));
                 }
             }
         }
     }
-    // the partials of target 16 tb + col sit in the four lane groups kq: sum them, lane L keeps target L
-    const int myTb = lane >> 4;
-    float v[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int tb = 0; tb < 4; ++tb)
-    {
-        float p[4] = {ph[tb], ax[tb], ay[tb], az[tb]};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-        {
-            float s = p[q];
-            s += __shfl_xor(s, 16);
-            s += __shfl_xor(s, 32);
-            v[q] = (tb == myTb) ? s : v[q];
-        }
-    }
-    acc[0] += v[0];
-    acc[1] += v[1];
-    acc[2] += v[2];
-    acc[3] += v[3];
 }
-
-//! float4 slots of the per-wave staging area used by evalM2PMfma2 (64 nodes per batch)
-constexpr int kM2P2Stage = 64 + 16 + 256 + 160;
-
-/*! @brief M2P with every bilinear part of the pair on the matrix cores: separation, quadrupole-vector product and the
- *         quadratic form, leaving the VALU the radial factors and the accumulation.
- *
- * With t the target and c the node center (both relative to the group center) and Q traceless (p2m/addQuadrupole):
- *     R2[n][t]  = |t|^2 + sum_k [-2c_x, -2c_y, -2c_z, |c|^2]_k [t_x, t_y, t_z, 1]_k              (C input |t|^2)
- *     Qr_a[n][t] = sum_k [Q_ax, Q_ay, Q_az, -(Q c)_a]_k [t_x, t_y, t_z, 1]_k                        (= (Q r)_a)
- *     rQr[n][t] = c.Qc + [Q_xx, Q_yy, 2Q_xy, 2Q_xz | 2Q_yz, -2(Qc)_x, -2(Qc)_y, -2(Qc)_z]
- *                      . [t_x^2 - t_z^2, t_y^2 - t_z^2, t_x t_y, t_x t_z | t_y t_z, t_x, t_y, t_z]    (C input c.Qc)
- * i.e. six v_mfma_f32_16x16x4_f32 per 16-node x 16-target block. The acceleration sum_n (r5 Qr + comb r) is kept as
- * sum_n (r5 Qr - comb c) + t sum_n comb, so no per-pair separation vector is formed: 16 VALU + one rsqrt per pair
- * instead of 25 (evalM2PMfma). The expansions carry rounding ~eps (|t| + |c|)^2 against |r|^2, and |c| <= |r| + |t| for
- * nodes accepted by the MAC against the group box. Padding nodes: center 1e10 away, zero mass and quadrupole.
- */
-__device__ inline void evalM2PMfma2(const int32_t* list, int n, const GravTree& t, const double tcv[3], float xr,
-                                    float yr, float zr, float4* stage, float acc[4])
-{
-    n = __builtin_amdgcn_readfirstlane(n);
-    if (n <= 0) return;
-    // the group center is wave-uniform: keep it in SGPRs (VGPR copies are spilled around the batch loop)
-    double tc[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d)
-    {
-        const uint64_t u = __builtin_bit_cast(uint64_t, tcv[d]);
-        const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(u)), hi = __builtin_amdgcn_readfirstlane(uint32_t(u >> 32));
-        tc[d] = __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
-    }
-    const int lane = laneId(), kq = lane >> 4, col = lane & 15;
-    float4* sC = stage;                                      // 64 x {-c_x, -c_y, -c_z, M}
-    float* sD  = reinterpret_cast<float*>(stage + 64);       // 64 x c.Qc
-    float4* sA = stage + 80;                                 // (node, k) -> {Qr_x, Qr_y, Qr_z, R2} A operands
-    float2* sB = reinterpret_cast<float2*>(stage + 336);     // (k, node) -> the two rQr A operands (rows of 80)
-    float bT[4], b2a[4], b2b[4], tt[4];
-#pragma unroll
-    for (int tb = 0; tb < 4; ++tb)
-    {
-        const int src = tb * 16 + col;
-        const float X = __shfl(xr, src), Y = __shfl(yr, src), Z = __shfl(zr, src);
-        bT[tb]  = kq == 0 ? X : (kq == 1 ? Y : (kq == 2 ? Z : 1.f));
-        b2a[tb] = kq == 0 ? X * X - Z * Z : (kq == 1 ? Y * Y - Z * Z : (kq == 2 ? X * Y : X * Z));
-        b2b[tb] = kq == 0 ? Y * Z : (kq == 1 ? X : (kq == 2 ? Y : Z));
-        tt[tb]  = X * X + Y * Y + Z * Z;
-    }
-    float ph[4] = {0, 0, 0, 0}, ax[4] = {0, 0, 0, 0}, ay[4] = {0, 0, 0, 0}, az[4] = {0, 0, 0, 0};
-    float sc[4] = {0, 0, 0, 0};
-
-    double rc[3];
-    float4 q0, q1;
-    auto gather = [&](int32_t nd)
-    {
-        const double* c = t.centers + 4 * nd;
-        const float4* q = reinterpret_cast<const float4*>(t.mp + nd);
-        rc[0] = c[0], rc[1] = c[1], rc[2] = c[2];
-        q0 = q[0], q1 = q[1];
-    };
-    int32_t idxN  = lane < n ? list[lane] : 0;
-    int32_t idxNN = 64 + lane < n ? list[64 + lane] : 0;
-    gather(idxN);
-    for (int b0 = 0; b0 < n; b0 += 64)
-    {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // previous batch fully read before it is overwritten
-        {
-            const bool live = b0 + lane < n;
-            const float cx = live ? float(rc[0] - tc[0]) : 1e10f, cy = live ? float(rc[1] - tc[1]) : 1e10f,
-                        cz = live ? float(rc[2] - tc[2]) : 1e10f;
-            const float M   = live ? q0.x : 0.f;
-            const float Qxx = live ? q0.y : 0.f, Qxy = live ? q0.z : 0.f, Qxz = live ? q0.w : 0.f;
-            const float Qyy = live ? q1.x : 0.f, Qyz = live ? q1.y : 0.f, Qzz = live ? q1.z : 0.f;
-            const float Qcx = Qxx * cx + Qxy * cy + Qxz * cz;
-            const float Qcy = Qxy * cx + Qyy * cy + Qyz * cz;
-            const float Qcz = Qxz * cx + Qyz * cy + Qzz * cz;
-            sC[lane]         = make_float4(-cx, -cy, -cz, M);
-            sD[lane]         = cx * Qcx + cy * Qcy + cz * Qcz;
-            sA[lane]         = make_float4(Qxx, Qxy, Qxz, -2.f * cx);
-            sA[64 + lane]    = make_float4(Qxy, Qyy, Qyz, -2.f * cy);
-            sA[128 + lane]   = make_float4(Qxz, Qyz, Qzz, -2.f * cz);
-            sA[192 + lane]   = make_float4(-Qcx, -Qcy, -Qcz, cx * cx + cy * cy + cz * cz);
-            sB[lane]         = make_float2(Qxx, 2.f * Qyz);
-            sB[80 + lane]    = make_float2(Qyy, -2.f * Qcx);
-            sB[160 + lane]   = make_float2(2.f * Qxy, -2.f * Qcy);
-            sB[240 + lane]   = make_float2(2.f * Qxz, -2.f * Qcz);
-        }
-        idxN  = idxNN;
-        idxNN = b0 + 128 + lane < n ? list[b0 + 128 + lane] : 0;
-        gather(idxN);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const int ntile = (min(64, n - b0) + 15) >> 4;
-        for (int tile = 0; tile < ntile; ++tile)
-        {
-            const float4 A  = sA[64 * kq + 16 * tile + col];
-            const float2 A2 = sB[80 * kq + 16 * tile + col];
-            const float4 D  = reinterpret_cast<const float4*>(sD)[4 * tile + kq]; // c.Qc of rows 4 kq + r
-            float4 C[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                C[r] = sC[16 * tile + 4 * kq + r];
-            const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-            const f32x4 cQc  = {D.x, D.y, D.z, D.w};
-#pragma unroll
-            for (int tb = 0; tb < 4; ++tb)
-            {
-                const f32x4 cT  = {tt[tb], tt[tb], tt[tb], tt[tb]};
-                const f32x4 R2  = __builtin_amdgcn_mfma_f32_16x16x4f32(A.w, bT[tb], cT, 0, 0, 0);
-                const f32x4 Qx  = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, bT[tb], zero, 0, 0, 0);
-                const f32x4 Qy  = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, bT[tb], zero, 0, 0, 0);
-                const f32x4 Qz  = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, bT[tb], zero, 0, 0, 0);
-                const f32x4 rQa = __builtin_amdgcn_mfma_f32_16x16x4f32(A2.x, b2a[tb], cQc, 0, 0, 0);
-                const f32x4 rQr = __builtin_amdgcn_mfma_f32_16x16x4f32(A2.y, b2b[tb], rQa, 0, 0, 0);
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    // explicit fmas: a + (b*c + d*e) would cost a multiply, an fma and an add
-                    const float ir  = __builtin_amdgcn_rsqf(R2[r]);
-                    const float ir2 = ir * ir;
-                    const float ir5 = ir2 * (ir2 * ir);
-                    const float Mir = C[r].w * ir;
-                    const float t1  = rQr[r] * ir5;
-                    const float cmb = __builtin_fmaf(-2.5f, t1, -Mir) * ir2;
-                    ph[tb]          = __builtin_fmaf(-0.5f, t1, ph[tb] - Mir);
-                    ax[tb]          = __builtin_fmaf(cmb, C[r].x, __builtin_fmaf(ir5, Qx[r], ax[tb]));
-                    ay[tb]          = __builtin_fmaf(cmb, C[r].y, __builtin_fmaf(ir5, Qy[r], ay[tb]));
-                    az[tb]          = __builtin_fmaf(cmb, C[r].z, __builtin_fmaf(ir5, Qz[r], az[tb]));
-                    sc[tb] += cmb;
-                }
-#ifndef SPHX_M2P2_NOBARRIER
-                __builtin_amdgcn_sched_barrier(0); // one block's MFMA results live at a time (4 waves per SIMD)
-#endif
-            }
-        }
-    }
-    // partials of target 16 tb + col sit in the four lane groups kq: sum them, lane L keeps target L
-    const int myTb = lane >> 4;
-    float v[5] = {0, 0, 0, 0, 0};
-#pragma unroll
-    for (int tb = 0; tb < 4; ++tb)
-    {
-        float p[5] = {ph[tb], ax[tb], ay[tb], az[tb], sc[tb]};
-#pragma unroll
-        for (int q = 0; q < 5; ++q)
-        {
-            float s = p[q];
-            s += __shfl_xor(s, 16);
-            s += __shfl_xor(s, 32);
-            v[q] = (tb == myTb) ? s : v[q];
-        }
-    }
-    acc[0] += v[0];
-    acc[1] += v[1] + xr * v[4];
-    acc[2] += v[2] + yr * v[4];
-    acc[3] += v[3] + zr * v[4];
-}
-
 
 //! @brief v_max_f32 without the NaN-quieting canonicalization fmaxf adds for MFMA results (inputs are finite)
 __device__ __forceinline__ float maxNoCanon(float a, float b)
@@ -786,10 +696,12 @@ __device__ __forceinline__ float maxNoCanon(float a, float b)
  * that is below ~4e-6 of the smallest softening radius (h_s + h_t)^2 in the tile, otherwise (sparse groups much
  * larger than h) with the plain VALU pair loop over the same staged sources.
  */
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 struct P2PTarget
 {
     float bR2[4], bH2[4];
-    float sx[4], sy[4], sz[4], sw[4], phi[4];
+    f32x2 sx[4], sy[4], sz[4], sw[4], phi[4]; // per target block: partial sums over even / odd source rows
     float xr, yr, zr, hi, v[4]; // VALU path: own target, own accumulators
     float maxT2, hminT;         // group extent for the accuracy test
     int nMfma, nValu;           // 64-source chunks evaluated on the MFMA tile / the VALU fallback (wave-uniform)
@@ -809,7 +721,7 @@ __device__ __forceinline__ void p2pInit(P2PTarget& T, float xr, float yr, float 
         float H = __shfl(hi, src);
         T.bR2[tb] = k == 0 ? -2.f * X : (k == 1 ? -2.f * Y : (k == 2 ? -2.f * Z : R));
         T.bH2[tb] = k == 0 ? 1.f : (k == 1 ? 2.f * H : (k == 2 ? H * H : 0.f));
-        T.sx[tb] = T.sy[tb] = T.sz[tb] = T.sw[tb] = T.phi[tb] = 0.f;
+        T.sx[tb] = T.sy[tb] = T.sz[tb] = T.sw[tb] = T.phi[tb] = f32x2{0.f, 0.f};
     }
     T.xr = xr, T.yr = yr, T.zr = zr, T.hi = hi;
     T.v[0] = T.v[1] = T.v[2] = T.v[3] = 0.f;
@@ -827,7 +739,8 @@ __device__ __forceinline__ void p2pFinish(const P2PTarget& T, float acc[4])
 #pragma unroll
     for (int b = 0; b < 4; ++b)
     {
-        float p[5] = {T.phi[b], T.sx[b], T.sy[b], T.sz[b], T.sw[b]};
+        float p[5] = {T.phi[b].x + T.phi[b].y, T.sx[b].x + T.sx[b].y, T.sy[b].x + T.sy[b].y,
+                      T.sz[b].x + T.sz[b].y, T.sw[b].x + T.sw[b].y};
 #pragma unroll
         for (int q = 0; q < 5; ++q)
         {
@@ -843,63 +756,159 @@ __device__ __forceinline__ void p2pFinish(const P2PTarget& T, float acc[4])
     acc[3] += v[3] - T.zr * v[4] + T.v[3];
 }
 
-//! @brief source index at offset o of a plain index list
+/* Source index generators of flushP2P: next(o, oEnd) returns the particle index of list offset min(o, oEnd - 1) for
+ * the lane's o; successive calls cover successive 64-offset chunks in increasing order. */
+
+//! @brief a plain index list in LDS (the fused fallback kernel's queue)
 struct ListIdx
 {
     const int32_t* p;
-    __device__ __forceinline__ int32_t operator()(int o) const { return p[o]; }
+    __device__ __forceinline__ int32_t next(int o, int oEnd) { return p[min(o, oEnd - 1)]; }
 };
 
-/*! @brief source index at offset o of a window of opened leaves: pre = exclusive prefix of the leaf sizes (+ total),
- *         st = first particle of each leaf, both in LDS; binary search for the leaf (the P2P kernel generates its
- *         source indices from the leaf list instead of reading an expanded per-group index list) */
-struct LeafIdx
+/*! @brief a window of opened leaves: pre = exclusive prefix of the leaf sizes (pre[nw] = total), st = first particle of
+ *         each leaf, both in LDS. A wave-uniform cursor (the leaf holding the previous chunk's last offset) advances
+ *         over the leaf starts inside the chunk: one LDS read of the next 64 starts, a uniform loop over those below
+ *         the chunk end (leaves hold ~16-64 particles: a few per chunk) and one read of the lane's leaf start. A
+ *         per-lane binary search over the window instead was 8 dependent LDS reads per chunk that the wave waited for
+ *         (the P2P kernel is latency-bound: SQ_WAIT_INST_ANY 0.40 of the cycles, profiles/r4/gravity_lds_pmc.txt).
+ */
+struct LeafCursor
 {
     const int32_t* pre;
     const int32_t* st;
     int nw;
-    __device__ __forceinline__ int32_t operator()(int o) const
+    int cur;    // leaf holding the last offset handed out (initially: the first leaf of the pass)
+    int preCur; // pre[cur]
+    __device__ __forceinline__ int32_t next(int o, int oEnd)
     {
-        int lo = 0, hi = nw; // pre[lo] <= o < pre[hi]
-        while (hi - lo > 1)
+        o                = min(o, oEnd - 1);
+        const int lane   = laneId();
+        const int k      = cur + 1 + lane;
+        const int p      = k <= nw ? pre[k] : INT32_MAX; // starts of the following leaves (increasing)
+        const int oMax   = __builtin_amdgcn_readfirstlane(waveMax(o));
+        const int nb     = __popcll(ballot(p <= oMax)); // leaf starts up to the chunk's last offset: a prefix
+        int leaf = cur, base = preCur;
+        for (int q = 0; q < nb; ++q)
         {
-            const int mid = (lo + hi) >> 1;
-            if (pre[mid] <= o) lo = mid;
-            else hi = mid;
+            const int pk = __builtin_amdgcn_readlane(p, q);
+            if (o >= pk) leaf = cur + 1 + q, base = pk;
         }
-        return st[lo] + (o - pre[lo]);
+        cur    = __builtin_amdgcn_readlane(leaf, 63);
+        preCur = __builtin_amdgcn_readlane(base, 63);
+        return st[leaf] + (o - base);
     }
 };
 
-//! @brief all queued P2P particles against the group's 64 targets, 64 sources per staged LDS tile
-template<class Idx>
-__device__ inline void flushP2P(const Idx& plst, int n, const GravLists& L, const double* x, const double* y,
-                                const double* z, const float* h, const float* m, const double gc[3], P2PTarget& T)
+//! source classes of a P2P pass (flushP2P): all sources apply to both halves / to half A only / to half B only, or
+//! a mixed list whose indices carry their half masks (the fused fallback kernel's list)
+enum P2PMode
+{
+    kP2PMixed = 0,
+    kP2PHalfA = 1,
+    kP2PHalfB = 2,
+    kP2PBoth  = 3
+};
+
+/*! @brief one 16-source block of the staged MFMA P2P tile against target blocks [kTb0, kTb1) (blocks 0-1: half A,
+ *         2-3: half B). All tiles of the block are issued up front, then the pair arithmetic runs source-outer /
+ *         target-block-inner: independent accumulator chains per step instead of one chain of dependent updates per
+ *         target block (issue stalls on the accumulations and the MFMA results were ~40 % of the cycles,
+ *         profiles/r3_grav_pmc.md). The arithmetic is written on pairs of source rows (r, r + 1), which sit in
+ *         adjacent registers of the MFMA results and of the SoA-staged source data, so every multiply / fma is one
+ *         v_pk_*_f32 for two pairs without operand moves (6 VALU per pair instead of 8; left to the compiler the
+ *         packing varied between 8 and 12.6 per pair with unrelated code changes). kMixed: per-source masses of half B
+ *         in smB (sM: half A).
+ */
+template<int kTb0, int kTb1, bool kMixed>
+__device__ __forceinline__ void p2pBlock(const GravLists& L, int sb, int kq, int col, P2PTarget& T)
+{
+    const float2 ab = L.sab[kq * kAbRow + sb * 16 + col];
+    const float4 c4 = reinterpret_cast<const float4*>(L.sm)[sb * 4 + kq]; // |x_s|^2 of the lane's 4 sources
+    const f32x4 cR  = {c4.x, c4.y, c4.z, c4.w};
+    const f32x4 c0v = {0.f, 0.f, 0.f, 0.f};
+    f32x4 R2[4], H2[4];
+#pragma unroll
+    for (int tb = kTb0; tb < kTb1; ++tb)
+    {
+        R2[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ab.x, T.bR2[tb], cR, 0, 0, 0);
+        H2[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ab.y, T.bH2[tb], c0v, 0, 0, 0);
+    }
+    // SoA source data of the lane's 4 source rows: x | y | z | m (64 each)
+    const float* sp = reinterpret_cast<const float*>(L.spos);
+    const float4 X4 = reinterpret_cast<const float4*>(sp)[sb * 4 + kq];
+    const float4 Y4 = reinterpret_cast<const float4*>(sp + 64)[sb * 4 + kq];
+    const float4 Z4 = reinterpret_cast<const float4*>(sp + 128)[sb * 4 + kq];
+    const float4 M4 = reinterpret_cast<const float4*>(sp + 192)[sb * 4 + kq];
+    float4 B4       = M4;
+    if constexpr (kMixed) B4 = reinterpret_cast<const float4*>(L.smB)[sb * 4 + kq];
+    __builtin_amdgcn_sched_barrier(0);
+    const f32x2 Xp[2] = {{X4.x, X4.y}, {X4.z, X4.w}}, Yp[2] = {{Y4.x, Y4.y}, {Y4.z, Y4.w}};
+    const f32x2 Zp[2] = {{Z4.x, Z4.y}, {Z4.z, Z4.w}}, Mp[2] = {{M4.x, M4.y}, {M4.z, M4.w}};
+    const f32x2 Bp[2] = {{B4.x, B4.y}, {B4.z, B4.w}};
+#pragma unroll
+    for (int rp = 0; rp < 2; ++rp)
+    {
+#pragma unroll
+        for (int tb = kTb0; tb < kTb1; ++tb)
+        {
+            const f32x2 R  = {R2[tb][2 * rp], R2[tb][2 * rp + 1]};
+            const f32x2 re = {maxNoCanon(R2[tb][2 * rp], H2[tb][2 * rp]),
+                              maxNoCanon(R2[tb][2 * rp + 1], H2[tb][2 * rp + 1])};
+            const f32x2 ir = {__builtin_amdgcn_rsqf(re.x), __builtin_amdgcn_rsqf(re.y)};
+            const f32x2 w  = ((kMixed && tb >= 2) ? Bp[rp] : Mp[rp]) * (ir * (ir * ir));
+            T.phi[tb] -= w * R;
+            T.sx[tb] += w * Xp[rp];
+            T.sy[tb] += w * Yp[rp];
+            T.sz[tb] += w * Zp[rp];
+            T.sw[tb] += w;
+        }
+    }
+}
+
+/*! @brief the queued P2P sources plst(o0 .. o0 + n) against the group's targets, 64 sources per staged LDS tile.
+ *         kMode (P2PMode): the sources apply to both target halves, to one half only (the target blocks of the other
+ *         half are not evaluated), or carry their half masks in the index (kP2PMixed: per-source masses per half).
+ */
+template<int kMode, class Idx>
+__device__ inline void flushP2P(Idx plst, int o0, int n, const GravLists& L, const P2PSrc& S, P2PTarget& T)
 {
     n = __builtin_amdgcn_readfirstlane(n);
     if (n <= 0) return;
-    const int lane = laneId(), kq = lane >> 4;
+    constexpr int kTb0 = kMode == kP2PHalfB ? 2 : 0, kTb1 = kMode == kP2PHalfA ? 2 : 4;
+    const int lane = laneId(), kq = lane >> 4, col = lane & 15;
     // particle indices are read two chunks ahead, particle data one chunk ahead of the tile arithmetic; the data
     // of the chunk in flight stay raw (unconditional loads at a clamped index) until they are staged
-    double rx, ry, rz;
-    float rh, rm;
-    auto gather = [&](int32_t j)
+    int4 rq;
+    float rm;
+    auto gather = [&](int32_t e)
     {
-        rx = x[j], ry = y[j], rz = z[j];
-        rh = h[j], rm = m[j];
+        const int32_t j = e & kIdMask;
+        rq = S.rec[j];
+        rm = S.m[j];
     };
-    int32_t jN  = lane < n ? plst(lane) : plst(0);
-    int32_t jNN = 64 + lane < n ? plst(64 + lane) : plst(0);
+    int32_t jN  = plst.next(o0 + lane, o0 + n);
+    int32_t jNN = plst.next(o0 + 64 + lane, o0 + n);
     gather(jN);
     for (int c0 = 0; c0 < n; c0 += 64)
     {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // previous tile fully read before it is overwritten
         const bool valid = c0 + lane < n;
-        float sx = float(rx - gc[0]), sy = float(ry - gc[1]), sz = float(rz - gc[2]);
+        const float sx = float(int(uint32_t(rq.x) - S.qc[0])) * S.inv[0];
+        const float sy = float(int(uint32_t(rq.y) - S.qc[1])) * S.inv[1];
+        const float sz = float(int(uint32_t(rq.z) - S.qc[2])) * S.inv[2];
+        const float rh = __int_as_float(rq.w);
         // padding source: m = 0 at the group center with h = 1 (finite weight, zero contribution)
         const float4 Pn = valid ? make_float4(sx, sy, sz, sx * sx + sy * sy + sz * sz) : make_float4(0, 0, 0, 0);
         const float4 Qn = valid ? make_float4(rm, rh, rh * rh, 0.f) : make_float4(0.f, 1.f, 1.f, 0.f);
-        const int cnt   = min(64, n - c0);
+        float mA = Qn.x, mB = 0.f;
+        if constexpr (kMode == kP2PMixed)
+        {
+            const unsigned hm = tagOf(jN);
+            mA                = (hm & kHalfA) ? Qn.x : 0.f;
+            mB                = (hm & kHalfB) ? Qn.x : 0.f;
+        }
+        const int cnt = min(64, n - c0);
 #ifdef SPHX_GRAV_VALU_P2P
         const bool mfma = false;
 #else
@@ -912,13 +921,13 @@ __device__ inline void flushP2P(const Idx& plst, int n, const GravLists& L, cons
             // A operands of the R2 / H2 tiles stored k-major, so lane (kq, col) fetches its {aR, aH} pair with one
             // conflict-free ds_read_b64 (a per-lane component select of source-major records became divergent
             // 8-way conflicted ds_read_b32s: SQ_LDS_BANK_CONFLICT 2044 per wave, profiles/r3_grav_pmc.md)
-#ifdef SPHX_P2P_V2
-            L.spos[lane] = make_float4(Pn.x, Pn.y, Pn.z, Qn.x);
-            L.sm[lane]   = Pn.w; // |x|^2: the C input of the R2 tiles, 4 consecutive sources per b128 read
-#else
-            L.spos[lane]             = Pn;
-            L.sm[lane]               = Qn.x;
-#endif
+            float* sp     = reinterpret_cast<float*>(L.spos); // SoA: x | y | z | m, 4 consecutive sources per b128
+            sp[lane]       = Pn.x;
+            sp[64 + lane]  = Pn.y;
+            sp[128 + lane] = Pn.z;
+            sp[192 + lane] = mA;
+            L.sm[lane]     = Pn.w; // |x|^2: the C input of the R2 tiles
+            if constexpr (kMode == kP2PMixed) L.smB[lane] = mB;
             L.sab[lane]              = make_float2(Pn.x, Qn.z);
             L.sab[kAbRow + lane]     = make_float2(Pn.y, Qn.y);
             L.sab[2 * kAbRow + lane] = make_float2(Pn.z, 1.f);
@@ -929,16 +938,20 @@ __device__ inline void flushP2P(const Idx& plst, int n, const GravLists& L, cons
         {
             // VALU tile: one broadcast ds_read_b128 per source plus one per four h values (a float4 {x,y,z,|x|^2}
             // + {m,h,h^2,0} pair is read as b96 + half a read2_b64: 8-cycle instructions on a shared LDS)
-            L.sxm[lane]                            = make_float4(Pn.x, Pn.y, Pn.z, Qn.x);
+            L.sxm[lane]                                = make_float4(Pn.x, Pn.y, Pn.z, mA);
             reinterpret_cast<float*>(L.sxm + 64)[lane] = Qn.y;
+            if constexpr (kMode == kP2PMixed) reinterpret_cast<float*>(L.sxm + 80)[lane] = mB;
             ++T.nValu;
         }
         jN = jNN;
-        jNN = c0 + 128 + lane < n ? plst(c0 + 128 + lane) : plst(0);
+        jNN = plst.next(o0 + c0 + 128 + lane, o0 + n);
         gather(jN); // unconditional (past the end: clamped index) so the loads land in the loop registers directly
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (!mfma)
         {
+            // the lane's own target is in half A (lanes 0-31) or B; sources of the other half only weigh zero
+            const bool halfB = lane >= 32;
+            const bool mine  = kMode == kP2PBoth || kMode == kP2PMixed || (kMode == kP2PHalfB) == halfB;
             int k = 0;
             for (; k + 4 <= cnt; k += 4)
             {
@@ -952,116 +965,38 @@ __device__ inline void flushP2P(const Idx& plst, int n, const GravLists& L, cons
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     asm volatile("" : "+v"(P[u].x), "+v"(P[u].y), "+v"(P[u].z), "+v"(P[u].w));
+                float mu[4] = {P[0].w, P[1].w, P[2].w, P[3].w};
+                if constexpr (kMode == kP2PMixed)
+                {
+                    const float4 MB = L.sxm[80 + (k >> 2)];
+                    if (halfB) mu[0] = MB.x, mu[1] = MB.y, mu[2] = MB.z, mu[3] = MB.w;
+                }
                 const float hu[4] = {H.x, H.y, H.z, H.w};
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    p2p(P[u].x - T.xr, P[u].y - T.yr, P[u].z - T.zr, P[u].w, T.hi, hu[u], T.v);
+                    p2p(P[u].x - T.xr, P[u].y - T.yr, P[u].z - T.zr, mine ? mu[u] : 0.f, T.hi, hu[u], T.v);
             }
             for (; k < cnt; ++k)
             {
                 float4 P = L.sxm[k];
-                p2p(P.x - T.xr, P.y - T.yr, P.z - T.zr, P.w, T.hi, reinterpret_cast<const float*>(L.sxm + 64)[k], T.v);
+                float w  = mine ? P.w : 0.f;
+                if constexpr (kMode == kP2PMixed)
+                    if (halfB) w = reinterpret_cast<const float*>(L.sxm + 80)[k];
+                p2p(P.x - T.xr, P.y - T.yr, P.z - T.zr, w, T.hi, reinterpret_cast<const float*>(L.sxm + 64)[k], T.v);
             }
             continue;
         }
         const int nsb = (cnt + 15) >> 4;
-#ifdef SPHX_P2P_V2
-        // all eight tiles of a 16-source block (4 target blocks x R2, H2) issued up front, then the pair arithmetic
-        // source-outer / target-block-inner: four independent accumulator chains per step instead of one chain of
-        // four dependent updates per target block (issue stalls on the accumulations and the MFMA results were ~40 %
-        // of the cycles, profiles/r3_grav_pmc.md)
         for (int sb = 0; sb < nsb; ++sb)
-        {
-            const float2 ab = L.sab[kq * kAbRow + sb * 16 + (lane & 15)];
-            const float4 c4 = reinterpret_cast<const float4*>(L.sm)[sb * 4 + kq]; // |x_s|^2 of the lane's 4 sources
-            const f32x4 cR  = {c4.x, c4.y, c4.z, c4.w};
-            const f32x4 c0v = {0.f, 0.f, 0.f, 0.f};
-            f32x4 R2[4], H2[4];
-#pragma unroll
-            for (int tb = 0; tb < 4; ++tb)
-            {
-                R2[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ab.x, T.bR2[tb], cR, 0, 0, 0);
-                H2[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ab.y, T.bH2[tb], c0v, 0, 0, 0);
-            }
-            float4 Pr[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                Pr[r] = L.spos[sb * 16 + 4 * kq + r]; // {x, y, z, m}
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-            {
-#pragma unroll
-                for (int tb = 0; tb < 4; ++tb)
-                {
-                    float re = maxNoCanon(R2[tb][r], H2[tb][r]);
-                    float ir = __builtin_amdgcn_rsqf(re);
-                    float w  = Pr[r].w * ir * (ir * ir);
-                    T.phi[tb] -= w * R2[tb][r];
-                    T.sx[tb] += w * Pr[r].x;
-                    T.sy[tb] += w * Pr[r].y;
-                    T.sz[tb] += w * Pr[r].z;
-                    T.sw[tb] += w;
-                }
-            }
-        }
-        continue;
-#endif
-        for (int sb = 0; sb < nsb; ++sb)
-        {
-            const float2 ab = L.sab[kq * kAbRow + sb * 16 + (lane & 15)];
-            const float aR  = ab.x, aH = ab.y;
-            float4 Pr[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                Pr[r] = L.spos[sb * 16 + 4 * kq + r];
-            const float4 m4   = reinterpret_cast<const float4*>(L.sm)[sb * 4 + kq];
-            const float mr[4] = {m4.x, m4.y, m4.z, m4.w};
-            const f32x4 cR  = {Pr[0].w, Pr[1].w, Pr[2].w, Pr[3].w};
-            const f32x4 c0v = {0.f, 0.f, 0.f, 0.f};
-#ifndef SPHX_P2P_NOPIPE
-            // the next target block's tiles are issued before this block's VALU work, so the ~40-cycle MFMA result
-            // latency is covered by the wave's own pair arithmetic instead of stalling it once per block
-            f32x4 R2n = __builtin_amdgcn_mfma_f32_16x16x4f32(aR, T.bR2[0], cR, 0, 0, 0);
-            f32x4 H2n = __builtin_amdgcn_mfma_f32_16x16x4f32(aH, T.bH2[0], c0v, 0, 0, 0);
-#endif
-#pragma unroll
-            for (int tb = 0; tb < 4; ++tb)
-            {
-#ifdef SPHX_P2P_NOPIPE
-                f32x4 R2 = __builtin_amdgcn_mfma_f32_16x16x4f32(aR, T.bR2[tb], cR, 0, 0, 0);
-                f32x4 H2 = __builtin_amdgcn_mfma_f32_16x16x4f32(aH, T.bH2[tb], c0v, 0, 0, 0);
-#else
-                const f32x4 R2 = R2n, H2 = H2n;
-                if (tb < 3)
-                {
-                    R2n = __builtin_amdgcn_mfma_f32_16x16x4f32(aR, T.bR2[tb + 1], cR, 0, 0, 0);
-                    H2n = __builtin_amdgcn_mfma_f32_16x16x4f32(aH, T.bH2[tb + 1], c0v, 0, 0, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0); // keep the scheduler from sinking them back to their first use
-#endif
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    float re = maxNoCanon(R2[r], H2[r]);
-                    float ir = __builtin_amdgcn_rsqf(re);
-                    float w  = mr[r] * ir * (ir * ir);
-                    T.phi[tb] -= w * R2[r];
-                    T.sx[tb] += w * Pr[r].x;
-                    T.sy[tb] += w * Pr[r].y;
-                    T.sz[tb] += w * Pr[r].z;
-                    T.sw[tb] += w;
-                }
-            }
-        }
+            p2pBlock<kTb0, kTb1, kMode == kP2PMixed>(L, sb, kq, col, T);
     }
 }
 
 //! @brief append the particles of leaf (a0, n0) to the P2P list, evaluating the list whenever it is full
-__device__ __forceinline__ void queueLeaf(int a0, int n0, int& np, const GravLists& L, const double* x,
-                                          const double* y, const double* z, const float* h, const float* m,
-                                          const double tc[3], P2PTarget& T)
+__device__ __forceinline__ void queueLeaf(int a0, int n0, unsigned halves, int& np, const GravLists& L,
+                                          const P2PSrc& S, P2PTarget& T)
 {
+    const int32_t tag = int32_t(halves << kTagShift);
     const int lane = laneId();
     for (int off = 0; off < n0; off += 64)
     {
@@ -1069,10 +1004,10 @@ __device__ __forceinline__ void queueLeaf(int a0, int n0, int& np, const GravLis
         if (np + c > kGP2P)
         {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            flushP2P(ListIdx{L.plst}, np, L, x, y, z, h, m, tc, T);
+            flushP2P<kP2PMixed>(ListIdx{L.plst}, 0, np, L, S, T);
             np = 0;
         }
-        if (lane < c) L.plst[np + lane] = a0 + off + lane;
+        if (lane < c) L.plst[np + lane] = (a0 + off + lane) | tag;
         np += c;
     }
 }
@@ -1104,39 +1039,68 @@ __device__ __forceinline__ void groupBox(double xi, double yi, double zi, double
     }
 }
 
-/*! @brief one LIFO pop of up to 64 nodes: each lane tests one node against the vector MAC of the group box.
- *         Children of opened internal nodes are pushed on the stack (most recently pushed popped first, so the stack
- *         holds O(depth x 8 x 64) entries instead of a whole tree level). Returns false on stack overflow.
- */
+//! @brief center and half extent of the bounding boxes of lanes 0-31 (A) and 32-63 (B), fp64, wave-uniform
+__device__ __forceinline__ void halfBoxes(double xi, double yi, double zi, double ac[3], double as[3], double bc[3],
+                                          double bs[3])
+{
+    const double p[3] = {xi, yi, zi};
+    for (int d = 0; d < 3; ++d)
+    {
+        double a = p[d], b = p[d];
+        for (int o = 16; o > 0; o >>= 1) // within each 32-lane half
+        {
+            a = fmin(a, __shfl_xor(a, o));
+            b = fmax(b, __shfl_xor(b, o));
+        }
+        const double aLo = readLaneD(a, 0), aHi = readLaneD(b, 0), bLo = readLaneD(a, 32), bHi = readLaneD(b, 32);
+        ac[d] = 0.5 * (aLo + aHi);
+        as[d] = 0.5 * (aHi - aLo);
+        bc[d] = 0.5 * (bLo + bHi);
+        bs[d] = 0.5 * (bHi - bLo);
+    }
+}
+
+/*! @brief popAndTest against the two half boxes: stack entries are node | half mask << 30 (the halves that still
+ *         walk the node); mM2P / mLeaf receive the half masks for which the node is an accepted multipole / an opened
+ *         leaf, children of internal nodes are pushed with the mask of the halves that opened them */
 template<bool kSpill>
-__device__ __forceinline__ bool popAndTest(const GravTree& t, int32_t* stack, int& sp, int stackCap,
-                                           const double tc[3], const double ts[3], int32_t& nd, bool& isM2P,
-                                           bool& isLeaf)
+__device__ __forceinline__ bool popAndTestHalves(const GravTree& t, int32_t* stack, int& sp, int stackCap,
+                                                 const double ac[3], const double as[3], const double bc[3],
+                                                 const double bs[3], int32_t& nd, unsigned& mM2P, unsigned& mLeaf)
 {
     const int lane = laneId();
     const int cnt  = min(sp, 64);
     const int base = sp - cnt;
-    nd             = lane < cnt ? gLoad<kSpill>(stack + base + lane) : -1;
-    sp             = base;
-    gWaveSync<kSpill>(); // all lanes read their node before the pushes below overwrite the popped slots
-    isM2P = isLeaf = false;
+    const int32_t e = lane < cnt ? gLoad<kSpill>(stack + base + lane) : -1; // (negative when bit 31 is set)
+    sp              = base;
+    gWaveSync<kSpill>(); // all lanes read their entry before the pushes below overwrite the popped slots
+    mM2P = mLeaf   = 0;
+    unsigned open  = 0;
     bool isInt     = false;
-    if (nd >= 0)
+    nd             = e != -1 ? (e & kIdMask) : -1;
+    if (e != -1)
     {
-        const double* c = t.centers + 4 * nd;
-        bool violated   = macViolated(c, c[3], tc, ts);
-        const bool leaf = t.n2l[nd] >= 0;
-        isM2P           = !violated && c[3] != 0.0;
-        isLeaf          = violated && leaf;
-        isInt           = violated && !leaf;
+        const unsigned tag = tagOf(e);
+        const double* c    = t.centers + 4 * nd;
+        const bool vA      = (tag & kHalfA) && macViolated(c, c[3], ac, as);
+        const bool vB      = (tag & kHalfB) && macViolated(c, c[3], bc, bs);
+        open               = (vA ? kHalfA : 0u) | (vB ? kHalfB : 0u);
+#ifdef SPHX_GRAV_FULLBOX
+        open = open ? tag : 0u; // (A/B: one decision for the whole group, as with the group box)
+#endif
+        const unsigned acc = tag & ~open;
+        const bool leaf    = t.n2l[nd] >= 0;
+        mM2P               = c[3] != 0.0 ? acc : 0u;
+        mLeaf              = leaf ? open : 0u;
+        isInt              = !leaf && open;
     }
     const uint64_t bi = ballot(isInt);
     const int ci      = __popcll(bi);
     if (sp + 8 * ci > stackCap) return false;
     if (isInt)
     {
-        int pos    = sp + 8 * __popcll(bi & lanemaskLt());
-        int32_t co = t.child[nd];
+        int pos          = sp + 8 * __popcll(bi & lanemaskLt());
+        const int32_t co = t.child[nd] | int32_t(open << kTagShift);
         for (int k = 0; k < 8; ++k)
             stack[pos + k] = co + k;
     }
@@ -1188,28 +1152,33 @@ __device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t l
                                              const float* __restrict__ m, float G, float* __restrict__ ax,
                                              float* __restrict__ ay, float* __restrict__ az,
                                              double* __restrict__ ugrav, unsigned long long* __restrict__ stats,
-                                             int32_t* stack, const GravLists& L, int stackCap, double& upot)
+                                             int32_t* stack, const GravLists& L, int stackCap, double& upot,
+                                             const int4* __restrict__ rec, const double* __restrict__ mm)
 {
     const int lane   = laneId();
     const int64_t ii = min(first + g * 64 + lane, last - 1);
     double xi = x[ii], yi = y[ii], zi = z[ii];
     float hi  = h[ii];
-    double tc[3], ts[3];
+    double tc[3], ts[3], ac[3], as[3], bc[3], bs[3];
     groupBox(xi, yi, zi, tc, ts);
+    halfBoxes(xi, yi, zi, ac, as, bc, bs);
+    const P2PSrc S = p2pSrc(rec, m, mm, tc);
     float xr = float(xi - tc[0]), yr = float(yi - tc[1]), zr = float(zi - tc[2]);
     float acc[4] = {0, 0, 0, 0};
     P2PTarget T;
-    p2pInit(T, xr, yr, zr, hi);
+    p2pInit(T, xr + S.dc[0], yr + S.dc[1], zr + S.dc[2], hi);
 
+    // the same half-box traversal as gravityListKernel (same interactions), evaluated on the fly
     int sp = 1, nm = 0, np = 0;
-    unsigned long long totM2P = 0, totP2P = 0;
-    if (lane == 0) stack[0] = 0;
+    unsigned long long totM2P = 0, totP2P = 0; // half-group units
+    if (lane == 0) stack[0] = int32_t((kHalfA | kHalfB) << kTagShift);
     gWaveSync<kSpill>();
     while (sp > 0)
     {
         int32_t nd;
-        bool isM2P, isLeaf;
-        if (!popAndTest<kSpill>(t, stack, sp, stackCap, tc, ts, nd, isM2P, isLeaf)) return false;
+        unsigned mM2P, mLeaf;
+        if (!popAndTestHalves<kSpill>(t, stack, sp, stackCap, ac, as, bc, bs, nd, mM2P, mLeaf)) return false;
+        const bool isM2P = mM2P != 0, isLeaf = mLeaf != 0;
         int32_t la = isLeaf ? t.ns[nd] : 0, lb = isLeaf ? t.ne[nd] : 0;
         uint64_t bm = ballot(isM2P), bl = ballot(isLeaf);
         int cm      = __popcll(bm);
@@ -1219,23 +1188,26 @@ __device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t l
             evalM2P(L.mlst, nm, t, tc, xr, yr, zr, L.spos, acc);
             nm = 0;
         }
-        if (isM2P) L.mlst[nm + __popcll(bm & lanemaskLt())] = nd;
+        if (isM2P) L.mlst[nm + __popcll(bm & lanemaskLt())] = nd | int32_t(mM2P << kTagShift);
         nm += cm;
-        totM2P += cm;
+        totM2P += waveSum(int(__popc(mM2P)));
         while (bl)
         {
             const int src = __builtin_ctzll(bl);
             bl &= bl - 1;
             const int a0 = readLaneI(la, src), n0 = readLaneI(lb, src) - a0;
-            totP2P += n0;
-            queueLeaf(a0, n0, np, L, x, y, z, h, m, tc, T);
+            const unsigned hv = unsigned(readLaneI(int(mLeaf), src));
+            totP2P += (unsigned long long)n0 * __popc(hv);
+            queueLeaf(a0, n0, hv, np, L, S, T);
         }
         gWaveSync<kSpill>();
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     evalM2P(L.mlst, nm, t, tc, xr, yr, zr, L.spos, acc);
-    flushP2P(ListIdx{L.plst}, np, L, x, y, z, h, m, tc, T);
+    flushP2P<kP2PMixed>(ListIdx{L.plst}, 0, np, L, S, T);
     p2pFinish(T, acc);
+    totP2P = (totP2P + 1) / 2;
+    totM2P = (totM2P + 1) / 2;
     gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, totP2P, totM2P, upot);
     return true;
 }
@@ -1258,14 +1230,15 @@ struct GravLds
 {
     int32_t mlst[kGM2P];
     int32_t plst[kGP2P];
-    float4 stage[64 + 2 * kAbRow + 16]; // P2P tile (positions | k-major A operands | masses) or M2P batch (3 x 64)
+    float4 stage[64 + 2 * kAbRow + 32]; // P2P tile: positions | k-major A operands | |x|^2 | half-B masses
 };
 
 __device__ __forceinline__ GravLists listsOf(GravLds& s)
 {
     // the VALU tile aliases the MFMA tile
     return GravLists{s.mlst, s.plst, s.stage, reinterpret_cast<float2*>(s.stage + 64),
-                     reinterpret_cast<float*>(s.stage + 64 + 2 * kAbRow), s.stage};
+                     reinterpret_cast<float*>(s.stage + 64 + 2 * kAbRow),
+                     reinterpret_cast<float*>(s.stage + 64 + 2 * kAbRow + 16), s.stage};
 }
 
 //! @brief global-memory interaction list slabs: per group capM node ids and capL leaf ids + 2 counts (-1: fallback)
@@ -1273,7 +1246,8 @@ struct GravSlabs
 {
     int32_t* mlist;
     int32_t* llist;
-    int32_t* counts; // per group: M2P nodes, P2P leaves (-1: evaluated by the fused fallback kernel)
+    int32_t* counts; // per group: M2P nodes of both halves, opened leaves (-1: evaluated by the fused fallback kernel),
+                     // M2P nodes of half A only (back of mlist), of half B only (back of llist)
     int32_t* pcount; // per group: P2P particles (sum of the opened leaves' sizes), 0 for fallback groups
     int capM;
     int capL;
@@ -1293,39 +1267,49 @@ __global__ __launch_bounds__(256) void gravityListKernel(int64_t first, int64_t 
     if (g >= numGroups) return;
     int32_t* stack   = stackAll[wave];
     const int64_t ii = min(first + g * 64 + lane, last - 1);
-    double tc[3], ts[3];
-    groupBox(x[ii], y[ii], z[ii], tc, ts);
+    double ac[3], as[3], bc[3], bs[3];
+    halfBoxes(x[ii], y[ii], z[ii], ac, as, bc, bs);
 
+    // M2P entries of both halves fill the M2P slab from the front, those of half A only from its back; opened leaves
+    // fill the leaf slab from the front, M2P entries of half B only from its back. The evaluation kernels run each
+    // class as its own pass (no per-entry masks in the inner loops).
     int32_t* ml = S.mlist + g * S.capM;
     int32_t* ll = S.llist + g * S.capL;
-    int sp = 1, nm = 0, nl = 0, np = 0;
+    int sp = 1, nm = 0, nA = 0, nB = 0, nl = 0, np = 0;
     bool ok = true, slabFull = false;
-    if (lane == 0) stack[0] = 0;
+    if (lane == 0) stack[0] = int32_t((kHalfA | kHalfB) << kTagShift); // the root, walked by both halves
     gWaveSync<false>();
     while (sp > 0)
     {
         int32_t nd;
-        bool isM2P, isLeaf;
-        if (!popAndTest<false>(t, stack, sp, stackCap, tc, ts, nd, isM2P, isLeaf))
+        unsigned mM2P, mLeaf;
+        if (!popAndTestHalves<false>(t, stack, sp, stackCap, ac, as, bc, bs, nd, mM2P, mLeaf))
         {
             ok = false;
             break;
         }
-        uint64_t bm = ballot(isM2P), bl = ballot(isLeaf);
-        int cm = __popcll(bm), cl = __popcll(bl);
+        const bool isBoth = mM2P == (kHalfA | kHalfB), isA = mM2P == kHalfA, isB = mM2P == kHalfB;
+        const bool isLeaf = mLeaf != 0;
+        const uint64_t b3 = ballot(isBoth), bA = ballot(isA), bB = ballot(isB), bl = ballot(isLeaf);
+        const int c3 = __popcll(b3), cA = __popcll(bA), cB = __popcll(bB), cl = __popcll(bl);
         // a group that outgrows its slabs finishes the traversal counting only, so the host learns the whole
-        // demand ([6] leaves, [7] M2P nodes) and sizes the slabs for it in one step (the group itself falls back)
-        slabFull = slabFull || nm + cm > S.capM || nl + cl > S.capL;
+        // demand ([6] leaf slab, [7] M2P slab) and sizes the slabs for it in one step (the group itself falls back)
+        slabFull = slabFull || nm + nA + c3 + cA > S.capM || nl + nB + cl + cB > S.capL;
         if (!slabFull)
         {
-            if (isM2P) ml[nm + __popcll(bm & lanemaskLt())] = nd;
+            const uint64_t lt = lanemaskLt();
+            if (isBoth) ml[nm + __popcll(b3 & lt)] = nd;
+            if (isA) ml[S.capM - 1 - nA - __popcll(bA & lt)] = nd;
+            if (isB) ll[S.capL - 1 - nB - __popcll(bB & lt)] = nd;
             if (isLeaf)
             {
-                ll[nl + __popcll(bl & lanemaskLt())] = nd;
-                np += t.ne[nd] - t.ns[nd];
+                ll[nl + __popcll(bl & lt)] = nd | int32_t(mLeaf << kTagShift);
+                np += (t.ne[nd] - t.ns[nd]) * __popc(mLeaf); // half-group units
             }
         }
-        nm += cm;
+        nm += c3;
+        nA += cA;
+        nB += cB;
         nl += cl;
         gWaveSync<false>();
     }
@@ -1333,49 +1317,20 @@ __global__ __launch_bounds__(256) void gravityListKernel(int64_t first, int64_t 
     {
         if (lane == 0)
         {
-            atomicMax(&stats[6], (unsigned long long)nl);
-            atomicMax(&stats[7], (unsigned long long)nm);
+            atomicMax(&stats[6], (unsigned long long)(nl + nB));
+            atomicMax(&stats[7], (unsigned long long)(nm + nA));
         }
         ok = false;
     }
     np = waveSum(np);
     if (lane == 0)
     {
-        S.counts[2 * g]     = ok ? nm : -1;
-        S.counts[2 * g + 1] = ok ? nl : -1;
-        S.pcount[g]         = ok ? np : 0;
+        S.counts[4 * g]     = ok ? nm : -1;
+        S.counts[4 * g + 1] = ok ? nl : -1;
+        S.counts[4 * g + 2] = ok ? nA : 0;
+        S.counts[4 * g + 3] = ok ? nB : 0;
+        S.pcount[g]         = ok ? (np + 1) / 2 : 0;
         if (!ok) spillList[atomicAdd(&stats[5], 1ull)] = int32_t(g);
-    }
-}
-
-/*! @brief expand each group's opened leaves into its contiguous run of P2P particle indices pidx[poff[g] ..) (one
- *         wave per group; coalesced writes of up to 64 indices per leaf)
- */
-__global__ __launch_bounds__(256) void gravityExpandKernel(int64_t first, int64_t last, GravTree t, GravSlabs S,
-                                                           const int64_t* __restrict__ poff,
-                                                           int32_t* __restrict__ pidx)
-{
-    const int lane          = laneId();
-    const int64_t numGroups = (last - first + 63) / 64;
-    const int64_t g         = int64_t(blockIdx.x) * kGWaves + (threadIdx.x >> 6);
-    if (g >= numGroups) return;
-    const int nl = __builtin_amdgcn_readfirstlane(S.counts[2 * g + 1]);
-    if (nl <= 0) return;
-    const int32_t* ll = S.llist + g * S.capL;
-    int32_t* out      = pidx + poff[g];
-    int64_t pos       = 0;
-    for (int b0 = 0; b0 < nl; b0 += 64)
-    {
-        int32_t leaf = b0 + lane < nl ? ll[b0 + lane] : -1;
-        int32_t la = leaf >= 0 ? t.ns[leaf] : 0, lb = leaf >= 0 ? t.ne[leaf] : 0;
-        const int cnt = min(64, nl - b0);
-        for (int q = 0; q < cnt; ++q)
-        {
-            const int a0 = readLaneI(la, q), n0 = readLaneI(lb, q) - a0;
-            for (int off = lane; off < n0; off += 64)
-                out[pos + off] = a0 + off;
-            pos += n0;
-        }
     }
 }
 
@@ -1400,7 +1355,9 @@ __device__ __forceinline__ int costBin(int c)
 //! @brief work of group g in evaluation kernel k (0: M2P nodes, 1: P2P particles)
 __device__ __forceinline__ int groupWork(const GravSlabs& S, int64_t g, int k)
 {
-    return k == 0 ? S.counts[2 * g] : (S.counts[2 * g] < 0 ? 0 : S.pcount[g]);
+    const int nm = S.counts[4 * g];
+    return k == 0 ? (nm < 0 ? nm : nm + (S.counts[4 * g + 2] + S.counts[4 * g + 3]) / 2)
+                  : (nm < 0 ? 0 : S.pcount[g]);
 }
 
 __global__ __launch_bounds__(256) void gravityOrderHistKernel(int64_t groups, GravSlabs S, int32_t* __restrict__ hist)
@@ -1607,35 +1564,36 @@ __global__ __launch_bounds__(256, SPHX_M2P_WAVES) void gravityM2PKernel(int64_t 
                                                            float* __restrict__ az, double* __restrict__ ugrav,
                                                            double* __restrict__ out,
                                                            unsigned long long* __restrict__ stats, GravSlabs S,
-                                                           const int32_t* __restrict__ order, int64_t numSlots)
+                                                           const int32_t* __restrict__ order, int64_t numSlots,
+                                                           NodeRecs R, const double* __restrict__ mm)
 {
-#ifdef SPHX_GRAV_M2P_MFMA2
-    __shared__ float4 stage[kGWaves][kM2P2Stage];
-#else
     __shared__ float4 stage[kGWaves][5 * 64];
-#endif
     __shared__ double red[kGWaves];
     const int wave          = threadIdx.x >> 6;
     const int64_t numGroups = (last - first + 63) / 64;
     const int64_t g         = evalGroup(order, numSlots, numGroups);
     double upot             = 0;
-    int nm                  = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[2 * g]) : -1;
+    int nm                  = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[4 * g]) : -1;
     SPHX_DCHECK(nm <= S.capM, 3);
 #ifdef SPHX_DEVICE_CHECKS
     nm = min(nm, S.capM);
 #endif
     if (nm >= 0)
     {
-        EvalTarget e = evalTarget(g, first, last, x, y, z, h);
+        const int nA = __builtin_amdgcn_readfirstlane(S.counts[4 * g + 2]);
+        const int nB = __builtin_amdgcn_readfirstlane(S.counts[4 * g + 3]);
+        EvalTarget e    = evalTarget(g, first, last, x, y, z, h);
+        const P2PSrc fr = p2pSrc(nullptr, nullptr, mm, e.tc); // quantized group center
+        M2PTarget T;
+        m2pInit(T, e.xr + fr.dc[0], e.yr + fr.dc[1], e.zr + fr.dc[2]);
+        // three passes: nodes of both halves, of half A only, of half B only
+        evalM2PMfma<0, 4>(S.mlist + g * S.capM, nm, R, fr, stage[wave], T);
+        evalM2PMfma<0, 2>(S.mlist + g * S.capM + S.capM - nA, nA, R, fr, stage[wave], T);
+        evalM2PMfma<2, 4>(S.llist + g * S.capL + S.capL - nB, nB, R, fr, stage[wave], T);
         float acc[4] = {0, 0, 0, 0};
-#ifdef SPHX_GRAV_VALU_M2P
-        evalM2P(S.mlist + g * S.capM, nm, t, e.tc, e.xr, e.yr, e.zr, stage[wave], acc);
-#elif defined(SPHX_GRAV_M2P_MFMA2)
-        evalM2PMfma2(S.mlist + g * S.capM, nm, t, e.tc, e.xr, e.yr, e.zr, stage[wave], acc);
-#else
-        evalM2PMfma(S.mlist + g * S.capM, nm, t, e.tc, e.xr, e.yr, e.zr, stage[wave], acc);
-#endif
-        gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, 0ull, (unsigned long long)nm, upot);
+        m2pFinish(T, acc);
+        gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, 0ull,
+                     (unsigned long long)(nm + (nA + nB + 1) / 2), upot);
     }
     blockEnergy(upot, red, kGWaves, out);
 }
@@ -1654,9 +1612,8 @@ __global__ __launch_bounds__(256, SPHX_P2P_WAVES) void gravityP2PKernel(int64_t 
                                                            float* __restrict__ az, double* __restrict__ ugrav,
                                                            double* __restrict__ out,
                                                            unsigned long long* __restrict__ stats, GravSlabs S,
-                                                           const int64_t* __restrict__ poff,
-                                                           const int32_t* __restrict__ pidx,
-                                                           float4* __restrict__ pacc,
+                                                           float4* __restrict__ pacc, const int4* __restrict__ rec,
+                                                           const double* __restrict__ mm,
                                                            const int32_t* __restrict__ order, int64_t numSlots)
 {
     __shared__ GravLds lds[kGWaves];
@@ -1666,63 +1623,83 @@ __global__ __launch_bounds__(256, SPHX_P2P_WAVES) void gravityP2PKernel(int64_t 
     const int64_t numGroups = (last - first + 63) / 64;
     const int64_t g         = evalGroup(order, numSlots, numGroups);
     double upot             = 0;
-    const int nl            = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[2 * g + 1]) : -1;
+    const int nl            = g < numGroups ? __builtin_amdgcn_readfirstlane(S.counts[4 * g + 1]) : -1;
     if (nl >= 0)
     {
         GravLists L  = listsOf(lds[wave]);
         EvalTarget e = evalTarget(g, first, last, x, y, z, h);
         float acc[4] = {0, 0, 0, 0};
+        const P2PSrc src = p2pSrc(rec, m, mm, e.tc);
         P2PTarget T;
-        p2pInit(T, e.xr, e.yr, e.zr, e.hi);
-        int np = 0;
-        if (pidx)
+        p2pInit(T, e.xr + src.dc[0], e.yr + src.dc[1], e.zr + src.dc[2], e.hi);
+        int np2 = 0; // applied sources in half-group units (2 per source of both halves)
+        // windows of up to 255 opened leaves: sizes prefix-summed into LDS (plst holds the prefix (256) | the starts
+        // (255)), the source indices generated per chunk (no expanded index list, no host-sized buffer). The window's
+        // leaves are ordered by half mask (both | A only | B only), and each class runs as its own pass
+        static_assert(kGP2P >= 2 * 256, "leaf window of the P2P kernel");
+        const int32_t* ll = S.llist + g * S.capL;
+        int32_t* pre      = L.plst;
+        int32_t* st       = L.plst + 256;
+        const uint64_t lt = lanemaskLt();
+        for (int w0 = 0; w0 < nl; w0 += 255)
         {
-            const int64_t p0 = poff[g];
-            np               = int(poff[g + 1] - p0);
-            flushP2P(ListIdx{pidx + p0}, np, L, x, y, z, h, m, e.tc, T);
-        }
-        else
-        {
-            // windows of up to 255 opened leaves: sizes prefix-summed into LDS (plst holds the prefix (256) | the
-            // starts (255)), the source indices generated per chunk (no expanded index list, no host-sized buffer)
-            static_assert(kGP2P >= 2 * 256, "leaf window of the P2P kernel");
-            const int32_t* ll = S.llist + g * S.capL;
-            int32_t* pre      = L.plst;
-            int32_t* st       = L.plst + 256;
-            for (int w0 = 0; w0 < nl; w0 += 255)
+            const int nw = min(255, nl - w0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the previous window's reads are done
+            int32_t a0[4], sz[4];
+            unsigned hm[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
             {
-                const int nw = min(255, nl - w0);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the previous window's reads are done
-                int run = 0;
-                for (int b = 0; b < nw; b += 64)
+                const int k      = 64 * b + lane;
+                const int32_t e  = k < nw ? ll[w0 + k] : -1;
+                const int32_t lf = e & kIdMask;
+                hm[b]            = e != -1 ? tagOf(e) : 0u;
+                a0[b]            = e != -1 ? t.ns[lf] : 0;
+                sz[b]            = e != -1 ? t.ne[lf] - a0[b] : 0;
+            }
+            int run = 0, placed = 0, bound[4] = {0, 0, 0, 0}, first[3] = {0, 0, 0}; // per class: offset, leaf
+            const unsigned order[3] = {kHalfA | kHalfB, kHalfA, kHalfB};
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+            {
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
                 {
-                    const int k      = b + lane;
-                    const int32_t lf = k < nw ? ll[w0 + k] : -1;
-                    const int32_t a0 = lf >= 0 ? t.ns[lf] : 0;
-                    const int sz     = lf >= 0 ? t.ne[lf] - a0 : 0;
-                    int inc          = sz; // inclusive wave scan of the sizes
+                    const bool sel    = hm[b] == order[c];
+                    const uint64_t bs = ballot(sel);
+                    if (bs == 0) continue;
+                    const int s = sel ? sz[b] : 0;
+                    int inc     = s; // inclusive wave scan of the selected sizes
                     for (int o = 1; o < 64; o <<= 1)
                     {
                         const int v = __shfl_up(inc, o);
                         if (lane >= o) inc += v;
                     }
-                    if (k < nw)
+                    if (sel)
                     {
-                        pre[k] = run + inc - sz;
-                        st[k]  = a0;
+                        const int k = placed + __popcll(bs & lt);
+                        pre[k]      = run + inc - s;
+                        st[k]       = a0[b];
                     }
                     run += __shfl(inc, 63);
+                    placed += __popcll(bs);
                 }
-                if (lane == 0) pre[nw] = run;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                flushP2P(LeafIdx{pre, st, nw}, run, L, x, y, z, h, m, e.tc, T);
-                np += run;
+                bound[c + 1] = run;
+                if (c < 2) first[c + 1] = placed;
             }
+            if (lane == 0) pre[nw] = run;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            flushP2P<kP2PBoth>(LeafCursor{pre, st, nw, 0, 0}, 0, bound[1], L, src, T);
+            flushP2P<kP2PHalfA>(LeafCursor{pre, st, nw, first[1], bound[1]}, bound[1], bound[2] - bound[1], L, src,
+                                T);
+            flushP2P<kP2PHalfB>(LeafCursor{pre, st, nw, first[2], bound[2]}, bound[2], bound[3] - bound[2], L, src,
+                                T);
+            np2 += 2 * bound[1] + (bound[3] - bound[1]);
         }
         p2pFinish(T, acc);
         // [8]: chunks on the MFMA tile (low 32 bits) / on the VALU fallback (high 32 bits)
         if (lane == 0) atomicAdd(&stats[8], (unsigned long long)T.nMfma | ((unsigned long long)T.nValu << 32));
-        unsigned long long totP2P = (unsigned long long)np;
+        unsigned long long totP2P = (unsigned long long)((np2 + 1) / 2);
         gravityStore(g, first, last, acc, G, m, ax, ay, az, ugrav, stats, totP2P, 0ull, upot, pacc);
     }
     else if (g < numGroups)
@@ -1759,7 +1736,8 @@ __global__ __launch_bounds__(64) void gravitySpillKernel(int64_t first, int64_t 
                                                          double* __restrict__ ugrav, double* __restrict__ out,
                                                          unsigned long long* __restrict__ stats,
                                                          const int32_t* __restrict__ spillList,
-                                                         int32_t* __restrict__ scratch)
+                                                         int32_t* __restrict__ scratch, const int4* __restrict__ rec,
+                                                         const double* __restrict__ mm)
 {
     __shared__ GravLds lds;
     __shared__ double red[1];
@@ -1770,7 +1748,7 @@ __global__ __launch_bounds__(64) void gravitySpillKernel(int64_t first, int64_t 
     {
         double u = 0;
         bool ok  = gravityGroup<true>(spillList[k], first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, stats,
-                                      stack, listsOf(lds), kGSpillFront, u);
+                                      stack, listsOf(lds), kGSpillFront, u, rec, mm);
         upot += u;
         if (!ok && threadIdx.x == 0) atomicAdd(&stats[1], 1ull);
     }
@@ -1782,7 +1760,7 @@ static int64_t padTo64(int64_t v) { return (v + 63) / 64 * 64; }
 size_t gravityScratchBytes(int64_t n, int capM, int capL)
 {
     int64_t groups = (n + 63) / 64;
-    return size_t(padTo64(groups) + int64_t(kGSpillWaves) * kGSpillFront + padTo64(2 * groups) + padTo64(groups) +
+    return size_t(padTo64(groups) + int64_t(kGSpillWaves) * kGSpillFront + padTo64(4 * groups) + padTo64(groups) +
                   groups * int64_t(capM + capL) + padTo64(2 * groups) + padTo64(4 * sgGridBlocks(groups)) +
                   4 * kOrdBins) *
            sizeof(int32_t);
@@ -1804,7 +1782,7 @@ static GravScratch carve(void* scratch, int64_t groups, int capM, int capL)
     c.spillList = static_cast<int32_t*>(scratch);
     c.spillMem  = c.spillList + padTo64(groups);
     int32_t* counts = c.spillMem + int64_t(kGSpillWaves) * kGSpillFront;
-    int32_t* pcount = counts + padTo64(2 * groups);
+    int32_t* pcount = counts + padTo64(4 * groups);
     int32_t* mlist  = pcount + padTo64(groups);
     int32_t* llist  = mlist + groups * int64_t(capM);
     c.S             = GravSlabs{mlist, llist, counts, pcount, capM, capL};
@@ -1812,11 +1790,6 @@ static GravScratch carve(void* scratch, int64_t groups, int capM, int capL)
     c.orderSG       = c.order + padTo64(2 * groups);
     c.hist          = c.orderSG + padTo64(4 * sgGridBlocks(groups));
     return c;
-}
-
-int32_t* gravityParticleCounts(void* scratch, int64_t n, int capM, int capL)
-{
-    return carve(scratch, (n + 63) / 64, capM, capL).S.pcount;
 }
 
 void computeGravityLists(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
@@ -1839,20 +1812,30 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
                         const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
                         const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
                         double* ugrav, double* out, unsigned long long* stats, void* scratch, int capM, int capL,
-                        const int64_t* poff, int32_t* pidx, void* paccBuf, hipStream_t s, int phase)
+                        void* paccBuf, int64_t nsrc, int64_t numNodes, void* recBuf, const double* mm,
+                        hipStream_t s)
 {
     float4* pacc = static_cast<float4*>(paccBuf);
+    int4* rec    = static_cast<int4*>(recBuf);
     int64_t n = last - first;
     if (n <= 0) return;
+    // P2P source records of all particles of the tree and M2P node records (frame: mm = [min, max] per dimension,
+    // on the device); the node records follow the particle records in the same buffer
+    gravityRecordsKernel<<<gridFor(nsrc, 256), 256, 0, s>>>(nsrc, x, y, z, h, mm, rec);
+    SPHX_LAUNCH_CHECK();
+    float4* nra = reinterpret_cast<float4*>(rec + nsrc);
+    float4* nrb = nra + numNodes;
+    float2* nrc = reinterpret_cast<float2*>(nrb + numNodes);
+    gravityNodeRecordsKernel<<<gridFor(numNodes, 256), 256, 0, s>>>(numNodes, centers, (const Quadrupole*)mp, mm, nra,
+                                                                   nrb, nrc);
+    SPHX_LAUNCH_CHECK();
+    const NodeRecs nrec{nra, nrb, nrc};
     GravTree t{child, n2l, ns, ne, centers, (const Quadrupole*)mp};
     int64_t groups = (n + 63) / 64;
     GravScratch c  = carve(scratch, groups, capM, capL);
     unsigned grid  = unsigned((groups + kGWaves - 1) / kGWaves);
     unsigned gridP = grid; // P2P grid (the super-group order pads it to whole runs on all XCDs)
     int64_t slotsP = groups; // valid entries of the P2P order
-    // phase 1: M2P only (needs no particle index list), phase 2: the P2P part, 0: both. Split so that the host
-    // reads the P2P list size while the M2P kernel runs (ops/gravity.py P2P_EXPAND; by default phase 0 runs everything
-    // with pidx == nullptr: the P2P kernel generates its sources from the leaf lists and nothing waits on the host)
 #ifdef SPHX_GRAV_SFC_ORDER
     const int32_t* orderM = nullptr;
     const int32_t* orderP = nullptr;
@@ -1864,7 +1847,6 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
 #else
     const int32_t* orderM = nullptr;
 #endif
-    if (phase != 2)
     {
         SPHX_CHECK(hipMemsetAsync(c.hist, 0, 4 * kOrdBins * sizeof(int32_t), s));
         const unsigned og = unsigned(std::min<int64_t>((groups + 255) / 256, 1024));
@@ -1889,18 +1871,6 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
     slotsP                = int64_t(gridP) * kGWaves;
 #endif
 #endif
-    if (phase == 1)
-    {
-        gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
-                                                       stats, c.S, orderM, groups);
-        SPHX_LAUNCH_CHECK();
-        return;
-    }
-    if (pidx)
-    {
-        gravityExpandKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, c.S, poff, pidx);
-        SPHX_LAUNCH_CHECK();
-    }
     // P2P partials land in pacc and are added by gravityCombineKernel. The two evaluation kernels run one after the
     // other on s: run concurrently (P2P on a side stream, SPHX_GRAV_CONCURRENT) they compete for the same SIMDs and
     // the step is ~1 ms slower on Evrard -n 200 (37.4 vs 38.4 ms, profiles/r2_perf_log.md)
@@ -1919,20 +1889,17 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
     SPHX_CHECK(hipEventRecord(fork, s));
     SPHX_CHECK(hipStreamWaitEvent(side, fork, 0));
     gravityP2PKernel<<<gridP, 64 * kGWaves, 0, side>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
-                                                      stats, c.S, poff, pidx, pacc, orderP, slotsP);
+                                                      stats, c.S, pacc, rec, mm, orderP, slotsP);
     SPHX_LAUNCH_CHECK();
     SPHX_CHECK(hipEventRecord(join, side));
-    if (phase == 0)
-    {
-        gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
-                                                       stats, c.S, orderM, groups);
-        SPHX_LAUNCH_CHECK();
-    }
+    gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
+                                                   c.S, orderM, groups, nrec, mm);
+    SPHX_LAUNCH_CHECK();
     SPHX_CHECK(hipStreamWaitEvent(s, join, 0));
     gravityCombineKernel<<<gridFor(n, 256), 256, 0, s>>>(first, last, pacc, m, G, ax, ay, az, ugrav);
     SPHX_LAUNCH_CHECK();
     gravitySpillKernel<<<kGSpillWaves, 64, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
-                                                   c.spillList, c.spillMem);
+                                                   c.spillList, c.spillMem, rec, mm);
     SPHX_LAUNCH_CHECK();
 }
 

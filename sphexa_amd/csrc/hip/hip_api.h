@@ -115,7 +115,8 @@ void markInBoxes(int64_t nb, const double* bc, const double* bh, const int32_t* 
 
 // neighbors.hip
 // stats: [0] h-iteration failures, [1] groups overflowing even the spill storage, [2] spilled groups, [3]/[4] rounds /
-// touched leaves (opt-in), [6] groups over the chunk-table capacity, [8 + 32 k] overflow-row stripe counters
+// touched leaves (opt-in), [6] groups over the chunk-table capacity | groups that recovered from it by halving h << 32,
+// [8 + 32 k] overflow-row stripe counters
 size_t neighborScratchBytes(int64_t n, unsigned ngmax);
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int home,
@@ -220,8 +221,8 @@ void gravityUpsweepLevel(int64_t a, int64_t b, const int32_t* n2l, const int32_t
                          hipStream_t s);
 void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, double invTheta, double* centers,
                    hipStream_t s);
-// Barnes-Hut in two phases: interaction lists (+ per-group P2P particle counts), then evaluation given the
-// exclusive scan poff (groups + 1 entries) of those counts and a pidx buffer of poff[groups] entries
+// Barnes-Hut in two phases: interaction lists (per 64-target group, tagged with the target halves they apply to),
+// then evaluation (M2P kernel, P2P kernel, combine, fused fallback for groups that overflowed the slabs)
 size_t gravityScratchBytes(int64_t n, int capM, int capL);
 
 // device-check build (common.h SPHX_DCHECK): read and clear the failed-check bits of each translation unit
@@ -229,7 +230,6 @@ unsigned dcheckHydro();
 unsigned dcheckSfc();
 unsigned dcheckGravity();
 bool deviceChecksEnabled();
-int32_t* gravityParticleCounts(void* scratch, int64_t n, int capM, int capL);
 void computeGravityLists(int64_t first, int64_t last, const int32_t* child, const int32_t* n2l, const int32_t* ns,
                          const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
                          const double* z, unsigned long long* stats, void* scratch, int testFrontCap, int capM,
@@ -238,7 +238,9 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
                         const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
                         const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
                         double* ugrav, double* out, unsigned long long* stats, void* scratch, int capM, int capL,
-                        const int64_t* poff, int32_t* pidx, void* pacc, hipStream_t s, int phase = 0);
+                        void* pacc, int64_t nsrc, int64_t numNodes, void* rec, const double* mm, hipStream_t s);
+//! bytes of the record buffer of computeGravityEval (16 B per source particle, 40 B per tree node)
+inline size_t gravityRecordBytes(int64_t nsrc, int64_t numNodes) { return size_t(16 * nsrc + 40 * numNodes); }
 void directSum(int64_t first, int64_t last, int64_t n, const double* x, const double* y, const double* z,
                const float* h, const float* m, float G, float* ax, float* ay, float* az, double* ugrav, double* out,
                hipStream_t s);

@@ -244,7 +244,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     unsigned long long nStagedLast = 0, nSubLast = 0;
     uint32_t selfCode = padCode;
     int round = 0;
-    bool chunkOvf = false, didSplit = false;
+    bool chunkOvf = false, didSplit = false, shrunk = false;
     // Sub-group passes (target-group splitting, reference traversal/groups.cuh:188-303): a group whose frontier or
     // candidate-leaf list overflows is searched as consecutive lane ranges of 32, 16, ... targets, each with its own
     // tight search box (a group straddling an SFC jump has one box over both regions: hundreds of candidate leaves).
@@ -732,7 +732,15 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         nT   = nTall;
         len0 = lenMin; // a group that had to split starts the next round split
 
-        // 5. smoothing length iteration
+        // 5. smoothing length iteration. A group whose candidates span more chunks than its table holds (> 32 k
+        //    source particles for 64 targets: an initial h far too large) halves every lane's h, as updateH does for
+        //    counts far above the target, and searches again; without h iteration the host raises
+        if (chunkOvf && (iterateH & 1) && round < 10)
+        {
+            hi *= 0.5f;
+            shrunk = true;
+            continue;
+        }
         bool repeat = (iterateH & 1) && valid && (ncSph < ngmin || (ncSph - 1) > ngmax);
         if (!ballot(repeat) || round >= 10 || chunkOvf) break;
         if (repeat) hi = sphx::updateH<float>(ng0, ncSph, hi);
@@ -794,6 +802,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     {
         if (round >= 10) atomicAdd(&stats[0], 1ull);
         if (chunkOvf) atomicAdd(&stats[6], 1ull);
+        if (shrunk) atomicAdd(&stats[6], 1ull << 32); // (high half) groups that halved h after a table overflow
         if (didSplit) atomicAdd(&stats[5], 1ull); // groups searched in sub-group passes (final round)
         if (iterateH & 2) // statistics (opt-in): search rounds and touched leaves, summed over groups
         {

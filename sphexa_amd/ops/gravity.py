@@ -31,17 +31,6 @@ def _round64(v: int) -> int:
     return (int(v) + 63) // 64 * 64
 
 
-def _int32_view(ptr: int, count: int, base: torch.Tensor) -> torch.Tensor:
-    """int32 tensor aliasing ``count`` elements at device address ``ptr`` inside the byte buffer ``base``"""
-    off = ptr - base.data_ptr()
-    assert off % 4 == 0 and 0 <= off and off + 4 * count <= base.numel() * base.element_size()
-    return base.view(torch.uint8)[off:off + 4 * count].view(torch.int32)
-
-
-# P2P sources through an expanded per-group particle index list (the host reads its size: one wait per evaluation)
-# instead of indices generated from the opened-leaf lists inside the P2P kernel (default)
-P2P_EXPAND = False
-
 # GPU upsweep in one launch (arrival counters) instead of leaves + one launch per level + MAC. Off: measured 8x slower
 # (Evrard -n 100: 1.17 ms vs ~0.15 ms; the per-node agent-scope fences write back / invalidate the XCD L2s), kept for
 # A/B and covered by tests/test_gravity.py::test_fused_upsweep_matches_levels
@@ -87,17 +76,6 @@ def upsweep(tree: Octree, x, y, z, m, box: Box, theta: float, sfc_kind: int = 0)
                                    x.data_ptr(), y.data_ptr(), z.data_ptr(), m.data_ptr(), box.to_array(), sfc_kind,
                                    inv_theta, centers.data_ptr(), mp.data_ptr())
     return centers, mp
-
-
-_PINNED: dict = {}
-
-
-def _pinned_total() -> torch.Tensor:
-    """one pinned int64 host word per process (device-to-host copies into it are asynchronous)"""
-    t = _PINNED.get("total")
-    if t is None:
-        t = _PINNED["total"] = torch.empty(1, dtype=torch.int64, pin_memory=True)
-    return t
 
 
 class GravityPending:
@@ -158,42 +136,20 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         hp.gravity_lists(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), st_dev.data_ptr(),
                          scratch.data_ptr(), TEST_FRONT_CAP, cap_m, cap_l, s)
         pacc = torch.empty(4 * n, dtype=torch.float32, device=x.device)  # P2P partials (phi, a) per target
-        if not P2P_EXPAND:
-            # the P2P kernel generates its source indices from the opened-leaf lists: no index list, no host wait
-            hp.gravity_eval(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
-                            m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
-                            0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), st_dev.data_ptr(),
-                            scratch.data_ptr(), cap_m, cap_l, 0, 0, pacc.data_ptr(), s, phase=0)
-            pending = GravityPending(torch.cat([st_dev.to(torch.float64), out]), groups, (cap_m, cap_l), stats,
-                                     x.device)
-            return pending if defer else pending.finish(pending.dev.cpu().tolist())
-        pcount = _int32_view(hp.gravity_particle_counts(scratch.data_ptr(), n, cap_m, cap_l), groups, scratch)
-        # per-group offsets of the P2P particle runs: exclusive scan (hand-written tile scan, sample_sort.hip) of the
-        # counts with a trailing zero, so poff[groups] is the total
-        poff = torch.zeros(groups + 1, dtype=torch.int64, device=x.device)
-        poff[:groups].copy_(pcount)
-        stmp = torch.empty(hp.scan_temp_bytes(groups + 1), dtype=torch.uint8, device=x.device)
-        hp.exclusive_scan_i64(poff.data_ptr(), poff.data_ptr(), groups + 1, stmp.data_ptr(), stmp.numel(), s)
-        # the P2P list size goes to pinned host memory ahead of the M2P kernel: the host waits for that copy only,
-        # and enqueues the P2P part while M2P runs (no idle gap on the GPU)
-        total_h = _pinned_total()
-        total_h.copy_(poff[-1:], non_blocking=True)
-        copied = torch.cuda.Event()
-        copied.record()
-        eval_args = (first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), m.data_ptr(),
-                     float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(), 0 if ugrav is None else ugrav.data_ptr(),
-                     out.data_ptr(), st_dev.data_ptr(), scratch.data_ptr(), cap_m, cap_l, poff.data_ptr())
-        # phase 2a: M2P of the accepted nodes
-        hp.gravity_eval(*eval_args, 0, pacc.data_ptr(), s, phase=1)
-        copied.synchronize()
-        total = int(total_h[0])
-        pidx = torch.empty(max(total, 1), dtype=torch.int32, device=x.device)
-        # phase 2b: expand leaves to particle runs, MFMA P2P, combine, fused fallback for overflowing groups
-        hp.gravity_eval(*eval_args, pidx.data_ptr(), pacc.data_ptr(), s, phase=2)
+        # the P2P kernel generates its source indices from the opened-leaf lists: no index list, no host wait
+        # P2P source records (fixed point in a frame over the particles' extent, gravity.hip gravityRecordsKernel)
+        from .reduce import min_max
+        nsrc = x.numel()
+        mm = min_max([x, y, z])
+        # records: 16 B per source particle + 40 B per node (M2P), gravity.hip gravityNodeRecordsKernel
+        rec = torch.empty(4 * nsrc + 10 * tree.num_nodes, dtype=torch.int32, device=x.device)
+        hp.gravity_eval(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
+                        m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
+                        0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), st_dev.data_ptr(),
+                        scratch.data_ptr(), cap_m, cap_l, pacc.data_ptr(), nsrc, tree.num_nodes, rec.data_ptr(),
+                        mm.data_ptr(), s)
         pending = GravityPending(torch.cat([st_dev.to(torch.float64), out]), groups, (cap_m, cap_l), stats, x.device)
-        if defer:
-            return pending
-        return pending.finish(pending.dev.cpu().tolist())
+        return pending if defer else pending.finish(pending.dev.cpu().tolist())
     st = torch.zeros(2, dtype=torch.int64)
     e = float(_lib.cpu().compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
                                          tree.node_start.data_ptr(), tree.node_end.data_ptr(), centers.data_ptr(),

@@ -246,6 +246,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         rec = _rec(d, 0, "xmass")
         ride_host = None
         spec_buf = None
+        shrunk = 0
         for _attempt in range(2):
             ov = ((buf.numel() - region) // 256 - num_groups * home) // K
             stats = torch.zeros(8 + 32 * K, dtype=torch.int64, device=x.device)
@@ -286,6 +287,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
             if ex is not None:
                 ride_host = host[8 + 6 * K:].view(np.float64).tolist()
             st = host[:8].tolist()
+            shrunk += int(st[6]) >> 32  # (a repeated search starts from the h this one left)
             ctr = host[8:8 + K]
             if int(ctr.max()) <= ov:
                 break
@@ -322,9 +324,13 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         plan = (num_groups, plan_home, plan_ov)
         if int(st[1]) > 0:
             raise NeighborSearchError(f"GPU traversal stack overflow in {int(st[1])} groups")
-        if int(st[6]) > 0:
-            raise NeighborSearchError(f"{int(st[6])} target groups touch more than {CHUNK_CAP - 1} source chunks "
-                                      f"(chunk-table capacity of the GPU lists)")
+        if int(st[6]) & 0xFFFFFFFF:
+            raise NeighborSearchError(f"{int(st[6]) & 0xFFFFFFFF} target groups touch more than {CHUNK_CAP - 1} "
+                                      f"source chunks (chunk-table capacity of the GPU lists)" +
+                                      ("" if iterate_h else "; with the h iteration on, such groups halve h and "
+                                       "search again"))
+        # groups whose candidates outgrew the chunk table with the initial h and that halved h (neighbors.hip)
+        d.nc_shrunk = shrunk
         _check_convergence(d, int(st[0]))
         d.nc_spilled = int(st[2])
         d.nc_split = int(st[5])  # groups searched in sub-group passes (neighbors.hip searchGroup)

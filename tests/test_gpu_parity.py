@@ -197,6 +197,32 @@ def test_neighbor_spill_path(gpu, monkeypatch):
     assert neighbor_lists_as_sets(nl, dg["nc"]) == sets_ref
 
 
+def test_neighbor_chunk_overflow_halves_h(gpu):
+    """an initial h seven times too large makes the groups' candidates span more chunks than their tables hold (64 000
+    lattice particles, ~34 000 per sphere): the search halves h for those groups and iterates on instead of failing,
+    and the final lists are exactly the neighbor sets of the final h (CPU search, no iteration)"""
+    from sphexa_amd.ops import neighbors as N
+
+    dg, pg, domg = _setup(gpu, 40, jitter=0.01)
+    pg.sync(domg, dg)
+    n = dg.size
+    dg["h"].mul_(7.0)
+    with pytest.raises(N.NeighborSearchError, match="chunk"):
+        find_neighbors(dg, domg.octree, domg.box, 0, n, iterate_h=False)
+    nl = find_neighbors(dg, domg.octree, domg.box, 0, n)
+    assert dg.nc_shrunk > (n + 63) // 128
+    nc = dg["nc"].cpu()
+    assert int(nc.min()) >= dg.ng0 // 4 and int(nc.max()) <= dg.ngmax + 1
+    # CPU reference: the same particles, the GPU's final h, no h iteration
+    dc, pc, domc = _setup("cpu", 40, jitter=0.01)
+    pc.sync(domc, dc)
+    assert torch.equal(dc["keys"], dg["keys"].cpu())
+    dc["h"] = dg["h"].cpu()
+    nl_c = find_neighbors(dc, domc.octree, domc.box, 0, n, iterate_h=False)
+    assert torch.equal(dc["nc"], nc)
+    assert neighbor_lists_as_sets(nl, dg["nc"]) == neighbor_lists_as_sets(nl_c, dc["nc"])
+
+
 @pytest.mark.parametrize("case", ["lattice", "glass_evrard"])
 def test_neighbor_subgroup_passes(gpu, monkeypatch, case):
     """target-group splitting: groups searched as sub-group passes of 16 lanes (each with its own search box, one
