@@ -478,6 +478,17 @@ struct P2PSrc
     float inv[3];
     float dc[3]; // group center minus the quantized one (added to the targets' offsets)
     float co[3]; // quantized group center minus the frame origin (M2P node offsets)
+
+    //! offset of particle i from the quantized center, computed exactly as for the sources (a target meets itself
+    //! at distance 0: with fp64 target offsets the self pair sat one quantum apart, and with h far below the
+    //! quantum's scale its softened weight times that offset blew up)
+    __device__ __forceinline__ void offset(int64_t i, float& xr, float& yr, float& zr) const
+    {
+        const int4 q = rec[i];
+        xr           = float(int(uint32_t(q.x) - qc[0])) * inv[0];
+        yr           = float(int(uint32_t(q.y) - qc[1])) * inv[1];
+        zr           = float(int(uint32_t(q.z) - qc[2])) * inv[2];
+    }
 };
 
 __device__ __forceinline__ P2PSrc p2pSrc(const int4* rec, const float* m, const double* mm, const double gc[3])
@@ -649,7 +660,9 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const NodeRecs& R
                 Qy[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, T.bT[tb], zero, 0, 0, 0);
                 Qz[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.z, T.bT[tb], zero, 0, 0, 0);
             }
+#ifndef SPHX_GRAV_NO_SCHED_BARRIER
             __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r)
             {
@@ -842,7 +855,9 @@ __device__ __forceinline__ void p2pBlock(const GravLists& L, int sb, int kq, int
     const float4 M4 = reinterpret_cast<const float4*>(sp + 192)[sb * 4 + kq];
     float4 B4       = M4;
     if constexpr (kMixed) B4 = reinterpret_cast<const float4*>(L.smB)[sb * 4 + kq];
+#ifndef SPHX_GRAV_NO_SCHED_BARRIER
     __builtin_amdgcn_sched_barrier(0);
+#endif
     const f32x2 Xp[2] = {{X4.x, X4.y}, {X4.z, X4.w}}, Yp[2] = {{Y4.x, Y4.y}, {Y4.z, Y4.w}};
     const f32x2 Zp[2] = {{Z4.x, Z4.y}, {Z4.z, Z4.w}}, Mp[2] = {{M4.x, M4.y}, {M4.z, M4.w}};
     const f32x2 Bp[2] = {{B4.x, B4.y}, {B4.z, B4.w}};
@@ -881,15 +896,27 @@ __device__ inline void flushP2P(Idx plst, int o0, int n, const GravLists& L, con
     // of the chunk in flight stay raw (unconditional loads at a clamped index) until they are staged
     int4 rq;
     float rm;
-    auto gather = [&](int32_t e)
+    auto gather = [&](int32_t e, int4& q, float& mm_)
     {
         const int32_t j = e & kIdMask;
-        rq = S.rec[j];
-        rm = S.m[j];
+        q   = S.rec[j];
+        mm_ = S.m[j];
     };
+#ifdef SPHX_P2P_PREFETCH2
+    // two chunks of source data in flight: chunk c's in rq/rm, c + 1's in rq1/rm1 (A/B: no gain, the kernel is at
+    // its VGPR limit and waits on the whole chain)
+    int4 rq1;
+    float rm1;
+    int32_t jN  = plst.next(o0 + lane, o0 + n);      // chunk c
+    int32_t jN1 = plst.next(o0 + 64 + lane, o0 + n);  // chunk c + 1
+    int32_t jNN = plst.next(o0 + 128 + lane, o0 + n); // chunk c + 2
+    gather(jN, rq, rm);
+    gather(jN1, rq1, rm1);
+#else
     int32_t jN  = plst.next(o0 + lane, o0 + n);
     int32_t jNN = plst.next(o0 + 64 + lane, o0 + n);
-    gather(jN);
+    gather(jN, rq, rm);
+#endif
     for (int c0 = 0; c0 < n; c0 += 64)
     {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // previous tile fully read before it is overwritten
@@ -943,9 +970,16 @@ __device__ inline void flushP2P(Idx plst, int o0, int n, const GravLists& L, con
             if constexpr (kMode == kP2PMixed) reinterpret_cast<float*>(L.sxm + 80)[lane] = mB;
             ++T.nValu;
         }
-        jN = jNN;
+#ifdef SPHX_P2P_PREFETCH2
+        jN = jN1, rq = rq1, rm = rm1;
+        jN1 = jNN;
+        jNN = plst.next(o0 + c0 + 192 + lane, o0 + n);
+        gather(jN1, rq1, rm1); // unconditional (past the end: clamped index)
+#else
+        jN  = jNN;
         jNN = plst.next(o0 + c0 + 128 + lane, o0 + n);
-        gather(jN); // unconditional (past the end: clamped index) so the loads land in the loop registers directly
+        gather(jN, rq, rm); // unconditional (past the end: clamped index) so the loads land in the loop registers
+#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (!mfma)
         {
@@ -1166,7 +1200,11 @@ __device__ __forceinline__ bool gravityGroup(int64_t g, int64_t first, int64_t l
     float xr = float(xi - tc[0]), yr = float(yi - tc[1]), zr = float(zi - tc[2]);
     float acc[4] = {0, 0, 0, 0};
     P2PTarget T;
-    p2pInit(T, xr + S.dc[0], yr + S.dc[1], zr + S.dc[2], hi);
+    {
+        float txr, tyr, tzr;
+        S.offset(ii, txr, tyr, tzr);
+        p2pInit(T, txr, tyr, tzr, hi);
+    }
 
     // the same half-box traversal as gravityListKernel (same interactions), evaluated on the fly
     int sp = 1, nm = 0, np = 0;
@@ -1630,8 +1668,10 @@ __global__ __launch_bounds__(256, SPHX_P2P_WAVES) void gravityP2PKernel(int64_t 
         EvalTarget e = evalTarget(g, first, last, x, y, z, h);
         float acc[4] = {0, 0, 0, 0};
         const P2PSrc src = p2pSrc(rec, m, mm, e.tc);
+        float txr, tyr, tzr;
+        src.offset(min(first + g * 64 + lane, last - 1), txr, tyr, tzr);
         P2PTarget T;
-        p2pInit(T, e.xr + src.dc[0], e.yr + src.dc[1], e.zr + src.dc[2], e.hi);
+        p2pInit(T, txr, tyr, tzr, e.hi);
         int np2 = 0; // applied sources in half-group units (2 per source of both halves)
         // windows of up to 255 opened leaves: sizes prefix-summed into LDS (plst holds the prefix (256) | the starts
         // (255)), the source indices generated per chunk (no expanded index list, no host-sized buffer). The window's

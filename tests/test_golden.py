@@ -265,11 +265,11 @@ def _check_scaled_loops(dev, f):
     cmax = max(abs(v) for v in c_ref)
     for k, c in enumerate(("c11", "c12", "c13", "c22", "c23", "c33")):
         assert abs(float(d[c][0]) - c_ref[k]) <= 2e-5 * cmax, c
-    assert float(d["divv"][0]) == pytest.approx(dv_ref[0], rel=1e-4)
-    assert float(d["curlv"][0]) == pytest.approx(dv_ref[1], rel=1e-4)
+    assert float(d["divv"][0]) == pytest.approx(dv_ref[0], rel=1e-5)
+    assert float(d["curlv"][0]) == pytest.approx(dv_ref[1], rel=1e-5)
     dvmax = max(abs(v) for v in dv_ref[2])
     for k, c in enumerate(("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")):
-        assert abs(float(d[c][0]) - dv_ref[2][k]) <= 1e-4 * dvmax, c
+        assert abs(float(d[c][0]) - dv_ref[2][k]) <= 1e-5 * dvmax, c
 
     # AV switches and momentum/energy on the (scaled) fixture fields
     for k, c in enumerate(("c11", "c12", "c13", "c22", "c23", "c33")):
@@ -288,8 +288,8 @@ def _check_scaled_loops(dev, f):
         H.compute_momentum_energy_ve(d, nl, B, av_clean)
         amax = max(abs(v) for v in ref[:3])
         for k, c in enumerate(("ax", "ay", "az")):
-            assert abs(float(d[c][0]) - ref[k]) <= 1e-4 * amax, (av_clean, c)
-        assert float(d["du"][0]) == pytest.approx(ref[3], rel=1e-4)
+            assert abs(float(d[c][0]) - ref[k]) <= 1e-5 * amax, (av_clean, c, float(d[c][0]), ref[k])
+        assert float(d["du"][0]) == pytest.approx(ref[3], rel=1e-5)
 
 
 def _check_std(dev, f):

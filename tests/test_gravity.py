@@ -126,6 +126,27 @@ def test_gravity_gpu_small_leaves(gpu, bucket):
 
 
 @pytest.mark.gpu
+def test_gravity_gpu_mfma_and_valu_tiles(gpu):
+    """one evaluation that takes both P2P paths: groups whose softening is tiny against their extent fail the
+    precision guard of the MFMA tile (expanded R2) and run the VALU pair loop, the others run on the matrix cores;
+    both agree with the direct sum"""
+    n = 20000
+    box, ot, x, y, z, m, h = _setup(n, gpu)
+    h = torch.where(x < 0, torch.full_like(h, 0.05), torch.full_like(h, 1e-6))
+    c, mp = G.upsweep(ot, x, y, z, m, box, 0.5)
+    acc = [torch.zeros(n, dtype=torch.float32, device=gpu) for _ in range(3)]
+    st = {}
+    eg = G.compute_gravity(ot, c, mp, 0, n, x, y, z, h, m, 1.0, *acc, stats=st)
+    assert st["p2p_mfma_chunks"] > 0 and st["p2p_valu_chunks"] > 0, st
+    r = [torch.zeros(n, dtype=torch.float32, device=gpu) for _ in range(3)]
+    egd = G.direct_sum(0, n, x, y, z, h, m, 1.0, *r)
+    a = torch.stack(acc, 1).cpu().numpy().astype(np.float64)
+    err = _errors(a, torch.stack(r, 1).cpu().numpy().astype(np.float64))
+    assert err[int(0.99 * n)] < 1e-3 and err[-1] < 3e-2, (err[int(0.99 * n)], err[-1])
+    assert abs(eg - egd) / abs(egd) < 1e-3
+
+
+@pytest.mark.gpu
 def test_let_kernels_gpu_match_cpu(gpu):
     """mark_let and the flat M2P on the GPU reproduce the OpenMP path"""
     n = 8000
