@@ -537,10 +537,12 @@ __global__ void gravityNodeRecordsKernel(int64_t N, const double* __restrict__ c
 
 //! @brief target side of the MFMA M2P: B operand [x, y, z, 1]_k of target 16 tb + col and the four targets' coordinates,
 //!        accumulators per target block (lane group kq holds partial sums over its node rows)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 struct M2PTarget
 {
     float bT[4], tx[4], ty[4], tz[4];
-    float ph[4], ax[4], ay[4], az[4];
+    f32x2 ph[4], ax[4], ay[4], az[4]; // per target block: partial sums over even / odd node rows
 };
 
 __device__ __forceinline__ void m2pInit(M2PTarget& T, float xr, float yr, float zr)
@@ -552,7 +554,7 @@ __device__ __forceinline__ void m2pInit(M2PTarget& T, float xr, float yr, float 
         const int src = tb * 16 + col;
         T.tx[tb] = __shfl(xr, src), T.ty[tb] = __shfl(yr, src), T.tz[tb] = __shfl(zr, src);
         T.bT[tb] = kq == 0 ? T.tx[tb] : (kq == 1 ? T.ty[tb] : (kq == 2 ? T.tz[tb] : 1.f));
-        T.ph[tb] = T.ax[tb] = T.ay[tb] = T.az[tb] = 0.f;
+        T.ph[tb] = T.ax[tb] = T.ay[tb] = T.az[tb] = f32x2{0.f, 0.f};
     }
 }
 
@@ -564,7 +566,8 @@ __device__ __forceinline__ void m2pFinish(const M2PTarget& T, float acc[4])
 #pragma unroll
     for (int tb = 0; tb < 4; ++tb)
     {
-        float p[4] = {T.ph[tb], T.ax[tb], T.ay[tb], T.az[tb]};
+        float p[4] = {T.ph[tb].x + T.ph[tb].y, T.ax[tb].x + T.ax[tb].y, T.ay[tb].x + T.ay[tb].y,
+                      T.az[tb].x + T.az[tb].y};
 #pragma unroll
         for (int q = 0; q < 4; ++q)
         {
@@ -606,8 +609,8 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const NodeRecs& R
     n = __builtin_amdgcn_readfirstlane(n);
     if (n <= 0) return;
     const int lane = laneId(), kq = lane >> 4, col = lane & 15;
-    float4* sC = stage;      // 64 x {cx, cy, cz, M}
-    float4* sA = stage + 64; // 4 (k) x 64 x {A_x[k], A_y[k], A_z[k], 0}
+    float* sC  = reinterpret_cast<float*>(stage); // SoA: 64 cx | 64 cy | 64 cz | 64 M
+    float4* sA = stage + 64;                       // 4 (k) x 64 x {A_x[k], A_y[k], A_z[k], 0}
     float4 ra, rb;
     float2 rq;
     auto gather = [&](int32_t e)
@@ -633,7 +636,10 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const NodeRecs& R
             const float Qcx = Qxx * cx + Qxy * cy + Qxz * cz;
             const float Qcy = Qxy * cx + Qyy * cy + Qyz * cz;
             const float Qcz = Qxz * cx + Qyz * cy + Qzz * cz;
-            sC[lane]        = make_float4(cx, cy, cz, M);
+            sC[lane]        = cx;
+            sC[64 + lane]   = cy;
+            sC[128 + lane]  = cz;
+            sC[192 + lane]  = M;
             sA[lane]        = make_float4(Qxx, Qxy, Qxz, 0.f);
             sA[64 + lane]   = make_float4(Qxy, Qyy, Qyz, 0.f);
             sA[128 + lane]  = make_float4(Qxz, Qyz, Qzz, 0.f);
@@ -647,10 +653,11 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const NodeRecs& R
         for (int tile = 0; tile < ntile; ++tile)
         {
             const float4 A = sA[64 * kq + 16 * tile + col];
-            float4 C[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                C[r] = sC[16 * tile + 4 * kq + r];
+            // node data of the lane's 4 rows 16 tile + 4 kq + r, SoA so that rows (r, r + 1) sit in adjacent registers
+            const float4 X4 = reinterpret_cast<const float4*>(sC)[4 * tile + kq];
+            const float4 Y4 = reinterpret_cast<const float4*>(sC + 64)[4 * tile + kq];
+            const float4 Z4 = reinterpret_cast<const float4*>(sC + 128)[4 * tile + kq];
+            const float4 M4 = reinterpret_cast<const float4*>(sC + 192)[4 * tile + kq];
             const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
             f32x4 Qx[4], Qy[4], Qz[4];
 #pragma unroll
@@ -663,25 +670,32 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const NodeRecs& R
 #ifndef SPHX_GRAV_NO_SCHED_BARRIER
             __builtin_amdgcn_sched_barrier(0);
 #endif
+            // pair arithmetic on pairs of node rows (r, r + 1): one v_pk_*_f32 per two pairs (13 VALU per pair
+            // instead of ~20; the M2P loop keeps the SIMD's VALU ~70 % busy, profiles/r4/pmc_grav.txt)
+            const f32x2 Cx[2] = {{X4.x, X4.y}, {X4.z, X4.w}}, Cy[2] = {{Y4.x, Y4.y}, {Y4.z, Y4.w}};
+            const f32x2 Cz[2] = {{Z4.x, Z4.y}, {Z4.z, Z4.w}}, Cm[2] = {{M4.x, M4.y}, {M4.z, M4.w}};
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+            for (int rp = 0; rp < 2; ++rp)
             {
 #pragma unroll
                 for (int tb = kTb0; tb < kTb1; ++tb)
                 {
-                    const float rx  = T.tx[tb] - C[r].x, ry = T.ty[tb] - C[r].y, rz = T.tz[tb] - C[r].z;
-                    const float r2  = rx * rx + ry * ry + rz * rz;
-                    const float ir  = __builtin_amdgcn_rsqf(r2);
-                    const float ir2 = ir * ir;
-                    const float ir5 = ir2 * ir2 * ir;
-                    const float rQr = rx * Qx[tb][r] + ry * Qy[tb][r] + rz * Qz[tb][r];
-                    const float Mir = C[r].w * ir;
-                    const float t1  = rQr * ir5;
-                    const float cmb = __builtin_fmaf(-2.5f, t1, -Mir) * ir2;
-                    T.ph[tb]        = __builtin_fmaf(-0.5f, t1, T.ph[tb] - Mir);
-                    T.ax[tb]        = __builtin_fmaf(cmb, rx, __builtin_fmaf(ir5, Qx[tb][r], T.ax[tb]));
-                    T.ay[tb]        = __builtin_fmaf(cmb, ry, __builtin_fmaf(ir5, Qy[tb][r], T.ay[tb]));
-                    T.az[tb]        = __builtin_fmaf(cmb, rz, __builtin_fmaf(ir5, Qz[tb][r], T.az[tb]));
+                    const f32x2 rx  = T.tx[tb] - Cx[rp], ry = T.ty[tb] - Cy[rp], rz = T.tz[tb] - Cz[rp];
+                    const f32x2 r2  = rx * rx + ry * ry + rz * rz;
+                    const f32x2 ir  = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
+                    const f32x2 ir2 = ir * ir;
+                    const f32x2 ir5 = ir2 * ir2 * ir;
+                    const f32x2 qx  = {Qx[tb][2 * rp], Qx[tb][2 * rp + 1]};
+                    const f32x2 qy  = {Qy[tb][2 * rp], Qy[tb][2 * rp + 1]};
+                    const f32x2 qz  = {Qz[tb][2 * rp], Qz[tb][2 * rp + 1]};
+                    const f32x2 rQr = rx * qx + ry * qy + rz * qz;
+                    const f32x2 Mir = Cm[rp] * ir;
+                    const f32x2 t1  = rQr * ir5;
+                    const f32x2 cmb = (-2.5f * t1 - Mir) * ir2;
+                    T.ph[tb]        = (T.ph[tb] - Mir) - 0.5f * t1;
+                    T.ax[tb]        = (T.ax[tb] + ir5 * qx) + cmb * rx;
+                    T.ay[tb]        = (T.ay[tb] + ir5 * qy) + cmb * ry;
+                    T.az[tb]        = (T.az[tb] + ir5 * qz) + cmb * rz;
                 }
             }
         }
@@ -709,7 +723,6 @@ __device__ __forceinline__ float maxNoCanon(float a, float b)
  * that is below ~4e-6 of the smallest softening radius (h_s + h_t)^2 in the tile, otherwise (sparse groups much
  * larger than h) with the plain VALU pair loop over the same staged sources.
  */
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct P2PTarget
 {
