@@ -172,8 +172,12 @@ def _run_case(init: str, n: int, args, comm, device) -> dict:
             print(f"# substep {k:28s} {1000.0 * v / nsteps:10.3f} ms/step", file=sys.stderr)
         if hasattr(d, "nc_rounds") and d.nc_rounds > 0:
             print(f"# neighbor search: {d.nc_rounds:.2f} rounds and {d.nc_leaves:.1f} touched leaves per "
-                  f"64-particle group (last step), {getattr(d, 'nc_split', 0)} groups split into sub-group passes, "
-                  f"{getattr(d, 'nc_spilled', 0)} spilled groups", file=sys.stderr)
+                  f"64-particle group (last step)", file=sys.stderr)
+        if hasattr(d, "nc_queued"):
+            print(f"# neighbor search paths (last step, of {(d.numParticlesGlobal + 63) // 64} groups): "
+                  f"{d.nc_queued} queued for the split kernel, {d.nc_split} searched in sub-group passes, "
+                  f"{d.nc_spilled} spilled ({d.nc_spill_chunks} of them on the chunk table), "
+                  f"{getattr(d, 'nc_shrunk', 0)} halved h on a chunk-table overflow", file=sys.stderr)
         for k, v in prop.timer.mem_peak.items():
             print(f"# memory peak in {k:28s} {v / max(d.numParticlesGlobal / size, 1):8.0f} B/particle",
                   file=sys.stderr)

@@ -72,7 +72,7 @@ constexpr int kCandWords     = kRingWords + kStageWords + kCbase;
 constexpr int kSubFront = 256;
 static_assert(2 * kSubFront <= kStageWords, "sub-pass frontiers fit the staging area");
 //! smallest lane range of a sub-group pass; a range this small that still overflows goes to the spill kernel
-constexpr int kMinSub = 4;
+constexpr int kMinSub = 1;
 //! per-wave LDS work area: the traversal frontiers, then (candidate phase) ring + staging + chunk bases
 constexpr int kWorkWords = 2 * kFrontCap > kCandWords ? 2 * kFrontCap : kCandWords;
 
@@ -228,9 +228,11 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     float* stage       = reinterpret_cast<float*>(work + kRingWords);
     int32_t* cbase     = work + kRingWords + kStageWords;
     // frontiers of the sub-group passes: the staging area (free between passes), or the spill kernel's global ones
-    int32_t* subA      = kSpill ? frontA : work + kRingWords;
-    int32_t* subB      = kSpill ? frontB : work + kRingWords + kSubFront;
-    const int subCap   = kSpill ? frontCap : min(frontCap, kSubFront);
+    // (the split and spill kernels have frontiers of their own, clear of the ring: every pass uses them)
+    constexpr bool kOwnFront = kSpill || kSplit;
+    int32_t* subA      = kOwnFront ? frontA : work + kRingWords;
+    int32_t* subB      = kOwnFront ? frontB : work + kRingWords + kSubFront;
+    const int subCap   = kOwnFront ? frontCap : min(frontCap, kSubFront);
     int32_t* rowsInt   = reinterpret_cast<int32_t*>(po.rows);
     const unsigned cap = ngmax + 1; // stored entries per lane, the target included
     const unsigned blocksMax = listBlocksMax(ngmax);
@@ -503,7 +505,12 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     ra.ensure(T, g, po);
                 }
                 if (kSplit && slot + nch > kChunkCap && !(pos == 0 && len == 64))
-                    return false; // passes re-staging shared chunks outgrow the table: the spill kernel (one pass)
+                {
+                    // passes re-staging shared chunks outgrow the table: the spill kernel (one pass); counted in the
+                    // high half of stats[1]
+                    if (lane == 0) atomicAdd(&stats[1], 1ull << 32);
+                    return false;
+                }
                 chunkOvf = slot + nch > kChunkCap;
                 if (chunkOvf) nT = 0; // reported below; the host raises
                 nTall += nT;
@@ -865,7 +872,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) SPHX_NS_OCC void findNeighbors
 /*! split path: persistent one-wave blocks take the groups the main kernel queued and search them in sub-group passes
  *  (LDS frontiers, searchGroup<kSplit>); groups that overflow even in passes of kMinSub lanes are queued again for the
  *  spill kernel (stats[7]). Kept out of the main kernel, whose registers and code stay those of the single pass. */
-constexpr int kSplitWaves = 1024;
+constexpr int kSplitWaves   = 1280; // 5 per CU (LDS: ~27 KiB per wave)
+constexpr int kSplitFront   = 2048; // frontier entries (x2) and candidate leaves of a split-kernel wave: 4x / 4x the
+constexpr int kSplitLeafCap = 1024; // main kernel's, so fewer groups need passes and fewer reach the spill kernel
 
 template<bool kCapped>
 __global__ __launch_bounds__(64) SPHX_NS_OCC void findNeighborsSplitKernel(int64_t first, int64_t last,
@@ -880,15 +889,16 @@ __global__ __launch_bounds__(64) SPHX_NS_OCC void findNeighborsSplitKernel(int64
                                                                const int32_t* __restrict__ splitList,
                                                                int32_t* __restrict__ spillList, int frontCap)
 {
-    __shared__ __attribute__((aligned(4096))) int32_t work[kWorkWords];
-    __shared__ int32_t leaves[kLeafCap];
+    __shared__ __attribute__((aligned(4096))) int32_t work[kCandWords];
+    __shared__ int32_t front[2][kSplitFront];
+    __shared__ int32_t leaves[kSplitLeafCap];
     const int64_t numSplit = int64_t(__hip_atomic_load(&stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     for (int64_t k = blockIdx.x; k < numSplit; k += gridDim.x)
     {
         const int64_t g = splitList[k];
         bool ok = searchGroup<false, kCapped, true>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po,
-                                                    nc, iterateH, stats, work, work + kFrontCap, leaves, frontCap,
-                                                    kLeafCap, work);
+                                                    nc, iterateH, stats, front[0], front[1], leaves, frontCap,
+                                                    kSplitLeafCap, work);
         if (!ok && threadIdx.x == 0) spillList[atomicAdd(&stats[7], 1ull)] = int32_t(g);
     }
 }
@@ -1020,9 +1030,10 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
                                                                      box, ng0, ngmax,
                                                                      groups, po, nc, iterateH, stats, splitList, fc);
         SPHX_LAUNCH_CHECK();
+        const int fcs = testFrontCap > 0 ? min(testFrontCap, kSplitFront) : kSplitFront;
         findNeighborsSplitKernel<kC><<<kSplitWaves, 64, 0, s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h, t,
                                                                 box, ng0, ngmax, po, nc, iterateH, stats, splitList,
-                                                                spillList, fc);
+                                                                spillList, fcs);
         SPHX_LAUNCH_CHECK();
         findNeighborsSpillKernel<kC><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h, t, box, ng0, ngmax, po, nc,
                                                                 iterateH, stats, spillList, spillMem);

@@ -322,8 +322,8 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         if max(hist) > need:
             plan_ov = -(-(max(hist) - num_groups * plan_home) // K)
         plan = (num_groups, plan_home, plan_ov)
-        if int(st[1]) > 0:
-            raise NeighborSearchError(f"GPU traversal stack overflow in {int(st[1])} groups")
+        if int(st[1]) & 0xFFFFFFFF:
+            raise NeighborSearchError(f"GPU traversal stack overflow in {int(st[1]) & 0xFFFFFFFF} groups")
         if int(st[6]) & 0xFFFFFFFF:
             raise NeighborSearchError(f"{int(st[6]) & 0xFFFFFFFF} target groups touch more than {CHUNK_CAP - 1} "
                                       f"source chunks (chunk-table capacity of the GPU lists)" +
@@ -332,8 +332,13 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         # groups whose candidates outgrew the chunk table with the initial h and that halved h (neighbors.hip)
         d.nc_shrunk = shrunk
         _check_convergence(d, int(st[0]))
-        d.nc_spilled = int(st[2])
-        d.nc_split = int(st[5])  # groups searched in sub-group passes (neighbors.hip searchGroup)
+        # search paths (neighbors.hip): groups the main kernel queued for the split kernel (LDS frontier or leaf
+        # list overflow), groups searched in sub-group passes, groups that went on to the spill kernel (global-memory
+        # frontiers) and, of those, the ones whose passes outgrew the chunk table
+        d.nc_queued = int(st[2])
+        d.nc_split = int(st[5])
+        d.nc_spilled = int(st[7])
+        d.nc_spill_chunks = int(st[1]) >> 32
         d.nc_rounds = int(st[3]) / num_groups  # mean search rounds per group (h iteration)
         d.nc_leaves = int(st[4]) / num_groups  # mean candidate leaves per group and step
         if COLLECT_STATS:  # staged candidates and hits per group; candidates inside sub-group boxes (what-if)
