@@ -578,7 +578,8 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                 else
                 {
                     // with the h iteration a lane past the cap repeats the round, and only the final round's lists are
-                    // kept: its blocks past the capacity are dropped (storeBlock), so the ring never overflows
+                    // kept: its blocks past the capacity are dropped (storeBlock), so the ring never overflows.
+#ifdef SPHX_NS_APPEND_EXEC
                     asm volatile("s_and_saveexec_b64 %[sv], %[m]\n"
                                  "ds_write_b32 %[wp], %[code]\n"
                                  "v_add_u32_e32 %[wp], 0x100, %[wp]\n"
@@ -586,6 +587,19 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                                  : [wp] "+v"(wp), [sv] "=&s"(save)
                                  : [m] "s"(hm), [code] "v"(code)
                                  : "memory");
+#else
+                    // every lane writes the code into its next free slot and only the hit lanes advance: no exec-mask
+                    // switching (two SALU per candidate, the loop's SALU count was as high as its VALU count); a miss
+                    // leaves its write in a free slot (at most 15 pending + this one: the ring has 16)
+                    uint32_t step;
+                    (void)save;
+                    asm volatile("ds_write_b32 %[wp], %[code]\n"
+                                 "v_cndmask_b32_e64 %[st], 0, 1, %[m]\n"
+                                 "v_lshl_add_u32 %[wp], %[st], 8, %[wp]"
+                                 : [wp] "+v"(wp), [st] "=&v"(step)
+                                 : [m] "s"(hm), [code] "v"(code)
+                                 : "memory");
+#endif
                 }
             };
             /* Test `count` (a multiple of 4, <= 64) staged candidates against every lane: four candidates (five
