@@ -20,15 +20,40 @@ def main():
     ap.add_argument("--init", default="sedov")
     ap.add_argument("-n", type=int, default=200)
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--at-sync", action="store_true", help="census at the start of the last step's domain sync "
+                    "(after the record workspaces are released) and the sync's own peak")
     args = ap.parse_args()
     from sphexa_amd.app.simulation import Simulation
     from sphexa_amd.parallel.comm import init_distributed
 
     comm = init_distributed("nccl")
     sim = Simulation(args.init, n=args.n, prop="ve", device=torch.device("cuda", 0), comm=comm, out=None, quiet=True)
-    for _ in range(args.steps):
+    for _ in range(args.steps - (1 if args.at_sync else 0)):
         sim.step()
     torch.cuda.synchronize()
+    if args.at_sync:
+        dom_cls = type(sim.domain)
+        orig = dom_cls.sync
+
+        def sync(self, *a, **k):
+            torch.cuda.synchronize()
+            census(sim, args, "at sync start")
+            torch.cuda.reset_peak_memory_stats()
+            base = torch.cuda.memory_allocated()
+            r = orig(self, *a, **k)
+            torch.cuda.synchronize()
+            n = sim.d.numParticlesGlobal
+            print(f"sync: allocated at start {base / n:.0f} B/p, peak inside {torch.cuda.max_memory_allocated() / n:.0f}"
+                  f" B/p, at end {torch.cuda.memory_allocated() / n:.0f} B/p")
+            return r
+
+        dom_cls.sync = sync
+        sim.step()
+        return
+    census(sim, args, "between steps")
+
+
+def census(sim, args, where):
     n = sim.d.numParticlesGlobal
     d = sim.d
     names = {}
@@ -50,11 +75,11 @@ def main():
         except Exception:
             pass
     total = sum(v[0] for v in seen.values())
-    print(f"{args.init} -n {args.n}: {n} particles; live tensors {total / 2**30:.2f} GiB ({total / n:.0f} B/particle); "
+    print(f"[{where}] {args.init} -n {args.n}: {n} particles; live tensors {total / 2**30:.2f} GiB ({total / n:.0f} B/particle); "
           f"allocator: allocated {torch.cuda.memory_allocated() / 2**30:.2f} GiB, peak "
           f"{torch.cuda.max_memory_allocated() / 2**30:.2f} GiB ({torch.cuda.max_memory_allocated() / n:.0f} B/particle)")
     rows = sorted(seen.items(), key=lambda kv: -kv[1][0])
-    for ptr, (nb, shape, dt) in rows[:40]:
+    for ptr, (nb, shape, dt) in rows[:12]:
         print(f"{nb / n:8.1f} B/p  {nb / 2**20:10.1f} MiB  {str(dt):14s} {str(shape):22s} {names.get(ptr, '')}")
 
 

@@ -13,6 +13,7 @@ records once per loop so every neighbor is a few 16-byte loads.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -27,7 +28,14 @@ DV = ("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")
 # runs: the fixed-point loops fall back to fp64-frame records in some cases (stored-mass Gradh: SrcPos 32 B; AV without
 # the IAD loop's S_i and STD IAD: SrcIad 48 B). The workspace is grow-only, so it settles at the momentum record:
 # SrcMom 96 B (fp64) or SrcMomQ 80 B (fixed point); SrcGradV (32 B) and the AV S_i (16 B) use the second buffer
-REC_BYTES = {"xmass": (32, 32), "gradh": (32, 32), "iad": (48, 48), "av": (48, 48), "mom": (96, 96), "std": (80, 80)}
+REC_BYTES = {"xmass": (32, 32), "gradh": (32, 32), "iad": (48, 32), "av": (48, 48), "mom": (96, 96), "std": (80, 80)}
+
+# fixed-point VE chain: the IAD and AV loops also write the momentum loop's own SrcMomQ records (workspace M, 80 B per
+# particle) so that the momentum loop packs only its halos. That holds workspace M from the IAD loop on, at the
+# step's memory high-water mark (IAD: lists + fields + workspaces 0, B, 1 and M). Off: the momentum loop packs its
+# records itself and the peak drops by 80 B per particle (Sedov -n 400: 622 -> ~540 B/particle) for one more
+# record pass (profiles/r4/memory.md).
+MOM_HANDOFF = os.environ.get("SPHX_MOM_HANDOFF") == "1"
 
 
 def _stream():
@@ -449,7 +457,7 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
             ho = _handoff(d)
             done = 1 if handoff_take(d, "iadq_own") else 0
             ho.clear()
-            mom = 0 if av_clean else _recM(d).data_ptr()
+            mom = _recM(d).data_ptr() if (MOM_HANDOFF and not av_clean) else 0
             _lib.hip().iad_divv_curlv(*args, d.size, _rec(d, 0, "iad").data_ptr(), _stream(),
                                       _rec(d, 1, "av").data_ptr(), inDone=done, avOut=_recB(d).data_ptr(),
                                       momOut=mom, cs=d["c"].data_ptr(), mm=d["m"].data_ptr(),
@@ -457,6 +465,8 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
             handoff_mark(d, "avv_own")
             if mom:
                 handoff_mark(d, "momq_iad")
+            # the SrcIadQ records are dead after this loop (stream-ordered reuse of the block by later loops)
+            d._rec0 = None
         else:
             _lib.hip().iad_divv_curlv(*args, *_gpu_tail(d, "iad"), _rec(d, 1, "av").data_ptr())
         d._av_s_valid = bool(d.fixedPoint)
@@ -514,7 +524,9 @@ def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = F
         ho = _handoff(d)
         done = 1 if handoff_take(d, "momq_own") else 0
         ho.clear()
-        # fixed point: SrcMomQ records in workspace M (own range from the IAD and AV loops)
+        # fixed point: SrcMomQ records in workspace M (own range from the IAD and AV loops with MOM_HANDOFF)
+        if not MOM_HANDOFF:
+            d._recB = None  # the AV records are dead: their block serves the momentum records (B is re-created by XMass)
         rec = _recM(d) if d.fixedPoint else _rec(d, 0, "mom")
         _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), d.size, rec.data_ptr(), gv, _stream(), inDone=done)
         d.minDtCourant_dev = dt
