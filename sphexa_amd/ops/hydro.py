@@ -28,7 +28,11 @@ DV = ("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")
 # runs: the fixed-point loops fall back to fp64-frame records in some cases (stored-mass Gradh: SrcPos 32 B; AV without
 # the IAD loop's S_i and STD IAD: SrcIad 48 B). The workspace is grow-only, so it settles at the momentum record:
 # SrcMom 96 B (fp64) or SrcMomQ 80 B (fixed point); SrcGradV (32 B) and the AV S_i (16 B) use the second buffer
-REC_BYTES = {"xmass": (32, 32), "gradh": (32, 32), "iad": (48, 32), "av": (48, 48), "mom": (96, 96), "std": (80, 80)}
+# record bytes per particle of workspace 0 per loop (fp64-coordinate records, fixed-point records); "iadq": the
+# fixed-point VE chain's SrcIadQ (Gradh hand-off -> IAD); "iad" is also the STD IAD, whose SrcIad records are 48 B
+# in either mode
+REC_BYTES = {"xmass": (32, 32), "gradh": (32, 32), "iad": (48, 48), "iadq": (32, 32), "av": (48, 48),
+             "mom": (96, 96), "std": (80, 80)}
 
 # fixed-point VE chain: the IAD and AV loops also write the momentum loop's own SrcMomQ records (workspace M, 80 B per
 # particle) so that the momentum loop packs only its halos. That holds workspace M from the IAD loop on, at the
@@ -388,7 +392,7 @@ def compute_ve_def_gradh(d, nl: NeighborList, box: Box):
             ho = _handoff(d)
             done = 1 if handoff_take(d, "xmq_own") else 0
             ho.clear()
-            w0 = _rec(d, 0, "iad").data_ptr()
+            w0 = _rec(d, 0, "iadq").data_ptr()
             _lib.hip().ve_def_gradh(*args, d.size, _recB(d).data_ptr(), _stream(), mu, inDone=done, out=w0,
                                     vx=d["vx"].data_ptr(), vy=d["vy"].data_ptr(), vz=d["vz"].data_ptr())
             handoff_mark(d, "iadq_own")
@@ -458,7 +462,7 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
             done = 1 if handoff_take(d, "iadq_own") else 0
             ho.clear()
             mom = _recM(d).data_ptr() if (MOM_HANDOFF and not av_clean) else 0
-            _lib.hip().iad_divv_curlv(*args, d.size, _rec(d, 0, "iad").data_ptr(), _stream(),
+            _lib.hip().iad_divv_curlv(*args, d.size, _rec(d, 0, "iadq").data_ptr(), _stream(),
                                       _rec(d, 1, "av").data_ptr(), inDone=done, avOut=_recB(d).data_ptr(),
                                       momOut=mom, cs=d["c"].data_ptr(), mm=d["m"].data_ptr(),
                                       prho=d["prho"].data_ptr())

@@ -352,8 +352,14 @@ class Domain:
         # index lists are compacted at their known sizes (scan + scatter: no further synchronization)
         dev = skeys.device
         n_own = skeys.numel()
-        flag_rows = torch.zeros((self.size, n_own), dtype=torch.uint8, device=dev)
-        node_rows = torch.zeros((self.size, ot.num_nodes), dtype=torch.bool, device=dev) if gravity else None
+        # per destination the flags are kept as bitmasks (size x n_own / 8 bytes instead of a size x n_own byte
+        # matrix; one byte row is reused for the marking) together with their counts
+        flag_bits = torch.zeros((self.size, _nbytes_bits(n_own)), dtype=torch.uint8, device=dev)
+        node_bits = torch.zeros((self.size, _nbytes_bits(ot.num_nodes)), dtype=torch.uint8, device=dev) if gravity \
+            else None
+        ncnt = 2 if gravity else 1
+        send_dev = torch.zeros((self.size, ncnt), dtype=torch.int64, device=dev)
+        row = torch.zeros(n_own, dtype=torch.uint8, device=dev) if not gravity else None
         for q in range(self.size):
             if q == self.rank or q not in peers or n_own == 0:
                 continue
@@ -361,24 +367,25 @@ class Domain:
                 failed = grav_ops.mark_let(ot, all_boxes[q], gcenters, self.box)
                 failed |= outside
                 pflags, nodes = grav_ops.let_selection_masks(ot, failed, gquads, n_own)
-                flag_rows[q] = pflags
-                node_rows[q] = nodes
+                send_dev[q, 1] = nodes.sum(dtype=torch.int64)
+                node_bits[q] = _pack_bits(nodes)
             else:
-                _mark_in_boxes(ot, all_boxes[q], x, y, z, self.box, out=flag_rows[q])
-        cnt = [flag_rows.sum(1, dtype=torch.int64)]
-        if gravity:
-            cnt.append(node_rows.sum(1, dtype=torch.int64))
-        send_dev = torch.stack(cnt, 1)  # (size, 1 or 2)
+                row.zero_()
+                pflags = _mark_in_boxes(ot, all_boxes[q], x, y, z, self.box, out=row)
+            send_dev[q, 0] = pflags.sum(dtype=torch.int64)
+            flag_bits[q] = _pack_bits(pflags)
+        del row
         recv_dev = self.comm.exchange_counts_dev(send_dev)
         host = torch.cat([send_dev, recv_dev]).cpu()
         send_h, recv_h = host[: self.size], host[self.size:]
         send_idx: List[torch.Tensor] = []
         mp_send: List[torch.Tensor] = []
         for q in range(self.size):
-            send_idx.append(sfc_ops.compact_indices(flag_rows[q], int(send_h[q, 0])))
+            send_idx.append(sfc_ops.compact_indices(_unpack_bits(flag_bits[q], n_own), int(send_h[q, 0])))
             if gravity:
-                mp_send.append(sfc_ops.compact_indices(node_rows[q], int(send_h[q, 1])))
-        del flag_rows, node_rows
+                mp_send.append(sfc_ops.compact_indices(_unpack_bits(node_bits[q], ot.num_nodes),
+                                                       int(send_h[q, 1])))
+        del flag_bits, node_bits
         if gravity:
             self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes, [int(v) for v in recv_h[:, 1]])
         self.halo_send_counts = [int(t.numel()) for t in send_idx]
@@ -571,6 +578,35 @@ def _coarse_cut(ot, center, half, max_boxes: int) -> torch.Tensor:
     out = out[:max_boxes]
     out[:, 3:] = torch.where(out[:, 3:4] >= 0, out[:, 3:], torch.full_like(out[:, 3:], -1.0))
     return out
+
+
+_BIT_WEIGHTS: dict = {}
+
+
+def _nbytes_bits(n: int) -> int:
+    return (int(n) + 7) // 8
+
+
+def _pack_bits(flags: torch.Tensor) -> torch.Tensor:
+    """0/1 flags (uint8 or bool, n) -> uint8 bitmask of ceil(n / 8) bytes, bit k of byte i = flag 8 i + k"""
+    n = flags.numel()
+    f = flags.reshape(-1).to(torch.uint8)
+    pad = _nbytes_bits(n) * 8 - n
+    if pad:
+        f = torch.cat([f, f.new_zeros(pad)])
+    w = _BIT_WEIGHTS.get(f.device)
+    if w is None:
+        w = _BIT_WEIGHTS[f.device] = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=f.device)
+    return (f.view(-1, 8) * w).sum(1, dtype=torch.uint8)
+
+
+def _unpack_bits(bits: torch.Tensor, n: int) -> torch.Tensor:
+    """inverse of _pack_bits: uint8 0/1 flags of length n"""
+    w = _BIT_WEIGHTS.get(bits.device)
+    if w is None:
+        w = _BIT_WEIGHTS[bits.device] = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8,
+                                                     device=bits.device)
+    return ((bits.reshape(-1, 1) & w) != 0).to(torch.uint8).reshape(-1)[:n]
 
 
 def _mark_in_boxes(ot, boxes: torch.Tensor, x, y, z, box: Box, out: Optional[torch.Tensor] = None) -> torch.Tensor:
