@@ -17,6 +17,7 @@ import os
 import sys
 from typing import List
 
+import numpy as np
 import torch
 
 from ..ops import hydro as H
@@ -95,7 +96,7 @@ class Propagator:
         self.nl = find_neighbors(d, domain.octree, domain.box, first, last,
                                  prev=self.nl,  # (not nidx=: an argument would pin the old GPU buffer)
                                  # global h minimum + mass extremes come back with the search statistics
-                                 ride_along=(lambda: H.global_h_min_device(d, domain.comm)) if gpu else None,
+                                 ride_along=(lambda out: H.global_h_min_device(d, domain.comm, out)) if gpu else None,
                                  speculate=speculate)
         if gpu:
             H.apply_global_h_min(d, self.nl.ride_along)
@@ -131,23 +132,30 @@ class Propagator:
             # the max divv of the IAD loop -> out = [dt, dt_m1, courant, rho] on the device
             others = min([d.maxDtIncrease * d.minDt] + [float(e) for e in extra])
             courant = d.minDtCourant_dev if d.minDtCourant is None else float(d.minDtCourant)
-            out = timestep_reduce(d["ax"], d["ay"], d["az"], first, last, grav, courant, d.minDtRho, d.Krho,
-                                  d.etaAcc, d.eps, others, d.minDt)
+            # one packet of 64-bit words for the host: [dt, dt_m1, courant, rho] (float64) | the gravity evaluations'
+            # raw statistics words | the domain's deferred checks (float64); filled in place (no torch cat or
+            # conversion kernels in the step: the gravity words by a device-to-device copy each)
+            nv = pend[0].NVALS if pend else 0
+            nchk = int(checks.numel()) if checks is not None else 0
+            packed = torch.empty(4 + nv * len(pend) + nchk, dtype=torch.int64, device=d.device)
+            out = packed[0:4].view(torch.float64)
+            timestep_reduce(d["ax"], d["ay"], d["az"], first, last, grav, courant, d.minDtRho, d.Krho, d.etaAcc,
+                            d.eps, others, d.minDt, out=out)
             domain.comm.allreduce(out[:1], MIN)
-            flat = [out[0:1], out[2:4]] + [p.dev for p in pend]
-            if checks is not None:
-                flat.append(checks.to(torch.float64).reshape(-1))
-            packed = torch.cat(flat)
+            for i, p in enumerate(pend):
+                packed[4 + nv * i:4 + nv * (i + 1)].copy_(p.dev)
+            if nchk:
+                packed[4 + nv * len(pend):].view(torch.float64).copy_(checks.reshape(-1))
             if self.defer_host and not self.needs_host_dt:
                 # [dt, dt_m1] for the position update on the device; the host values follow in finish_host()
                 d._dt_dev = out[0:2]
-                host = torch.empty(packed.numel(), dtype=torch.float64, pin_memory=True)
+                host = torch.empty(packed.numel(), dtype=torch.int64, pin_memory=True)
                 host.copy_(packed, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record()
                 self._host_pending = (host, ev, pend, checks is not None, domain)
                 return
-            self._apply_host(d, domain, packed.tolist(), pend, checks is not None)
+            self._apply_host(d, domain, packed.cpu().numpy(), pend, checks is not None)
             return
         else:
             if pend:
@@ -169,15 +177,17 @@ class Propagator:
         d.minDt_m1 = d.minDt
         d.minDt = dt
 
-    def _apply_host(self, d, domain, vals, pend, has_checks):
-        dt = vals[0]
-        d.minDtCourant, d.minDtRho = vals[1], vals[2]
+    def _apply_host(self, d, domain, raw, pend, has_checks):
+        """``raw``: the time-step packet as an int64 numpy array (see compute_timestep)"""
+        f = raw.view(np.float64)
+        dt = float(f[0])
+        d.minDtCourant, d.minDtRho = float(f[2]), float(f[3])
         nv = pend[0].NVALS if pend else 0
-        k = 3 + nv * len(pend)
+        k = 4 + nv * len(pend)
         if pend:
-            self.gravity.finish(d, [vals[3 + nv * i: 3 + nv * (i + 1)] for i in range(len(pend))])
+            self.gravity.finish(d, [raw[4 + nv * i: 4 + nv * (i + 1)].tolist() for i in range(len(pend))])
         if has_checks:
-            domain.finish_checks(vals[k:])
+            domain.finish_checks(f[k:].tolist())
         d.ttot += dt
         d.minDt_m1 = d.minDt
         d.minDt = dt
@@ -191,7 +201,7 @@ class Propagator:
             host, ev, pend, has_checks, domain = p
             ev.synchronize()
             d._dt_dev = None
-            self._apply_host(d, domain, host.tolist(), pend, has_checks)
+            self._apply_host(d, domain, host.numpy(), pend, has_checks)
         if self._observed is not None:
             self._observed.finish(d)
 

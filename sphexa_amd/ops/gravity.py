@@ -8,9 +8,11 @@ P2P tiles of 64 targets x 64 sources run on the f32 MFMA units (see csrc/hip/gra
 
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import _lib
+from .reduce import zero_
 from .octree import KEY_END, MAX_LEVEL, Octree
 from ..utils.box import Box
 
@@ -58,8 +60,9 @@ def upsweep(tree: Octree, x, y, z, m, box: Box, theta: float, sfc_kind: int = 0)
                                          centers.data_ptr(), mp.data_ptr(), _arrival_counters(N, x.device).data_ptr(),
                                          _stream())
         return centers, mp
-    mp = torch.zeros(8 * N, dtype=torch.float32, device=x.device)
+    mp = torch.empty(8 * N, dtype=torch.float32, device=x.device)
     if x.is_cuda:
+        zero_(mp)
         h = _lib.hip()
         s = _stream()
         h.gravity_leaves(tree.node_to_leaf.data_ptr(), N, tree.node_start.data_ptr(), tree.node_end.data_ptr(),
@@ -71,6 +74,7 @@ def upsweep(tree: Octree, x, y, z, m, box: Box, theta: float, sfc_kind: int = 0)
                                         centers.data_ptr(), mp.data_ptr(), s)
         h.gravity_set_mac(N, tree.prefixes.data_ptr(), box.to_array(), sfc_kind, inv_theta, centers.data_ptr(), s)
     else:
+        mp.zero_()
         _lib.cpu().gravity_upsweep(N, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.level_range,
                                    tree.prefixes.data_ptr(), tree.node_start.data_ptr(), tree.node_end.data_ptr(),
                                    x.data_ptr(), y.data_ptr(), z.data_ptr(), m.data_ptr(), box.to_array(), sfc_kind,
@@ -80,7 +84,8 @@ def upsweep(tree: Octree, x, y, z, m, box: Box, theta: float, sfc_kind: int = 0)
 
 class GravityPending:
     """statistics and energy of a GPU gravity evaluation still on the device (compute_gravity(defer=True)): the
-    caller brings ``dev`` (float64 [NVALS]) to the host with other per-step values and calls ``finish``"""
+    caller brings ``dev`` (int64 words [NVALS]: NSTATS counts, then the energy's float64 bits) to the host with other
+    per-step values and calls ``finish`` with the raw words"""
 
     NSTATS = 9   # int64 statistics of the kernels (gravity.hip gravityStore)
     NVALS = 11   # statistics + energy
@@ -90,11 +95,11 @@ class GravityPending:
 
     def energy_dev(self):
         """the evaluation's energy as a float64 device scalar (a view of ``dev``)"""
-        return self.dev[self.NSTATS:self.NSTATS + 1]
+        return self.dev[self.NSTATS:self.NSTATS + 1].view(torch.float64)
 
     def finish(self, vals) -> float:
-        st = [int(v) for v in vals[:self.NSTATS]]  # exact: counts below 2^53
-        energy = float(vals[self.NSTATS])
+        st = [int(v) for v in vals[:self.NSTATS]]
+        energy = float(np.array([int(vals[self.NSTATS])], dtype=np.int64).view(np.float64)[0])
         if TEST_CAPS is None and st[5] > 0:
             # groups fell back to the (slow, serial) fused kernel: grow the slabs to the observed demand while the
             # slab memory stays below ~6% of the device (it is 4 B x groups x (capM + capL))
@@ -120,8 +125,8 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         return 0.0
     if x.is_cuda:
         hp = _lib.hip()
-        # one fill: statistics (int64) + energy (float64)
-        zb = torch.zeros(GravityPending.NVALS, dtype=torch.int64, device=x.device)
+        # one native fill: statistics (int64) + energy (float64 bits)
+        zb = zero_(torch.empty(GravityPending.NVALS, dtype=torch.int64, device=x.device))
         st_dev, out = zb[:GravityPending.NSTATS], zb[GravityPending.NSTATS:].view(torch.float64)
         from .neighbors import _scratch
 
@@ -148,7 +153,7 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
                         0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), st_dev.data_ptr(),
                         scratch.data_ptr(), cap_m, cap_l, pacc.data_ptr(), nsrc, tree.num_nodes, rec.data_ptr(),
                         mm.data_ptr(), s)
-        pending = GravityPending(torch.cat([st_dev.to(torch.float64), out]), groups, (cap_m, cap_l), stats, x.device)
+        pending = GravityPending(zb, groups, (cap_m, cap_l), stats, x.device)
         return pending if defer else pending.finish(pending.dev.cpu().tolist())
     st = torch.zeros(2, dtype=torch.int64)
     e = float(_lib.cpu().compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),

@@ -200,17 +200,17 @@ def invalidate_h_cache(d):
 _SIGNS = {}
 
 
-def global_h_min_device(d, comm) -> torch.Tensor:
+def global_h_min_device(d, comm, out: torch.Tensor | None = None) -> torch.Tensor:
     """[min h, max h, min m, max m] over all ranks as a float64 device tensor (no host copy; see set_global_h_min); on
     one rank the reduction's own output (no further launches), on several one MIN allreduce of [min h, -max h, min m,
-    -max m] and a sign flip"""
+    -max m] and a sign flip. ``out``: destination (4 float64 on the device)"""
     h = d["h"][: d.size]
     m = d["m"][: d.size]
     multi = comm is not None and comm.size > 1
     if h.numel():
         from .reduce import min_max
 
-        mm = min_max([h, m])  # [min h, max h, min m, max m], one launch on the GPU
+        mm = min_max([h, m], out=None if multi else out)  # [min h, max h, min m, max m], one launch on the GPU
         if not multi:
             return mm
         sg = _SIGNS.get(h.device)
@@ -223,6 +223,9 @@ def global_h_min_device(d, comm) -> torch.Tensor:
     if multi:
         comm.allreduce(loc, "min")
         loc = loc * sg
+    if out is not None:
+        out.copy_(loc)
+        return out
     return loc
 
 

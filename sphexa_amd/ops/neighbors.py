@@ -24,6 +24,8 @@ import numpy as np
 import torch
 
 from . import _lib
+from .reduce import zero_
+from .sfc import gather
 from .octree import Octree
 from ..utils.box import Box
 
@@ -205,6 +207,19 @@ def _pool_plan(prev: NeighborList | None, groups: int, ng0: int, stripes: int):
     return max(1, round(ng0 / 8) + 1), max(8, -(-int(0.35 * ng0 / 8 * groups + 0.5) // stripes))
 
 
+_STATS_IDX: dict = {}
+
+
+def _stats_index(K: int, device) -> torch.Tensor:
+    """int32 device indices of the search statistics the host reads: words 0-7 and the stripe counters 8 + 32 k"""
+    key = (K, device)
+    t = _STATS_IDX.get(key)
+    if t is None:
+        t = _STATS_IDX[key] = torch.tensor(list(range(8)) + [8 + 32 * k for k in range(K)], dtype=torch.int32,
+                                           device=device)
+    return t
+
+
 def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
                    nidx: torch.Tensor | None = None, prev: NeighborList | None = None,
                    ride_along=None, speculate=None) -> NeighborList:
@@ -249,7 +264,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         shrunk = 0
         for _attempt in range(2):
             ov = ((buf.numel() - region) // 256 - num_groups * home) // K
-            stats = torch.zeros(8 + 32 * K, dtype=torch.int64, device=x.device)
+            stats = zero_(torch.empty(8 + 32 * K, dtype=torch.int64, device=x.device))
             hp.find_neighbors(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), tree.num_nodes,
                               tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
                               tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
@@ -260,17 +275,19 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               m=d["m"].data_ptr(), ntot=d.size, rec=rec.data_ptr())
             # per-stripe row demand of the five pool candidates of the next search (one kernel), the stripe
             # counters and the search statistics: one host copy
-            over = torch.zeros(5 * K, dtype=torch.int64, device=x.device)
+            # one packet for the host: [stats 0-7 | stripe counters | row demand | ride-along float64 words], written
+            # in place by native kernels (no torch cat / fill / conversion kernels in the step)
+            first_try = _attempt == 0
+            nex = 4 if (ride_along is not None and first_try) else 0
+            packed = torch.empty(8 + 6 * K + nex, dtype=torch.int64, device=x.device)
+            over = zero_(packed[8 + K:8 + 6 * K])
             hp.row_plan(num_groups, ngmax, buf.data_ptr(), home, over.data_ptr(), _stream())
+            gather(_stats_index(K, x.device), stats, out=packed[:8 + K])
             # evaluated once per call (it may issue a collective, so every rank calls it exactly once); a repeated
             # search keeps the converged h of the first one, so the first values stay valid
-            first_try = _attempt == 0
-            ex = (ride_along().to(torch.float64).reshape(-1).view(torch.int64)
-                  if (ride_along is not None and first_try) else None)
-            parts = [stats[:8], stats[8::32][:K], over]
+            ex = ride_along(packed[8 + 6 * K:].view(torch.float64)) if nex else None
             # (host-side bookkeeping in numpy: a torch op on a CPU tensor costs ~5-10 us of launch-path overhead,
             # and the GPU idles until the pair loops are enqueued)
-            packed = torch.cat(parts + ([ex] if ex is not None else []))
             if speculate is not None and first_try:
                 pinned = torch.empty(packed.numel(), dtype=torch.int64, pin_memory=True)
                 pinned.copy_(packed, non_blocking=True)

@@ -25,6 +25,13 @@ KEY_END = 1 << 63
 MAX_LEVEL = 21
 
 
+def _zeros_i32(n: int, device) -> torch.Tensor:
+    """zeroed int32 device tensor by the native fill (no torch fill kernel in the step)"""
+    from .reduce import zero_
+
+    return zero_(torch.empty(n, dtype=torch.int32, device=device))
+
+
 def _stream():
     return torch.cuda.current_stream().cuda_stream
 
@@ -90,7 +97,7 @@ def update_tree(tree: Optional[torch.Tensor], keys: torch.Tensor, bucket: int, m
             L = tree.numel() - 1
             counts = torch.empty(L, dtype=torch.int32, device=dev)
             ops = torch.empty(L + 1, dtype=torch.int64, device=dev)
-            flag = torch.zeros(1, dtype=torch.int32, device=dev)
+            flag = _zeros_i32(1, dev)
             h.node_counts(tree.data_ptr(), L, keys.data_ptr(), n, counts.data_ptr(), _stream())
             h.rebalance_ops(tree.data_ptr(), counts.data_ptr(), L, bucket, ops.data_ptr(), flag.data_ptr(), _stream())
             if int(flag.item()) == 0:
@@ -146,7 +153,7 @@ class TreeState:
         h = _lib.hip()
         L = self.tree.numel() - 1
         ops = torch.empty(L + 1, dtype=torch.int64, device=keys.device)
-        flag = torch.zeros(1, dtype=torch.int32, device=keys.device)
+        flag = _zeros_i32(1, keys.device)
         h.rebalance_ops(self.tree.data_ptr(), counts.data_ptr(), L, bucket, ops.data_ptr(), flag.data_ptr(),
                         _stream())
         if self._flag_h is None:

@@ -23,12 +23,13 @@ def _work(device) -> torch.Tensor:
     return t
 
 
-def min_max(tensors: Sequence[torch.Tensor]) -> torch.Tensor:
+def min_max(tensors: Sequence[torch.Tensor], out: torch.Tensor | None = None) -> torch.Tensor:
     """float64 tensor [min_0, max_0, min_1, max_1, ...] of 1 to 4 equal-length float32/float64 tensors (empty:
-    +max / -max of float64)"""
+    +max / -max of float64); ``out`` (GPU): destination (2 x count float64 on the device)"""
     dev = tensors[0].device
     if dev.type == "cuda":
-        out = torch.empty(2 * len(tensors), dtype=torch.float64, device=dev)
+        if out is None:
+            out = torch.empty(2 * len(tensors), dtype=torch.float64, device=dev)
         n = tensors[0].numel()
         _lib.hip().multi_min_max(n, [t.data_ptr() for t in tensors], [int(t.dtype == torch.float64) for t in tensors],
                                  out.data_ptr(), _work(dev).data_ptr(), torch.cuda.current_stream().cuda_stream)
@@ -94,7 +95,13 @@ def fill_f32(t: torch.Tensor, value: float):
 
 
 def zero_(t: torch.Tensor):
-    """stream-ordered native zeroing of a device tensor (hipMemsetAsync: no torch fill kernel)"""
-    if t.numel():
-        _lib.hip().memset(t.data_ptr(), 0, t.numel() * t.element_size(), torch.cuda.current_stream().cuda_stream)
+    """stream-ordered native zeroing of a contiguous device tensor (the fill32 kernel; hipMemsetAsync for sizes that
+    are not whole 32-bit words): no torch fill kernel"""
+    nb = t.numel() * t.element_size()
+    if nb:
+        s = torch.cuda.current_stream().cuda_stream
+        if nb % 4 == 0 and t.data_ptr() % 4 == 0:
+            _lib.hip().fill32(t.data_ptr(), 0, nb // 4, s)
+        else:
+            _lib.hip().memset(t.data_ptr(), 0, nb, s)
     return t

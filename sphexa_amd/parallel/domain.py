@@ -121,10 +121,16 @@ class Domain:
             return
         from ..ops.reduce import min_max
 
-        mm = min_max([x, y, z]).view(3, 2)  # one launch on the GPU
-        ext = torch.cat([mm[:, 0], -mm[:, 1]])
-        self.comm.allreduce(ext, MIN)
-        ext = ext.cpu().tolist()
+        mm = min_max([x, y, z])  # [min x, max x, min y, ...], one launch on the GPU
+        if self.size > 1:
+            mm = mm.view(3, 2)
+            ext = torch.cat([mm[:, 0], -mm[:, 1]])
+            self.comm.allreduce(ext, MIN)
+            ext = ext.cpu().tolist()
+        else:
+            # one rank: no collective, so no sign flip and concatenation kernels either
+            v = mm.cpu().tolist()
+            ext = [v[0], v[2], v[4], -v[1], -v[3], -v[5]]
         for d in range(3):
             if self.box.bc[d] != PERIODIC:
                 lo, hi = ext[d], -ext[3 + d]
