@@ -1035,7 +1035,18 @@ __device__ inline void flushP2P(Idx plst, int o0, int n, const GravLists& L, con
         }
         const int nsb = (cnt + 15) >> 4;
         for (int sb = 0; sb < nsb; ++sb)
-            p2pBlock<kTb0, kTb1, kMode == kP2PMixed>(L, sb, kq, col, T);
+        {
+#ifdef SPHX_P2P_SPLITTB
+            // (A/B variant: the four target blocks as two passes of two, half the MFMA result registers in flight)
+            if constexpr (kTb1 - kTb0 == 4)
+            {
+                p2pBlock<kTb0, kTb0 + 2, kMode == kP2PMixed>(L, sb, kq, col, T);
+                p2pBlock<kTb0 + 2, kTb1, kMode == kP2PMixed>(L, sb, kq, col, T);
+            }
+            else
+#endif
+                p2pBlock<kTb0, kTb1, kMode == kP2PMixed>(L, sb, kq, col, T);
+        }
     }
 }
 

@@ -286,7 +286,23 @@ class HydroVeProp(Propagator):
         first, last = domain.start_index(), domain.end_index()
         # velocity halos are not read before the IAD loop: their exchange overlaps the search, XMass and Gradh
         vel_halos = domain.exchange_halos_start(d, ["vx", "vy", "vz"])
-        done = self._neighbors(domain, d, first_loop=H.compute_xmass)
+        # on one rank (no xm halo exchange between them) XMass, Gradh and the EOS are all enqueued speculatively
+        # before the host waits for the search statistics: the ~100 us of host booking after that wait then overlaps
+        # Gradh instead of leaving the GPU idle after XMass (profiles/r4/e100_step_sequence_no_atnative.txt)
+        chain = domain.size == 1 and d.device.type == "cuda"
+
+        def gradh(d, nl, box):
+            if d.is_allocated("ay"):
+                d.release("ay")
+                d.acquire("gradh")
+            H.compute_ve_def_gradh(d, nl, box)
+
+        def first_loops(d, nl, box):
+            H.compute_xmass(d, nl, box)
+            gradh(d, nl, box)
+            H.compute_eos_ve(d, first, last)
+
+        done = self._neighbors(domain, d, first_loop=first_loops if chain else H.compute_xmass)
         t.step("FindNeighbors")
         nl = self.nl
 
@@ -296,11 +312,12 @@ class HydroVeProp(Propagator):
         domain.exchange_halos(d, ["xm"])
         t.step("mpi::synchronizeHalos")
 
-        d.release("ay")
-        d.acquire("gradh")
-        H.compute_ve_def_gradh(d, nl, box)
+        redo = not (done and chain)
+        if redo:
+            gradh(d, nl, box)
         t.step("Normalization & Gradh")
-        H.compute_eos_ve(d, first, last)
+        if redo:
+            H.compute_eos_ve(d, first, last)
         t.step("EquationOfState")
         domain.exchange_halos(d, ["prho", "c", "kx"])
         domain.exchange_halos_finish(vel_halos)
