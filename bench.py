@@ -136,7 +136,9 @@ def _run_case(init: str, n: int, args, comm, device) -> dict:
     prop, d = sim.propagator, sim.d
     prop.timer.sync = args.verbose
     # the time-step host copy rides until the next step's search synchronizes (Propagator.defer_host): the timed
-    # loop reads no host value between steps, and the final device synchronization covers all work
+    # loop reads no host value between steps, and the final device synchronization covers all work. The sphexa CLI
+    # runs the same step (defer_host, the device conserved-quantity reduction of Simulation.step/observe) and then
+    # collects the host values once per iteration for its output (app/sphexa.py)
     prop.defer_host = device.type == "cuda" and not args.verbose
 
     for _ in range(args.warmup):

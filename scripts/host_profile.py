@@ -21,11 +21,14 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--sort", default="tottime")
+    ap.add_argument("--filter", default=None, help="regex on file:line(function) of the printed rows")
     args = ap.parse_args()
     from sphexa_amd.app.simulation import Simulation
 
     sim = Simulation(args.init, n=args.n, device=torch.device("cuda", 0), out=None, quiet=True)
     sim.propagator.timer.sync = False  # as bench.py: no device synchronization at the substep boundaries
+    sim.propagator.defer_host = True  # as bench.py
     for _ in range(args.warmup):
         sim.step()
     torch.cuda.synchronize()
@@ -42,7 +45,11 @@ def main():
     prof.disable()
     s = io.StringIO()
     st = pstats.Stats(prof, stream=s)
-    st.sort_stats("tottime").print_stats(args.top)
+    st.sort_stats(args.sort)
+    if args.filter:
+        st.print_stats(args.filter, args.top)
+    else:
+        st.print_stats(args.top)
     print(f"{args.init} -n {args.n}: {1e3 * plain:.3f} ms/step without the profiler")
     print(s.getvalue())
 

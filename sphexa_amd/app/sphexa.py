@@ -145,11 +145,17 @@ def main(argv=None) -> int:
     viz = InsituHook(parser.get("--insitu", None), sim_init.constants(), comm, os.path.dirname(out_file) or ".")
 
     start_iteration = d.iteration
+    # the step bench.py times: the position update reads dt on the device and the conserved quantities are reduced on
+    # the device inside the iteration (Propagator.defer_host / observe); the loop then collects the host values once
+    # for its per-iteration output (the reference's time loop reads them each iteration as well, sphexa.cpp:150)
+    propagator.defer_host = d.device.type == "cuda"
     while not stop_simulation(d.iteration - 1, d.ttot, max_step):
         propagator.step(domain, d)
         _lib.raise_on_device_check(f"iteration {d.iteration}")  # SPHX_DEVICE_CHECKS=1 builds only
+        propagator.observe(domain, d)
+        propagator.finish_host(d)
         box = domain.box
-        observables.compute_and_write(d, domain, comm)
+        observables.compute_and_write(d, domain, comm, computed=True)
         if watchdog:
             check_finite(d)
         propagator.print_iteration_timings(domain, d)

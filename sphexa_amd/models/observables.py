@@ -104,8 +104,11 @@ class TimeAndEnergy:
     def extra_columns(self, d, domain):
         return []
 
-    def compute_and_write(self, d, domain, comm):
-        compute_conserved_quantities(d, domain.start_index(), domain.end_index(), comm)
+    def compute_and_write(self, d, domain, comm, computed: bool = False):
+        """``computed``: the conserved quantities of this iteration are already on the host (Propagator.observe +
+        finish_host, the device reduction inside the step, as bench.py times it)"""
+        if not computed:
+            compute_conserved_quantities(d, domain.start_index(), domain.end_index(), comm)
         extra = self.extra_columns(d, domain)
         if self._f:
             cols = [d.iteration, d.ttot, d.minDt, d.etot, d.ecin, d.eint, d.egrav, d.linmom, d.angmom] + extra

@@ -97,9 +97,9 @@ class TurbulenceMachRMS(TimeAndEnergy):
     def extra_columns(self, d, domain):
         return [mach_rms(d, domain, self._comm)]
 
-    def compute_and_write(self, d, domain, comm):
+    def compute_and_write(self, d, domain, comm, computed: bool = False):
         self._comm = comm
-        super().compute_and_write(d, domain, comm)
+        super().compute_and_write(d, domain, comm, computed)
 
 
 class TimeEnergyGrowth(TimeAndEnergy):
@@ -109,9 +109,9 @@ class TimeEnergyGrowth(TimeAndEnergy):
     def extra_columns(self, d, domain):
         return [kh_growth_rate(d, domain, self._comm)]
 
-    def compute_and_write(self, d, domain, comm):
+    def compute_and_write(self, d, domain, comm, computed: bool = False):
         self._comm = comm
-        super().compute_and_write(d, domain, comm)
+        super().compute_and_write(d, domain, comm, computed)
 
 
 class WindBubble(TimeAndEnergy):
@@ -128,9 +128,9 @@ class WindBubble(TimeAndEnergy):
         f = surviving_fraction(d, domain, self._comm, self.rho_bubble, temp_wind, self.initial_mass)
         return [f, d.ttot / self.T_KH]
 
-    def compute_and_write(self, d, domain, comm):
+    def compute_and_write(self, d, domain, comm, computed: bool = False):
         self._comm = comm
-        super().compute_and_write(d, domain, comm)
+        super().compute_and_write(d, domain, comm, computed)
 
 
 class GravWaves(TimeAndEnergy):
@@ -141,8 +141,9 @@ class GravWaves(TimeAndEnergy):
         self.theta = constants["gravWaveTheta"]
         self.phi = constants["gravWavePhi"]
 
-    def compute_and_write(self, d, domain, comm):
-        compute_conserved_quantities(d, domain.start_index(), domain.end_index(), comm)
+    def compute_and_write(self, d, domain, comm, computed: bool = False):
+        if not computed:
+            compute_conserved_quantities(d, domain.start_index(), domain.end_index(), comm)
         q = d2_quadrupole(d, domain, comm)
         hp, hx = strain(q, self.theta, self.phi)
         if self._f:
