@@ -212,6 +212,8 @@ class Propagator:
         from .observables import DeferredConserved, compute_conserved_quantities
 
         first, last = domain.start_index(), domain.end_index()
+        if hasattr(domain, "prefetch_box"):
+            domain.prefetch_box(d)  # (ahead of the reduction below: its host copy overlaps that kernel)
         if d.device.type == "cuda" and self.defer_host:
             if self._observed is None:
                 self._observed = DeferredConserved()

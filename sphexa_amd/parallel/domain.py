@@ -119,18 +119,12 @@ class Domain:
         """recompute extents of non-periodic dimensions from the owned particles (global MIN/MAX allreduce)"""
         if all(b == PERIODIC for b in self.box.bc):
             return
-        from ..ops.reduce import min_max
-
-        mm = min_max([x, y, z])  # [min x, max x, min y, ...], one launch on the GPU
-        if self.size > 1:
-            mm = mm.view(3, 2)
-            ext = torch.cat([mm[:, 0], -mm[:, 1]])
-            self.comm.allreduce(ext, MIN)
-            ext = ext.cpu().tolist()
+        pf, self._box_prefetch = getattr(self, "_box_prefetch", None), None
+        if pf is not None and pf[0] == self._box_key(x, y, z):
+            pf[2].synchronize()
+            ext = self._box_ext(pf[1].tolist())
         else:
-            # one rank: no collective, so no sign flip and concatenation kernels either
-            v = mm.cpu().tolist()
-            ext = [v[0], v[2], v[4], -v[1], -v[3], -v[5]]
+            ext = self._box_ext(self._box_reduce(x, y, z).cpu().tolist())
         for d in range(3):
             if self.box.bc[d] != PERIODIC:
                 lo, hi = ext[d], -ext[3 + d]
@@ -138,6 +132,43 @@ class Domain:
                     hi = lo + 1e-10
                 self.box.lo[d] = lo
                 self.box.hi[d] = hi
+
+    @staticmethod
+    def _box_key(x, y, z):
+        return tuple((t.data_ptr(), t.numel(), t._version) for t in (x, y, z))
+
+    def _box_reduce(self, x, y, z) -> torch.Tensor:
+        """device extents: [min x, max x, min y, ...] on one rank (no collective, so no sign flip and concatenation
+        kernels either), the allreduced [min x, min y, min z, -max x, -max y, -max z] on several"""
+        from ..ops.reduce import min_max
+
+        mm = min_max([x, y, z])  # one launch on the GPU
+        if self.size > 1:
+            mm = mm.view(3, 2)
+            ext = torch.cat([mm[:, 0], -mm[:, 1]])
+            self.comm.allreduce(ext, MIN)
+            return ext
+        return mm
+
+    def _box_ext(self, v):
+        return v if self.size > 1 else [v[0], v[2], v[4], -v[1], -v[3], -v[5]]
+
+    def prefetch_box(self, d):
+        """enqueue the next sync's box reduction right after the position update (GPU, open boundaries): its host
+        copy then completes while the GPU runs the work enqueued after it (the conserved-quantity reduction), and
+        update_box only collects it, instead of the GPU idling from the reduction until the host has launched the SFC
+        keys. Used if the coordinate buffers are unchanged at the sync (same storage and tensor version). One rank
+        only: on several, a rank whose buffers changed would re-reduce alone and mismatch the collective."""
+        if all(b == PERIODIC for b in self.box.bc) or not d["x"].is_cuda or self.size > 1 or self.end <= self.start:
+            return
+        s, e = self.start, self.end
+        x, y, z = d["x"][s:e], d["y"][s:e], d["z"][s:e]
+        dev = self._box_reduce(x, y, z)
+        host = torch.empty(dev.numel(), dtype=torch.float64, pin_memory=True)
+        host.copy_(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._box_prefetch = (self._box_key(x, y, z), host, ev)
 
     # --------------------------------------------------------------------------------------------- the sync
     def sync(self, d, conserved: Sequence[str], dependent: Sequence[str] = (), gravity: bool = False):
