@@ -175,6 +175,10 @@ def _run_case(init: str, n: int, args, comm, device) -> dict:
         if hasattr(d, "nc_rounds") and d.nc_rounds > 0:
             print(f"# neighbor search: {d.nc_rounds:.2f} rounds and {d.nc_leaves:.1f} touched leaves per "
                   f"64-particle group (last step)", file=sys.stderr)
+            if getattr(d, "nc_staged", 0) > 0:
+                print(f"# neighbor search: {d.nc_staged:.0f} staged candidates, {d.nc_hits:.0f} hits per group "
+                      f"({100.0 * d.nc_hits / max(d.nc_staged, 1):.1f} % of the candidates are neighbors), "
+                      f"{d.nc_subbox:.0f} candidates inside the sub-group boxes", file=sys.stderr)
         if hasattr(d, "nc_queued"):
             print(f"# neighbor search paths (last step, of {(d.numParticlesGlobal + 63) // 64} groups): "
                   f"{d.nc_queued} queued for the split kernel, {d.nc_split} searched in sub-group passes, "
