@@ -38,11 +38,16 @@ def test_case_gpu_matches_cpu(gpu, small_glass, case, prop, n):
     assert abs(dev.d.minDt - cpu.d.minDt) <= 1e-4 * cpu.d.minDt
     names = ["x", "vx", "h"] + (["temp"] if prop != "nbody" else [])
     a, b = _sorted_state(cpu, names), _sorted_state(dev, names)
-    # gravity: GPU (64-target groups) and CPU (16-target groups) traversals differ within the BH error
-    tol = 2e-2 if case == "evrard" else 2e-4
+    # gravity: GPU (64-target groups, half-box lists) and CPU (16-target groups) traversals differ within the BH
+    # error, which after one step from rest is the whole velocity (v = a dt); positions, h and temperature are held
+    # to the SPH tolerance
+    errs = {k: float((a[k] - b[k]).abs().max()) / (float(a[k].abs().max()) + 1e-30) for k in names}
+    print(case, prop, {k: f"{v:.2e}" for k, v in errs.items()})
     for k in names:
-        scale = float(a[k].abs().max()) + 1e-30
-        assert float((a[k] - b[k]).abs().max()) / scale < tol, k
+        tol = 2e-2 if (case == "evrard" and prop != "nbody" and k == "vx") else 2e-4
+        if prop == "nbody":
+            tol = 2e-2 if k == "vx" else 2e-4
+        assert errs[k] < tol, (k, errs[k])
 
 
 def test_turbulence_gpu(gpu, small_glass):
