@@ -78,12 +78,16 @@ def main():
     from sphexa_amd.parallel.comm import init_distributed
 
     use_cuda = args.device == "cuda" or (args.device == "auto" and torch.cuda.is_available())
-    comm = init_distributed("nccl" if use_cuda else "gloo")
+    # rehearsal of the multi-rank step on a one-GPU machine (SPHX_BENCH_SHARED_GPU=1): every rank on cuda:0 and gloo
+    # collectives with host staging, since RCCL refuses two ranks on one device (profiles/r4/rccl_shared_gpu_probe.txt);
+    # a plumbing and correctness run, not a scaling measurement
+    shared = use_cuda and os.environ.get("SPHX_BENCH_SHARED_GPU") == "1"
+    comm = init_distributed("nccl" if use_cuda and not shared else "gloo")
     rank, size = comm.rank, comm.size
     if size != args.gpus:
         raise SystemExit(f"bench: communicator has {size} ranks but --gpus {args.gpus} was requested")
     if use_cuda:
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        local = 0 if shared else int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
