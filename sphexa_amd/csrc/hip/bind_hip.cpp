@@ -150,6 +150,10 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("field_max", [](int64_t first, int64_t last, Ptr f, Ptr out, Ptr work, Ptr s)
           { fieldMax(first, last, P<float>(f), P<float>(out), P<void>(work), St(s)); });
     m.def("fill32", [](Ptr p, uint32_t value, int64_t n, Ptr s) { fill32(P<void>(p), value, n, St(s)); });
+    m.def("pack_bits", [](int64_t n, Ptr flags, Ptr bits, Ptr count, Ptr s)
+          { packBits(n, P<uint8_t>(flags), P<uint8_t>(bits), P<int64_t>(count), St(s)); });
+    m.def("unpack_bits", [](int64_t n, Ptr bits, Ptr flags, Ptr s)
+          { unpackBits(n, P<uint8_t>(bits), P<uint8_t>(flags), St(s)); });
     m.def("memset", [](Ptr p, int value, size_t bytes, Ptr s) { memsetAsync(P<void>(p), value, bytes, St(s)); });
     m.def("scan_temp_bytes", [](int64_t n) { return scanTempBytes(n); });
     m.def("exclusive_scan_i64", [](Ptr in, Ptr out, int64_t n, Ptr tmp, size_t tb, Ptr s)

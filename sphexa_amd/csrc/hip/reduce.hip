@@ -262,4 +262,53 @@ void fill32(void* p, uint32_t value, int64_t n, hipStream_t s)
     if (n > 0) SPHX_CHECK(hipMemsetD32Async(static_cast<hipDeviceptr_t>(p), int(value), size_t(n), s));
 }
 
+/* Halo-discovery flags as per-destination bitmasks (parallel/domain.py): one thread per output byte packs eight 0/1
+ * flags (bit k of byte b = flag 8 b + k) and the wave's popcount total is added to *count (the destination's send
+ * count), replacing the pad/multiply/sum/count torch kernels of a pack by one launch; unpack is its inverse. */
+__global__ void packBitsKernel(int64_t n, const uint8_t* __restrict__ flags, uint8_t* __restrict__ bits,
+                               int64_t* __restrict__ count)
+{
+    const int64_t b = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t nb = (n + 7) >> 3;
+    unsigned v = 0;
+    if (b < nb)
+    {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+        {
+            const int64_t i = 8 * b + k;
+            v |= (i < n && flags[i] != 0) ? (1u << k) : 0u;
+        }
+        bits[b] = uint8_t(v);
+    }
+    int c = __popc(v);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c != 0 && count != nullptr) atomicAdd(reinterpret_cast<unsigned long long*>(count),
+                                                                         (unsigned long long)c);
+}
+
+__global__ void unpackBitsKernel(int64_t n, const uint8_t* __restrict__ bits, uint8_t* __restrict__ flags)
+{
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    flags[i] = uint8_t((bits[i >> 3] >> (i & 7)) & 1u);
+}
+
+void packBits(int64_t n, const uint8_t* flags, uint8_t* bits, int64_t* count, hipStream_t s)
+{
+    const int64_t nb = (n + 7) >> 3;
+    if (nb <= 0) return;
+    packBitsKernel<<<unsigned((nb + 255) / 256), 256, 0, s>>>(n, flags, bits, count);
+    SPHX_LAUNCH_CHECK();
+}
+
+void unpackBits(int64_t n, const uint8_t* bits, uint8_t* flags, hipStream_t s)
+{
+    if (n <= 0) return;
+    unpackBitsKernel<<<unsigned((n + 255) / 256), 256, 0, s>>>(n, bits, flags);
+    SPHX_LAUNCH_CHECK();
+}
+
 } // namespace sphx::hip

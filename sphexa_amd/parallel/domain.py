@@ -44,6 +44,7 @@ from ..ops import _lib
 from ..ops import octree as octree_ops
 from ..ops import sfc as sfc_ops
 from ..utils.box import Box, PERIODIC
+from ..ops.reduce import zero_
 from .comm import Comm, MAX, MIN, SUM
 
 HALO_FIELDS = ("x", "y", "z", "h", "m")
@@ -404,13 +405,15 @@ class Domain:
                 failed = grav_ops.mark_let(ot, all_boxes[q], gcenters, self.box)
                 failed |= outside
                 pflags, nodes = grav_ops.let_selection_masks(ot, failed, gquads, n_own)
-                send_dev[q, 1] = nodes.sum(dtype=torch.int64)
-                node_bits[q] = _pack_bits(nodes)
+                _pack_bits(nodes, out=node_bits[q], count=send_dev[q, 1:2])
             else:
-                row.zero_()
+                if row.is_cuda:
+                    zero_(row)
+                else:
+                    row.zero_()
                 pflags = _mark_in_boxes(ot, all_boxes[q], x, y, z, self.box, out=row)
-            send_dev[q, 0] = pflags.sum(dtype=torch.int64)
-            flag_bits[q] = _pack_bits(pflags)
+            # (one launch on the GPU: bitmask row + send count)
+            _pack_bits(pflags, out=flag_bits[q], count=send_dev[q, 0:1])
         del row
         recv_dev = self.comm.exchange_counts_dev(send_dev)
         host = torch.cat([send_dev, recv_dev]).cpu()
@@ -624,9 +627,24 @@ def _nbytes_bits(n: int) -> int:
     return (int(n) + 7) // 8
 
 
-def _pack_bits(flags: torch.Tensor) -> torch.Tensor:
-    """0/1 flags (uint8 or bool, n) -> uint8 bitmask of ceil(n / 8) bytes, bit k of byte i = flag 8 i + k"""
+def _pack_bits(flags: torch.Tensor, out: Optional[torch.Tensor] = None,
+               count: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """0/1 flags (uint8 or bool, n) -> uint8 bitmask of ceil(n / 8) bytes, bit k of byte i = flag 8 i + k. ``out``:
+    destination bytes; ``count``: an int64 element that the number of set flags is added to. On the GPU one native
+    launch (reduce.hip packBits) does both."""
     n = flags.numel()
+    if flags.is_cuda:
+        f = flags.reshape(-1)
+        if f.dtype == torch.bool:
+            f = f.view(torch.uint8)
+        f = f.contiguous()
+        if out is None:
+            out = torch.empty(_nbytes_bits(n), dtype=torch.uint8, device=f.device)
+        _lib.hip().pack_bits(n, f.data_ptr(), out.data_ptr(), 0 if count is None else count.data_ptr(),
+                             torch.cuda.current_stream().cuda_stream)
+        return out
+    if count is not None:
+        count += flags.sum(dtype=torch.int64)
     f = flags.reshape(-1).to(torch.uint8)
     pad = _nbytes_bits(n) * 8 - n
     if pad:
@@ -634,11 +652,20 @@ def _pack_bits(flags: torch.Tensor) -> torch.Tensor:
     w = _BIT_WEIGHTS.get(f.device)
     if w is None:
         w = _BIT_WEIGHTS[f.device] = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=f.device)
-    return (f.view(-1, 8) * w).sum(1, dtype=torch.uint8)
+    r = (f.view(-1, 8) * w).sum(1, dtype=torch.uint8)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
 
 
 def _unpack_bits(bits: torch.Tensor, n: int) -> torch.Tensor:
     """inverse of _pack_bits: uint8 0/1 flags of length n"""
+    if bits.is_cuda:
+        flags = torch.empty(n, dtype=torch.uint8, device=bits.device)
+        _lib.hip().unpack_bits(n, bits.contiguous().data_ptr(), flags.data_ptr(),
+                               torch.cuda.current_stream().cuda_stream)
+        return flags
     w = _BIT_WEIGHTS.get(bits.device)
     if w is None:
         w = _BIT_WEIGHTS[bits.device] = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8,

@@ -85,3 +85,22 @@ def test_min_max_propagates_nan(gpu, where):
     ax = torch.zeros(100000, dtype=torch.float32, device=gpu)
     ax[where] = float("nan")
     assert math.isnan(R.max_norm2(ax, ax, ax, 0, 100000).item())
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 1000, 1_000_003])
+def test_pack_bits_native_matches_torch(gpu, n):
+    """halo-discovery bitmasks (reduce.hip packBits / unpackBits) against the torch (CPU) packing: same bytes, the
+    added count equals the number of set flags, and unpacking restores the flags"""
+    from sphexa_amd.parallel.domain import _nbytes_bits, _pack_bits, _unpack_bits
+
+    g = torch.Generator(device="cpu").manual_seed(n)
+    flags = (torch.rand(n, generator=g) < 0.3).to(torch.uint8)
+    ref = _pack_bits(flags)
+    cnt = torch.full((1,), 5, dtype=torch.int64, device=gpu)
+    out = torch.empty(_nbytes_bits(n), dtype=torch.uint8, device=gpu)
+    got = _pack_bits(flags.to(gpu), out=out, count=cnt)
+    assert torch.equal(got.cpu(), ref)
+    assert int(cnt.item()) == 5 + int(flags.sum())
+    assert torch.equal(_unpack_bits(got, n).cpu(), flags)
+    # bool flags take the same path
+    assert torch.equal(_pack_bits(flags.bool().to(gpu)).cpu(), ref)
