@@ -2061,6 +2061,44 @@ void markLet(int64_t nb, const double* bc, const double* bh, const int32_t* chil
     SPHX_LAUNCH_CHECK();
 }
 
+/* LET selection of one receiver from its open flags (failed | outside): particle flags of the opened leaves (one
+ * thread per leaf writes its particle range) and the send flags of the multipoles, the first unopened non-empty node
+ * below an opened one (reference the LET of ryoanji/interface/multipole_holder.cu via domain exchange). One launch
+ * instead of the torch gather/searchsorted/compare kernels of ops/gravity.py let_selection_masks. */
+__global__ void letSelectKernel(int64_t N, int64_t L, const uint8_t* __restrict__ failed,
+                                const uint8_t* __restrict__ outside, const int32_t* __restrict__ leafToNode,
+                                const int32_t* __restrict__ ns, const int32_t* __restrict__ ne, int64_t offset,
+                                const Quadrupole* __restrict__ mp, const int32_t* __restrict__ parents,
+                                uint8_t* __restrict__ pflags, uint8_t* __restrict__ send)
+{
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    auto open = [&](int64_t n) { return (failed[n] | (outside ? outside[n] : uint8_t(0))) != 0; };
+    if (i < N)
+    {
+        bool s = !open(i) && mp[i].q[qMass] > MT(0);
+        if (i > 0) s = s && open(parents[(i - 1) >> 3]);
+        send[i] = uint8_t(s);
+    }
+    if (i < L)
+    {
+        const int32_t nd = leafToNode[i];
+        const uint8_t v  = uint8_t(open(nd));
+        for (int64_t k = int64_t(ns[nd]) - offset; k < int64_t(ne[nd]) - offset; ++k)
+            pflags[k] = v;
+    }
+}
+
+void letSelect(int64_t N, int64_t L, const uint8_t* failed, const uint8_t* outside, const int32_t* leafToNode,
+               const int32_t* ns, const int32_t* ne, int64_t offset, const void* mp, const int32_t* parents,
+               uint8_t* pflags, uint8_t* send, hipStream_t s)
+{
+    const int64_t n = N > L ? N : L;
+    if (n <= 0) return;
+    letSelectKernel<<<gridFor(n, 256), 256, 0, s>>>(N, L, failed, outside, leafToNode, ns, ne, offset,
+                                                     static_cast<const Quadrupole*>(mp), parents, pflags, send);
+    SPHX_LAUNCH_CHECK();
+}
+
 //! @brief open every node whose key range is not inside the sender's assigned range [lo, hi): remote LET nodes of
 //!        different senders are then disjoint (cpu/let_tree_cpu.cpp)
 __global__ void markOutsideRangeKernel(int64_t N, const KeyT* __restrict__ prefixes, KeyT lo, KeyT hi,

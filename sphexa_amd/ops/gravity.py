@@ -184,7 +184,11 @@ def mark_let(tree: Octree, boxes: torch.Tensor, centers: torch.Tensor, box: Box)
     """per-node flags (uint8): node must be opened for a receiver whose particles lie in ``boxes`` (rows
     center[3], half[3]) — its tight box overlaps one of them or one of them violates its vector MAC"""
     N = tree.num_nodes
-    failed = torch.zeros(N, dtype=torch.uint8, device=centers.device)
+    failed = torch.empty(N, dtype=torch.uint8, device=centers.device)
+    if failed.is_cuda:
+        zero_(failed)
+    else:
+        failed.zero_()
     nb = boxes.shape[0]
     if nb == 0:
         return failed
@@ -199,11 +203,23 @@ def mark_let(tree: Octree, boxes: torch.Tensor, centers: torch.Tensor, box: Box)
     return failed
 
 
-def let_selection_masks(tree: Octree, failed: torch.Tensor, mp: torch.Tensor, n_particles: int | None = None):
-    """(particle flags over the tree's particles (uint8), node flags of the multipoles to send (bool)) from the open
-    flags: particles of opened leaves, and the first unopened non-empty node below an opened one. With the particle
-    count given there is no host copy."""
+def let_selection_masks(tree: Octree, failed: torch.Tensor, mp: torch.Tensor, n_particles: int | None = None,
+                        outside: torch.Tensor | None = None):
+    """(particle flags over the tree's particles (uint8), node flags of the multipoles to send (bool; uint8 0/1 on
+    the GPU)) from the open flags ``failed`` (| ``outside``): particles of opened leaves, and the first unopened
+    non-empty node below an opened one. With the particle count given there is no host copy; on the GPU one native
+    launch (gravity.hip letSelect)."""
     N = tree.num_nodes
+    if failed.is_cuda and n_particles is not None:
+        pflags = torch.empty(n_particles, dtype=torch.uint8, device=failed.device)
+        send = torch.empty(N, dtype=torch.uint8, device=failed.device)
+        _lib.hip().let_select(N, tree.leaf_to_node.numel(), failed.data_ptr(),
+                              0 if outside is None else outside.data_ptr(), tree.leaf_to_node.data_ptr(),
+                              tree.node_start.data_ptr(), tree.node_end.data_ptr(), int(tree.offset), mp.data_ptr(),
+                              tree.parents.data_ptr(), pflags.data_ptr(), send.data_ptr(), _stream())
+        return pflags, send
+    if outside is not None:
+        failed = failed | outside
     f = failed.bool()
     leaf_open = f[tree.leaf_to_node.long()]
     if n_particles is None:

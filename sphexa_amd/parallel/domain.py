@@ -376,7 +376,11 @@ class Domain:
             gcenters, gquads = grav_ops.upsweep(ot, x, y, z, own["m"], self.box, self.theta, self.sfc_kind)
             # only nodes inside this rank's SFC range may leave as multipoles: the remote LET trees then consist of
             # disjoint nodes (ops.gravity.remote_let_tree)
-            outside = torch.zeros(ot.num_nodes, dtype=torch.uint8, device=x.device)
+            outside = torch.empty(ot.num_nodes, dtype=torch.uint8, device=x.device)
+            if outside.is_cuda:
+                zero_(outside)
+            else:
+                outside.zero_()
             grav_ops.mark_outside_range(ot, self.assignment_keys[self.rank], self.assignment_keys[self.rank + 1],
                                         outside)
         # peer pruning (reference traversal/peers.hpp: only ranks whose domains interact exchange halos): a rank whose
@@ -403,8 +407,7 @@ class Domain:
                 continue
             if gravity:
                 failed = grav_ops.mark_let(ot, all_boxes[q], gcenters, self.box)
-                failed |= outside
-                pflags, nodes = grav_ops.let_selection_masks(ot, failed, gquads, n_own)
+                pflags, nodes = grav_ops.let_selection_masks(ot, failed, gquads, n_own, outside=outside)
                 _pack_bits(nodes, out=node_bits[q], count=send_dev[q, 1:2])
             else:
                 if row.is_cuda:

@@ -161,6 +161,16 @@ def test_let_kernels_gpu_match_cpu(gpu):
     assert torch.equal(fg.cpu(), fc)
     pf, nodes = G.let_selection(ot, fc, mc)
     assert 0 < nodes.numel() < ot.num_nodes
+    # the native selection (one launch, open flags OR-ed with an "outside" mask) matches the torch selection
+    outside = torch.zeros(ot.num_nodes, dtype=torch.uint8)
+    outside[torch.from_numpy(rng.choice(ot.num_nodes, ot.num_nodes // 7, replace=False))] = 1
+    pc, sc = G.let_selection_masks(ot, fc, mc, n, outside=outside)
+    pgg, sgg = G.let_selection_masks(otg, fg, mgp, n, outside=outside.to(gpu))
+    assert torch.equal(pgg.cpu(), pc.to(torch.uint8))
+    assert torch.equal(sgg.cpu().bool(), sc.bool())
+    pc0, sc0 = G.let_selection_masks(ot, fc, mc, n)
+    pg0, sg0 = G.let_selection_masks(otg, fg, mgp, n)
+    assert torch.equal(pg0.cpu(), pc0.to(torch.uint8)) and torch.equal(sg0.cpu().bool(), sc0.bool())
     # remote multipoles applied to far targets
     mcent = cc.view(-1, 4)[nodes, :3].contiguous()
     mq = mc.view(-1, 8)[nodes].contiguous()
