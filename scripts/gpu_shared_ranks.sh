@@ -3,6 +3,9 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=$GRAFT_REPO_ROOT/gpurun_out/shared; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gravity.py tests/test_gpu_reduce.py tests/test_distributed_gpu.py tests/test_gpu_cases.py \
+    tests/test_syncs_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { echo "gpu tests failed"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
 export SPHX_BENCH_SHARED_GPU=1
 for c in "2 sedov 150" "2 evrard 100" "4 sedov 150" "4 evrard 100"; do
   set -- $c
