@@ -210,3 +210,33 @@ def test_speculative_xmass(gpu, small_glass):
     for k in names:
         assert torch.allclose(a[k], b[k], rtol=1e-6, atol=1e-12), k
     assert spc.d.minDt == pytest.approx(ref.d.minDt, rel=1e-6)
+
+
+def test_speculation_rejected_redoes_chain(gpu, small_glass):
+    """a speculative XMass -> Gradh -> EOS chain whose record path does not hold (forced here) is redone after the
+    search statistics arrive: the run equals one without speculation"""
+    from sphexa_amd.models import propagators as PR
+    from sphexa_amd.ops import hydro as H
+
+    ref = Simulation("evrard", n=32, prop="ve", device=gpu)
+    spc = Simulation("evrard", n=32, prop="ve", device=gpu)
+    orig, holds = PR.Propagator._neighbors, H.speculation_holds
+
+    def no_spec(self, domain, d, first_loop=None):
+        return orig(self, domain, d)
+
+    try:
+        for _ in range(3):
+            PR.Propagator._neighbors = no_spec
+            ref.step()
+            PR.Propagator._neighbors = orig
+            H.speculation_holds = lambda d, box, spec: False
+            spc.step()
+            H.speculation_holds = holds
+    finally:
+        PR.Propagator._neighbors, H.speculation_holds = orig, holds
+    names = ["x", "vx", "h", "temp"]
+    a, b = _sorted_state(ref, names), _sorted_state(spc, names)
+    for k in names:
+        assert torch.allclose(a[k], b[k], rtol=1e-6, atol=1e-12), k
+    assert spc.d.minDt == pytest.approx(ref.d.minDt, rel=1e-6)
