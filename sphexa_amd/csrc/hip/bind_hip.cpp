@@ -524,10 +524,10 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("mark_outside_range", [](int64_t N, Ptr prefixes, uint64_t lo, uint64_t hi, Ptr failed, Ptr s)
           { markOutsideRange(N, P<KeyT>(prefixes), lo, hi, P<uint8_t>(failed), St(s)); });
     m.def("let_select",
-          [](int64_t N, int64_t L, Ptr failed, Ptr outside, Ptr l2n, Ptr ns, Ptr ne, int64_t offset, Ptr mp,
-             Ptr parents, Ptr pflags, Ptr send, Ptr s)
+          [](int64_t N, int64_t L, int64_t np, Ptr failed, Ptr outside, Ptr l2n, Ptr ns, Ptr ne, int64_t offset,
+             Ptr mp, Ptr parents, Ptr pflags, Ptr send, Ptr s)
           {
-              letSelect(N, L, P<uint8_t>(failed), P<uint8_t>(outside), P<int32_t>(l2n), P<int32_t>(ns),
+              letSelect(N, L, np, P<uint8_t>(failed), P<uint8_t>(outside), P<int32_t>(l2n), P<int32_t>(ns),
                         P<int32_t>(ne), offset, P<void>(mp), P<int32_t>(parents), P<uint8_t>(pflags),
                         P<uint8_t>(send), St(s));
           });

@@ -2065,7 +2065,7 @@ void markLet(int64_t nb, const double* bc, const double* bh, const int32_t* chil
  * thread per leaf writes its particle range) and the send flags of the multipoles, the first unopened non-empty node
  * below an opened one (reference the LET of ryoanji/interface/multipole_holder.cu via domain exchange). One launch
  * instead of the torch gather/searchsorted/compare kernels of ops/gravity.py let_selection_masks. */
-__global__ void letSelectKernel(int64_t N, int64_t L, const uint8_t* __restrict__ failed,
+__global__ void letSelectKernel(int64_t N, int64_t L, int64_t np, const uint8_t* __restrict__ failed,
                                 const uint8_t* __restrict__ outside, const int32_t* __restrict__ leafToNode,
                                 const int32_t* __restrict__ ns, const int32_t* __restrict__ ne, int64_t offset,
                                 const Quadrupole* __restrict__ mp, const int32_t* __restrict__ parents,
@@ -2083,18 +2083,19 @@ __global__ void letSelectKernel(int64_t N, int64_t L, const uint8_t* __restrict_
     {
         const int32_t nd = leafToNode[i];
         const uint8_t v  = uint8_t(open(nd));
-        for (int64_t k = int64_t(ns[nd]) - offset; k < int64_t(ne[nd]) - offset; ++k)
+        const int64_t k0 = int64_t(ns[nd]) - offset, k1 = int64_t(ne[nd]) - offset;
+        for (int64_t k = k0 > 0 ? k0 : 0; k < k1 && k < np; ++k) // (clamped to the flag array)
             pflags[k] = v;
     }
 }
 
-void letSelect(int64_t N, int64_t L, const uint8_t* failed, const uint8_t* outside, const int32_t* leafToNode,
-               const int32_t* ns, const int32_t* ne, int64_t offset, const void* mp, const int32_t* parents,
-               uint8_t* pflags, uint8_t* send, hipStream_t s)
+void letSelect(int64_t N, int64_t L, int64_t np, const uint8_t* failed, const uint8_t* outside,
+               const int32_t* leafToNode, const int32_t* ns, const int32_t* ne, int64_t offset, const void* mp,
+               const int32_t* parents, uint8_t* pflags, uint8_t* send, hipStream_t s)
 {
     const int64_t n = N > L ? N : L;
     if (n <= 0) return;
-    letSelectKernel<<<gridFor(n, 256), 256, 0, s>>>(N, L, failed, outside, leafToNode, ns, ne, offset,
+    letSelectKernel<<<gridFor(n, 256), 256, 0, s>>>(N, L, np, failed, outside, leafToNode, ns, ne, offset,
                                                      static_cast<const Quadrupole*>(mp), parents, pflags, send);
     SPHX_LAUNCH_CHECK();
 }

@@ -253,9 +253,9 @@ void markLet(int64_t nb, const double* bc, const double* bh, const int32_t* chil
 void markOutsideRange(int64_t N, const KeyT* prefixes, KeyT lo, KeyT hi, uint8_t* failed, hipStream_t s);
 //! LET selection from the open flags (failed | outside, outside may be null): particle flags (over the tree's particles
 //! starting at offset) of opened leaves, send flags of the first unopened non-empty nodes below opened ones
-void letSelect(int64_t N, int64_t L, const uint8_t* failed, const uint8_t* outside, const int32_t* leafToNode,
-               const int32_t* ns, const int32_t* ne, int64_t offset, const void* mp, const int32_t* parents,
-               uint8_t* pflags, uint8_t* send, hipStream_t s);
+void letSelect(int64_t N, int64_t L, int64_t np, const uint8_t* failed, const uint8_t* outside,
+               const int32_t* leafToNode, const int32_t* ns, const int32_t* ne, int64_t offset, const void* mp,
+               const int32_t* parents, uint8_t* pflags, uint8_t* send, hipStream_t s);
 void m2pFlat(int64_t first, int64_t last, const double* x, const double* y, const double* z, const float* m,
              int64_t M, const double* mc, const void* mp, float G, float* ax, float* ay, float* az, double* ugrav,
              double* out, hipStream_t s);

@@ -211,9 +211,15 @@ def let_selection_masks(tree: Octree, failed: torch.Tensor, mp: torch.Tensor, n_
     launch (gravity.hip letSelect)."""
     N = tree.num_nodes
     if failed.is_cuda and n_particles is not None:
-        pflags = torch.empty(n_particles, dtype=torch.uint8, device=failed.device)
+        pflags = zero_(torch.empty(n_particles, dtype=torch.uint8, device=failed.device))  # (defined past the leaves)
         send = torch.empty(N, dtype=torch.uint8, device=failed.device)
-        _lib.hip().let_select(N, tree.leaf_to_node.numel(), failed.data_ptr(),
+        if mp.dtype != torch.float32:
+            raise ValueError("let_selection_masks: multipoles must be the float32 Quadrupole records")
+        if not (failed.numel() == N and mp.numel() >= 8 * N and tree.parents.numel() >= (N - 1) // 8 + 1):
+            raise ValueError("let_selection_masks: flag/multipole/parent arrays do not match the tree")
+        if outside is not None and outside.numel() != N:
+            raise ValueError("let_selection_masks: outside mask does not match the tree")
+        _lib.hip().let_select(N, tree.leaf_to_node.numel(), int(n_particles), failed.data_ptr(),
                               0 if outside is None else outside.data_ptr(), tree.leaf_to_node.data_ptr(),
                               tree.node_start.data_ptr(), tree.node_end.data_ptr(), int(tree.offset), mp.data_ptr(),
                               tree.parents.data_ptr(), pflags.data_ptr(), send.data_ptr(), _stream())
