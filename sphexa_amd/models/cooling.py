@@ -59,7 +59,7 @@ class Cooler:
         args = (first, last, float(self.gamma), d["rho"].data_ptr(), d["u"].data_ptr(), d["p"].data_ptr(),
                 d["c"].data_ptr())
         if d["u"].is_cuda:
-            _lib.hip().cooling_eos(*args, torch.cuda.current_stream().cuda_stream)
+            _lib.hip().cooling_eos(*args, _lib.stream())
         else:
             _lib.cpu().cooling_eos(*args)
 
@@ -69,7 +69,7 @@ class Cooler:
         if d["u"].is_cuda:
             out = torch.full((1,), 1e300, dtype=torch.float64, device=d["u"].device)
             _lib.hip().cooling_timestep(first, last, d["rho"].data_ptr(), d["u"].data_ptr(), self.params(),
-                                        out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                                        out.data_ptr(), _lib.stream())
             v = float(out.item())
         else:
             v = _lib.cpu().cooling_timestep(first, last, d["rho"].data_ptr(), d["u"].data_ptr(), self.params())
@@ -78,7 +78,7 @@ class Cooler:
     def cool(self, d, first, last, dt: float):
         args = (first, last, float(dt), d["rho"].data_ptr(), d["u"].data_ptr(), d["du"].data_ptr(), self.params())
         if d["u"].is_cuda:
-            _lib.hip().cool_particles(*args, torch.cuda.current_stream().cuda_stream)
+            _lib.hip().cool_particles(*args, _lib.stream())
         else:
             _lib.cpu().cool_particles(*args)
 

@@ -18,7 +18,7 @@ from ..parallel.comm import SUM
 
 
 def _stream():
-    return torch.cuda.current_stream().cuda_stream
+    return _lib.stream()
 
 
 def local_conserved(d, first: int, last: int, egrav=None) -> torch.Tensor:

@@ -141,7 +141,7 @@ class TurbulenceData:
             self._dev_table = t  # keep alive until the kernel ran
             _lib.hip().compute_stirring(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), ax.data_ptr(),
                                         ay.data_ptr(), az.data_ptr(), self.num_modes, t.data_ptr(),
-                                        self.sol_weight_norm, torch.cuda.current_stream().cuda_stream)
+                                        self.sol_weight_norm, _lib.stream())
         else:
             m = np.ascontiguousarray(self.modes)
             re, im, amp = np.ascontiguousarray(re), np.ascontiguousarray(im), np.ascontiguousarray(self.amplitudes)

@@ -95,3 +95,20 @@ def raise_on_device_check(where: str = ""):
         names = [v for b, v in DEVICE_CHECK_BITS.items() if flags >> b & 1]
         raise DeviceCheckError(f"device checks failed{(' in ' + where) if where else ''}: {', '.join(names)} "
                                f"(flags {flags:#x})")
+
+
+try:  # the raw current-stream query torch's own generated launch code uses (no Stream object, no device checks)
+    from torch._C import _cuda_getCurrentRawStream as _raw_stream, _cuda_getDevice as _cur_dev
+except ImportError:  # pragma: no cover
+    _raw_stream = _cur_dev = None
+
+
+def stream() -> int:
+    """the current HIP stream of the current device as an integer handle for the native launchers: what
+    ``torch.cuda.current_stream().cuda_stream`` returns (a ``with torch.cuda.stream(...)`` block included), without
+    building a Stream object (~0.3 instead of ~4 us per launch; ~40 launches per step)"""
+    if _raw_stream is not None:
+        return _raw_stream(_cur_dev())
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream

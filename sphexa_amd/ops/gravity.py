@@ -18,7 +18,7 @@ from ..utils.box import Box
 
 
 def _stream():
-    return torch.cuda.current_stream().cuda_stream
+    return _lib.stream()
 
 
 # test hook: >0 shrinks the LDS frontier of the GPU traversal so that groups take the global-memory spill path

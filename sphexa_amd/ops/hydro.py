@@ -43,7 +43,7 @@ MOM_HANDOFF = os.environ.get("SPHX_MOM_HANDOFF") == "1"
 
 
 def _stream():
-    return torch.cuda.current_stream().cuda_stream
+    return _lib.stream()
 
 
 def _p(t):

@@ -33,7 +33,7 @@ GROUP = 64
 
 
 def _stream():
-    return torch.cuda.current_stream().cuda_stream
+    return _lib.stream()
 
 
 @dataclass

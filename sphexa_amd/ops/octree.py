@@ -33,7 +33,7 @@ def _zeros_i32(n: int, device) -> torch.Tensor:
 
 
 def _stream():
-    return torch.cuda.current_stream().cuda_stream
+    return _lib.stream()
 
 
 @dataclass

@@ -32,7 +32,7 @@ def min_max(tensors: Sequence[torch.Tensor], out: torch.Tensor | None = None) ->
             out = torch.empty(2 * len(tensors), dtype=torch.float64, device=dev)
         n = tensors[0].numel()
         _lib.hip().multi_min_max(n, [t.data_ptr() for t in tensors], [int(t.dtype == torch.float64) for t in tensors],
-                                 out.data_ptr(), _work(dev).data_ptr(), torch.cuda.current_stream().cuda_stream)
+                                 out.data_ptr(), _work(dev).data_ptr(), _lib.stream())
         return out
     big = torch.finfo(torch.float64).max
     vals = []
@@ -51,7 +51,7 @@ def max_norm2(ax: torch.Tensor, ay: torch.Tensor, az: torch.Tensor, first: int, 
     if dev.type == "cuda":
         out = torch.empty(1, dtype=torch.float64, device=dev)
         _lib.hip().max_norm2(first, last, ax.data_ptr(), ay.data_ptr(), az.data_ptr(), out.data_ptr(),
-                             _work(dev).data_ptr(), torch.cuda.current_stream().cuda_stream)
+                             _work(dev).data_ptr(), _lib.stream())
         return out.reshape(())
     return (ax[first:last].double() ** 2 + ay[first:last].double() ** 2 + az[first:last].double() ** 2).max()
 
@@ -73,7 +73,7 @@ def timestep_reduce(ax, ay, az, first: int, last: int, grav: bool, courant, divv
         raise TypeError("divv_max must be a float32 device scalar")
     _lib.hip().timestep_reduce(first, last, ax.data_ptr() if grav else 0, ay.data_ptr(), az.data_ptr(), c_dev, c_host,
                                r_dev, r_host, float(Krho), float(eta_acc), float(eps), float(others), float(prev_dt),
-                               out.data_ptr(), _work(dev).data_ptr(), torch.cuda.current_stream().cuda_stream)
+                               out.data_ptr(), _work(dev).data_ptr(), _lib.stream())
     return out
 
 
@@ -81,7 +81,7 @@ def field_max(f: torch.Tensor, first: int, last: int) -> torch.Tensor:
     """max of a float32 field over [first, last) as a float32 device scalar (two native launches, no torch reduce)"""
     out = torch.empty(1, dtype=torch.float32, device=f.device)
     _lib.hip().field_max(first, last, f.data_ptr(), out.data_ptr(), _work(f.device).data_ptr(),
-                         torch.cuda.current_stream().cuda_stream)
+                         _lib.stream())
     return out.reshape(())
 
 
@@ -90,7 +90,7 @@ def fill_f32(t: torch.Tensor, value: float):
     import struct
 
     bits = struct.unpack("<I", struct.pack("<f", value))[0]
-    _lib.hip().fill32(t.data_ptr(), bits, t.numel(), torch.cuda.current_stream().cuda_stream)
+    _lib.hip().fill32(t.data_ptr(), bits, t.numel(), _lib.stream())
     return t
 
 
@@ -99,7 +99,7 @@ def zero_(t: torch.Tensor):
     are not whole 32-bit words): no torch fill kernel"""
     nb = t.numel() * t.element_size()
     if nb:
-        s = torch.cuda.current_stream().cuda_stream
+        s = _lib.stream()
         if nb % 4 == 0 and t.data_ptr() % 4 == 0:
             _lib.hip().fill32(t.data_ptr(), 0, nb // 4, s)
         else:

@@ -21,7 +21,7 @@ HILBERT, MORTON = 0, 1
 
 
 def _stream():
-    return torch.cuda.current_stream().cuda_stream
+    return _lib.stream()
 
 
 def compute_keys(x: torch.Tensor, y: torch.Tensor, z: torch.Tensor, box: Box, kind: int = HILBERT,

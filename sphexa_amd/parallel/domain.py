@@ -57,7 +57,7 @@ class HaloOwnershipError(RuntimeError):
 
 
 def _stream():
-    return torch.cuda.current_stream().cuda_stream
+    return _lib.stream()
 
 
 class Domain:
@@ -644,7 +644,7 @@ def _pack_bits(flags: torch.Tensor, out: Optional[torch.Tensor] = None,
         if out is None:
             out = torch.empty(_nbytes_bits(n), dtype=torch.uint8, device=f.device)
         _lib.hip().pack_bits(n, f.data_ptr(), out.data_ptr(), 0 if count is None else count.data_ptr(),
-                             torch.cuda.current_stream().cuda_stream)
+                             _lib.stream())
         return out
     if count is not None:
         count += flags.sum(dtype=torch.int64)
@@ -667,7 +667,7 @@ def _unpack_bits(bits: torch.Tensor, n: int) -> torch.Tensor:
     if bits.is_cuda:
         flags = torch.empty(n, dtype=torch.uint8, device=bits.device)
         _lib.hip().unpack_bits(n, bits.contiguous().data_ptr(), flags.data_ptr(),
-                               torch.cuda.current_stream().cuda_stream)
+                               _lib.stream())
         return flags
     w = _BIT_WEIGHTS.get(bits.device)
     if w is None:
