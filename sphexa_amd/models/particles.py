@@ -123,6 +123,7 @@ class ParticlesData:
             if self._state[n] != DEPENDENT:
                 raise FieldStateError(f"can only release dependent fields, {n} is in state {self._state[n]}")
             self._state[n] = RELEASED
+            self._drop_views(n)
 
     def acquire(self, *names: str):
         """turn an unused field into a dependent one, reusing the storage of a released field of the same type"""
@@ -133,6 +134,7 @@ class ParticlesData:
                          None)
             if donor is None:
                 raise FieldStateError(f"no released field of type {FIELD_DTYPES[n]} available for {n}")
+            self._drop_views(n, donor)
             self._buf[n] = self._buf.pop(donor)
             self._state[donor] = UNUSED
             self._state[n] = DEPENDENT
@@ -161,11 +163,13 @@ class ParticlesData:
             if old is not None and old.numel() > 0:
                 k = min(old.numel(), self._capacity)
                 t[:k] = old[:k]
+            self._drop_views(n)
             self._buf[n] = t
 
     def resize(self, size: int, keep: bool = True):
         """set the active size, growing all allocated buffers by the growth factor when needed"""
         if size > self._capacity:
+            self._drop_views()
             self._capacity = int(math.ceil(size * self.growth)) + 64
             for n in list(self._buf.keys()):
                 if self.is_allocated(n) or n in self._buf:
@@ -180,7 +184,16 @@ class ParticlesData:
     def __getitem__(self, name: str) -> torch.Tensor:
         if not self.is_allocated(name):
             raise FieldStateError(f"field {name} is not allocated")
-        return self._buf[name][: self.size]
+        # the active-range view is cached per (storage tensor, size): a step reads fields ~200 times and a torch slice
+        # costs ~1.5 us of host time each (the GPU idles on host time at small per-rank sizes)
+        t = self._buf[name]
+        views = self.__dict__.setdefault("_views", {})
+        c = views.get(name)
+        if c is not None and c[0] is t and c[1] == self.size:
+            return c[2]
+        v = t[: self.size]
+        views[name] = (t, self.size, v)
+        return v
 
     def __setitem__(self, name: str, value):
         self[name].copy_(torch.as_tensor(value, dtype=FIELD_DTYPES[name]))
@@ -198,7 +211,18 @@ class ParticlesData:
         """the full-capacity storage of a field (used to swap in reordered data)"""
         return self._buf[name]
 
+    def _drop_views(self, *names):
+        """forget cached views (they hold their storage: a replaced buffer must be freeable right away)"""
+        views = self.__dict__.get("_views")
+        if views:
+            if names:
+                for n in names:
+                    views.pop(n, None)
+            else:
+                views.clear()
+
     def set_buffer(self, name: str, t: torch.Tensor):
+        self._drop_views(name)
         assert t.dtype == FIELD_DTYPES[name]
         if t.numel() < self._capacity:
             full = torch.empty(self._capacity, dtype=t.dtype, device=self.device)
