@@ -222,7 +222,13 @@ class Domain:
         per = len(rest) if cap * 8 * max(len(rest), 1) <= REORDER_ALL_BYTES else REORDER_BATCH
         for c in range(0, len(rest), max(per, 1)):
             batch = rest[c:c + max(per, 1)]
-            bufs = [torch.empty(cap, dtype=d.buffer(f).dtype, device=d.device) for f in batch]
+            if len(batch) == len(rest) and d.device.type == "cuda":
+                # one launch-bound batch: one allocation per dtype, 256-B aligned field slices (host time: ~3 us per
+                # torch allocation and the GPU idles on host time at these sizes); the block is freed once the
+                # next sync has replaced all of its fields
+                bufs = _field_block(d, batch, cap)
+            else:
+                bufs = [torch.empty(cap, dtype=d.buffer(f).dtype, device=d.device) for f in batch]
             sfc_ops.gather_many(perm, [own[f] for f in batch], [b[self.start:self.end] for b in bufs])
             for f, b in zip(batch, bufs):
                 own[f] = None
@@ -628,6 +634,20 @@ _BIT_WEIGHTS: dict = {}
 
 def _nbytes_bits(n: int) -> int:
     return (int(n) + 7) // 8
+
+
+def _field_block(d, names, cap: int) -> list:
+    """``cap``-element buffers for ``names``, carved from one allocation per dtype at 64-element (>= 256 B) strides"""
+    stride = -(-cap // 64) * 64
+    groups: Dict[torch.dtype, list] = {}
+    for f in names:
+        groups.setdefault(d.buffer(f).dtype, []).append(f)
+    out = {}
+    for dt, fs in groups.items():
+        block = torch.empty(stride * len(fs), dtype=dt, device=d.device)
+        for i, f in enumerate(fs):
+            out[f] = block[i * stride:i * stride + cap]
+    return [out[f] for f in names]
 
 
 def _pack_bits(flags: torch.Tensor, out: Optional[torch.Tensor] = None,
