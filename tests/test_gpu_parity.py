@@ -150,7 +150,7 @@ def test_ve_step_matches_cpu(gpu, av_clean):
     assert torch.equal(c["nc"], g["nc"])
     for f in ("x", "y", "z", "temp", "h", "xm", "kx", "c11", "alpha"):
         assert _rel(g[f], c[f]) < 2e-5, f
-    _check(g, c, ("vx", "vy", "vz", "ax", "du"), 2e-3)
+    _check(g, c, ("vx", "vy", "vz", "ax", "du"), 2e-5)
 
 
 def test_std_step_matches_cpu(gpu):
@@ -167,7 +167,7 @@ def test_std_step_matches_cpu(gpu):
     c, g = results["cpu"], results[str(gpu)]
     for f in ("x", "temp", "rho", "p"):
         assert _rel(g[f], c[f]) < 2e-5, f
-    _check(g, c, ("ax", "du"), 2e-3)
+    _check(g, c, ("ax", "du"), 2e-5)
 
 
 def test_conserved_quantities(gpu):
@@ -303,7 +303,7 @@ def test_ve_step_nonuniform_mass_matches_cpu(gpu):
     c, g = results["cpu"], results[str(gpu)]
     for f in ("kx", "xm", "c11", "alpha"):
         assert _rel(g[f], c[f]) < 2e-5, f
-    _check(g, c, ("ax", "du"), 2e-3)
+    _check(g, c, ("ax", "du"), 2e-5)
 
 
 def test_uniform_mass_detection(gpu):
@@ -333,7 +333,7 @@ def test_ve_step_fp64_records_matches_cpu(gpu, monkeypatch):
     c, g = results["cpu"], results[str(gpu)]
     for f in ("kx", "xm", "c11", "alpha"):
         assert _rel(g[f], c[f]) < 2e-5, f
-    _check(g, c, ("ax", "du"), 2e-3)
+    _check(g, c, ("ax", "du"), 2e-5)
 
 
 
