@@ -10,7 +10,11 @@ The global bucket size follows the reference: max(bucketSizeFocus, N / (100 * nu
 
 from __future__ import annotations
 
+import os
+
 import torch
+
+from ..parallel.domain import default_bucket_size_focus
 
 from ..models import particles as P
 from ..models.init import initializer_factory
@@ -24,7 +28,7 @@ from ..ops import _lib
 class Simulation:
     def __init__(self, init: str, n: int = 50, prop: str = "ve", device=None, glass=None, av_clean=False,
                  comm: Comm | None = None, theta: float | None = None, G: float | None = None, out=None,
-                 quiet=True, bucket_size_focus: int = 64, initializer=None):
+                 quiet=True, bucket_size_focus: int | None = None, initializer=None):
         self.comm = comm or Comm()
         rank, size = self.comm.rank, self.comm.size
         if device is None:
@@ -42,6 +46,10 @@ class Simulation:
             self.d.g = float(G)
         if theta is None:
             theta = 0.5 if self.d.g != 0.0 else 1.0
+        # (tuning: SPHX_BUCKET_FOCUS overrides the local octree's leaf capacity, reference bucketSizeFocus = 64)
+        if bucket_size_focus is None:
+            bucket_size_focus = default_bucket_size_focus(self.d.g != 0.0)
+        bucket_size_focus = int(os.environ.get("SPHX_BUCKET_FOCUS", bucket_size_focus))
         bucket = max(bucket_size_focus, int(self.d.numParticlesGlobal) // (100 * size))
         self.domain = Domain(self.comm, box, bucket_size_focus=bucket_size_focus, bucket_size=bucket, theta=theta)
         self.propagator.sync(self.domain, self.d)

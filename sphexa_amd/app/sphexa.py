@@ -134,7 +134,9 @@ def main(argv=None) -> int:
     if rank == 0:
         print(f"Data generated for {d.numParticlesGlobal} global particles", flush=True)
 
-    bucket_focus = 64
+    from ..parallel.domain import default_bucket_size_focus
+
+    bucket_focus = int(os.environ.get("SPHX_BUCKET_FOCUS", default_bucket_size_focus(have_grav)))
     bucket = max(bucket_focus, d.numParticlesGlobal // (100 * num_ranks))
     domain = Domain(comm, box, bucket_size_focus=bucket_focus, bucket_size=bucket, theta=theta)
     propagator.sync(domain, d)

@@ -48,6 +48,17 @@ from ..ops.reduce import zero_
 from .comm import Comm, MAX, MIN, SUM
 
 HALO_FIELDS = ("x", "y", "z", "h", "m")
+# leaf capacity of the local (focus) octree: the reference's 64 (bucketSizeFocus) with self-gravity, 128 without.
+# 128 leaves the lattice and collapse cases unchanged (a level holds ~30 particles per cell there either way) and
+# makes the glass of Noh -n 300 ~11 % faster per step (its level-7 cells hold ~13 particles: 64 split them into 2.4x
+# as many leaves per search, profiles/r4_perf_log.md "Octree leaf capacity"); with gravity, larger leaves would
+# enlarge the LET particle halos (opened leaves travel whole)
+BUCKET_SIZE_FOCUS = 64
+BUCKET_SIZE_FOCUS_HYDRO = 128
+
+
+def default_bucket_size_focus(gravity: bool) -> int:
+    return BUCKET_SIZE_FOCUS if gravity else BUCKET_SIZE_FOCUS_HYDRO
 REORDER_BATCH = 3  # conserved fields reordered per gather launch in sync (bounds the transient memory)
 REORDER_ALL_BYTES = 1 << 30  # below this transient size all remaining fields are reordered together
 
@@ -61,7 +72,7 @@ def _stream():
 
 
 class Domain:
-    def __init__(self, comm: Comm, box: Box, bucket_size_focus: int = 64, bucket_size: Optional[int] = None,
+    def __init__(self, comm: Comm, box: Box, bucket_size_focus: int = BUCKET_SIZE_FOCUS, bucket_size: Optional[int] = None,
                  theta: float = 1.0, sfc_kind: int = sfc_ops.HILBERT, halo_cut_boxes: int = 4096,
                  check_halos: bool | str = True):
         self.comm = comm
