@@ -48,13 +48,13 @@ from ..ops.reduce import zero_
 from .comm import Comm, MAX, MIN, SUM
 
 HALO_FIELDS = ("x", "y", "z", "h", "m")
-# leaf capacity of the local (focus) octree: the reference's 64 (bucketSizeFocus) with self-gravity, 128 without.
-# 128 leaves the lattice and collapse cases unchanged (a level holds ~30 particles per cell there either way) and
-# makes the glass of Noh -n 300 ~11 % faster per step (its level-7 cells hold ~13 particles: 64 split them into 2.4x
-# as many leaves per search, profiles/r4_perf_log.md "Octree leaf capacity"); with gravity, larger leaves would
-# enlarge the LET particle halos (opened leaves travel whole)
+# leaf capacity of the local (focus) octree: the reference's 64 (bucketSizeFocus) with self-gravity, 256 without.
+# Larger leaves make the glass of Noh -n 300 ~11 % faster per step (its level-7 cells hold ~13 particles: 64 split
+# them into 2.4x as many leaves per search), Turbulence -n 600 515 -> 459 ms and Sedov -n 400 -1.4 % (256); Sedov
+# -n 100 +2.5 %, the rest unchanged (profiles/r4_perf_log.md "Octree leaf capacity"). With gravity, larger leaves
+# would enlarge the LET particle halos (opened leaves travel whole)
 BUCKET_SIZE_FOCUS = 64
-BUCKET_SIZE_FOCUS_HYDRO = 128
+BUCKET_SIZE_FOCUS_HYDRO = 256
 
 
 def default_bucket_size_focus(gravity: bool) -> int:
