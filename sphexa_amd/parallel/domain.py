@@ -48,13 +48,14 @@ from ..ops.reduce import zero_
 from .comm import Comm, MAX, MIN, SUM
 
 HALO_FIELDS = ("x", "y", "z", "h", "m")
-# leaf capacity of the local (focus) octree: the reference's 64 (bucketSizeFocus) with self-gravity, 256 without.
+# leaf capacity of the local (focus) octree: the reference's 64 (bucketSizeFocus) with self-gravity, 512 without.
 # Larger leaves make the glass of Noh -n 300 ~11 % faster per step (its level-7 cells hold ~13 particles: 64 split
-# them into 2.4x as many leaves per search), Turbulence -n 600 515 -> 459 ms and Sedov -n 400 -1.4 % (256); Sedov
-# -n 100 +2.5 %, the rest unchanged (profiles/r4_perf_log.md "Octree leaf capacity"). With gravity, larger leaves
-# would enlarge the LET particle halos (opened leaves travel whole)
+# them into 2.4x as many leaves per search) and Turbulence -n 600 515 -> 459 ms; 512 rather than 256 also keeps
+# lattice cells of ~244 particles from splitting and merging every step (Sedov -n 100/200/400 -4 / -1.6 / -0.4 %;
+# profiles/r4_perf_log.md "Octree leaf capacity"). With gravity, larger leaves would enlarge the LET particle halos
+# (opened leaves travel whole)
 BUCKET_SIZE_FOCUS = 64
-BUCKET_SIZE_FOCUS_HYDRO = 256
+BUCKET_SIZE_FOCUS_HYDRO = 512
 
 
 def default_bucket_size_focus(gravity: bool) -> int:
