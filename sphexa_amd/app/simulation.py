@@ -48,7 +48,7 @@ class Simulation:
             theta = 0.5 if self.d.g != 0.0 else 1.0
         # (tuning: SPHX_BUCKET_FOCUS overrides the local octree's leaf capacity, reference bucketSizeFocus = 64)
         if bucket_size_focus is None:
-            bucket_size_focus = default_bucket_size_focus(self.d.g != 0.0)
+            bucket_size_focus = default_bucket_size_focus(self.d.g != 0.0, size)
         bucket_size_focus = int(os.environ.get("SPHX_BUCKET_FOCUS", bucket_size_focus))
         bucket = max(bucket_size_focus, int(self.d.numParticlesGlobal) // (100 * size))
         self.domain = Domain(self.comm, box, bucket_size_focus=bucket_size_focus, bucket_size=bucket, theta=theta)

@@ -53,13 +53,17 @@ HALO_FIELDS = ("x", "y", "z", "h", "m")
 # them into 2.4x as many leaves per search) and Turbulence -n 600 515 -> 459 ms; 512 rather than 256 also keeps
 # lattice cells of ~244 particles from splitting and merging every step (Sedov -n 100/200/400 -4 / -1.6 / -0.4 %;
 # profiles/r4_perf_log.md "Octree leaf capacity"). With gravity, larger leaves would enlarge the LET particle halos
-# (opened leaves travel whole)
+# (opened leaves travel whole); on one rank there is no LET, and 128 makes Evrard -n 200 29.5 -> 29.0 ms (256:
+# 34.9, the P2P share grows)
 BUCKET_SIZE_FOCUS = 64
 BUCKET_SIZE_FOCUS_HYDRO = 512
+BUCKET_SIZE_FOCUS_GRAVITY_1RANK = 128
 
 
-def default_bucket_size_focus(gravity: bool) -> int:
-    return BUCKET_SIZE_FOCUS if gravity else BUCKET_SIZE_FOCUS_HYDRO
+def default_bucket_size_focus(gravity: bool, nranks: int = 1) -> int:
+    if not gravity:
+        return BUCKET_SIZE_FOCUS_HYDRO
+    return BUCKET_SIZE_FOCUS_GRAVITY_1RANK if nranks == 1 else BUCKET_SIZE_FOCUS
 REORDER_BATCH = 3  # conserved fields reordered per gather launch in sync (bounds the transient memory)
 REORDER_ALL_BYTES = 1 << 30  # below this transient size all remaining fields are reordered together
 
