@@ -47,9 +47,10 @@ class Simulation:
         if theta is None:
             theta = 0.5 if self.d.g != 0.0 else 1.0
         # (tuning: SPHX_BUCKET_FOCUS overrides the local octree's leaf capacity, reference bucketSizeFocus = 64)
+        # (an explicit argument wins over the environment)
         if bucket_size_focus is None:
-            bucket_size_focus = default_bucket_size_focus(self.d.g != 0.0, size)
-        bucket_size_focus = int(os.environ.get("SPHX_BUCKET_FOCUS", bucket_size_focus))
+            bucket_size_focus = int(os.environ.get("SPHX_BUCKET_FOCUS", default_bucket_size_focus(self.d.g != 0.0,
+                                                                                                    size)))
         bucket = max(bucket_size_focus, int(self.d.numParticlesGlobal) // (100 * size))
         self.domain = Domain(self.comm, box, bucket_size_focus=bucket_size_focus, bucket_size=bucket, theta=theta)
         self.propagator.sync(self.domain, self.d)
@@ -72,6 +73,9 @@ class Simulation:
     def conserved(self):
         from ..models.observables import compute_conserved_quantities
 
+        # a deferred host copy (defer_host) still holds the previous evaluation's values (gravitational energy): collect
+        # it first so the sums below are not mixed with the step before
+        self.propagator.finish_host(self.d)
         compute_conserved_quantities(self.d, self.domain.start_index(), self.domain.end_index(), self.comm)
         d = self.d
         return dict(etot=d.etot, ecin=d.ecin, eint=d.eint, egrav=d.egrav, linmom=d.linmom, angmom=d.angmom,

@@ -41,8 +41,20 @@ def _common_fill(d, alpha=None):
     d.fill_if_allocated("alpha", d.alphamin if alpha is None else alpha)
 
 
+def _icbrt(v):
+    """exact cube root of a perfect cube (the glass blocks hold k^3 particles), else the nearest-integer root"""
+    r = int(round(v ** (1.0 / 3.0)))
+    for c in (r - 1, r, r + 1):
+        if c ** 3 == v:
+            return c
+    return v ** (1.0 / 3.0)
+
+
 def _multi(n, block):
-    return max(int(round(n / len(block) ** (1.0 / 3.0))), 1)
+    """block replication count per dimension: std::rint(n / std::cbrt(blockSize)) (reference
+    main/src/init/evrard_init.hpp:158), i.e. round half to even on an exact cube root (Python's round is
+    half-to-even; a float ``** (1/3)`` of 4096 gives 15.999999999999998 and turned 12.5 into 13)"""
+    return max(int(round(n / _icbrt(len(block)))), 1)
 
 
 # ----------------------------------------------------------------------------------------------------- Noh

@@ -61,9 +61,12 @@ BUCKET_SIZE_FOCUS_GRAVITY_1RANK = 128
 
 
 def default_bucket_size_focus(gravity: bool, nranks: int = 1) -> int:
-    if not gravity:
-        return BUCKET_SIZE_FOCUS_HYDRO
-    return BUCKET_SIZE_FOCUS_GRAVITY_1RANK if nranks == 1 else BUCKET_SIZE_FOCUS
+    """leaf capacity of the local octree. The larger capacities were measured on one rank only; on several ranks the
+    leaves also set the halo search boxes (one per own-tree leaf) and opened LET leaves travel whole, so multi-rank
+    runs keep the reference's 64 (bucketSizeFocus)"""
+    if nranks > 1:
+        return BUCKET_SIZE_FOCUS
+    return BUCKET_SIZE_FOCUS_GRAVITY_1RANK if gravity else BUCKET_SIZE_FOCUS_HYDRO
 REORDER_BATCH = 3  # conserved fields reordered per gather launch in sync (bounds the transient memory)
 REORDER_ALL_BYTES = 1 << 30  # below this transient size all remaining fields are reordered together
 
@@ -91,6 +94,7 @@ class Domain:
         self.check_halos = check_halos
         # peer pruning costs one host copy per step and pays off only when many ranks are far apart
         self.peer_prune_min_ranks = 16
+        self.sync_count = 0  # completed syncs (keys the prefetched box to the step it was taken in)
 
         self.start = 0
         self.end = 0
@@ -150,9 +154,10 @@ class Domain:
                 self.box.lo[d] = lo
                 self.box.hi[d] = hi
 
-    @staticmethod
-    def _box_key(x, y, z):
-        return tuple((t.data_ptr(), t.numel(), t._version) for t in (x, y, z))
+    def _box_key(self, x, y, z):
+        # native kernels write through data_ptr without bumping _version: the sync counter ties a prefetch to the
+        # positions of the step it was taken after (prefetch_box runs after the update of that step)
+        return (self.sync_count,) + tuple((t.data_ptr(), t.numel(), t._version) for t in (x, y, z))
 
     def _box_reduce(self, x, y, z) -> torch.Tensor:
         """device extents: [min x, max x, min y, ...] on one rank (no collective, so no sign flip and concatenation
@@ -169,6 +174,10 @@ class Domain:
 
     def _box_ext(self, v):
         return v if self.size > 1 else [v[0], v[2], v[4], -v[1], -v[3], -v[5]]
+
+    def drop_box_prefetch(self):
+        """forget a prefetched box (paths that rewrite coordinates outside the step: restarts, user edits)"""
+        self._box_prefetch = None
 
     def prefetch_box(self, d):
         """enqueue the next sync's box reduction right after the position update (GPU, open boundaries): its host
@@ -284,6 +293,7 @@ class Domain:
         self.octree = st.build(self.local_tree, counts, all_keys, d["x"], d["y"], d["z"], 0)
         self.stats["local_leaves"] = self.octree.num_leaves
         self.stats["halos"] = total - n_own
+        self.sync_count += 1
 
     # ------------------------------------------------------------------------------------ global assignment
     def _global_bucket(self, n_global: int) -> int:

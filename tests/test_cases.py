@@ -55,6 +55,31 @@ def test_evrard_gravity():
     assert float(radial.mean()) < 0
 
 
+def test_block_multiplicity_matches_reference():
+    """std::rint(n / std::cbrt(blockSize)) (reference main/src/init/evrard_init.hpp:158): exact cube root, half to
+    even. With the 16^3 glass block, -n 200 replicates 12 blocks per dimension (12.5 -> 12), not 13."""
+    blk = np.zeros((4096, 3))
+    assert cases._multi(200, blk) == 12
+    assert cases._multi(100, blk) == 6
+    assert cases._multi(50, blk) == 3  # 3.125
+    assert cases._multi(56, blk) == 4  # 3.5 -> 4 (even)
+    assert cases._multi(40, blk) == 2  # 2.5 -> 2 (even)
+    assert cases._multi(200, np.zeros((216, 3))) == 33  # 33.33
+
+
+@pytest.mark.slow
+def test_evrard_n200_particle_count():
+    """Evrard -n 200 on the built-in 16^3 glass: 12^3 blocks cut to the unit sphere = 3,706,143 particles, the count
+    the reference logs for the same configuration (profiles/r4/reference_anchor.md)"""
+    from sphexa_amd.models.init.glass import load_block as real_load_block  # (the autouse fixture swaps cases')
+
+    blk = real_load_block(None)
+    assert len(blk) == 4096
+    m1 = cases._multi(200, blk)
+    X = cases.cut_sphere(cases.assemble_cuboid(blk, [-1.0] * 3, [1.0] * 3, (m1, m1, m1), 0, 1), 1.0)
+    assert X.shape[0] == 3_706_143
+
+
 def test_isobaric_cube():
     sim = Simulation("isobaric-cube", n=24, device="cpu")
     x = sim.local("x")
