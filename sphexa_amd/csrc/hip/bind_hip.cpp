@@ -332,7 +332,7 @@ PYBIND11_MODULE(_sphx_hip, m)
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr prho, Ptr cs, const std::array<Ptr, 6>& cij, Ptr kx, Ptr xm,
              Ptr alpha, const std::array<Ptr, 6>& dV, Ptr wh, bool avClean, Ptr ax, Ptr ay, Ptr az, Ptr du,
-             Ptr minDt, int64_t ntot, Ptr rec, Ptr rec2, Ptr s, int inDone)
+             Ptr minDt, int64_t ntot, Ptr rec, Ptr rec2, Ptr s, int inDone, float mUniform)
           {
               auto sc = toConsts(c);
               MomFields f;
@@ -356,14 +356,14 @@ PYBIND11_MODULE(_sphx_hip, m)
               f.alpha = P<float>(alpha);
               momentumEnergyVe(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, f, avClean, P<float>(wh),
                                P<void>(rec), P<void>(rec2), P<float>(ax), P<float>(ay), P<float>(az), P<double>(du),
-                               P<float>(minDt), St(s), inDone);
+                               P<float>(minDt), St(s), inDone, mUniform);
           },
           py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
           py::arg("x"), py::arg("y"), py::arg("z"), py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("h"),
           py::arg("mm"), py::arg("prho"), py::arg("cs"), py::arg("cij"), py::arg("kx"), py::arg("xm"),
           py::arg("alpha"), py::arg("dV"), py::arg("wh"), py::arg("avClean"), py::arg("ax"), py::arg("ay"),
           py::arg("az"), py::arg("du"), py::arg("minDt"), py::arg("ntot"), py::arg("rec"), py::arg("rec2"),
-          py::arg("s"), py::arg("inDone") = 0);
+          py::arg("s"), py::arg("inDone") = 0, py::arg("mUniform") = 0.f);
     m.def("momentum_energy_std",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr rho, Ptr pp, Ptr cs, const std::array<Ptr, 6>& cij, Ptr wh,

@@ -183,7 +183,7 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                 void* momOut = nullptr, float* alphaOut = nullptr, const double* dtDev = nullptr);
 void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const MomFields& f,
                       bool avClean, const float* wh, void* rec, void* recGradV, float* ax, float* ay, float* az,
-                      double* du, float* minDt, hipStream_t s, int inDone = 0);
+                      double* du, float* minDt, hipStream_t s, int inDone = 0, float mUniform = 0.f);
 void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const StdFields& f,
                        const float* wh, void* rec, float* ax, float* ay, float* az, double* du, float* minDt,
                        hipStream_t s);

@@ -293,6 +293,33 @@ __global__ void packMomQKernel(int64_t lo, int64_t n, MomFields f, QFrame q, Src
     }
 }
 
+//! @brief split momentum records (SrcMomQ64 + SrcMomSide, uniform mass): as packMomQKernel without m and m/rho
+__global__ void packMomQ64Kernel(int64_t lo, int64_t n, MomFields f, QFrame q, SrcMomQ64* __restrict__ out,
+                                 SrcMomSide* __restrict__ side)
+{
+    int64_t i = lo + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SrcMomQ64 r;
+    r.x    = quantize(f.x[i], q.lo[0], q.s[0]);
+    r.y    = quantize(f.y[i], q.lo[1], q.s[1]);
+    r.z    = quantize(f.z[i], q.lo[2], q.s[2]);
+    r.vx   = f.vx[i];
+    r.vy   = f.vy[i];
+    r.vz   = f.vz[i];
+    r.ih   = 1.0f / f.h[i];
+    r.c11  = f.cij[0][i];
+    r.c12  = f.cij[1][i];
+    r.c13  = f.cij[2][i];
+    r.c22  = f.cij[3][i];
+    r.c23  = f.cij[4][i];
+    r.c33  = f.cij[5][i];
+    r.c    = f.c[i];
+    r.xm   = f.xm[i];
+    r.prho = f.prho[i];
+    out[i]  = r;
+    side[i] = SrcMomSide{f.kx[i] * f.m[i] / f.xm[i], f.alpha[i]};
+}
+
 __global__ void packAvVKernel(int64_t lo, int64_t n, const double* __restrict__ x, const double* __restrict__ y,
                               const double* __restrict__ z, const float* __restrict__ kx,
                               const float* __restrict__ vx, const float* __restrict__ vy,
@@ -753,6 +780,35 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     momentumEnergyVeBody<false>(a, sc, box, rec, nullptr, wh, ax, ay, az, du, minDt, tile);
 }
 
+//! @brief the split-record instance (uniform mass, SrcMomQ64 + SrcMomSide), 4 waves per SIMD as above
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void momentumEnergyVeQ64Kernel(
+    NbrArgs a, SphConsts sc, QFrame box, const SrcMomQ64* __restrict__ rec, const SrcMomSide* __restrict__ side,
+    float mU, const float* __restrict__ wh, float* __restrict__ ax, float* __restrict__ ay, float* __restrict__ az,
+    double* __restrict__ du, float* __restrict__ minDt)
+{
+    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcMomQ64>::S];
+    int64_t i;
+    PackedLane pl;
+    unsigned n;
+    bool valid = targetOf(a, i, pl, n);
+    float dti  = FLT_MAX;
+    float mvs, axi, ayi, azi;
+    double dui;
+    const MomSplitLoader ld{coopOf(rec, tile, i, a), side, mU};
+    momentumEnergyJLoop<false>(unsigned(i), sc, box, &pl, 0, n, ld, GradVLoader{nullptr},
+                               KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui, mvs);
+    if (valid)
+    {
+        ax[i] = axi;
+        ay[i] = ayi;
+        az[i] = azi;
+        du[i] = dui;
+        const SrcMomQ64 ri = rec[i];
+        dti                = tsKCourant(mvs, 1.0f / ri.ih, ri.c, float(sc.Kcour));
+    }
+    reduceMinDt(dti, minDt);
+}
+
 __global__ __launch_bounds__(kBlock) void momentumEnergyStdKernel(NbrArgs a, SphConsts sc, Box box,
                                                                   const SrcStd* __restrict__ rec,
                                                                   const float* __restrict__ wh,
@@ -1062,11 +1118,28 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
     SPHX_LAUNCH_CHECK();
 }
 
+//! byte offset of the side records in a split momentum workspace of ntot records (256-B aligned after the main ones)
+inline size_t momSideOffset(int64_t ntot) { return (size_t(ntot) * sizeof(SrcMomQ64) + 255) & ~size_t(255); }
+
 void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const MomFields& f,
                       bool avClean, const float* wh, void* rec, void* recGradV, float* ax, float* ay, float* az,
-                      double* du, float* minDt, hipStream_t s, int inDone)
+                      double* du, float* minDt, hipStream_t s, int inDone, float mUniform)
 {
     if (a.last <= a.first) return;
+    if (sc.fixedPoint && mUniform > 0.f && !avClean)
+    {
+        // split records: rec holds ntot SrcMomQ64 (64-B aligned) then ntot SrcMomSide
+        if (reinterpret_cast<uintptr_t>(rec) & 63) throw std::invalid_argument("momentum records: 64-B alignment");
+        const QFrame q  = qframeOf(box, sc.fixedPoint);
+        auto* main      = static_cast<SrcMomQ64*>(rec);
+        auto* side      = reinterpret_cast<SrcMomSide*>(static_cast<char*>(rec) + momSideOffset(ntot));
+        packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
+                   { packMomQ64Kernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, f, q, main, side); });
+        momentumEnergyVeQ64Kernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, main, side, mUniform, wh, ax,
+                                                              ay, az, du, minDt);
+        SPHX_LAUNCH_CHECK();
+        return;
+    }
     SrcGradV* gv = avClean ? (SrcGradV*)recGradV : nullptr;
     if (!sc.fixedPoint)
     {

@@ -2,7 +2,7 @@
  *  allocated per 64-particle target group.
  *
  * The reference keeps no neighbor lists on the GPU (each of its five SPH kernels re-traverses the tree,
- * sph/hydro_ve/*_gpu.cu); here the search stores them once per step and every pair loop streams them. Stored as
+ * sph/hydro_ve/ *_gpu.cu); here the search stores them once per step and every pair loop streams them. Stored as
  * int32 at a fixed ngmax stride they cost 608 B/particle (ngmax 150).
  *
  * The search of a group tests the sources of its candidate leaves in chunks of at most 64 consecutive particles

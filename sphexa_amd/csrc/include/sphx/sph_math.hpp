@@ -304,6 +304,56 @@ struct alignas(16) SrcMomQ
 };
 static_assert(!kHydroF32 || sizeof(SrcMomQ) == 80, "SrcMomQ is five 16-byte chunks");
 
+/*! @brief VE momentum records of the fixed-point, uniform-mass path: a 64-B main record plus an 8-B side record.
+ *
+ * The pair loops are bound by the texture addresser, which spends one cycle per 64-B cache segment a wave
+ * instruction touches (profiles/r5: TA_BUSY ~= TCP_TOTAL_CACHE_ACCESSES, 28.6 accesses per cooperative SrcMomQ load =
+ * 13 records x 2.25 segments). A 64-B record in a 64-B aligned array is exactly one segment: the cooperative gather
+ * of a step then touches 64 segments instead of 143. With the mass uniform (taken from the launch) and m/rho derived
+ * from rho, the momentum loop's 18 source dwords are these 16 + {rho, alpha} in the side array (one dwordx2 gather).
+ */
+struct alignas(64) SrcMomQ64
+{
+    uint32_t x, y, z;
+    HT vx, vy, vz;
+    HT ih;
+    HT c11, c12, c13, c22, c23, c33;
+    HT c, xm, prho;
+};
+static_assert(!kHydroF32 || sizeof(SrcMomQ64) == 64, "SrcMomQ64 is one 64-byte segment");
+
+struct alignas(8) SrcMomSide
+{
+    HT rho, alpha;
+};
+
+//! @brief the momentum loop's record from the split form (m uniform, m/rho derived)
+SPHX_HD SrcMomQ momOfSplit(const SrcMomQ64& a, const SrcMomSide& s, HT m)
+{
+    SrcMomQ r;
+    r.x     = a.x;
+    r.y     = a.y;
+    r.z     = a.z;
+    r.vx    = a.vx;
+    r.vy    = a.vy;
+    r.vz    = a.vz;
+    r.ih    = a.ih;
+    r.c11   = a.c11;
+    r.c12   = a.c12;
+    r.c13   = a.c13;
+    r.c22   = a.c22;
+    r.c23   = a.c23;
+    r.c33   = a.c33;
+    r.m     = m;
+    r.c     = a.c;
+    r.xm    = a.xm;
+    r.rho   = s.rho;
+    r.prho  = a.prho;
+    r.alpha = s.alpha;
+    r.mrho  = m * rcpF(s.rho);
+    return r;
+}
+
 //! @brief source mass of a Gradh record: stored, or the uniform mass of the launch (SrcXmQ)
 SPHX_HD HT massOf(const SrcPos& p, HT) { return p.m; }
 SPHX_HD HT massOf(const SrcXmQ&, HT mUniform) { return mUniform; }
@@ -556,6 +606,31 @@ __device__ __forceinline__ SrcMomQ coopUnpack<SrcMomQ>(const float4* o)
     r.prho  = o[4].y;
     r.alpha = o[4].z;
     r.mrho  = o[4].w;
+    return r;
+}
+
+template<>
+__device__ __forceinline__ SrcMomQ64 coopUnpack<SrcMomQ64>(const float4* o)
+{
+    static_assert(offsetof(SrcMomQ64, vx) == 12 && offsetof(SrcMomQ64, c11) == 28 && offsetof(SrcMomQ64, c) == 52,
+                  "SrcMomQ64 layout");
+    SrcMomQ64 r;
+    r.x    = __float_as_uint(o[0].x);
+    r.y    = __float_as_uint(o[0].y);
+    r.z    = __float_as_uint(o[0].z);
+    r.vx   = o[0].w;
+    r.vy   = o[1].x;
+    r.vz   = o[1].y;
+    r.ih   = o[1].z;
+    r.c11  = o[1].w;
+    r.c12  = o[2].x;
+    r.c13  = o[2].y;
+    r.c22  = o[2].z;
+    r.c23  = o[2].w;
+    r.c33  = o[3].x;
+    r.c    = o[3].y;
+    r.xm   = o[3].z;
+    r.prho = o[3].w;
     return r;
 }
 
@@ -825,6 +900,104 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const Coop
                 A[q]  = ld.issue(I2[q], q);
             }
             consume(Bf, D[u + 1]);
+        }
+        decodeChecked(W, more);
+    }
+}
+
+/*! @brief loader of the split momentum records (SrcMomQ64 cooperative + SrcMomSide per lane, uniform mass): returns
+ *         the assembled SrcMomQ, so momentumEnergyJLoop runs unchanged on it */
+struct MomSplitLoader
+{
+    CoopLoader<SrcMomQ64> main;
+    const SrcMomSide* side;
+    HT m;
+    __device__ SrcMomQ operator()(unsigned j) const { return momOfSplit(main.r[j], side[j], m); }
+};
+
+/*! @brief the cooperative loop of forEachNeighbor(CoopLoader) for the split momentum records: the 64-B main records
+ *         move as 4 chunks per record (16 records per wave instruction, one 64-B segment each), and each lane gathers
+ *         its own 8-B side record with the same one-step-ahead schedule */
+template<int B, class F>
+__device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const MomSplitLoader& ldm, F&& f)
+{
+    using R            = SrcMomQ64;
+    const auto& ld     = ldm.main;
+    constexpr int C    = CoopLoader<R>::C;
+    const PackedLane& pl = *plp;
+    const unsigned nblk  = pl.nblk;
+    if (nblk == 0) return;
+    auto consume = [&](const float4 (&raw)[C], const SrcMomSide& sd, unsigned j)
+    {
+        float4 o[C];
+#pragma unroll
+        for (int q = 0; q < C; ++q)
+            ld.stage(raw[q], q);
+#pragma unroll
+        for (int p = 0; p < C; ++p)
+            o[p] = ld.own(p);
+#pragma unroll
+        for (int p = 0; p < C; ++p)
+            asm volatile("" : "+v"(o[p].x), "+v"(o[p].y), "+v"(o[p].z), "+v"(o[p].w));
+        const SrcMomQ rec = momOfSplit(coopUnpack<R>(o), sd, ldm.m);
+        if (j != pl.self) f(j, rec);
+    };
+    unsigned D[8];
+    auto decodeChecked = [&](int4 w, bool used)
+    {
+        decodeBlock(w, pl.ctab, D);
+#ifdef SPHX_DEVICE_CHECKS
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            D[u] = used ? pl.checked(D[u]) : D[u];
+#endif
+    };
+    decodeChecked(pl.block(0), true);
+    unsigned I1[C], I2[C];
+    float4 A[C], Bf[C];
+    SrcMomSide As, Bs;
+#pragma unroll
+    for (int q = 0; q < C; ++q)
+    {
+        A[q]  = ld.issue(ld.spread(D[0], q), q);
+        I1[q] = ld.spread(D[1], q);
+    }
+    As = ldm.side[D[0]];
+    for (unsigned b = 0; b < nblk; ++b)
+    {
+        const int4 W    = pl.block(b + 1);
+        const bool more = b + 1 < nblk;
+#pragma unroll
+        for (int u = 0; u < 8; u += 2)
+        {
+            unsigned jA, jB;
+            if (u < 6)
+            {
+                jA = D[u + 2];
+                jB = D[u + 3];
+            }
+            else
+            {
+                decodeWord(W.x, pl.ctab, jA, jB);
+                jA = more ? pl.checked(jA) : pl.self;
+                jB = more ? pl.checked(jB) : pl.self;
+            }
+#pragma unroll
+            for (int q = 0; q < C; ++q)
+            {
+                I2[q] = ld.spread(jA, q);
+                Bf[q] = ld.issue(I1[q], q);
+            }
+            Bs = ldm.side[D[u + 1]];
+            consume(A, As, D[u]);
+#pragma unroll
+            for (int q = 0; q < C; ++q)
+            {
+                I1[q] = ld.spread(jB, q);
+                A[q]  = ld.issue(I2[q], q);
+            }
+            As = ldm.side[jA];
+            consume(Bf, Bs, D[u + 1]);
         }
         decodeChecked(W, more);
     }
@@ -1119,6 +1292,23 @@ struct alignas(16) SrcAvV
     HT c;
 };
 static_assert(!kHydroF32 || sizeof(SrcAvV) == 32, "SrcAvV is two 16-byte chunks");
+
+#if defined(__HIPCC__)
+template<>
+__device__ __forceinline__ SrcAvV coopUnpack<SrcAvV>(const float4* o)
+{
+    SrcAvV r;
+    r.x  = __float_as_uint(o[0].x);
+    r.y  = __float_as_uint(o[0].y);
+    r.z  = __float_as_uint(o[0].z);
+    r.vd = o[0].w;
+    r.vx = o[1].x;
+    r.vy = o[1].y;
+    r.vz = o[1].z;
+    r.c  = o[1].w;
+    return r;
+}
+#endif
 
 template<class G, class Idx, class Ld>
 SPHX_HD HT avSwitchesVJLoop(unsigned i, double K, const G& box, const Idx* nbr, int stride, unsigned nc, HT hi,

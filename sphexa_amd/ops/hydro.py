@@ -40,6 +40,8 @@ REC_BYTES = {"xmass": (32, 32), "gradh": (32, 32), "iad": (48, 48), "iadq": (32,
 # records itself and the peak drops by 80 B per particle (Sedov -n 400: 622 -> ~540 B/particle) for one more
 # record pass (profiles/r4/memory.md).
 MOM_HANDOFF = os.environ.get("SPHX_MOM_HANDOFF") == "1"
+# split momentum records (SrcMomQ64 + SrcMomSide) on the fixed-point uniform-mass path; 0: the 80-B SrcMomQ (A/B)
+MOM_SPLIT = os.environ.get("SPHX_MOM_SPLIT", "1") == "1"
 
 
 def _stream():
@@ -125,9 +127,16 @@ def _recB(d):
     return _wbuf(d, "_recB", 32)
 
 
-def _recM(d):
-    """workspace M: SrcMomQ records (IAD + AV -> momentum), 80 B per particle"""
-    return _wbuf(d, "_recM", 80)
+def _recM(d, split: bool = False):
+    """workspace M: SrcMomQ records (IAD + AV -> momentum), 80 B per particle; split: SrcMomQ64 (64 B, 64-B aligned)
+    then SrcMomSide (8 B) records (hydro.hip momSideOffset)"""
+    return _wbuf(d, "_recM", 72 if split else 80)
+
+
+def mom_split(d, av_clean: bool) -> bool:
+    """whether the momentum loop takes the split 64-B + 8-B records (sph_math.hpp SrcMomQ64): fixed-point frame,
+    uniform mass, no AV cleaning"""
+    return MOM_SPLIT and bool(d.fixedPoint) and not av_clean and uniform_mass(d) > 0
 
 
 def _rec(d, which: int = 0, loop: str = "mom"):
@@ -464,7 +473,7 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
             ho = _handoff(d)
             done = 1 if handoff_take(d, "iadq_own") else 0
             ho.clear()
-            mom = _recM(d).data_ptr() if (MOM_HANDOFF and not av_clean) else 0
+            mom = _recM(d).data_ptr() if (MOM_HANDOFF and not av_clean and not mom_split(d, av_clean)) else 0
             _lib.hip().iad_divv_curlv(*args, d.size, _rec(d, 0, "iadq").data_ptr(), _stream(),
                                       _rec(d, 1, "av").data_ptr(), inDone=done, avOut=_recB(d).data_ptr(),
                                       momOut=mom, cs=d["c"].data_ptr(), mm=d["m"].data_ptr(),
@@ -534,8 +543,10 @@ def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = F
         # fixed point: SrcMomQ records in workspace M (own range from the IAD and AV loops with MOM_HANDOFF)
         if not MOM_HANDOFF:
             d._recB = None  # the AV records are dead: their block serves the momentum records (B is re-created by XMass)
-        rec = _recM(d) if d.fixedPoint else _rec(d, 0, "mom")
-        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), d.size, rec.data_ptr(), gv, _stream(), inDone=done)
+        split = mom_split(d, av_clean)
+        rec = _recM(d, split) if d.fixedPoint else _rec(d, 0, "mom")
+        _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), d.size, rec.data_ptr(), gv, _stream(),
+                                      inDone=0 if split else done, mUniform=uniform_mass(d) if split else 0.0)
         d.minDtCourant_dev = dt
         d.minDtCourant = None
     else:
