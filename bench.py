@@ -159,6 +159,9 @@ def _run_case(init: str, n: int, args, comm, device) -> dict:
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
+    from sphexa_amd.utils.phase_prof import PROF as _PROF
+
+    _PROF.reset()  # (profiled runs only: the attribution covers the timed steps)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sim.step()
@@ -204,6 +207,12 @@ def _run_case(init: str, n: int, args, comm, device) -> dict:
         if nl is not None and nl.grouped and nl.nidx is not None:
             print(f"# neighbor lists: {nl.nidx.numel() * 4 / max(nl.last - nl.first, 1):.0f} B/particle "
                   f"(rows used {nl.rows_used}, pool plan {nl.plan})", file=sys.stderr)
+        from sphexa_amd.utils.phase_prof import ENABLED as _PROF_ON, PROF as _PROF
+
+        if _PROF_ON:
+            print("# domain sync wall-time attribution (SPHX_SYNC_PROFILE=1, device synchronized at every mark; "
+                  "collective times are included in the phase that issues them):\n" +
+                  "\n".join("#   " + ln for ln in _PROF.report(args.steps).splitlines()), file=sys.stderr)
         if prop.gravity is not None and prop.gravity.stats:
             print(f"# gravity stats {prop.gravity.stats}", file=sys.stderr)
         if device.type == "cuda":

@@ -16,6 +16,8 @@ def main():
     ap.add_argument("--init", default="sedov")
     ap.add_argument("-n", type=int, default=400)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-iterate", action="store_true", help="one round, no h iteration (timing variants whose lists "
+                    "are unusable would otherwise repeat rounds)")
     args = ap.parse_args()
     from sphexa_amd.app.simulation import Simulation
     from sphexa_amd.ops import neighbors as N
@@ -30,7 +32,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         # (iterate_h: the production kernel; after the first call h is converged and the search is one round)
-        N.find_neighbors(d, dom.octree, dom.box, dom.start_index(), dom.end_index(), iterate_h=True)
+        N.find_neighbors(d, dom.octree, dom.box, dom.start_index(), dom.end_index(), iterate_h=not args.no_iterate)
         torch.cuda.synchronize()
         ts.append(1e3 * (time.perf_counter() - t0))
     print(f"search {os.environ.get('SPHX_HIP_VARIANT', 'default')}: " + " ".join(f"{t:.1f}" for t in ts) + " ms",

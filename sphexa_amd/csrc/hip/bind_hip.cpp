@@ -128,6 +128,12 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("gather_multi",
           [](int64_t n, Ptr perm, const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst, int es, Ptr s)
           { gatherMulti(n, P<int32_t>(perm), src, dst, es, St(s)); });
+    m.def("gather_merged",
+          [](int64_t n, Ptr pm, int64_t nLo, int64_t nStay, Ptr permStay, const std::vector<uintptr_t>& own,
+             const std::vector<uintptr_t>& recv, const std::vector<uintptr_t>& dst, int es, Ptr s)
+          { gatherMerged(n, P<int32_t>(pm), nLo, nStay, P<int32_t>(permStay), own, recv, dst, es, St(s)); });
+    m.def("leaving_indices", [](int64_t nSend, Ptr perm, int64_t eSelf, int64_t nStay, Ptr out, Ptr s)
+          { leavingIndices(nSend, P<int32_t>(perm), eSelf, nStay, P<int64_t>(out), St(s)); });
     m.def("row_bytes", [](const std::vector<int>& sizes) { return rowBytes(sizes); });
     m.def("pack_rows", [](int64_t n, Ptr idx, const std::vector<uintptr_t>& src, const std::vector<int>& sizes, Ptr rows,
                           Ptr s) { packRows(n, P<int64_t>(idx), src, sizes, P<void>(rows), St(s)); });

@@ -56,6 +56,10 @@ constexpr int kMergeRuns = 16;
 void mergeSortedRuns(int64_t n, const KeyT* keys, const int64_t* runOffsets, int numRuns, KeyT* out, int32_t* perm,
                      hipStream_t s);
 void gather(int64_t n, const int32_t* perm, const void* src, void* dst, int elemSize, hipStream_t s);
+void gatherMerged(int64_t n, const int32_t* pm, int64_t nLo, int64_t nStay, const int32_t* permStay,
+                  const std::vector<uintptr_t>& own, const std::vector<uintptr_t>& recv,
+                  const std::vector<uintptr_t>& dst, int elemSize, hipStream_t s);
+void leavingIndices(int64_t nSend, const int32_t* perm, int64_t eSelf, int64_t nStay, int64_t* out, hipStream_t s);
 void gatherMulti(int64_t n, const int32_t* perm, const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,
                  int elemSize, hipStream_t s);
 //! halo message rows of several fields (8-byte fields first, rows padded to 8 bytes); idx == nullptr: rows 0..n-1

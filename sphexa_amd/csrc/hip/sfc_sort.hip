@@ -221,6 +221,78 @@ void gatherMulti(int64_t n, const int32_t* perm, const std::vector<uintptr_t>& s
     SPHX_LAUNCH_CHECK();
 }
 
+/*! @brief final order of a migration without the staying particles in the message: output k takes entry c = pm[k]
+ *         of the merged runs [received from lower ranks (nLo) | staying own particles (nStay) | received from higher
+ *         ranks]; a staying particle is read from the unsorted own field at permStay[c - nLo] (the local sort's
+ *         permutation of the own range), a received one from its unpacked row. The fields are read once, straight
+ *         into their new buffers: no migration copy of the particles that stay (reference domain.hpp:196-232 sends
+ *         only the particles that change rank as well).
+ */
+template<class T>
+struct FieldPtrs2
+{
+    const T* own[kMaxGatherFields];
+    const T* recv[kMaxGatherFields];
+    T* dst[kMaxGatherFields];
+};
+
+template<class T>
+__global__ void gatherMergedKernel(int64_t n, const int32_t* __restrict__ pm, int64_t nLo, int64_t nStay,
+                                   const int32_t* __restrict__ permStay, FieldPtrs2<T> f, int numFields)
+{
+    int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int64_t c    = pm[k];
+    const bool stay    = c >= nLo && c < nLo + nStay;
+    const int64_t j    = stay ? int64_t(permStay[c - nLo]) : (c < nLo ? c : c - nStay);
+#pragma unroll 4
+    for (int q = 0; q < numFields; ++q)
+        f.dst[q][k] = stay ? f.own[q][j] : f.recv[q][j];
+}
+
+void gatherMerged(int64_t n, const int32_t* pm, int64_t nLo, int64_t nStay, const int32_t* permStay,
+                  const std::vector<uintptr_t>& own, const std::vector<uintptr_t>& recv,
+                  const std::vector<uintptr_t>& dst, int elemSize, hipStream_t s)
+{
+    if (n == 0 || own.empty()) return;
+    const int nf = int(own.size());
+    if (nf > kMaxGatherFields || recv.size() != own.size() || dst.size() != own.size())
+        throw std::runtime_error("gatherMerged: field lists");
+    auto go = [&](auto tag)
+    {
+        using T = decltype(tag);
+        FieldPtrs2<T> f;
+        for (int q = 0; q < nf; ++q)
+        {
+            f.own[q]  = reinterpret_cast<const T*>(own[q]);
+            f.recv[q] = reinterpret_cast<const T*>(recv[q]);
+            f.dst[q]  = reinterpret_cast<T*>(dst[q]);
+        }
+        gatherMergedKernel<<<gridFor(n, 256), 256, 0, s>>>(n, pm, nLo, nStay, permStay, f, nf);
+    };
+    if (elemSize == 4) go(uint32_t{});
+    else if (elemSize == 8) go(uint64_t{});
+    else throw std::runtime_error("gatherMerged: unsupported element size");
+    SPHX_LAUNCH_CHECK();
+}
+
+//! @brief row indices of the particles that leave: the sorted positions outside [eSelf, eSelf + nStay), as the
+//!        unsorted indices perm[] (int64, the row packer's index type)
+__global__ void leavingIndicesKernel(int64_t nSend, const int32_t* __restrict__ perm, int64_t eSelf, int64_t nStay,
+                                     int64_t* __restrict__ out)
+{
+    int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (k >= nSend) return;
+    out[k] = perm[k < eSelf ? k : k + nStay];
+}
+
+void leavingIndices(int64_t nSend, const int32_t* perm, int64_t eSelf, int64_t nStay, int64_t* out, hipStream_t s)
+{
+    if (nSend <= 0) return;
+    leavingIndicesKernel<<<gridFor(nSend, 256), 256, 0, s>>>(nSend, perm, eSelf, nStay, out);
+    SPHX_LAUNCH_CHECK();
+}
+
 /*! @brief halo message rows: field k of row r at byte offset off[k] of a row of rowWords 4-byte words (8-byte fields
  *         first, so every field is naturally aligned); one thread per row, all fields of a message in one launch
  */

@@ -127,6 +127,60 @@ def gather_many(perm: torch.Tensor, srcs: Sequence[torch.Tensor], outs: Sequence
     return outs
 
 
+def leaving_indices(perm: torch.Tensor, e_self: int, n_stay: int) -> torch.Tensor:
+    """int64 unsorted indices of the particles that leave a rank: the sorted positions outside [e_self, e_self +
+    n_stay) mapped through the local sort's permutation ``perm`` (int32)"""
+    n_send = perm.numel() - n_stay
+    out = torch.empty(max(n_send, 0), dtype=torch.int64, device=perm.device)
+    if n_send <= 0:
+        return out
+    if perm.is_cuda:
+        _lib.hip().leaving_indices(n_send, perm.data_ptr(), e_self, n_stay, out.data_ptr(), _stream())
+    else:
+        out.copy_(torch.cat([perm[:e_self], perm[e_self + n_stay:]]).to(torch.int64))
+    return out
+
+
+class MergedSource:
+    """the particles a rank owns after a migration, in their new SFC order, without materializing them: entry c = pm[k]
+    of the merged runs [received from lower ranks (n_lo) | staying own (n_stay) | received from higher ranks] reads a
+    staying particle from the unsorted own fields at perm_stay[c - n_lo] and a received one from its unpacked row
+    (csrc/hip/sfc_sort.hip gatherMerged)"""
+
+    def __init__(self, pm, n_lo: int, n_stay: int, perm_stay, own: dict, recv: dict):
+        self.pm, self.n_lo, self.n_stay, self.perm_stay, self.own, self.recv = pm, n_lo, n_stay, perm_stay, own, recv
+
+    def gather(self, names: Sequence[str], outs: Sequence[torch.Tensor] | None = None):
+        n = self.pm.numel()
+        srcs = [self.own[f] for f in names]
+        if outs is None:
+            outs = [torch.empty(n, dtype=s.dtype, device=s.device) for s in srcs]
+        outs = list(outs)
+        if n == 0 or not names:
+            return outs
+        if srcs[0].is_cuda:
+            h = _lib.hip()
+            for size in (4, 8):
+                idx = [i for i, s in enumerate(srcs) if s.element_size() == size]
+                for c in range(0, len(idx), 16):
+                    chunk = idx[c:c + 16]
+                    h.gather_merged(n, self.pm.data_ptr(), self.n_lo, self.n_stay, self.perm_stay.data_ptr(),
+                                    [srcs[i].data_ptr() for i in chunk], [self.recv[names[i]].data_ptr() for i in chunk],
+                                    [outs[i].data_ptr() for i in chunk], size, _stream())
+            return outs
+        c = self.pm.to(torch.int64)
+        stay = (c >= self.n_lo) & (c < self.n_lo + self.n_stay)
+        own_idx = self.perm_stay.to(torch.int64)[(c - self.n_lo).clamp(0, max(self.n_stay - 1, 0))] \
+            if self.n_stay else torch.zeros_like(c)
+        r = torch.where(c < self.n_lo, c, c - self.n_stay)
+        for f, o in zip(names, outs):
+            a = self.own[f][own_idx] if self.n_stay else self.own[f][:0]
+            rv = self.recv[f]
+            b = rv[r.clamp(0, max(rv.numel() - 1, 0))] if rv.numel() else a
+            o.copy_(torch.where(stay, a, b) if self.n_stay and rv.numel() else (a if self.n_stay else b))
+        return outs
+
+
 def exclusive_scan(t: torch.Tensor) -> torch.Tensor:
     """exclusive prefix sum (int64) of a 1-D tensor; on the GPU the hand-written tile scan (csrc/hip/sample_sort.hip),
     so a time step runs no library (rocPRIM) scan"""

@@ -27,6 +27,8 @@ from typing import List, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from ..utils.phase_prof import timed_comm
+
 SUM, MIN, MAX = "sum", "min", "max"
 _OPS = {SUM: dist.ReduceOp.SUM, MIN: dist.ReduceOp.MIN, MAX: dist.ReduceOp.MAX}
 # element types RCCL can reduce / move (ncclDataType_t)
@@ -101,12 +103,13 @@ class Comm:
     def allreduce(self, t: torch.Tensor, op: str = SUM) -> torch.Tensor:
         if self.size > 1:
             self._audit("allreduce_" + op, t)
-            if self._staged(t):
-                h = _stage_host(t)
-                dist.all_reduce(h, op=_OPS[op], group=self.group)
-                t.copy_(_stage_dev(h, t.device))
-            else:
-                dist.all_reduce(t, op=_OPS[op], group=self.group)
+            with timed_comm("allreduce", t, self._staged(t)):
+                if self._staged(t):
+                    h = _stage_host(t)
+                    dist.all_reduce(h, op=_OPS[op], group=self.group)
+                    t.copy_(_stage_dev(h, t.device))
+                else:
+                    dist.all_reduce(t, op=_OPS[op], group=self.group)
         return t
 
     def allreduce_scalar(self, v: float, op: str = SUM, device=None, dtype=torch.float64) -> float:
@@ -145,22 +148,24 @@ class Comm:
             return counts.clone()
         s = counts.contiguous()
         staged = self._staged(s)
-        src = _stage_host(s) if staged else s
-        r = torch.empty_like(src)
-        self._audit("exchange_counts", src, r)
-        dist.all_to_all_single(r, src, group=self.group)
-        return _stage_dev(r, counts.device) if staged else r
+        with timed_comm("exchange_counts", s, staged):
+            src = _stage_host(s) if staged else s
+            r = torch.empty_like(src)
+            self._audit("exchange_counts", src, r)
+            dist.all_to_all_single(r, src, group=self.group)
+            return _stage_dev(r, counts.device) if staged else r
 
     def allgather_fixed(self, t: torch.Tensor) -> List[torch.Tensor]:
         """all-gather of equal-shape tensors (no size exchange, no host copy over RCCL)"""
         if self.size == 1:
             return [t]
         staged = self._staged(t)
-        src = _stage_host(t) if staged else t.contiguous()
-        outs = [torch.empty_like(src) for _ in range(self.size)]
-        self._audit("allgather", src)
-        dist.all_gather(outs, src, group=self.group)
-        return [_stage_dev(o, t.device) for o in outs] if staged else outs
+        with timed_comm("allgather_fixed", t, staged):
+            src = _stage_host(t) if staged else t.contiguous()
+            outs = [torch.empty_like(src) for _ in range(self.size)]
+            self._audit("allgather", src)
+            dist.all_gather(outs, src, group=self.group)
+            return [_stage_dev(o, t.device) for o in outs] if staged else outs
 
     def alltoallv(self, send: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int] | None = None,
                   ) -> Tuple[torch.Tensor, List[int]]:
@@ -173,12 +178,13 @@ class Comm:
         recv_counts = [int(v) for v in recv_counts]
         shape = (sum(recv_counts),) + tuple(send.shape[1:])
         staged = self._staged(send)
-        src = _stage_host(send) if staged else send.contiguous()
-        recv = torch.empty(shape, dtype=send.dtype, device=src.device)
-        self._audit("alltoallv", src, recv, splits=(send_counts, recv_counts))
-        dist.all_to_all_single(recv, src, output_split_sizes=list(recv_counts),
-                               input_split_sizes=list(send_counts), group=self.group)
-        return (_stage_dev(recv, send.device) if staged else recv), list(recv_counts)
+        with timed_comm("alltoallv", send, staged):
+            src = _stage_host(send) if staged else send.contiguous()
+            recv = torch.empty(shape, dtype=send.dtype, device=src.device)
+            self._audit("alltoallv", src, recv, splits=(send_counts, recv_counts))
+            dist.all_to_all_single(recv, src, output_split_sizes=list(recv_counts),
+                                   input_split_sizes=list(send_counts), group=self.group)
+            return (_stage_dev(recv, send.device) if staged else recv), list(recv_counts)
 
     def alltoallv_start(self, send: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int]
                         ) -> "PendingExchange":
@@ -192,12 +198,13 @@ class Comm:
         recv_counts = [int(v) for v in recv_counts]
         shape = (sum(recv_counts),) + tuple(send.shape[1:])
         staged = self._staged(send)
-        src = _stage_host(send) if staged else send.contiguous()
-        recv = torch.empty(shape, dtype=send.dtype, device=src.device)
-        self._audit("alltoallv", src, recv, splits=(send_counts, recv_counts))
-        work = dist.all_to_all_single(recv, src, output_split_sizes=recv_counts, input_split_sizes=send_counts,
-                                      group=self.group, async_op=not staged)
-        return PendingExchange(recv, work, send.device, src)
+        with timed_comm("alltoallv_start", send, staged):
+            src = _stage_host(send) if staged else send.contiguous()
+            recv = torch.empty(shape, dtype=send.dtype, device=src.device)
+            self._audit("alltoallv", src, recv, splits=(send_counts, recv_counts))
+            work = dist.all_to_all_single(recv, src, output_split_sizes=recv_counts, input_split_sizes=send_counts,
+                                          group=self.group, async_op=not staged)
+            return PendingExchange(recv, work, send.device, src)
 
     def allgather_var(self, t: torch.Tensor) -> List[torch.Tensor]:
         """gather tensors of different first-dimension sizes from all ranks"""
@@ -227,11 +234,12 @@ class PendingExchange:
         self._keep = keep  # the packed send buffer stays alive until the exchange has completed
 
     def wait(self) -> torch.Tensor:
-        if self.work is not None:
-            self.work.wait()
-            self.work = None
-        self._keep = None
-        return self.recv if self.recv.device == self.device else _stage_dev(self.recv, self.device)
+        with timed_comm("alltoallv_wait"):
+            if self.work is not None:
+                self.work.wait()
+                self.work = None
+            self._keep = None
+            return self.recv if self.recv.device == self.device else _stage_dev(self.recv, self.device)
 
 
 def init_distributed(backend: str | None = None) -> Comm:

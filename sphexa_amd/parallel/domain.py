@@ -46,6 +46,7 @@ from ..ops import sfc as sfc_ops
 from ..utils.box import Box, PERIODIC
 from ..ops.reduce import zero_
 from .comm import Comm, MAX, MIN, SUM
+from ..utils.phase_prof import PROF
 
 HALO_FIELDS = ("x", "y", "z", "h", "m")
 # leaf capacity of the local (focus) octree: the reference's 64 (bucketSizeFocus) with self-gravity, 512 without.
@@ -207,27 +208,38 @@ class Domain:
             # first call: everything held by this rank is owned (initial conditions / file read)
             self.start, self.end = 0, d.size
         s, e = self.start, self.end
+        PROF.start(d.device)
         own = {f: d[f][s:e] for f in conserved}
         x, y, z = own["x"], own["y"], own["z"]
 
         self.update_box(x, y, z)
+        PROF.mark("sync: box")
         keys = sfc_ops.compute_keys(x, y, z, self.box, self.sfc_kind)
+        PROF.mark("sync: keys")
 
         if self.size > 1:
-            keys, own = self._distribute(keys, own, conserved)
-            # the received particles are one SFC-sorted run per source rank: merged, not sorted again
-            skeys, perm = sfc_ops.merge_sorted_runs(keys, self._recv_run_counts)
+            # the staying particles are not moved: skeys is the new SFC order, src reads it from the own fields and the
+            # received rows (sfc_ops.MergedSource)
+            skeys, src = self._distribute(keys, own, conserved)
         else:
             skeys, perm = sfc_ops.sort_keys(keys)
+            src = None
+            PROF.mark("sync: sort")
         names = list(own.keys())
         n_own = skeys.numel()
 
+        def gather(fs, outs=None):
+            if src is not None:
+                return src.gather(fs, outs)
+            return sfc_ops.gather_many(perm, [own[f] for f in fs], outs)
+
+        sorted_fields = {}
         if self.size > 1:
             # halo discovery reads the sorted own coordinates (+ h, m)
             disc = [f for f in HALO_FIELDS if f in own]
-            for f, t in zip(disc, sfc_ops.gather_many(perm, [own[f] for f in disc])):
-                own[f] = t
-            self._discover_halos(skeys, own, gravity)
+            sorted_fields = dict(zip(disc, gather(disc)))
+            PROF.mark("sync: gather halo-discovery fields")
+            self._discover_halos(skeys, sorted_fields, gravity)
             sorted_done = set(disc)
         else:
             self.n_lo = self.n_hi = 0
@@ -254,17 +266,21 @@ class Domain:
                 bufs = _field_block(d, batch, cap)
             else:
                 bufs = [torch.empty(cap, dtype=d.buffer(f).dtype, device=d.device) for f in batch]
-            sfc_ops.gather_many(perm, [own[f] for f in batch], [b[self.start:self.end] for b in bufs])
+            gather(batch, [b[self.start:self.end] for b in bufs])
             for f, b in zip(batch, bufs):
                 own[f] = None
+                if src is not None:
+                    src.own[f] = None
                 d.set_buffer(f, b)
         for f in sorted_done:
-            d.buffer(f)[self.start:self.end].copy_(own[f])
-        del own
+            d.buffer(f)[self.start:self.end].copy_(sorted_fields[f])
+        del own, src, sorted_fields
         d.buffer("keys")[self.start:self.end].copy_(skeys)
+        PROF.mark("sync: reorder fields")
 
         if self.size > 1:
             self.exchange_halos(d, [f for f in HALO_FIELDS])
+            PROF.mark("sync: halo exchange x,y,z,h,m")
             hs = [slice(0, self.start), slice(self.end, total)]
             for sl in hs:
                 if sl.stop > sl.start:
@@ -280,6 +296,7 @@ class Domain:
                         self._pending_bad = bad if self._pending_bad is None else self._pending_bad + bad
                     else:
                         self._raise_bad_halos(int(bad))
+            PROF.mark("sync: halo keys + ownership check")
         # native kernels write h in place (h iteration, h update) without bumping the tensor version: drop the
         # cached per-step reductions of h and m so the pair loops re-derive them for the new particle set
         d._h_min = None
@@ -291,6 +308,7 @@ class Domain:
         st = self._local_state
         self.local_tree, counts = st.update(all_keys, self.bucket_size_focus)
         self.octree = st.build(self.local_tree, counts, all_keys, d["x"], d["y"], d["z"], 0)
+        PROF.mark("sync: local octree")
         self.stats["local_leaves"] = self.octree.num_leaves
         self.stats["halos"] = total - n_own
         self.sync_count += 1
@@ -323,6 +341,7 @@ class Domain:
         self._pinned_keep = []
         dev = keys.device
         skeys, perm = sfc_ops.sort_keys(keys)
+        PROF.mark("distribute: sort")
         if self._n_global is None:
             self._n_global = int(self.comm.allreduce_scalar(float(skeys.numel()), SUM, device=dev))
         bucket = self._global_bucket(self._n_global)
@@ -344,6 +363,7 @@ class Domain:
             tree = self._upload(tree_np.view(np.int64), dev)
         L = tree_np.size - 1
         self.global_tree, self.global_counts, self._tree_np = tree, gcounts, tree_np
+        PROF.mark("distribute: global tree counts + rebalance")
         n_global = int(c_np.sum())
         self._n_global = n_global
 
@@ -373,21 +393,39 @@ class Domain:
         recv_dev = self.comm.exchange_counts_dev(send_dev)
         counts = torch.cat([send_dev, recv_dev]).view(-1).cpu().tolist()
         send_counts, recv_counts = counts[: self.size], counts[self.size:]
-        self._recv_run_counts = recv_counts
+        PROF.mark("distribute: assignment + send/recv counts")
 
+        # only the particles that change rank travel: one packed all-to-all of keys + every conserved field (rows of
+        # bytes, like the halo exchange) over the sorted ranges of the other ranks; the own range stays in place
+        r = self.rank
+        e_self = sum(send_counts[:r])
+        n_stay = send_counts[r]
         names = list(own.keys())
-        sorted_fields = sfc_ops.gather_many(perm, [own[f] for f in names])
-        # one packed all-to-all for keys + every conserved field (rows of bytes, like the halo exchange)
-        tensors = [skeys] + sorted_fields
-        packed = _pack_rows(tensors, None)
-        recv, _ = self.comm.alltoallv(packed, send_counts, recv_counts)
-        n_new = recv.shape[0]
-        outs = [torch.empty(n_new, dtype=t.dtype, device=t.device) for t in tensors]
+        idx = sfc_ops.leaving_indices(perm, e_self, n_stay)
+        packed = _pack_rows([keys] + [own[f] for f in names], idx)
+        PROF.mark("distribute: pack leaving particles")
+        sc = list(send_counts)
+        rc = list(recv_counts)
+        sc[r] = rc[r] = 0
+        recv, _ = self.comm.alltoallv(packed, sc, rc)
+        PROF.mark("distribute: migration alltoallv")
+        n_recv = recv.shape[0]
+        outs = [torch.empty(n_recv, dtype=t.dtype, device=keys.device) for t in [keys] + [own[f] for f in names]]
         _unpack_rows(recv, outs, 0)
-        new_keys = outs[0]
-        out = dict(zip(names, outs[1:]))
-        self.stats["migrated_out"] = sum(send_counts) - send_counts[self.rank]
-        return new_keys, out
+        del recv, packed
+        # runs in rank order: received from lower ranks | the staying own range (sorted) | received from higher ranks;
+        # each run is SFC-sorted, so one merge gives the new order
+        n_lo = sum(rc[:r])
+        rkeys = outs[0]
+        kcat = torch.cat([rkeys[:n_lo], skeys[e_self:e_self + n_stay], rkeys[n_lo:]]) if n_recv else \
+            skeys[e_self:e_self + n_stay]
+        runs = rc[:r] + [n_stay] + rc[r + 1:]
+        fkeys, pm = sfc_ops.merge_sorted_runs(kcat, runs)
+        PROF.mark("distribute: unpack + merge")
+        self.stats["migrated_out"] = sum(sc)
+        src = sfc_ops.MergedSource(pm, n_lo, n_stay, perm[e_self:e_self + n_stay], dict(own),
+                                   dict(zip(names, outs[1:])))
+        return fkeys, src
 
     # ------------------------------------------------------------------------------------------------ halos
     def _discover_halos(self, skeys, own, gravity: bool = False):
@@ -397,10 +435,13 @@ class Domain:
         # from the root, each a host round trip)
         tree, counts = self._own_state.update(skeys, self.bucket_size_focus)
         ot = self._own_state.build(tree, counts, skeys, x, y, z, 0)
+        PROF.mark("halos: own octree")
         c, hf = _search_boxes(ot, x, y, z, h, 2.0)
         # a fixed-size list of coarse search boxes (empty slots: half < 0): no size exchange, no host copy
         boxes = _coarse_cut(ot, c, hf, self.halo_cut_boxes)
+        PROF.mark("halos: search boxes + coarse cut")
         all_boxes = self.comm.allgather_fixed(boxes)
+        PROF.mark("halos: allgather boxes")
 
         if gravity:
             from ..ops import gravity as grav_ops
@@ -415,6 +456,7 @@ class Domain:
                 outside.zero_()
             grav_ops.mark_outside_range(ot, self.assignment_keys[self.rank], self.assignment_keys[self.rank + 1],
                                         outside)
+            PROF.mark("halos: own upsweep (LET)")
         # peer pruning (reference traversal/peers.hpp: only ranks whose domains interact exchange halos): a rank whose
         # search boxes do not reach this rank's particle bounding box receives no SPH halos, and its marking pass is
         # skipped (with gravity every rank still gets the LET multipoles, so all ranks stay peers)
@@ -450,8 +492,10 @@ class Domain:
             # (one launch on the GPU: bitmask row + send count)
             _pack_bits(pflags, out=flag_bits[q], count=send_dev[q, 0:1])
         del row
+        PROF.mark("halos: mark per destination")
         recv_dev = self.comm.exchange_counts_dev(send_dev)
         host = torch.cat([send_dev, recv_dev]).cpu()
+        PROF.mark("halos: count exchange")
         send_h, recv_h = host[: self.size], host[self.size:]
         send_idx: List[torch.Tensor] = []
         mp_send: List[torch.Tensor] = []
@@ -461,8 +505,10 @@ class Domain:
                 mp_send.append(sfc_ops.compact_indices(_unpack_bits(node_bits[q], ot.num_nodes),
                                                        int(send_h[q, 1])))
         del flag_bits, node_bits
+        PROF.mark("halos: compact send lists")
         if gravity:
             self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes, [int(v) for v in recv_h[:, 1]])
+            PROF.mark("halos: multipole exchange + remote LET tree")
         self.halo_send_counts = [int(t.numel()) for t in send_idx]
         self.halo_recv_counts = [int(v) for v in recv_h[:, 0]]
         self.n_lo = sum(self.halo_recv_counts[: self.rank])
