@@ -132,6 +132,40 @@ PYBIND11_MODULE(_sphx_hip, m)
           [](int64_t n, Ptr pm, int64_t nLo, int64_t nStay, Ptr permStay, const std::vector<uintptr_t>& own,
              const std::vector<uintptr_t>& recv, const std::vector<uintptr_t>& dst, int es, Ptr s)
           { gatherMerged(n, P<int32_t>(pm), nLo, nStay, P<int32_t>(permStay), own, recv, dst, es, St(s)); });
+    m.def("mark_halos_multi",
+          [](int nDest, int nbPer, Ptr boxes, Ptr enabled, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr center, Ptr half,
+             Ptr x, Ptr y, Ptr z, int64_t n, const BoxArr& box, Ptr flags, Ptr s)
+          {
+              markHalosMulti(nDest, nbPer, P<double>(boxes), P<uint8_t>(enabled), P<int32_t>(child), P<int32_t>(n2l),
+                             P<int32_t>(ns), P<int32_t>(ne), P<double>(center), P<double>(half), P<double>(x),
+                             P<double>(y), P<double>(z), n, toBox(box), P<uint8_t>(flags), St(s));
+          });
+    m.def("mark_let_multi",
+          [](int nDest, int nbPer, Ptr boxes, Ptr enabled, Ptr child, Ptr n2l, Ptr tc, Ptr th, Ptr gc, int64_t N,
+             const BoxArr& box, Ptr failed, Ptr s)
+          {
+              markLetMulti(nDest, nbPer, P<double>(boxes), P<uint8_t>(enabled), P<int32_t>(child), P<int32_t>(n2l),
+                           P<double>(tc), P<double>(th), P<double>(gc), N, toBox(box), P<uint8_t>(failed), St(s));
+          });
+    m.def("let_select_multi",
+          [](int nDest, int64_t N, int64_t L, int64_t np, Ptr enabled, Ptr failed, Ptr outside, Ptr leafToNode,
+             Ptr ns, Ptr ne, int64_t offset, Ptr mp, Ptr parents, Ptr pflags, Ptr send, Ptr s)
+          {
+              letSelectMulti(nDest, N, L, np, P<uint8_t>(enabled), P<uint8_t>(failed), P<uint8_t>(outside),
+                             P<int32_t>(leafToNode), P<int32_t>(ns), P<int32_t>(ne), offset, P<void>(mp),
+                             P<int32_t>(parents), P<uint8_t>(pflags), P<uint8_t>(send), St(s));
+          });
+    m.def("flag_words", [](int nRows, int64_t n, Ptr flags, Ptr wcnt, Ptr count, int countStride, Ptr s)
+          { flagWords(nRows, n, P<uint8_t>(flags), P<int64_t>(wcnt), P<int64_t>(count), countStride, St(s)); });
+    m.def("scatter_flag_indices", [](int nRows, int64_t n, Ptr flags, Ptr wpos, Ptr out, Ptr s)
+          { scatterFlagIndices(nRows, n, P<uint8_t>(flags), P<int64_t>(wpos), P<int64_t>(out), St(s)); });
+    m.def("halo_owner_check",
+          [](int64_t nLo, int64_t nHalo, int64_t end, Ptr keys, Ptr bounds, int nBounds, Ptr recvStart, Ptr senders,
+             int nSenders, int self, Ptr bad, Ptr s)
+          {
+              haloOwnerCheck(nLo, nHalo, end, P<uint64_t>(keys), P<uint64_t>(bounds), nBounds, P<int64_t>(recvStart),
+                             P<int32_t>(senders), nSenders, self, P<unsigned long long>(bad), St(s));
+          });
     m.def("leaving_indices", [](int64_t nSend, Ptr perm, int64_t eSelf, int64_t nStay, Ptr out, Ptr s)
           { leavingIndices(nSend, P<int32_t>(perm), eSelf, nStay, P<int64_t>(out), St(s)); });
     m.def("row_bytes", [](const std::vector<int>& sizes) { return rowBytes(sizes); });

@@ -1,0 +1,215 @@
+/*! Halo discovery for every destination rank in one launch per stage (parallel/domain.py _discover_halos).
+ *
+ * Parity: reference traversal/collisions_gpu.cu:39-67 (findHalosKernel) and domain.hpp:246-313 (syncGrav: nodes that
+ * fail the MAC become halos), as push-based selections: each rank marks, for every other rank q, its own particles
+ * inside q's search boxes (hydro) or the nodes q's boxes open (LET, gravity), then compacts the marks into one
+ * concatenated list of send indices in rank order.
+ *
+ * The round-4 code ran three launches and a Python iteration per destination (zero, mark, pack) and a chain of torch
+ * kernels per destination for the compaction; here the destinations are the grid's y dimension:
+ *   markHalosMulti / markLetMulti + letSelectMulti   flags[q][i] (uint8 rows, one per destination)
+ *   flagWords                                          64-flag words: per-word counts + the per-destination totals
+ *   (exclusive scan of the word counts, sample_sort.hip tile scan)
+ *   scatterFlagIndices                                 the index i of every set flag at its word's offset + rank
+ * so a sync with any number of ranks enqueues a fixed number of launches and copies one count table to the host.
+ */
+#include "common.h"
+#include "hip_api.h"
+#include "sphx/box.hpp"
+#include "sphx/gravity.hpp"
+
+namespace sphx::hip
+{
+
+/*! @brief one thread per (query box, destination): walk the own tree and flag the particles inside the box. Boxes
+ *         of destination q are rows [q * nbPer, (q + 1) * nbPer) of (center[3], half[3]) doubles; empty slots have
+ *         half < 0; destinations with enabled[q] == 0 (this rank, pruned peers) are skipped */
+__global__ void markHalosMultiKernel(int nbPer, const double* __restrict__ boxes, const uint8_t* __restrict__ enabled,
+                                     const int32_t* __restrict__ child, const int32_t* __restrict__ n2l,
+                                     const int32_t* __restrict__ ns, const int32_t* __restrict__ ne,
+                                     const double* __restrict__ center, const double* __restrict__ half,
+                                     const double* __restrict__ x, const double* __restrict__ y,
+                                     const double* __restrict__ z, int64_t n, Box box, uint8_t* __restrict__ flags)
+{
+    const int q = blockIdx.y;
+    const int b = int(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (b >= nbPer || !enabled[q]) return;
+    const double* r = boxes + (int64_t(q) * nbPer + b) * 6;
+    const double c[3] = {r[0], r[1], r[2]};
+    const double s[3] = {r[3], r[4], r[5]};
+    if (!(s[0] >= 0.0)) return;
+    uint8_t* f  = flags + int64_t(q) * n;
+    int32_t stack[192];
+    int sp      = 0;
+    stack[sp++] = 0;
+    while (sp > 0)
+    {
+        const int32_t node = stack[--sp];
+        if (!boxesOverlap(c, s, center + 3 * node, half + 3 * node, box)) continue;
+        if (n2l[node] >= 0)
+        {
+            for (int32_t j = ns[node]; j < ne[node]; ++j)
+            {
+                const double p[3] = {x[j], y[j], z[j]};
+                if (pointBoxDistSq(p, c, s, box) <= 0.0) f[j] = 1;
+            }
+        }
+        else
+        {
+            const int32_t co = child[node];
+            for (int k = 7; k >= 0; --k)
+                stack[sp++] = co + k;
+        }
+    }
+}
+
+void markHalosMulti(int nDest, int nbPer, const double* boxes, const uint8_t* enabled, const int32_t* child,
+                    const int32_t* n2l, const int32_t* ns, const int32_t* ne, const double* center, const double* half,
+                    const double* x, const double* y, const double* z, int64_t n, const Box& box, uint8_t* flags,
+                    hipStream_t s)
+{
+    if (nDest == 0 || nbPer == 0) return;
+    markHalosMultiKernel<<<dim3(gridFor(nbPer, 64), nDest), 64, 0, s>>>(nbPer, boxes, enabled, child, n2l, ns, ne,
+                                                                        center, half, x, y, z, n, box, flags);
+    SPHX_LAUNCH_CHECK();
+}
+
+//! @brief LET marking of every destination (gravity.hpp markLetBox): failed[q][node]
+__global__ void markLetMultiKernel(int nbPer, const double* __restrict__ boxes, const uint8_t* __restrict__ enabled,
+                                   const int32_t* __restrict__ child, const int32_t* __restrict__ n2l,
+                                   const double* __restrict__ tc, const double* __restrict__ th,
+                                   const double* __restrict__ gc, int64_t N, Box box, uint8_t* __restrict__ failed)
+{
+    const int q = blockIdx.y;
+    const int b = int(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (b >= nbPer || !enabled[q]) return;
+    const double* r = boxes + (int64_t(q) * nbPer + b) * 6;
+    markLetBox(r, r + 3, child, n2l, tc, th, gc, box, failed + int64_t(q) * N);
+}
+
+void markLetMulti(int nDest, int nbPer, const double* boxes, const uint8_t* enabled, const int32_t* child,
+                  const int32_t* n2l, const double* tc, const double* th, const double* gc, int64_t N, const Box& box,
+                  uint8_t* failed, hipStream_t s)
+{
+    if (nDest == 0 || nbPer == 0) return;
+    markLetMultiKernel<<<dim3(gridFor(nbPer, 64), nDest), 64, 0, s>>>(nbPer, boxes, enabled, child, n2l, tc, th, gc,
+                                                                      N, box, failed);
+    SPHX_LAUNCH_CHECK();
+}
+
+/*! @brief LET selection of every destination (as gravity.hip letSelectKernel): particle flags of the opened leaves
+ *         and the send flags of the first unopened non-empty nodes, rows q of pflags (np) and send (N) */
+__global__ void letSelectMultiKernel(int64_t N, int64_t L, int64_t np, const uint8_t* __restrict__ enabled,
+                                     const uint8_t* __restrict__ failed, const uint8_t* __restrict__ outside,
+                                     const int32_t* __restrict__ leafToNode, const int32_t* __restrict__ ns,
+                                     const int32_t* __restrict__ ne, int64_t offset, const Quadrupole* __restrict__ mp,
+                                     const int32_t* __restrict__ parents, uint8_t* __restrict__ pflags,
+                                     uint8_t* __restrict__ send)
+{
+    const int q       = blockIdx.y;
+    const int64_t i   = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (!enabled[q]) return;
+    const uint8_t* fq = failed + int64_t(q) * N;
+    auto open = [&](int64_t nd) { return (fq[nd] | (outside ? outside[nd] : uint8_t(0))) != 0; };
+    if (i < N)
+    {
+        bool s = !open(i) && mp[i].q[qMass] > MT(0);
+        if (i > 0) s = s && open(parents[(i - 1) >> 3]);
+        send[int64_t(q) * N + i] = uint8_t(s);
+    }
+    if (i < L)
+    {
+        const int32_t nd = leafToNode[i];
+        const uint8_t v  = uint8_t(open(nd));
+        const int64_t k0 = int64_t(ns[nd]) - offset, k1 = int64_t(ne[nd]) - offset;
+        uint8_t* pq      = pflags + int64_t(q) * np;
+        for (int64_t k = k0 > 0 ? k0 : 0; k < k1 && k < np; ++k)
+            pq[k] = v;
+    }
+}
+
+void letSelectMulti(int nDest, int64_t N, int64_t L, int64_t np, const uint8_t* enabled, const uint8_t* failed,
+                    const uint8_t* outside, const int32_t* leafToNode, const int32_t* ns, const int32_t* ne,
+                    int64_t offset, const void* mp, const int32_t* parents, uint8_t* pflags, uint8_t* send,
+                    hipStream_t s)
+{
+    const int64_t n = N > L ? N : L;
+    if (n <= 0 || nDest == 0) return;
+    letSelectMultiKernel<<<dim3(gridFor(n, 256), nDest), 256, 0, s>>>(N, L, np, enabled, failed, outside, leafToNode,
+                                                                      ns, ne, offset,
+                                                                      static_cast<const Quadrupole*>(mp), parents,
+                                                                      pflags, send);
+    SPHX_LAUNCH_CHECK();
+}
+
+/*! @brief words of 64 flags of rows of length n: the set flags per word (int64, row-major [q][w]) and each row's total
+ *         added to count[q * countStride] (one atomic per wave and row) */
+__global__ void flagWordsKernel(int64_t n, int64_t nw, const uint8_t* __restrict__ flags, int64_t* __restrict__ wcnt,
+                                int64_t* __restrict__ count, int countStride)
+{
+    const int q       = blockIdx.y;
+    const int64_t w   = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint8_t* fq = flags + int64_t(q) * n;
+    int c             = 0;
+    if (w < nw)
+    {
+        const int64_t i0 = w * 64;
+        const int64_t i1 = i0 + 64 < n ? i0 + 64 : n;
+        if (i1 - i0 == 64 && (reinterpret_cast<uintptr_t>(fq + i0) & 15) == 0)
+        {
+            const uint4* v = reinterpret_cast<const uint4*>(fq + i0);
+            for (int k = 0; k < 4; ++k)
+            {
+                const uint4 u = v[k];
+                // flags are 0/1 bytes: the byte sum of a word is its popcount of ones
+                c += __popc(u.x) + __popc(u.y) + __popc(u.z) + __popc(u.w);
+            }
+        }
+        else
+        {
+            for (int64_t i = i0; i < i1; ++i)
+                c += fq[i] != 0;
+        }
+        wcnt[int64_t(q) * nw + w] = c;
+    }
+    int t = c;
+    for (int o = 32; o > 0; o >>= 1)
+        t += __shfl_xor(t, o);
+    if ((threadIdx.x & 63) == 0 && t != 0 && count)
+        atomicAdd(reinterpret_cast<unsigned long long*>(count + int64_t(q) * countStride), (unsigned long long)t);
+}
+
+void flagWords(int nRows, int64_t n, const uint8_t* flags, int64_t* wcnt, int64_t* count, int countStride,
+               hipStream_t s)
+{
+    const int64_t nw = (n + 63) / 64;
+    if (nw <= 0 || nRows == 0) return;
+    flagWordsKernel<<<dim3(unsigned((nw + 255) / 256), nRows), 256, 0, s>>>(n, nw, flags, wcnt, count, countStride);
+    SPHX_LAUNCH_CHECK();
+}
+
+/*! @brief out[wpos[q][w] + rank of i within its word] = i for every set flag i of row q (the rows' lists concatenate
+ *         in row order: wpos is the exclusive scan of the word counts over all rows) */
+__global__ void scatterFlagIndicesKernel(int64_t n, int64_t nw, const uint8_t* __restrict__ flags,
+                                         const int64_t* __restrict__ wpos, int64_t* __restrict__ out)
+{
+    const int q       = blockIdx.y;
+    const int64_t w   = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    const uint8_t* fq = flags + int64_t(q) * n;
+    int64_t pos       = wpos[int64_t(q) * nw + w];
+    const int64_t i0  = w * 64;
+    const int64_t i1  = i0 + 64 < n ? i0 + 64 : n;
+    for (int64_t i = i0; i < i1; ++i)
+        if (fq[i]) out[pos++] = i;
+}
+
+void scatterFlagIndices(int nRows, int64_t n, const uint8_t* flags, const int64_t* wpos, int64_t* out, hipStream_t s)
+{
+    const int64_t nw = (n + 63) / 64;
+    if (nw <= 0 || nRows == 0) return;
+    scatterFlagIndicesKernel<<<dim3(unsigned((nw + 255) / 256), nRows), 256, 0, s>>>(n, nw, flags, wpos, out);
+    SPHX_LAUNCH_CHECK();
+}
+
+} // namespace sphx::hip

@@ -59,6 +59,24 @@ void gather(int64_t n, const int32_t* perm, const void* src, void* dst, int elem
 void gatherMerged(int64_t n, const int32_t* pm, int64_t nLo, int64_t nStay, const int32_t* permStay,
                   const std::vector<uintptr_t>& own, const std::vector<uintptr_t>& recv,
                   const std::vector<uintptr_t>& dst, int elemSize, hipStream_t s);
+// halo_discovery.hip: every destination rank in one launch per stage
+void markHalosMulti(int nDest, int nbPer, const double* boxes, const uint8_t* enabled, const int32_t* child,
+                    const int32_t* n2l, const int32_t* ns, const int32_t* ne, const double* center, const double* half,
+                    const double* x, const double* y, const double* z, int64_t n, const Box& box, uint8_t* flags,
+                    hipStream_t s);
+void markLetMulti(int nDest, int nbPer, const double* boxes, const uint8_t* enabled, const int32_t* child,
+                  const int32_t* n2l, const double* tc, const double* th, const double* gc, int64_t N, const Box& box,
+                  uint8_t* failed, hipStream_t s);
+void letSelectMulti(int nDest, int64_t N, int64_t L, int64_t np, const uint8_t* enabled, const uint8_t* failed,
+                    const uint8_t* outside, const int32_t* leafToNode, const int32_t* ns, const int32_t* ne,
+                    int64_t offset, const void* mp, const int32_t* parents, uint8_t* pflags, uint8_t* send,
+                    hipStream_t s);
+void flagWords(int nRows, int64_t n, const uint8_t* flags, int64_t* wcnt, int64_t* count, int countStride,
+               hipStream_t s);
+void scatterFlagIndices(int nRows, int64_t n, const uint8_t* flags, const int64_t* wpos, int64_t* out, hipStream_t s);
+void haloOwnerCheck(int64_t nLo, int64_t nHalo, int64_t end, const uint64_t* keys, const uint64_t* bounds, int nBounds,
+                    const int64_t* recvStart, const int32_t* senders, int nSenders, int self, unsigned long long* bad,
+                    hipStream_t s);
 void leavingIndices(int64_t nSend, const int32_t* perm, int64_t eSelf, int64_t nStay, int64_t* out, hipStream_t s);
 void gatherMulti(int64_t n, const int32_t* perm, const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,
                  int elemSize, hipStream_t s);

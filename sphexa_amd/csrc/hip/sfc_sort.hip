@@ -293,6 +293,52 @@ void leavingIndices(int64_t nSend, const int32_t* perm, int64_t eSelf, int64_t n
     SPHX_LAUNCH_CHECK();
 }
 
+/*! @brief halo ownership check (push-based analog of the reference's checkHalos, halos/halos.hpp:73-105) in one
+ *         launch: halo p of the [lower | upper] halo blocks came from the sender whose receive range holds p
+ *         (recvStart: cumulative receive counts of the other ranks in rank order); its key must lie in that sender's
+ *         SFC range (owner = number of inner assignment bounds <= key) and not in this rank's. Mismatches are counted
+ *         into *bad (one atomic per wave).
+ */
+__global__ void haloOwnerCheckKernel(int64_t nLo, int64_t nHalo, int64_t end, const uint64_t* __restrict__ keys,
+                                     const uint64_t* __restrict__ bounds, int nBounds,
+                                     const int64_t* __restrict__ recvStart, const int32_t* __restrict__ senders,
+                                     int nSenders, int self, unsigned long long* __restrict__ bad)
+{
+    const int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    bool wrong      = false;
+    if (p < nHalo)
+    {
+        const uint64_t k = keys[p < nLo ? p : end + (p - nLo)];
+        int lo = 0, hi = nBounds; // owner: first bound > k (upper_bound)
+        while (lo < hi)
+        {
+            const int mid = (lo + hi) >> 1;
+            if (bounds[mid] <= k) lo = mid + 1;
+            else hi = mid;
+        }
+        int a = 0, b = nSenders; // sender slot: last recvStart <= p
+        while (b - a > 1)
+        {
+            const int mid = (a + b) >> 1;
+            if (recvStart[mid] <= p) a = mid;
+            else b = mid;
+        }
+        wrong = lo != senders[a] || lo == self;
+    }
+    const uint64_t m = __ballot(wrong);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, (unsigned long long)__popcll(m));
+}
+
+void haloOwnerCheck(int64_t nLo, int64_t nHalo, int64_t end, const uint64_t* keys, const uint64_t* bounds, int nBounds,
+                    const int64_t* recvStart, const int32_t* senders, int nSenders, int self, unsigned long long* bad,
+                    hipStream_t s)
+{
+    if (nHalo <= 0) return;
+    haloOwnerCheckKernel<<<gridFor(nHalo, 256), 256, 0, s>>>(nLo, nHalo, end, keys, bounds, nBounds, recvStart,
+                                                             senders, nSenders, self, bad);
+    SPHX_LAUNCH_CHECK();
+}
+
 /*! @brief halo message rows: field k of row r at byte offset off[k] of a row of rowWords 4-byte words (8-byte fields
  *         first, so every field is naturally aligned); one thread per row, all fields of a message in one launch
  */

@@ -167,6 +167,20 @@ class Comm:
             dist.all_gather(outs, src, group=self.group)
             return [_stage_dev(o, t.device) for o in outs] if staged else outs
 
+    def allgather_stacked(self, t: torch.Tensor) -> torch.Tensor:
+        """all-gather of equal-shape tensors into one (size, *shape) tensor: over RCCL straight into the stacked
+        buffer (all_gather_into_tensor), over gloo the list form + one stack"""
+        if self.size == 1:
+            return t.unsqueeze(0)
+        if self.backend == "nccl" and t.is_cuda:
+            src = t.contiguous()
+            out = torch.empty((self.size,) + tuple(src.shape), dtype=src.dtype, device=src.device)
+            with timed_comm("allgather_fixed", src):
+                self._audit("allgather", src)
+                dist.all_gather_into_tensor(out, src, group=self.group)
+            return out
+        return torch.stack(self.allgather_fixed(t))
+
     def alltoallv(self, send: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int] | None = None,
                   ) -> Tuple[torch.Tensor, List[int]]:
         """variable all-to-all along dim 0. ``send`` rows are grouped by destination rank in rank order."""

@@ -440,7 +440,7 @@ class Domain:
         # a fixed-size list of coarse search boxes (empty slots: half < 0): no size exchange, no host copy
         boxes = _coarse_cut(ot, c, hf, self.halo_cut_boxes)
         PROF.mark("halos: search boxes + coarse cut")
-        all_boxes = self.comm.allgather_fixed(boxes)
+        all_boxes = self.comm.allgather_stacked(boxes)
         PROF.mark("halos: allgather boxes")
 
         if gravity:
@@ -468,6 +468,10 @@ class Domain:
         # index lists are compacted at their known sizes (scan + scatter: no further synchronization)
         dev = skeys.device
         n_own = skeys.numel()
+        if skeys.is_cuda:
+            self._discover_halos_gpu(ot, all_boxes, peers, x, y, z, gravity,
+                                     (gcenters, gquads, outside) if gravity else None, n_own)
+            return
         # per destination the flags are kept as bitmasks (size x n_own / 8 bytes instead of a size x n_own byte
         # matrix; one byte row is reused for the marking) together with their counts
         flag_bits = torch.zeros((self.size, _nbytes_bits(n_own)), dtype=torch.uint8, device=dev)
@@ -517,6 +521,85 @@ class Domain:
         self.halo_send_idx = [t + self.n_lo for t in send_idx]
         self._halo_send_cat = None  # concatenated once per sync by exchange_halos
 
+    def _discover_halos_gpu(self, ot, all_boxes, peers, x, y, z, gravity, grav, n_own: int):
+        """the marking and compaction of _discover_halos for every destination at once (csrc/hip/halo_discovery.hip):
+        a fixed number of launches whatever the number of ranks, one host copy (the count table)"""
+        import numpy as np
+
+        from ..ops.reduce import zero_
+
+        hp, st, dev, size = _lib.hip(), _stream(), x.device, self.size
+        boxes = all_boxes if torch.is_tensor(all_boxes) else torch.stack(all_boxes)
+        boxes = boxes.contiguous()
+        nb = boxes.shape[1]
+        en = np.zeros(size, dtype=np.uint8)
+        for q in peers:
+            if q != self.rank:
+                en[q] = 1
+        enabled = self._upload(en, dev)
+        ncnt = 2 if gravity else 1
+        send_dev = zero_(torch.empty((size, ncnt), dtype=torch.int64, device=dev))
+        N = ot.num_nodes
+        nw_p = (n_own + 63) // 64
+        pflags = zero_(torch.empty(size * max(n_own, 1), dtype=torch.uint8, device=dev))
+        if gravity:
+            gcenters, gquads, outside = grav
+            failed = zero_(torch.empty(size * N, dtype=torch.uint8, device=dev))
+            hp.mark_let_multi(size, nb, boxes.data_ptr(), enabled.data_ptr(), ot.child_offsets.data_ptr(),
+                              ot.node_to_leaf.data_ptr(), ot.center.data_ptr(), ot.half.data_ptr(),
+                              gcenters.data_ptr(), N, self.box.to_array(), failed.data_ptr(), st)
+            nflags = zero_(torch.empty(size * N, dtype=torch.uint8, device=dev))
+            hp.let_select_multi(size, N, ot.leaf_to_node.numel(), n_own, enabled.data_ptr(), failed.data_ptr(),
+                                outside.data_ptr(), ot.leaf_to_node.data_ptr(), ot.node_start.data_ptr(),
+                                ot.node_end.data_ptr(), int(ot.offset), gquads.data_ptr(), ot.parents.data_ptr(),
+                                pflags.data_ptr(), nflags.data_ptr(), st)
+            del failed
+        elif n_own:
+            hp.mark_halos_multi(size, nb, boxes.data_ptr(), enabled.data_ptr(), ot.child_offsets.data_ptr(),
+                                ot.node_to_leaf.data_ptr(), ot.node_start.data_ptr(), ot.node_end.data_ptr(),
+                                ot.center.data_ptr(), ot.half.data_ptr(), x.data_ptr(), y.data_ptr(), z.data_ptr(),
+                                n_own, self.box.to_array(), pflags.data_ptr(), st)
+        wcnt_p = torch.empty(size * nw_p, dtype=torch.int64, device=dev)
+        hp.flag_words(size, n_own, pflags.data_ptr(), wcnt_p.data_ptr(), send_dev.data_ptr(), ncnt, st)
+        if gravity:
+            nw_n = (N + 63) // 64
+            wcnt_n = torch.empty(size * nw_n, dtype=torch.int64, device=dev)
+            hp.flag_words(size, N, nflags.data_ptr(), wcnt_n.data_ptr(), send_dev[:, 1:].data_ptr(), ncnt, st)
+        PROF.mark("halos: mark per destination")
+        recv_dev = self.comm.exchange_counts_dev(send_dev)
+        host = torch.cat([send_dev, recv_dev]).cpu()
+        send_h, recv_h = host[: size], host[size:]
+        PROF.mark("halos: count exchange")
+
+        def compact(flags, n, wcnt, col):
+            total = int(send_h[:, col].sum())
+            out = torch.empty(total + 1, dtype=torch.int64, device=dev)
+            if total:
+                pos = sfc_ops.exclusive_scan(wcnt)
+                hp.scatter_flag_indices(size, n, flags.data_ptr(), pos.data_ptr(), out.data_ptr(), st)
+            offs = np.cumsum([0] + [int(v) for v in send_h[:, col]])
+            return out[:total], [out[offs[q]:offs[q + 1]] for q in range(size)]
+
+        cat_p, send_idx = compact(pflags, n_own, wcnt_p, 0)
+        if gravity:
+            _, mp_send = compact(nflags, N, wcnt_n, 1)
+            del nflags
+        del pflags
+        PROF.mark("halos: compact send lists")
+        if gravity:
+            self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes, [int(v) for v in recv_h[:, 1]])
+            PROF.mark("halos: multipole exchange + remote LET tree")
+        self.halo_send_counts = [int(t.numel()) for t in send_idx]
+        self.halo_recv_counts = [int(v) for v in recv_h[:, 0]]
+        self.n_lo = sum(self.halo_recv_counts[: self.rank])
+        self.n_hi = sum(self.halo_recv_counts[self.rank + 1:])
+        self._halo_send_rel = send_idx
+        # absolute indices: one add over the concatenated list; the per-destination lists are views of it
+        cat_abs = cat_p + self.n_lo
+        offs = np.cumsum([0] + self.halo_send_counts)
+        self.halo_send_idx = [cat_abs[offs[q]:offs[q + 1]] for q in range(size)]
+        self._halo_send_cat = cat_abs
+
     def _halo_peers(self, all_boxes, ot) -> set:
         """ranks whose search-box union overlaps this rank's particle bounding box (periodic images included)"""
         if ot.num_nodes == 0:
@@ -550,6 +633,23 @@ class Domain:
         if self.n_lo + self.n_hi == 0:
             return None
         dev = keys.device
+        if keys.is_cuda:
+            # one native launch (sfc_sort.hip haloOwnerCheck); the small tables go up through pinned memory, so the
+            # check enqueues without a host synchronization
+            import numpy as np
+
+            from ..ops.reduce import zero_
+
+            senders = [q for q in range(self.size) if q != self.rank]
+            starts = np.cumsum([0] + [self.halo_recv_counts[q] for q in senders[:-1]]).astype(np.int64)
+            bnd = self._upload(np.array(self.assignment_keys[1:-1], dtype=np.uint64).view(np.int64), dev)
+            rs = self._upload(starts, dev)
+            sd = self._upload(np.array(senders, dtype=np.int32), dev)
+            bad = zero_(torch.empty(1, dtype=torch.int64, device=dev))
+            _lib.hip().halo_owner_check(self.n_lo, self.n_lo + self.n_hi, self.end, keys.data_ptr(), bnd.data_ptr(),
+                                        bnd.numel(), rs.data_ptr(), sd.data_ptr(), len(senders), self.rank,
+                                        bad.data_ptr(), _stream())
+            return bad[0]
         bounds = torch.tensor([k if k < 2 ** 63 else 2 ** 63 - 1 for k in self.assignment_keys[1:-1]],
                               dtype=torch.int64).to(dev, non_blocking=True)
         halo_keys = torch.cat([keys[: self.start], keys[self.end:]])

@@ -118,10 +118,12 @@ def _run(target, world, *args):
     return [out[r] for r in range(world)]
 
 
-def test_two_ranks_one_gpu_ve_step_matches_single_rank():
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_one_gpu_ve_step_matches_single_rank(world):
+    """(4 ranks: every rank has two or three peers, the multi-destination halo discovery of halo_discovery.hip)"""
     n = 14
     ref = _run(_sph_worker, 1, n, 2)[0]
-    res = _run(_sph_worker, 2, n, 2)
+    res = _run(_sph_worker, world, n, 2)
     assert sum(r["n_own"] for r in res) == n ** 3
     assert all(r["halos"] > 0 for r in res)
     assert res[0]["nsum"] == ref["nsum"]
@@ -134,11 +136,12 @@ def test_two_ranks_one_gpu_ve_step_matches_single_rank():
     assert np.allclose(temp[o], ref["temp"][ro], rtol=1e-5)
 
 
-def test_two_ranks_one_gpu_let_gravity_vs_direct():
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_one_gpu_let_gravity_vs_direct(world):
     from test_gravity_mpi import plummer
 
     n = 6000
-    res = _run(_grav_worker, 2, n)
+    res = _run(_grav_worker, world, n)
     X = plummer(n)
     pos = np.concatenate([np.stack([r["x"], r["y"], r["z"]], 1) for r in res])
     acc = np.concatenate([np.stack([r["ax"], r["ay"], r["az"]], 1) for r in res])
