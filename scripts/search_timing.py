@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--init", default="sedov")
     ap.add_argument("-n", type=int, default=400)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--presteps", type=int, default=0, help="time steps run first (converged h, steady-state lists)")
     ap.add_argument("--no-iterate", action="store_true", help="one round, no h iteration (timing variants whose lists "
                     "are unusable would otherwise repeat rounds)")
     args = ap.parse_args()
@@ -25,7 +26,9 @@ def main():
 
     comm = init_distributed("nccl")
     sim = Simulation(args.init, n=args.n, prop="ve", device=torch.device("cuda", 0), comm=comm, out=None, quiet=True)
-    dom, d, prop = sim.domain, sim.d, sim.propagator  # no step: only the search runs (variants may leave lists unusable)
+    for _ in range(args.presteps):
+        sim.step()
+    dom, d, prop = sim.domain, sim.d, sim.propagator  # (variants may leave lists unusable: only the search runs now)
     N.ALLOW_NC_FAIL = True
     ts = []
     for _ in range(args.reps):

@@ -159,6 +159,18 @@ PYBIND11_MODULE(_sphx_hip, m)
           { flagWords(nRows, n, P<uint8_t>(flags), P<int64_t>(wcnt), P<int64_t>(count), countStride, St(s)); });
     m.def("scatter_flag_indices", [](int nRows, int64_t n, Ptr flags, Ptr wpos, Ptr out, Ptr s)
           { scatterFlagIndices(nRows, n, P<uint8_t>(flags), P<int64_t>(wpos), P<int64_t>(out), St(s)); });
+    m.def("range_counts", [](int64_t n, Ptr keys, Ptr bounds, int nRanks, Ptr out, int outStride, Ptr s)
+          { rangeCounts(n, P<uint64_t>(keys), P<uint64_t>(bounds), nRanks, P<int64_t>(out), outStride, St(s)); });
+    m.def("coarse_cut",
+          [](int64_t N, const std::vector<int64_t>& levelRange, int maxDepth, Ptr n2l, Ptr center, Ptr half,
+             int maxBoxes, Ptr out, Ptr s)
+          {
+              if (levelRange.size() != size_t(kMaxLevel + 2)) throw std::invalid_argument("coarse_cut: level range");
+              coarseCut(N, levelRange.data(), maxDepth, P<int32_t>(n2l), P<double>(center), P<double>(half), maxBoxes,
+                        P<double>(out), St(s));
+          });
+    m.def("pack_multipole_rows", [](int64_t n, Ptr idx, Ptr gc, Ptr mp, Ptr prefixes, Ptr rows, Ptr s)
+          { packMultipoleRows(n, P<int64_t>(idx), P<double>(gc), P<void>(mp), P<uint64_t>(prefixes), P<double>(rows), St(s)); });
     m.def("halo_owner_check",
           [](int64_t nLo, int64_t nHalo, int64_t end, Ptr keys, Ptr bounds, int nBounds, Ptr recvStart, Ptr senders,
              int nSenders, int self, Ptr bad, Ptr s)

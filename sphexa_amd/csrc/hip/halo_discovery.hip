@@ -17,6 +17,7 @@
 #include "hip_api.h"
 #include "sphx/box.hpp"
 #include "sphx/gravity.hpp"
+#include "sphx/sfc.hpp"
 
 namespace sphx::hip
 {
@@ -209,6 +210,188 @@ void scatterFlagIndices(int nRows, int64_t n, const uint8_t* flags, const int64_
     const int64_t nw = (n + 63) / 64;
     if (nw <= 0 || nRows == 0) return;
     scatterFlagIndicesKernel<<<dim3(unsigned((nw + 255) / 256), nRows), 256, 0, s>>>(n, nw, flags, wpos, out);
+    SPHX_LAUNCH_CHECK();
+}
+
+/*! @brief the fixed-size list of coarse search boxes of this rank (parallel/domain.py _coarse_cut) in one launch of
+ *         one block: per level, the non-empty nodes and the non-empty leaves; the deepest cut level c whose cut (the
+ *         non-empty nodes at level c + the non-empty leaves above it) fits maxBoxes, as do all shallower cuts; then
+ *         the selected nodes in node order as rows [center | half], empty slots half = -1. Nodes are stored level by
+ *         level (levelRange, host-known), so a node's level needs no lookup.
+ */
+struct LevelRange
+{
+    int64_t r[kMaxLevel + 2];
+};
+
+__global__ __launch_bounds__(1024) void coarseCutKernel(int64_t N, LevelRange lr, int maxDepth,
+                                                        const int32_t* __restrict__ n2l,
+                                                        const double* __restrict__ center,
+                                                        const double* __restrict__ half, int maxBoxes,
+                                                        double* __restrict__ out)
+{
+    constexpr int NL = kMaxLevel + 1;
+    __shared__ int atLevel[NL], leavesAt[NL];
+    __shared__ int best;
+    __shared__ int wsum[16];
+    __shared__ int base;
+    const int t = threadIdx.x;
+    if (t < NL)
+    {
+        atLevel[t]  = 0;
+        leavesAt[t] = 0;
+    }
+    __syncthreads();
+    for (int l = 0; l < NL; ++l)
+    {
+        int cN = 0, cL = 0;
+        for (int64_t i = lr.r[l] + t; i < lr.r[l + 1]; i += blockDim.x)
+        {
+            const bool ne = half[3 * i] >= 0.0;
+            cN += ne;
+            cL += ne && n2l[i] >= 0;
+        }
+        cN = waveSum(cN);
+        cL = waveSum(cL);
+        if ((t & 63) == 0 && (cN || cL))
+        {
+            atomicAdd(&atLevel[l], cN);
+            atomicAdd(&leavesAt[l], cL);
+        }
+    }
+    __syncthreads();
+    if (t == 0)
+    {
+        // sizes[c] = atLevel[c] + leaves above c; deepest c with every cut up to it fitting (the root always fits)
+        int above = 0, b = 0;
+        for (int c = 0; c < min(NL, maxDepth + 2); ++c)
+        {
+            const int size = atLevel[c] + above;
+            if (c > 0 && size > maxBoxes) break;
+            b = c;
+            above += leavesAt[c];
+        }
+        best = b;
+        base = 0;
+    }
+    __syncthreads();
+    const int bl = best;
+    // ordered compaction of the selected nodes (levels 0..best, in node order)
+    for (int64_t i0 = 0; i0 < lr.r[bl + 1]; i0 += blockDim.x)
+    {
+        const int64_t i = i0 + t;
+        bool sel        = false;
+        if (i < lr.r[bl + 1])
+        {
+            const bool ne  = half[3 * i] >= 0.0;
+            const bool atB = i >= lr.r[bl];
+            sel            = ne && (atB || n2l[i] >= 0);
+        }
+        const uint64_t m = ballot(sel);
+        const int w      = t >> 6;
+        if ((t & 63) == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int k = 0; k < w; ++k)
+            off += wsum[k];
+        off += __popcll(m & lanemaskLt());
+        if (sel && off < maxBoxes)
+        {
+            double* r = out + 6 * int64_t(off);
+            r[0]      = center[3 * i];
+            r[1]      = center[3 * i + 1];
+            r[2]      = center[3 * i + 2];
+            r[3]      = half[3 * i];
+            r[4]      = half[3 * i + 1];
+            r[5]      = half[3 * i + 2];
+        }
+        __syncthreads();
+        if (t == 0)
+        {
+            int tot = 0;
+            for (int k = 0; k < int(blockDim.x >> 6); ++k)
+                tot += wsum[k];
+            base += tot;
+        }
+        __syncthreads();
+    }
+    // empty slots
+    for (int k = base + t; k < maxBoxes; k += blockDim.x)
+    {
+        double* r = out + 6 * int64_t(k);
+        r[0] = r[1] = r[2] = 0.0;
+        r[3] = r[4] = r[5] = -1.0;
+    }
+}
+
+void coarseCut(int64_t N, const int64_t* levelRange, int maxDepth, const int32_t* n2l, const double* center,
+               const double* half, int maxBoxes, double* out, hipStream_t s)
+{
+    LevelRange lr;
+    for (int l = 0; l < kMaxLevel + 2; ++l)
+        lr.r[l] = levelRange[l];
+    coarseCutKernel<<<1, 1024, 0, s>>>(N, lr, maxDepth, n2l, center, half, maxBoxes, out);
+    SPHX_LAUNCH_CHECK();
+}
+
+/*! @brief particles per destination of a migration: the sorted local keys cut at the inner assignment bounds
+ *         (lower bounds), out[q] = count of destination q (reference domaindecomp.hpp createSendRanges) */
+__global__ void rangeCountsKernel(int64_t n, const uint64_t* __restrict__ keys, const uint64_t* __restrict__ bounds,
+                                  int nRanks, int64_t* __restrict__ out, int outStride)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nRanks) return;
+    auto lowerBound = [&](uint64_t k)
+    {
+        int64_t lo = 0, hi = n;
+        while (lo < hi)
+        {
+            const int64_t mid = (lo + hi) >> 1;
+            if (keys[mid] < k) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    const int64_t a = q == 0 ? 0 : lowerBound(bounds[q - 1]);
+    const int64_t b = q == nRanks - 1 ? n : lowerBound(bounds[q]);
+    out[int64_t(q) * outStride] = b - a;
+}
+
+void rangeCounts(int64_t n, const uint64_t* keys, const uint64_t* bounds, int nRanks, int64_t* out, int outStride,
+                 hipStream_t s)
+{
+    if (nRanks <= 0) return;
+    rangeCountsKernel<<<(nRanks + 63) / 64, 64, 0, s>>>(n, keys, bounds, nRanks, out, outStride);
+    SPHX_LAUNCH_CHECK();
+}
+
+/*! @brief rows of the LET multipole exchange: (center xyz f64, quadrupole 8 x f32, placeholder code) = 8 x 8 B per
+ *         selected node idx[k] (one launch instead of the torch index/cat kernels of the row assembly) */
+__global__ void packMultipoleRowsKernel(int64_t n, const int64_t* __restrict__ idx, const double* __restrict__ gc,
+                                        const Quadrupole* __restrict__ mp, const uint64_t* __restrict__ prefixes,
+                                        double* __restrict__ rows)
+{
+    const int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int64_t i = idx[k];
+    double* r       = rows + 8 * k;
+    r[0]            = gc[4 * i];
+    r[1]            = gc[4 * i + 1];
+    r[2]            = gc[4 * i + 2];
+    const double* q = reinterpret_cast<const double*>(mp + i);
+    r[3]            = q[0];
+    r[4]            = q[1];
+    r[5]            = q[2];
+    r[6]            = q[3];
+    r[7]            = __longlong_as_double((long long)prefixes[i]);
+}
+
+void packMultipoleRows(int64_t n, const int64_t* idx, const double* gc, const void* mp, const uint64_t* prefixes,
+                       double* rows, hipStream_t s)
+{
+    if (n <= 0) return;
+    packMultipoleRowsKernel<<<gridFor(n, 256), 256, 0, s>>>(n, idx, gc, static_cast<const Quadrupole*>(mp), prefixes,
+                                                            rows);
     SPHX_LAUNCH_CHECK();
 }
 

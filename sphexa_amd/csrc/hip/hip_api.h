@@ -74,6 +74,12 @@ void letSelectMulti(int nDest, int64_t N, int64_t L, int64_t np, const uint8_t* 
 void flagWords(int nRows, int64_t n, const uint8_t* flags, int64_t* wcnt, int64_t* count, int countStride,
                hipStream_t s);
 void scatterFlagIndices(int nRows, int64_t n, const uint8_t* flags, const int64_t* wpos, int64_t* out, hipStream_t s);
+void rangeCounts(int64_t n, const uint64_t* keys, const uint64_t* bounds, int nRanks, int64_t* out, int outStride,
+                 hipStream_t s);
+void coarseCut(int64_t N, const int64_t* levelRange, int maxDepth, const int32_t* n2l, const double* center,
+               const double* half, int maxBoxes, double* out, hipStream_t s);
+void packMultipoleRows(int64_t n, const int64_t* idx, const double* gc, const void* mp, const uint64_t* prefixes,
+                       double* rows, hipStream_t s);
 void haloOwnerCheck(int64_t nLo, int64_t nHalo, int64_t end, const uint64_t* keys, const uint64_t* bounds, int nBounds,
                     const int64_t* recvStart, const int32_t* senders, int nSenders, int self, unsigned long long* bad,
                     hipStream_t s);

@@ -269,7 +269,7 @@ FORCE_ACCEPT_MAC2 = -1.0
 
 
 def remote_let_tree(codes: torch.Tensor, rcenters: torch.Tensor, rquads: torch.Tensor, box: Box, theta: float,
-                    sfc_kind: int = 0):
+                    sfc_kind: int = 0, host_codes: torch.Tensor | None = None):
     """Octree over the remote multipoles received from the other ranks (one leaf per received node, placeholder
     ``codes`` (M) int64, centers (M, 3) f64, quadrupoles (M, 8) f32), upswept so internal nodes carry the combined
     multipoles and vector-MAC radii. Returns (octree, centers N x 4, quadrupoles N x 8) for ``compute_gravity``: a
@@ -283,7 +283,8 @@ def remote_let_tree(codes: torch.Tensor, rcenters: torch.Tensor, rquads: torch.T
     from .octree import build_octree
 
     dev = rcenters.device
-    leaves, leaf_of = _lib.cpu().remote_leaf_array(codes.cpu().numpy().view(np.uint64))
+    hc = host_codes if host_codes is not None else codes.cpu()  # (a copy already made by the caller, pinned)
+    leaves, leaf_of = _lib.cpu().remote_leaf_array(hc.numpy().view(np.uint64))
     tree_h = torch.from_numpy(leaves.view(np.int64).copy())
     L = tree_h.numel() - 1
     nox = torch.empty(0, dtype=torch.float64)

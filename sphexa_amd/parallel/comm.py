@@ -141,19 +141,25 @@ class Comm:
         dist.all_to_all_single(r, s, group=self.group)
         return [int(v) for v in r.cpu().tolist()]
 
-    def exchange_counts_dev(self, counts: torch.Tensor) -> torch.Tensor:
+    def exchange_counts_dev(self, counts: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """all-to-all of the rows of a (size, k) int64 tensor (row q goes to rank q), on the device: no host copy.
-        The caller brings send and receive counts to the host together (one synchronization)."""
+        The caller brings send and receive counts to the host together (one synchronization). ``out``: contiguous
+        destination of the received rows (e.g. the second half of one send|recv buffer)"""
         if self.size == 1:
-            return counts.clone()
+            return counts.clone() if out is None else out.copy_(counts)
         s = counts.contiguous()
         staged = self._staged(s)
         with timed_comm("exchange_counts", s, staged):
             src = _stage_host(s) if staged else s
-            r = torch.empty_like(src)
+            r = torch.empty_like(src) if (staged or out is None) else out
             self._audit("exchange_counts", src, r)
             dist.all_to_all_single(r, src, group=self.group)
-            return _stage_dev(r, counts.device) if staged else r
+            if staged:
+                r = _stage_dev(r, counts.device)
+                if out is not None:
+                    out.copy_(r)
+                    return out
+            return r
 
     def allgather_fixed(self, t: torch.Tensor) -> List[torch.Tensor]:
         """all-gather of equal-shape tensors (no size exchange, no host copy over RCCL)"""

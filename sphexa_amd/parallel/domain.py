@@ -386,12 +386,21 @@ class Domain:
         # send ranges: lower_bound of the boundary keys in the sorted local keys, on the device; send and receive
         # counts come to the host in one copy
         bkeys = self._upload(np.array(keys_b[1:-1], dtype=np.uint64).view(np.int64), dev)
-        pos = torch.searchsorted(skeys, bkeys)
-        edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), pos,
-                           torch.full((1,), skeys.numel(), dtype=torch.int64, device=dev)])
-        send_dev = (edges[1:] - edges[:-1]).view(-1, 1)
-        recv_dev = self.comm.exchange_counts_dev(send_dev)
-        counts = torch.cat([send_dev, recv_dev]).view(-1).cpu().tolist()
+        if skeys.is_cuda:
+            # send counts by one native launch (lower bounds of the boundary keys), received into the second half of
+            # the same buffer: one host copy for both
+            sr = torch.empty((2 * self.size, 1), dtype=torch.int64, device=dev)
+            _lib.hip().range_counts(skeys.numel(), skeys.data_ptr(), bkeys.data_ptr(), self.size, sr.data_ptr(), 1,
+                                    _stream())
+            self.comm.exchange_counts_dev(sr[: self.size], out=sr[self.size:])
+            counts = sr.view(-1).cpu().tolist()
+        else:
+            pos = torch.searchsorted(skeys, bkeys)
+            edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), pos,
+                               torch.full((1,), skeys.numel(), dtype=torch.int64, device=dev)])
+            send_dev = (edges[1:] - edges[:-1]).view(-1, 1)
+            recv_dev = self.comm.exchange_counts_dev(send_dev)
+            counts = torch.cat([send_dev, recv_dev]).view(-1).cpu().tolist()
         send_counts, recv_counts = counts[: self.size], counts[self.size:]
         PROF.mark("distribute: assignment + send/recv counts")
 
@@ -538,7 +547,8 @@ class Domain:
                 en[q] = 1
         enabled = self._upload(en, dev)
         ncnt = 2 if gravity else 1
-        send_dev = zero_(torch.empty((size, ncnt), dtype=torch.int64, device=dev))
+        sr = zero_(torch.empty((2 * size, ncnt), dtype=torch.int64, device=dev))  # send | recv counts
+        send_dev = sr[:size]
         N = ot.num_nodes
         nw_p = (n_own + 63) // 64
         pflags = zero_(torch.empty(size * max(n_own, 1), dtype=torch.uint8, device=dev))
@@ -566,8 +576,8 @@ class Domain:
             wcnt_n = torch.empty(size * nw_n, dtype=torch.int64, device=dev)
             hp.flag_words(size, N, nflags.data_ptr(), wcnt_n.data_ptr(), send_dev[:, 1:].data_ptr(), ncnt, st)
         PROF.mark("halos: mark per destination")
-        recv_dev = self.comm.exchange_counts_dev(send_dev)
-        host = torch.cat([send_dev, recv_dev]).cpu()
+        self.comm.exchange_counts_dev(send_dev, out=sr[size:])
+        host = sr.cpu()
         send_h, recv_h = host[: size], host[size:]
         PROF.mark("halos: count exchange")
 
@@ -582,12 +592,13 @@ class Domain:
 
         cat_p, send_idx = compact(pflags, n_own, wcnt_p, 0)
         if gravity:
-            _, mp_send = compact(nflags, N, wcnt_n, 1)
+            mp_cat, mp_send = compact(nflags, N, wcnt_n, 1)
             del nflags
         del pflags
         PROF.mark("halos: compact send lists")
         if gravity:
-            self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes, [int(v) for v in recv_h[:, 1]])
+            self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes, [int(v) for v in recv_h[:, 1]],
+                                      idx_cat=mp_cat)
             PROF.mark("halos: multipole exchange + remote LET tree")
         self.halo_send_counts = [int(t.numel()) for t in send_idx]
         self.halo_recv_counts = [int(v) for v in recv_h[:, 0]]
@@ -682,25 +693,63 @@ class Domain:
         if vals:
             self._raise_bad_halos(int(vals[0]))
 
-    def _exchange_multipoles(self, mp_send, gcenters, gquads, prefixes, recv_counts=None):
+    def _exchange_multipoles(self, mp_send, gcenters, gquads, prefixes, recv_counts=None, idx_cat=None):
         """one alltoallv of (center xyz f64, quadrupole 8 x f32, placeholder code) rows for the LET far field; the
         received nodes become the leaves of this rank's remote LET tree (ops.gravity.remote_let_tree)"""
         from ..ops import gravity as grav_ops
 
-        idx = torch.cat(mp_send)
-        rows = torch.cat([gcenters.view(-1, 4)[idx, :3], gquads.view(-1, 8)[idx].contiguous().view(torch.float64),
-                          prefixes[idx].view(torch.float64).view(-1, 1)], dim=1)
         counts = [int(t.numel()) for t in mp_send]
+        if gcenters.is_cuda:
+            # (idx_cat: the destinations' lists as one tensor, _discover_halos_gpu) one packing launch
+            idx = idx_cat if idx_cat is not None else torch.cat(mp_send)
+            rows = torch.empty((idx.numel(), 8), dtype=torch.float64, device=gcenters.device)
+            _lib.hip().pack_multipole_rows(idx.numel(), idx.data_ptr(), gcenters.data_ptr(), gquads.data_ptr(),
+                                           prefixes.data_ptr(), rows.data_ptr(), _stream())
+        else:
+            idx = torch.cat(mp_send)
+            rows = torch.cat([gcenters.view(-1, 4)[idx, :3], gquads.view(-1, 8)[idx].contiguous().view(torch.float64),
+                              prefixes[idx].view(torch.float64).view(-1, 1)], dim=1)
         recv, _ = self.comm.alltoallv(rows, counts, recv_counts)
         self.remote_centers = recv[:, :3].contiguous()
         self.remote_quads = recv[:, 3:7].contiguous().view(torch.float32).view(-1, 8)
         self.remote_codes = recv[:, 7].contiguous().view(torch.int64)
         self.stats["remote_multipoles"] = recv.shape[0]
+        self._remote_tree = None
+        self._remote_pending = None
         if recv.shape[0] > 0:
-            self.remote_tree = grav_ops.remote_let_tree(self.remote_codes, self.remote_centers, self.remote_quads,
-                                                        self.box, self.theta, self.sfc_kind)
-        else:
-            self.remote_tree = None
+            if self.remote_codes.is_cuda:
+                # the tree over the received nodes is built on the host from their codes; it is first needed by the
+                # gravity traversal after the SPH loops, so the codes' copy is only started here and collected there
+                # (remote_tree): the host then waits for a copy the GPU finished long before, instead of draining
+                # the stream in the sync
+                host = torch.empty(self.remote_codes.numel(), dtype=torch.int64, pin_memory=True)
+                host.copy_(self.remote_codes, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                self._remote_pending = (host, ev, self.box.copy())
+            else:
+                self._remote_tree = grav_ops.remote_let_tree(self.remote_codes, self.remote_centers,
+                                                             self.remote_quads, self.box, self.theta, self.sfc_kind)
+
+    @property
+    def remote_tree(self):
+        """(octree, centers, quadrupoles) of the received remote multipoles (ops.gravity.remote_let_tree), built on
+        first use from the codes copied to the host during the sync; None without remote multipoles"""
+        p = getattr(self, "_remote_pending", None)
+        if p is not None:
+            from ..ops import gravity as grav_ops
+
+            self._remote_pending = None
+            host, ev, box = p
+            ev.synchronize()
+            self._remote_tree = grav_ops.remote_let_tree(self.remote_codes, self.remote_centers, self.remote_quads,
+                                                         box, self.theta, self.sfc_kind, host_codes=host)
+        return getattr(self, "_remote_tree", None)
+
+    @remote_tree.setter
+    def remote_tree(self, value):
+        self._remote_pending = None
+        self._remote_tree = value
 
     def exchange_halos(self, d, fields: Sequence[str]):
         """fill halo slots of ``fields`` from their owners. One packed all_to_all per call (all fields fused)."""
@@ -777,6 +826,19 @@ def _coarse_cut(ot, center, half, max_boxes: int) -> torch.Tensor:
     """search boxes of a tree cut with at most max_boxes non-empty nodes (the nodes at the cut level + shallower
     leaves; the deepest level whose cut still fits) as a fixed (max_boxes, 6) tensor [center | half], empty slots with
     half = -1. Chosen and compacted on the device: no host copy."""
+    dev = center.device
+    if center.is_cuda:
+        # one single-block launch (csrc/hip/halo_discovery.hip coarseCut)
+        out = torch.empty((max_boxes, 6), dtype=torch.float64, device=dev)
+        _lib.hip().coarse_cut(ot.num_nodes, [int(v) for v in ot.level_range], ot.max_depth(),
+                              ot.node_to_leaf.data_ptr(), center.data_ptr(), half.data_ptr(), max_boxes,
+                              out.data_ptr(), _stream())
+        return out
+    return _coarse_cut_torch(ot, center, half, max_boxes)
+
+
+def _coarse_cut_torch(ot, center, half, max_boxes: int) -> torch.Tensor:
+    """tensor-op form of _coarse_cut (CPU path; the GPU kernel is tested against it)"""
     dev = center.device
     lv = ot.node_levels().long()
     is_leaf = ot.node_to_leaf >= 0
