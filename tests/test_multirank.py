@@ -360,6 +360,17 @@ def test_let_cost_quantified():
         assert r["rm2p"] < r["lm2p"] and r["rp2p"] == 0
 
 
+@pytest.mark.slow
+def test_let_cost_at_8gpu_evrard_share():
+    """the same at Evrard -n 200 (3.7 M particles, 0.46 M per rank: the 8-GPU share of the headline config, verdict r4
+    item 8): gravity halos <= 0.6 x the owned particles (measured 0.55 x, profiles/r5/let_cost_evrard200_8ranks.md)"""
+    res = run_ranks(_let_cost_worker, 8, 200)
+    assert sum(r["n"] for r in res) == 3_706_143
+    for r in res:
+        assert r["sph_halos"] <= r["grav_halos"] <= 0.6 * r["n"], r
+        assert r["rp2p"] == 0 and r["rm2p"] < r["lm2p"]
+
+
 # ------------------------------------------------------------------------ multi-step equivalence per test case
 def _case_worker(rank, world, comm, init, n, steps, prop):
     """``steps`` iterations of a test case (Simulation: propagator step + per-iteration conserved quantities) on
