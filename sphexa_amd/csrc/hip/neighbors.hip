@@ -602,6 +602,37 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
 #endif
                 }
             };
+            // the four appends of a test step in one asm statement: the compiler pads every inline-asm statement
+            // with an s_nop (hazard handling it cannot see into), four per step when each append is its own
+            auto append4 = [&](const uint64_t (&hm)[4], const uint32_t (&code)[4])
+            {
+                if constexpr (kCapped)
+                {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        append(hm[u], code[u]);
+                }
+                else
+                {
+                    uint32_t st;
+                    asm volatile("ds_write_b32 %[wp], %[c0]\n"
+                                 "v_cndmask_b32_e64 %[st], 0, 1, %[m0]\n"
+                                 "v_lshl_add_u32 %[wp], %[st], 8, %[wp]\n"
+                                 "ds_write_b32 %[wp], %[c1]\n"
+                                 "v_cndmask_b32_e64 %[st], 0, 1, %[m1]\n"
+                                 "v_lshl_add_u32 %[wp], %[st], 8, %[wp]\n"
+                                 "ds_write_b32 %[wp], %[c2]\n"
+                                 "v_cndmask_b32_e64 %[st], 0, 1, %[m2]\n"
+                                 "v_lshl_add_u32 %[wp], %[st], 8, %[wp]\n"
+                                 "ds_write_b32 %[wp], %[c3]\n"
+                                 "v_cndmask_b32_e64 %[st], 0, 1, %[m3]\n"
+                                 "v_lshl_add_u32 %[wp], %[st], 8, %[wp]"
+                                 : [wp] "+v"(wp), [st] "=&v"(st)
+                                 : [m0] "s"(hm[0]), [m1] "s"(hm[1]), [m2] "s"(hm[2]), [m3] "s"(hm[3]),
+                                   [c0] "v"(code[0]), [c1] "v"(code[1]), [c2] "v"(code[2]), [c3] "v"(code[3])
+                                 : "memory");
+                }
+            };
             /* Test `count` (a multiple of 4, <= 64) staged candidates against every lane: four candidates (five
              * broadcast ds_read_b128) per step, one ring check per step. A test always starts at a half of the staging
              * ring (sHead is a multiple of 64) and never wraps. Measured alternative (profiles/r3_perf_log.md): per-lane
@@ -644,7 +675,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     for (int u = 0; u < 4; ++u)
                     {
                         hm[u] = ballot(dd[u] < thLoI);
-                        anyBand |= ballot(dd[u] <= thHiI) ^ hm[u]; // (lane masks: SALU only)
+                        anyBand |= ballot(dd[u] <= thHiI) & ~hm[u]; // (lane masks: SALU only; hm is a subset)
                     }
                     if (__builtin_expect(anyBand != 0, 0))
                     {
@@ -652,9 +683,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                         for (int u = 0; u < 4; ++u)
                             if (ballot(dd[u] <= thHiI) != hm[u]) hm[u] = bandRetest(dd[u], code[u], hm[u]);
                     }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        append(hm[u], code[u]);
+                    append4(hm, code);
                     if (ballot(wp >= wFlush)) storeBlock(wp >= laneBase + 8u * 256u, 8);
                 }
                 sHead += count;
