@@ -202,6 +202,8 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("field_max", [](int64_t first, int64_t last, Ptr f, Ptr out, Ptr work, Ptr s)
           { fieldMax(first, last, P<float>(f), P<float>(out), P<void>(work), St(s)); });
     m.def("fill32", [](Ptr p, uint32_t value, int64_t n, Ptr s) { fill32(P<void>(p), value, n, St(s)); });
+    m.def("add3", [](int64_t first, int64_t last, Ptr bx, Ptr by, Ptr bz, Ptr ax, Ptr ay, Ptr az, Ptr s)
+          { add3(first, last, P<float>(bx), P<float>(by), P<float>(bz), P<float>(ax), P<float>(ay), P<float>(az), St(s)); });
     m.def("pack_bits", [](int64_t n, Ptr flags, Ptr bits, Ptr count, Ptr s)
           { packBits(n, P<uint8_t>(flags), P<uint8_t>(bits), P<int64_t>(count), St(s)); });
     m.def("unpack_bits", [](int64_t n, Ptr bits, Ptr flags, Ptr s)

@@ -114,6 +114,8 @@ void timestepReduce(int64_t first, int64_t last, const float* ax, const float* a
 void fieldMax(int64_t first, int64_t last, const float* f, float* out, void* work, hipStream_t s);
 //! n 32-bit words at p set to value (hipMemsetD32Async: e.g. +inf for a min-reduced scalar), stream-ordered
 void fill32(void* p, uint32_t value, int64_t n, hipStream_t s);
+void add3(int64_t first, int64_t last, const float* bx, const float* by, const float* bz, float* ax, float* ay,
+          float* az, hipStream_t s);
 //! 0/1 byte flags -> bitmask (bit k of byte b = flag 8 b + k); *count (int64, may be null) += number of set flags
 void packBits(int64_t n, const uint8_t* flags, uint8_t* bits, int64_t* count, hipStream_t s);
 void unpackBits(int64_t n, const uint8_t* bits, uint8_t* flags, hipStream_t s);

@@ -257,6 +257,27 @@ void memsetAsync(void* p, int value, size_t bytes, hipStream_t s)
     if (bytes > 0) SPHX_CHECK(hipMemsetAsync(p, value, bytes, s));
 }
 
+//! @brief a[i] += b[i] for the three components over [first, last) (gravitational accelerations computed on a
+//!        second stream into their own buffers, added after the momentum loop: models/propagators.py)
+__global__ void add3Kernel(int64_t first, int64_t last, const float* __restrict__ bx, const float* __restrict__ by,
+                           const float* __restrict__ bz, float* __restrict__ ax, float* __restrict__ ay,
+                           float* __restrict__ az)
+{
+    const int64_t i = first + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= last) return;
+    ax[i] += bx[i];
+    ay[i] += by[i];
+    az[i] += bz[i];
+}
+
+void add3(int64_t first, int64_t last, const float* bx, const float* by, const float* bz, float* ax, float* ay,
+          float* az, hipStream_t s)
+{
+    if (last <= first) return;
+    add3Kernel<<<gridFor(last - first, 256), 256, 0, s>>>(first, last, bx, by, bz, ax, ay, az);
+    SPHX_LAUNCH_CHECK();
+}
+
 void fill32(void* p, uint32_t value, int64_t n, hipStream_t s)
 {
     if (n > 0) SPHX_CHECK(hipMemsetD32Async(static_cast<hipDeviceptr_t>(p), int(value), size_t(n), s));

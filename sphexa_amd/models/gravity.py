@@ -33,20 +33,22 @@ class MultipoleHolder:
         self.centers, self.multipoles = G.upsweep(ot, d["x"], d["y"], d["z"], d["m"], domain.box, domain.theta,
                                                   domain.sfc_kind)
 
-    def traverse(self, d, domain):
+    def traverse(self, d, domain, out=None, scratch_key: str = ""):
         """accelerations now; on the GPU the energy and statistics stay on the device until the propagator's time
-        step copies them to the host together with its own inputs (``pending`` / ``finish``)"""
+        step copies them to the host together with its own inputs (``pending`` / ``finish``). ``out``: (ax, ay, az)
+        the gravitational accelerations are added to (default: the particle fields)"""
         self.finish_sync(d)  # a previous step's values, if nobody collected them
         first, last = domain.start_index(), domain.end_index()
         ot = domain.octree
+        ax, ay, az = out if out is not None else (d["ax"], d["ay"], d["az"])
         parts = [G.compute_gravity(ot, self.centers, self.multipoles, first, last, d["x"], d["y"], d["z"], d["h"],
-                                   d["m"], d.g, d["ax"], d["ay"], d["az"], stats=self.stats, defer=True)]
+                                   d["m"], d.g, ax, ay, az, stats=self.stats, defer=True, scratch_key=scratch_key)]
         self._rstats = None
         if domain.size > 1 and getattr(domain, "remote_tree", None) is not None:
             rt, rc, rmp = domain.remote_tree
             self._rstats = {}
             parts.append(G.compute_gravity(rt, rc, rmp, first, last, d["x"], d["y"], d["z"], d["h"], d["m"], d.g,
-                                           d["ax"], d["ay"], d["az"], stats=self._rstats, defer=True))
+                                           ax, ay, az, stats=self._rstats, defer=True, scratch_key=scratch_key))
         self.pending = [p for p in parts if isinstance(p, G.GravityPending)]
         self._host_energy = sum(float(p) for p in parts if not isinstance(p, G.GravityPending))
         if not self.pending:

@@ -20,9 +20,14 @@ from typing import List
 import numpy as np
 import torch
 
+from ..ops import _lib
 from ..ops import hydro as H
 from ..ops.neighbors import find_neighbors
 from ..parallel.comm import MIN
+
+# self-gravity on a second stream, overlapping the SPH loops between the neighbor search and the momentum loop
+# (GPU; Propagator._gravity_start). 0: gravity after the momentum loop on the main stream
+GRAVITY_OVERLAP = os.environ.get("SPHX_GRAV_OVERLAP", "1") == "1"
 from ..utils.timer import Timer
 
 # XMass (STD: density) computed inside the GPU neighbor search instead of a separate pass over the lists. Off by
@@ -103,6 +108,49 @@ class Propagator:
             # the previous step's time-step copy completed before the search statistics did (same stream)
             self.finish_host(d)
         return bool(spec) and self.nl.speculated and H.speculation_holds(d, domain.box, spec[0])
+
+    def _gravity_start(self, domain, d):
+        """GPU: the gravity upsweep and traversal on a second stream, overlapping the SPH loops that follow the
+        neighbor search (they read positions, masses and the smoothing lengths the search settled, and write nothing
+        the SPH loops read); the accelerations go to buffers of their own that _gravity_join adds after the momentum
+        loop. Returns None (gravity runs in _gravity as before) without gravity, on the CPU or with
+        SPHX_GRAV_OVERLAP=0."""
+        if d.g == 0.0 or d.device.type != "cuda" or not GRAVITY_OVERLAP:
+            return None
+        from ..ops.reduce import zero_
+
+        if self.gravity is None:
+            from .gravity import MultipoleHolder
+
+            self.gravity = MultipoleHolder()
+        main = torch.cuda.current_stream(d.device)
+        side = getattr(self, "_side_stream", None)
+        if side is None:
+            side = self._side_stream = torch.cuda.Stream(d.device)
+        n = d.size
+        gacc = zero_(torch.empty(3 * n, dtype=torch.float32, device=d.device))  # (main stream)
+        fork = torch.cuda.Event()
+        fork.record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(fork)
+            self.gravity.upsweep(d, domain)
+            self.timer.step("Upsweep")
+            self.gravity.traverse(d, domain, out=(gacc[:n], gacc[n:2 * n], gacc[2 * n:]), scratch_key="overlap")
+            joined = torch.cuda.Event()
+            joined.record(side)
+        gacc.record_stream(side)
+        for p in self.gravity.pending:
+            p.dev.record_stream(main)  # (read by the time-step packet on the main stream after the join)
+        return gacc, joined
+
+    def _gravity_join(self, domain, d, handle):
+        gacc, joined = handle
+        torch.cuda.current_stream(d.device).wait_event(joined)
+        n = d.size
+        _lib.hip().add3(domain.start_index(), domain.end_index(), gacc[:n].data_ptr(), gacc[n:2 * n].data_ptr(),
+                        gacc[2 * n:].data_ptr(), d["ax"].data_ptr(), d["ay"].data_ptr(), d["az"].data_ptr(),
+                        _lib.stream())
+        self.timer.step("Gravity")
 
     def _gravity(self, domain, d):
         if d.g != 0.0:
@@ -307,6 +355,7 @@ class HydroVeProp(Propagator):
         done = self._neighbors(domain, d, first_loop=first_loops if chain else H.compute_xmass)
         t.step("FindNeighbors")
         nl = self.nl
+        grav = self._gravity_start(domain, d)
 
         if not done:
             H.compute_xmass(d, nl, box)
@@ -350,7 +399,10 @@ class HydroVeProp(Propagator):
         d.acquire("ay", "az")
         H.compute_momentum_energy_ve(d, nl, box, self.av_clean)
         t.step("MomentumAndEnergy")
-        self._gravity(domain, d)
+        if grav is not None:
+            self._gravity_join(domain, d, grav)
+        else:
+            self._gravity(domain, d)
 
     def step(self, domain, d):
         self.compute_forces(domain, d)

@@ -117,7 +117,7 @@ class GravityPending:
 
 
 def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h, m, G: float, ax, ay, az,
-                    ugrav=None, stats: dict | None = None, defer: bool = False):
+                    ugrav=None, stats: dict | None = None, defer: bool = False, scratch_key: str = ""):
     """add G * a_grav to ax, ay, az for targets [first, last); returns this rank's 0.5 * sum G m phi.
     On the GPU ``stats`` (if given) receives p2p/m2p (summed over targets) and max_p2p/max_m2p (per target).
     ``defer`` (GPU): return a GravityPending instead of copying the energy and statistics to the host here."""
@@ -133,7 +133,7 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
         cap_m, cap_l = TEST_CAPS if TEST_CAPS is not None else (_CAPS["m"], _CAPS["l"])
         n = last - first
         groups = (n + 63) // 64
-        scratch = _scratch(hp.gravity_scratch_bytes(n, cap_m, cap_l), x.device)
+        scratch = _scratch(hp.gravity_scratch_bytes(n, cap_m, cap_l), x.device, scratch_key)
         tree_args = (tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
                      tree.node_end.data_ptr(), centers.data_ptr(), mp.data_ptr())
         s = _stream()

@@ -189,12 +189,14 @@ def _check_convergence(d, fails: int):
                                   f"(ng0={d.ng0}, ngmax={d.ngmax}); set SPHX_ALLOW_NC_FAIL=1 to continue anyway")
 
 
-def _scratch(nbytes: int, device) -> torch.Tensor:
-    """grow-only device workspace of the neighbor search spill path (overflow queue + global frontiers)"""
-    t = _SCRATCH.get(device)
+def _scratch(nbytes: int, device, key: str = "") -> torch.Tensor:
+    """grow-only device workspace of the neighbor search spill path (overflow queue + global frontiers), shared with
+    the gravity traversal when both run on one stream; ``key`` names a separate one (gravity overlapping the SPH loops
+    on a second stream)"""
+    t = _SCRATCH.get((device, key))
     if t is None or t.numel() < nbytes:
         t = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        _SCRATCH[device] = t
+        _SCRATCH[(device, key)] = t
     return t
 
 
