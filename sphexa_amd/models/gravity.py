@@ -33,7 +33,17 @@ class MultipoleHolder:
         self.centers, self.multipoles = G.upsweep(ot, d["x"], d["y"], d["z"], d["m"], domain.box, domain.theta,
                                                   domain.sfc_kind)
 
-    def traverse(self, d, domain, out=None, scratch_key: str = ""):
+    def prepare(self, d, domain, scratch_key: str = ""):
+        """GPU: the upsweep and the interaction lists of the local tree (positions and masses only: they may run
+        before the neighbor search has settled h); traverse(prepared=True) evaluates them"""
+        self.upsweep(d, domain)
+        first, last = domain.start_index(), domain.end_index()
+        self._lists = None
+        if last > first:
+            self._lists = G.gravity_lists(domain.octree, self.centers, self.multipoles, first, last, d["x"], d["y"],
+                                          d["z"], stats=self.stats, scratch_key=scratch_key)
+
+    def traverse(self, d, domain, out=None, scratch_key: str = "", prepared: bool = False):
         """accelerations now; on the GPU the energy and statistics stay on the device until the propagator's time
         step copies them to the host together with its own inputs (``pending`` / ``finish``). ``out``: (ax, ay, az)
         the gravitational accelerations are added to (default: the particle fields)"""
@@ -41,8 +51,13 @@ class MultipoleHolder:
         first, last = domain.start_index(), domain.end_index()
         ot = domain.octree
         ax, ay, az = out if out is not None else (d["ax"], d["ay"], d["az"])
-        parts = [G.compute_gravity(ot, self.centers, self.multipoles, first, last, d["x"], d["y"], d["z"], d["h"],
-                                   d["m"], d.g, ax, ay, az, stats=self.stats, defer=True, scratch_key=scratch_key)]
+        if prepared:
+            gl, self._lists = self._lists, None
+            parts = [G.gravity_eval(gl, d["x"], d["y"], d["z"], d["h"], d["m"], d.g, ax, ay, az)] if gl else [0.0]
+        else:
+            parts = [G.compute_gravity(ot, self.centers, self.multipoles, first, last, d["x"], d["y"], d["z"],
+                                       d["h"], d["m"], d.g, ax, ay, az, stats=self.stats, defer=True,
+                                       scratch_key=scratch_key)]
         self._rstats = None
         if domain.size > 1 and getattr(domain, "remote_tree", None) is not None:
             rt, rc, rmp = domain.remote_tree

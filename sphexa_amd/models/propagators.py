@@ -28,6 +28,8 @@ from ..parallel.comm import MIN
 # self-gravity on a second stream, overlapping the SPH loops between the neighbor search and the momentum loop
 # (GPU; Propagator._gravity_start). 0: gravity after the momentum loop on the main stream
 GRAVITY_OVERLAP = os.environ.get("SPHX_GRAV_OVERLAP", "1") == "1"
+# upsweep + interaction lists forked right after the sync (overlapping the neighbor search), evaluation after it
+GRAVITY_PREPARE = os.environ.get("SPHX_GRAV_PREPARE", "1") == "1"
 from ..utils.timer import Timer
 
 # XMass (STD: density) computed inside the GPU neighbor search instead of a separate pass over the lists. Off by
@@ -109,7 +111,29 @@ class Propagator:
             self.finish_host(d)
         return bool(spec) and self.nl.speculated and H.speculation_holds(d, domain.box, spec[0])
 
-    def _gravity_start(self, domain, d):
+    def _gravity_prepare(self, domain, d):
+        """GPU (overlap on): fork the second stream right after the sync: the upsweep and the local interaction lists
+        run while the neighbor search does (they read positions, masses and the tree); _gravity_start then adds the
+        evaluation, which needs the settled smoothing lengths"""
+        if d.g == 0.0 or d.device.type != "cuda" or not GRAVITY_OVERLAP or not GRAVITY_PREPARE:
+            return None
+        if self.gravity is None:
+            from .gravity import MultipoleHolder
+
+            self.gravity = MultipoleHolder()
+        main = torch.cuda.current_stream(d.device)
+        side = getattr(self, "_side_stream", None)
+        if side is None:
+            side = self._side_stream = torch.cuda.Stream(d.device)
+        fork = torch.cuda.Event()
+        fork.record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(fork)
+            self.gravity.prepare(d, domain, scratch_key="overlap")
+        self.timer.step("Upsweep")
+        return True
+
+    def _gravity_start(self, domain, d, prepared=None):
         """GPU: the gravity upsweep and traversal on a second stream, overlapping the SPH loops that follow the
         neighbor search (they read positions, masses and the smoothing lengths the search settled, and write nothing
         the SPH loops read); the accelerations go to buffers of their own that _gravity_join adds after the momentum
@@ -133,9 +157,11 @@ class Propagator:
         fork.record(main)
         with torch.cuda.stream(side):
             side.wait_event(fork)
-            self.gravity.upsweep(d, domain)
-            self.timer.step("Upsweep")
-            self.gravity.traverse(d, domain, out=(gacc[:n], gacc[n:2 * n], gacc[2 * n:]), scratch_key="overlap")
+            if not prepared:
+                self.gravity.upsweep(d, domain)
+                self.timer.step("Upsweep")
+            self.gravity.traverse(d, domain, out=(gacc[:n], gacc[n:2 * n], gacc[2 * n:]), scratch_key="overlap",
+                                  prepared=bool(prepared))
             joined = torch.cuda.Event()
             joined.record(side)
         gacc.record_stream(side)
@@ -332,6 +358,7 @@ class HydroVeProp(Propagator):
         t.start()
         self.sync(domain, d)
         t.step("domain::sync")
+        prep = self._gravity_prepare(domain, d)
         box = domain.box
         first, last = domain.start_index(), domain.end_index()
         # velocity halos are not read before the IAD loop: their exchange overlaps the search, XMass and Gradh
@@ -355,7 +382,7 @@ class HydroVeProp(Propagator):
         done = self._neighbors(domain, d, first_loop=first_loops if chain else H.compute_xmass)
         t.step("FindNeighbors")
         nl = self.nl
-        grav = self._gravity_start(domain, d)
+        grav = self._gravity_start(domain, d, prepared=prep)
 
         if not done:
             H.compute_xmass(d, nl, box)

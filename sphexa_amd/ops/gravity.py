@@ -116,6 +116,62 @@ class GravityPending:
         return energy
 
 
+class GravityLists:
+    """phase 1 of a GPU gravity evaluation (gravity_lists): the interaction lists of every target group in the
+    scratch slabs and the statistics/energy words; gravity_eval runs phase 2 on them. The lists need positions and
+    the tree only, so they may be built before the smoothing lengths are final (models/propagators.py)."""
+
+    def __init__(self, tree, centers, mp, first, last, zb, scratch, caps, stats, device):
+        self.tree, self.centers, self.mp, self.first, self.last = tree, centers, mp, first, last
+        self.zb, self.scratch, self.caps, self.stats, self.device = zb, scratch, caps, stats, device
+
+    def tree_args(self):
+        t = self.tree
+        return (t.child_offsets.data_ptr(), t.node_to_leaf.data_ptr(), t.node_start.data_ptr(),
+                t.node_end.data_ptr(), self.centers.data_ptr(), self.mp.data_ptr())
+
+
+def gravity_lists(tree: Octree, centers, mp, first: int, last: int, x, y, z, stats: dict | None = None,
+                  scratch_key: str = "") -> GravityLists:
+    """GPU phase 1 (interaction lists + per-group P2P particle counts) of compute_gravity"""
+    hp = _lib.hip()
+    # one native fill: statistics (int64) + energy (float64 bits)
+    zb = zero_(torch.empty(GravityPending.NVALS, dtype=torch.int64, device=x.device))
+    from .neighbors import _scratch
+
+    cap_m, cap_l = TEST_CAPS if TEST_CAPS is not None else (_CAPS["m"], _CAPS["l"])
+    n = last - first
+    scratch = _scratch(hp.gravity_scratch_bytes(n, cap_m, cap_l), x.device, scratch_key)
+    gl = GravityLists(tree, centers, mp, first, last, zb, scratch, (cap_m, cap_l), stats, x.device)
+    hp.gravity_lists(first, last, *gl.tree_args(), x.data_ptr(), y.data_ptr(), z.data_ptr(),
+                     zb[:GravityPending.NSTATS].data_ptr(), scratch.data_ptr(), TEST_FRONT_CAP, cap_m, cap_l, _stream())
+    return gl
+
+
+def gravity_eval(gl: GravityLists, x, y, z, h, m, G: float, ax, ay, az, ugrav=None) -> "GravityPending":
+    """GPU phase 2 of compute_gravity on the lists of ``gl``: M2P + P2P, G a added to ax, ay, az"""
+    hp = _lib.hip()
+    first, last, tree = gl.first, gl.last, gl.tree
+    n = last - first
+    cap_m, cap_l = gl.caps
+    zb = gl.zb
+    st_dev, out = zb[:GravityPending.NSTATS], zb[GravityPending.NSTATS:].view(torch.float64)
+    pacc = torch.empty(4 * n, dtype=torch.float32, device=x.device)  # P2P partials (phi, a) per target
+    # the P2P kernel generates its source indices from the opened-leaf lists: no index list, no host wait
+    # P2P source records (fixed point in a frame over the particles' extent, gravity.hip gravityRecordsKernel)
+    from .reduce import min_max
+    nsrc = x.numel()
+    mm = min_max([x, y, z])
+    # records: 16 B per source particle + 40 B per node (M2P), gravity.hip gravityNodeRecordsKernel
+    rec = torch.empty(4 * nsrc + 10 * tree.num_nodes, dtype=torch.int32, device=x.device)
+    hp.gravity_eval(first, last, *gl.tree_args(), x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
+                    m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
+                    0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), st_dev.data_ptr(),
+                    gl.scratch.data_ptr(), cap_m, cap_l, pacc.data_ptr(), nsrc, tree.num_nodes, rec.data_ptr(),
+                    mm.data_ptr(), _stream())
+    return GravityPending(zb, (n + 63) // 64, (cap_m, cap_l), gl.stats, x.device)
+
+
 def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h, m, G: float, ax, ay, az,
                     ugrav=None, stats: dict | None = None, defer: bool = False, scratch_key: str = ""):
     """add G * a_grav to ax, ay, az for targets [first, last); returns this rank's 0.5 * sum G m phi.
@@ -124,36 +180,8 @@ def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h
     if last <= first:
         return 0.0
     if x.is_cuda:
-        hp = _lib.hip()
-        # one native fill: statistics (int64) + energy (float64 bits)
-        zb = zero_(torch.empty(GravityPending.NVALS, dtype=torch.int64, device=x.device))
-        st_dev, out = zb[:GravityPending.NSTATS], zb[GravityPending.NSTATS:].view(torch.float64)
-        from .neighbors import _scratch
-
-        cap_m, cap_l = TEST_CAPS if TEST_CAPS is not None else (_CAPS["m"], _CAPS["l"])
-        n = last - first
-        groups = (n + 63) // 64
-        scratch = _scratch(hp.gravity_scratch_bytes(n, cap_m, cap_l), x.device, scratch_key)
-        tree_args = (tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
-                     tree.node_end.data_ptr(), centers.data_ptr(), mp.data_ptr())
-        s = _stream()
-        # phase 1: interaction lists + per-group P2P particle counts
-        hp.gravity_lists(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), st_dev.data_ptr(),
-                         scratch.data_ptr(), TEST_FRONT_CAP, cap_m, cap_l, s)
-        pacc = torch.empty(4 * n, dtype=torch.float32, device=x.device)  # P2P partials (phi, a) per target
-        # the P2P kernel generates its source indices from the opened-leaf lists: no index list, no host wait
-        # P2P source records (fixed point in a frame over the particles' extent, gravity.hip gravityRecordsKernel)
-        from .reduce import min_max
-        nsrc = x.numel()
-        mm = min_max([x, y, z])
-        # records: 16 B per source particle + 40 B per node (M2P), gravity.hip gravityNodeRecordsKernel
-        rec = torch.empty(4 * nsrc + 10 * tree.num_nodes, dtype=torch.int32, device=x.device)
-        hp.gravity_eval(first, last, *tree_args, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
-                        m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
-                        0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), st_dev.data_ptr(),
-                        scratch.data_ptr(), cap_m, cap_l, pacc.data_ptr(), nsrc, tree.num_nodes, rec.data_ptr(),
-                        mm.data_ptr(), s)
-        pending = GravityPending(zb, groups, (cap_m, cap_l), stats, x.device)
+        gl = gravity_lists(tree, centers, mp, first, last, x, y, z, stats, scratch_key)
+        pending = gravity_eval(gl, x, y, z, h, m, G, ax, ay, az, ugrav)
         return pending if defer else pending.finish(pending.dev.cpu().tolist())
     st = torch.zeros(2, dtype=torch.int64)
     e = float(_lib.cpu().compute_gravity(first, last, tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(),
