@@ -197,6 +197,7 @@ def _run_case(init: str, n: int, args, comm, device) -> dict:
                       f"{d.nc_subbox:.0f} candidates inside the sub-group boxes", file=sys.stderr)
         if hasattr(d, "nc_queued"):
             print(f"# neighbor search paths (last step, of {(d.numParticlesGlobal + 63) // 64} groups): "
+                  f"{getattr(d, 'nc_predicted', 0)} predicted (split kernel on a second stream), "
                   f"{d.nc_queued} queued for the split kernel, {d.nc_split} searched in sub-group passes, "
                   f"{d.nc_spilled} spilled ({d.nc_spill_chunks} of them on the chunk table), "
                   f"{getattr(d, 'nc_shrunk', 0)} halved h on a chunk-table overflow", file=sys.stderr)

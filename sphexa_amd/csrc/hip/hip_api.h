@@ -151,10 +151,22 @@ void markInBoxes(int64_t nb, const double* bc, const double* bh, const int32_t* 
 // touched leaves (opt-in), [6] groups over the chunk-table capacity | groups that recovered from it by halving h << 32,
 // [8 + 32 k] overflow-row stripe counters
 size_t neighborScratchBytes(int64_t n, unsigned ngmax);
+//! overflow prediction of the neighbor search (neighbors.hip PredOut / predMarkKernel); all null: off
+struct SplitPredict
+{
+    const uint64_t* keys = nullptr;              // SFC keys, index = particle index
+    const unsigned long long* predIn = nullptr;  // [count, key pairs] recorded by the previous search
+    unsigned long long* predOut = nullptr;       // this search's record (for the next one)
+    int32_t* flags = nullptr;                    // per-group stamps (>= groups entries)
+    int stamp = 0;
+    int cap = 0;                                 // key pairs per record
+    unsigned long long* listCount = nullptr;     // predicted groups: count + list (>= 3 cap entries)
+    int32_t* list = nullptr;
+};
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int home,
                    int ovStride, int32_t* nc, int iterateH, unsigned long long* stats, void* scratch,
-                   int testFrontCap, const float* m, int64_t ntot, void* rec, hipStream_t s);
+                   int testFrontCap, const float* m, int64_t ntot, void* rec, hipStream_t s, const SplitPredict& sp = SplitPredict{});
 //! fixed-point {x, y, z, m} records (QFrame of the box) of particles [0, n): the search and the XMass loop read them
 void packPosQ(int64_t n, const double* x, const double* y, const double* z, const float* m, const QFrame& q,
               SrcPosQ* out, hipStream_t s);

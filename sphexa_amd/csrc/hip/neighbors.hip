@@ -200,7 +200,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                                             unsigned ngmax, const PackedOut& po, int32_t* __restrict__ nc,
                                             int iterateH, unsigned long long* __restrict__ stats, int32_t* frontA,
                                             int32_t* frontB, int32_t* leaves, int frontCap, int leafCap,
-                                            int32_t* work)
+                                            int32_t* work, bool* ovfMain = nullptr, int mainFront = 0)
 {
     const TreeView t{tree.child, tree.n2l, tree.ns, tree.ne, tree.center, tree.half};
     const Fold fold(box);
@@ -256,8 +256,10 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     // global frontiers otherwise). Only a range of kMinSub lanes that still overflows goes to the spill kernel.
     // range length the round starts with: the previous round's split level (iterateH bit 2, tests: passes of 16)
     // (kSplit = false: the main kernel's single whole-group pass; an overflow queues the group for the split kernel)
-    int len0 = (kSplit && (iterateH & 4)) ? 16 : 64;
+    int len0 = (kSplit && (iterateH & 20)) ? 16 : (kSplit && (iterateH & 8)) ? 32 : 64;
     if (!kSplit && !kSpill && (iterateH & 4)) return false; // (tests: every group through the split kernel)
+    // split kernel: would the main kernel's single pass have overflowed its LDS lists (the group stays predicted)?
+    if (kSplit && ovfMain) *ovfMain = len0 < 64 || (iterateH & 4);
     for (;; ++round)
     {
         fb        = 0;
@@ -375,6 +377,8 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     nn += 8 * __popcll(mi);
                 }
                 waveSync<kSpill>();
+                if constexpr (kSplit)
+                    if (ovfMain && pos == 0 && len == 64 && (nn > mainFront || nLeaves > kLeafCap)) *ovfMain = true;
                 if (nn > fcap || nLeaves > leafCap)
                 {
                     overflow = true;
@@ -891,7 +895,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) SPHX_NS_OCC void findNeighbors
                                                            NsTree t, Box box, unsigned ng0, unsigned ngmax,
                                                            int64_t groups, PackedOut po, int32_t* __restrict__ nc,
                                                            int iterateH, unsigned long long* __restrict__ stats,
-                                                           int32_t* __restrict__ spillList, int frontCap)
+                                                           int32_t* __restrict__ spillList, int frontCap,
+                                                           const int32_t* __restrict__ predFlags, int stamp)
 {
     // (4 KiB aligned: the hit ring at its start is addressed with v_and_or_b32, testOne)
     static_assert(kWorkWords * 4 % 4096 == 0 || kWavesPerBlock == 1, "hit rings of the waves 4 KiB aligned");
@@ -902,6 +907,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) SPHX_NS_OCC void findNeighbors
     const unsigned lb = xcdRemap(blockIdx.x, gridDim.x);
     const int64_t g   = int64_t(lb) * kWavesPerBlock + wave;
     if (g >= groups) return;
+    if (predFlags && predFlags[g] == stamp) return; // predicted overflow: the split kernel searches it concurrently
     bool ok = searchGroup<false, kCapped, false>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po, nc,
                                                  iterateH, stats, work[wave], work[wave] + kFrontCap, leaves[wave],
                                                  frontCap, kLeafCap, work[wave]);
@@ -914,7 +920,69 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) SPHX_NS_OCC void findNeighbors
 
 /*! split path: persistent one-wave blocks take the groups the main kernel queued and search them in sub-group passes
  *  (LDS frontiers, searchGroup<kSplit>); groups that overflow even in passes of kMinSub lanes are queued again for the
- *  spill kernel (stats[7]). Kept out of the main kernel, whose registers and code stay those of the single pass. */
+ *  spill kernel (stats[7]). Kept out of the main kernel, whose registers and code stay those of the single pass.
+ *
+ *  Overflow prediction: the groups that overflow the main kernel's LDS lists are few and spatially persistent (the
+ *  same SFC-key ranges step after step), and one wave per group after the main kernel was a serial tail (Evrard
+ *  -n 100: 0.26 ms of 10 waves after a 0.39-ms main kernel). Every group the split kernel finds that the main kernel
+ *  could not take is recorded by the SFC keys of its first and last particle (PredOut); the next search maps the keys
+ *  back to groups (predMarkKernel), the main kernel skips them and a split-kernel launch on a second stream searches
+ *  them while the main kernel runs. A wrong prediction only moves a group between kernels. */
+struct PredOut
+{
+    const uint64_t* keys;     // SFC keys of the particles (index = particle index)
+    unsigned long long* out;  // [count, (first key, last key) x cap] of the next search's prediction
+    int cap;
+    int mainFront;            // the main kernel's frontier capacity
+};
+
+__device__ __forceinline__ void predRecord(const PredOut& pr, int64_t g, int64_t first, int64_t last)
+{
+    const unsigned long long k = atomicAdd(pr.out, 1ull);
+    if (k < (unsigned long long)pr.cap)
+    {
+        pr.out[1 + 2 * k] = pr.keys[first + g * 64];
+        pr.out[2 + 2 * k] = pr.keys[min(first + g * 64 + 63, last - 1)];
+    }
+}
+
+/*! predicted groups of this search: the groups holding each recorded key range (at most 3), flagged with this search's
+ *  stamp (a group once) and listed for the concurrent split kernel */
+__global__ void predMarkKernel(const uint64_t* __restrict__ keys, int64_t first, int64_t last,
+                               const unsigned long long* __restrict__ predIn, int cap, int32_t* __restrict__ flags,
+                               int stamp, unsigned long long* __restrict__ count, int32_t* __restrict__ list,
+                               unsigned long long* __restrict__ stats)
+{
+    const int64_t groups        = (last - first + 63) / 64;
+    const unsigned long long nk = min(predIn[0], (unsigned long long)cap);
+    for (unsigned long long k = threadIdx.x; k < nk; k += blockDim.x)
+    {
+        const uint64_t ka = predIn[1 + 2 * k], kb = predIn[2 + 2 * k];
+        int64_t lo = first, hi = last;
+        while (lo < hi)
+        {
+            const int64_t mid = (lo + hi) >> 1;
+            if (keys[mid] < ka) lo = mid + 1;
+            else hi = mid;
+        }
+        const int64_t ga = min((lo - first) / 64, groups - 1);
+        lo = first;
+        hi = last;
+        while (lo < hi)
+        {
+            const int64_t mid = (lo + hi) >> 1;
+            if (keys[mid] <= kb) lo = mid + 1;
+            else hi = mid;
+        }
+        const int64_t gb = min(min((max(lo - 1, first) - first) / 64, groups - 1), ga + 2);
+        for (int64_t g = ga; g <= gb; ++g)
+            if (atomicExch(flags + g, stamp) != stamp)
+            {
+                list[atomicAdd(count, 1ull)] = int32_t(g);
+                atomicAdd(&stats[5], 1ull << 32); // (high half) predicted groups
+            }
+    }
+}
 constexpr int kSplitWaves   = 1280; // 5 per CU (LDS: ~27 KiB per wave)
 constexpr int kSplitFront   = 2048; // frontier entries (x2) and candidate leaves of a split-kernel wave: 4x / 4x the
 constexpr int kSplitLeafCap = 1024; // main kernel's, so fewer groups need passes and fewer reach the spill kernel
@@ -930,19 +998,27 @@ __global__ __launch_bounds__(64) SPHX_NS_OCC void findNeighborsSplitKernel(int64
                                                                int32_t* __restrict__ nc, int iterateH,
                                                                unsigned long long* __restrict__ stats,
                                                                const int32_t* __restrict__ splitList,
-                                                               int32_t* __restrict__ spillList, int frontCap)
+                                                               const unsigned long long* __restrict__ splitCount,
+                                                               int32_t* __restrict__ spillList, int frontCap,
+                                                               PredOut pred)
 {
     __shared__ __attribute__((aligned(4096))) int32_t work[kCandWords];
     __shared__ int32_t front[2][kSplitFront];
     __shared__ int32_t leaves[kSplitLeafCap];
-    const int64_t numSplit = int64_t(__hip_atomic_load(&stats[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const int64_t numSplit = int64_t(__hip_atomic_load(splitCount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (int64_t(blockIdx.x) >= numSplit) return;
+    // a few long single-wave groups: issue ahead of the main kernel's waves on a shared SIMD (the predicted groups run
+    // next to the main kernel, and a serial wave there at normal priority took 5x its time alone)
+    __builtin_amdgcn_s_setprio(3);
     for (int64_t k = blockIdx.x; k < numSplit; k += gridDim.x)
     {
         const int64_t g = splitList[k];
-        bool ok = searchGroup<false, kCapped, true>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po,
-                                                    nc, iterateH, stats, front[0], front[1], leaves, frontCap,
-                                                    kSplitLeafCap, work);
+        bool ovf = false;
+        bool ok  = searchGroup<false, kCapped, true>(g, first, last, x, y, z, xq, qf, ntot, h, t, box, ng0, ngmax, po,
+                                                     nc, iterateH, stats, front[0], front[1], leaves, frontCap,
+                                                     kSplitLeafCap, work, pred.out ? &ovf : nullptr, pred.mainFront);
         if (!ok && threadIdx.x == 0) spillList[atomicAdd(&stats[7], 1ull)] = int32_t(g);
+        if (pred.out && (ovf || !ok) && threadIdx.x == 0) predRecord(pred, g, first, last);
     }
 }
 
@@ -1035,10 +1111,37 @@ size_t neighborScratchBytes(int64_t n, unsigned)
     return size_t(total) * sizeof(int32_t);
 }
 
+namespace
+{
+//! second stream of the predicted split kernel (highest priority: its few long groups should start first) + events
+struct SideStream
+{
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+
+SideStream& sideStream()
+{
+    static SideStream side[64];
+    int dev = 0;
+    SPHX_CHECK(hipGetDevice(&dev));
+    SideStream& st = side[dev & 63];
+    if (!st.s)
+    {
+        int lo = 0, hi = 0;
+        SPHX_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        SPHX_CHECK(hipStreamCreateWithPriority(&st.s, hipStreamNonBlocking, hi));
+        SPHX_CHECK(hipEventCreateWithFlags(&st.fork, hipEventDisableTiming));
+        SPHX_CHECK(hipEventCreateWithFlags(&st.join, hipEventDisableTiming));
+    }
+    return st;
+}
+} // namespace
+
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int home,
                    int ovStride, int32_t* nc, int iterateH, unsigned long long* stats, void* scratch,
-                   int testFrontCap, const float* m, int64_t ntot, void* rec, hipStream_t s)
+                   int testFrontCap, const float* m, int64_t ntot, void* rec, hipStream_t s, const SplitPredict& sp)
 {
     int64_t n = last - first;
     if (n <= 0) return;
@@ -1066,18 +1169,40 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
     const QFrame qf     = qframeOf(box);
     SrcPosQ* xq         = static_cast<SrcPosQ*>(rec);
     packPosQ(ntot, x, y, z, m, qf, xq, s);
+    const bool predict = sp.keys && sp.predIn && sp.predOut && sp.flags && sp.list && sp.cap > 0;
+    const PredOut pout{sp.keys, predict ? sp.predOut : nullptr, sp.cap, fc};
+    SideStream* side = predict ? &sideStream() : nullptr;
     auto launch = [&](auto capped)
     {
         constexpr bool kC = decltype(capped)::value;
+        const int fcs = testFrontCap > 0 ? min(testFrontCap, kSplitFront) : kSplitFront;
+        if (predict)
+        {
+            // the predicted groups: listed on this stream, searched on the side stream while the main kernel runs
+            SPHX_CHECK(hipMemsetAsync(sp.predOut, 0, sizeof(unsigned long long), s));
+            SPHX_CHECK(hipMemsetAsync(sp.listCount, 0, sizeof(unsigned long long), s));
+            predMarkKernel<<<1, 256, 0, s>>>(sp.keys, first, last, sp.predIn, sp.cap, sp.flags, sp.stamp,
+                                             sp.listCount, sp.list, stats);
+            SPHX_LAUNCH_CHECK();
+            SPHX_CHECK(hipEventRecord(side->fork, s));
+            SPHX_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
+            findNeighborsSplitKernel<kC><<<kSplitWaves, 64, 0, side->s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h,
+                                                                           t, box, ng0, ngmax, po, nc, iterateH, stats,
+                                                                           sp.list, sp.listCount, spillList, fcs,
+                                                                           pout);
+            SPHX_LAUNCH_CHECK();
+            SPHX_CHECK(hipEventRecord(side->join, side->s));
+        }
         findNeighborsKernel<kC><<<grid, 64 * kWavesPerBlock, 0, s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h, t,
                                                                      box, ng0, ngmax,
-                                                                     groups, po, nc, iterateH, stats, splitList, fc);
+                                                                     groups, po, nc, iterateH, stats, splitList, fc,
+                                                                     predict ? sp.flags : nullptr, sp.stamp);
         SPHX_LAUNCH_CHECK();
-        const int fcs = testFrontCap > 0 ? min(testFrontCap, kSplitFront) : kSplitFront;
         findNeighborsSplitKernel<kC><<<kSplitWaves, 64, 0, s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h, t,
                                                                 box, ng0, ngmax, po, nc, iterateH, stats, splitList,
-                                                                spillList, fcs);
+                                                                stats + 2, spillList, fcs, pout);
         SPHX_LAUNCH_CHECK();
+        if (predict) SPHX_CHECK(hipStreamWaitEvent(s, side->join, 0));
         findNeighborsSpillKernel<kC><<<kSpillWaves, 64, 0, s>>>(first, last, x, y, z, xq, qf, uint32_t(ntot), h, t, box, ng0, ngmax, po, nc,
                                                                 iterateH, stats, spillList, spillMem);
         SPHX_LAUNCH_CHECK();

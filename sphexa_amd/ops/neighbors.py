@@ -173,6 +173,9 @@ TEST_FRONT_CAP = 0
 TEST_FORCE_SPLIT = False
 # collect per-step search statistics on the GPU (rounds, candidate leaves; a few atomics per group)
 COLLECT_STATS = os.environ.get("SPHX_SEARCH_STATS") == "1"
+# first pass length of the split kernel (64: one whole-group pass with the larger LDS frontier; 32 / 16: sub-group
+# passes from the start). Experiment knob.
+SPLIT_LEN = {"64": 0, "32": 8, "16": 16}[os.environ.get("SPHX_SPLIT_LEN", "64")]
 # the reference throws when the coupled nc/h iteration has not converged after 10 rounds
 # (sph/hydro_ve/xmass_gpu.cu:82-92,131): a particle left with more than ngmax neighbors gets its sums over a truncated
 # list. SPHX_ALLOW_NC_FAIL=1 turns the error into a counter (d.nc_fail) for exploratory runs.
@@ -222,6 +225,37 @@ def _stats_index(K: int, device) -> torch.Tensor:
     return t
 
 
+# overflow prediction (neighbors.hip PredOut): the groups the main kernel's LDS lists cannot take are recorded by SFC
+# key range and searched by the split kernel on a second stream while the next search's main kernel runs
+SPLIT_PREDICT = os.environ.get("SPHX_SPLIT_PREDICT", "1") == "1"
+PRED_CAP = 1024  # recorded key ranges per search
+
+
+class _PredState:
+    """per-device prediction buffers: two [count | key pairs] records (read one, write the other), per-group stamps
+    and the predicted-group list"""
+
+    def __init__(self, device):
+        self.rec = [zero_(torch.empty(1 + 2 * PRED_CAP, dtype=torch.int64, device=device)) for _ in range(2)]
+        self.plist = torch.empty(1 + (3 * PRED_CAP + 1) // 2, dtype=torch.int64, device=device)
+        self.flags = None
+        self.stamp = 0
+        self.cur = 0
+
+    def args(self, groups: int, device) -> dict:
+        if self.flags is None or self.flags.numel() < groups:
+            self.flags = zero_(torch.empty(max(groups, 1024) * 5 // 4, dtype=torch.int32, device=device))
+        self.stamp = self.stamp % (2**31 - 2) + 1
+        return dict(pred_in=self.rec[self.cur].data_ptr(), pred_out=self.rec[1 - self.cur].data_ptr(),
+                    flags=self.flags.data_ptr(), stamp=self.stamp, pred_cap=PRED_CAP, plist=self.plist.data_ptr())
+
+    def swap(self):
+        self.cur = 1 - self.cur
+
+
+_PRED: dict = {}
+
+
 def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
                    nidx: torch.Tensor | None = None, prev: NeighborList | None = None,
                    ride_along=None, speculate=None) -> NeighborList:
@@ -264,17 +298,23 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         ride_host = None
         spec_buf = None
         shrunk = 0
+        pred = None
+        if SPLIT_PREDICT and d.is_allocated("keys") and d["keys"].numel() >= last:
+            pred = _PRED.get(x.device)
+            if pred is None:
+                pred = _PRED[x.device] = _PredState(x.device)
         for _attempt in range(2):
+            pkw = dict(keys=d["keys"].data_ptr(), **pred.args(num_groups, x.device)) if pred is not None else {}
             ov = ((buf.numel() - region) // 256 - num_groups * home) // K
             stats = zero_(torch.empty(8 + 32 * K, dtype=torch.int64, device=x.device))
             hp.find_neighbors(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(), tree.num_nodes,
                               tree.child_offsets.data_ptr(), tree.node_to_leaf.data_ptr(), tree.node_start.data_ptr(),
                               tree.node_end.data_ptr(), tree.center.data_ptr(), tree.half.data_ptr(), box.to_array(),
                               d.ng0, ngmax, buf.data_ptr(), nc.data_ptr(),
-                              int(iterate_h) | (2 if COLLECT_STATS else 0) | (4 if TEST_FORCE_SPLIT else 0),
+                              int(iterate_h) | (2 if COLLECT_STATS else 0) | (4 if TEST_FORCE_SPLIT else 0) | SPLIT_LEN,
                               stats.data_ptr(),
                               scratch.data_ptr(), TEST_FRONT_CAP, _stream(), home=home, ov_stride=ov,
-                              m=d["m"].data_ptr(), ntot=d.size, rec=rec.data_ptr())
+                              m=d["m"].data_ptr(), ntot=d.size, rec=rec.data_ptr(), **pkw)
             # per-stripe row demand of the five pool candidates of the next search (one kernel), the stripe
             # counters and the search statistics: one host copy
             # one packet for the host: [stats 0-7 | stripe counters | row demand | ride-along float64 words], written
@@ -318,6 +358,8 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               dtype=torch.int32, device=x.device)
         else:
             raise NeighborSearchError("packed neighbor lists: overflow rows exhausted twice")
+        if pred is not None:
+            pred.swap()
         speculated = spec_buf is not None and spec_buf is buf
         if not speculated:
             # the search packed every particle's SrcPosQ record into workspace 0: the XMass loop reads them as they
@@ -355,7 +397,8 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         # list overflow), groups searched in sub-group passes, groups that went on to the spill kernel (global-memory
         # frontiers) and, of those, the ones whose passes outgrew the chunk table
         d.nc_queued = int(st[2])
-        d.nc_split = int(st[5])
+        d.nc_split = int(st[5]) & 0xFFFFFFFF
+        d.nc_predicted = int(st[5]) >> 32  # groups the split kernel took on the second stream (predicted overflow)
         d.nc_spilled = int(st[7])
         d.nc_spill_chunks = int(st[1]) >> 32
         d.nc_rounds = int(st[3]) / num_groups  # mean search rounds per group (h iteration)

@@ -256,6 +256,40 @@ def test_neighbor_subgroup_passes(gpu, monkeypatch, case):
     assert neighbor_lists_as_sets(nl, dg["nc"]) == sets_ref
 
 
+@pytest.mark.parametrize("case", ["lattice", "glass_evrard"])
+def test_neighbor_split_prediction(gpu, monkeypatch, case):
+    """overflow prediction (neighbors.hip PredOut): the groups the main kernel had to queue are recorded by SFC key
+    range; the next search hands them to the split kernel on a second stream, its main kernel queues fewer groups, and
+    h, counts and neighbor sets stay those of the search without prediction"""
+    from sphexa_amd.app.simulation import Simulation
+    from sphexa_amd.ops import neighbors as N
+
+    if case == "lattice":
+        dg, pg, domg = _setup(gpu, 16, jitter=0.01)
+        pg.sync(domg, dg)
+        tree, box, n = domg.octree, domg.box, dg.size
+    else:
+        sim = Simulation("evrard", n=30, device=gpu)
+        dg, tree, box, n = sim.d, sim.domain.octree, sim.domain.box, sim.d.size
+    monkeypatch.setattr(N, "TEST_FRONT_CAP", 40)  # main-kernel frontier overflows in many groups
+    h0 = dg["h"].clone()
+    monkeypatch.setattr(N, "SPLIT_PREDICT", False)
+    nl_ref = find_neighbors(dg, tree, box, 0, n)
+    nc_ref, h_ref = dg["nc"].clone(), dg["h"].clone()
+    sets_ref = neighbor_lists_as_sets(nl_ref, nc_ref)
+    queued = dg.nc_queued
+    assert queued > 0
+    monkeypatch.setattr(N, "SPLIT_PREDICT", True)
+    N._PRED.clear()
+    for k in range(2):
+        dg["h"].copy_(h0)
+        nl = find_neighbors(dg, tree, box, 0, n)
+        assert torch.equal(dg["nc"], nc_ref) and torch.equal(dg["h"], h_ref)
+        assert neighbor_lists_as_sets(nl, dg["nc"]) == sets_ref
+        # first search: nothing predicted; second: the main kernel skipped the recorded groups
+        assert dg.nc_queued == queued if k == 0 else dg.nc_queued <= queued // 4
+
+
 @pytest.mark.parametrize("hook", ["front", "caps"])
 def test_gravity_spill_path(gpu, monkeypatch, hook):
     """groups overflowing the LDS stack (front) or the interaction-list slabs (caps) are evaluated by the fused
