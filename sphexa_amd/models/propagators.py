@@ -89,7 +89,7 @@ class Propagator:
         pass
 
     # ---------------------------------------------------------------------------------------------- shared
-    def _neighbors(self, domain, d, first_loop=None):
+    def _neighbors(self, domain, d, first_loop=None, after_launch=None):
         """neighbor search + h iteration. ``first_loop(d, nl, box)`` (GPU): the pair loop that follows the search; it
         is enqueued speculatively before the host waits for the search statistics (find_neighbors ``speculate``), so
         the GPU does not idle while the host books the search. Returns True if it ran and holds."""
@@ -104,7 +104,7 @@ class Propagator:
                                  prev=self.nl,  # (not nidx=: an argument would pin the old GPU buffer)
                                  # global h minimum + mass extremes come back with the search statistics
                                  ride_along=(lambda out: H.global_h_min_device(d, domain.comm, out)) if gpu else None,
-                                 speculate=speculate)
+                                 speculate=speculate, after_launch=after_launch)
         if gpu:
             H.apply_global_h_min(d, self.nl.ride_along)
             # the previous step's time-step copy completed before the search statistics did (same stream)
@@ -114,24 +114,27 @@ class Propagator:
     def _gravity_prepare(self, domain, d):
         """GPU (overlap on): fork the second stream right after the sync: the upsweep and the local interaction lists
         run while the neighbor search does (they read positions, masses and the tree); _gravity_start then adds the
-        evaluation, which needs the settled smoothing lengths"""
+        evaluation, which needs the settled smoothing lengths. Returns the launcher of the side-stream work: the
+        search calls it right after enqueueing its kernels, so the ~15 gravity launches' host time does not delay
+        the search (the fork point is recorded here, before the search)"""
         if d.g == 0.0 or d.device.type != "cuda" or not GRAVITY_OVERLAP or not GRAVITY_PREPARE:
             return None
+        fork = torch.cuda.Event()
+        fork.record(torch.cuda.current_stream(d.device))
+        return lambda: self._gravity_prepare_launch(domain, d, fork)
+
+    def _gravity_prepare_launch(self, domain, d, fork):
         if self.gravity is None:
             from .gravity import MultipoleHolder
 
             self.gravity = MultipoleHolder()
-        main = torch.cuda.current_stream(d.device)
         side = getattr(self, "_side_stream", None)
         if side is None:
             side = self._side_stream = torch.cuda.Stream(d.device)
-        fork = torch.cuda.Event()
-        fork.record(main)
         with torch.cuda.stream(side):
             side.wait_event(fork)
             self.gravity.prepare(d, domain, scratch_key="overlap")
-        self.timer.step("Upsweep")
-        return True
+        self._prepared = True
 
     def _gravity_start(self, domain, d, prepared=None):
         """GPU: the gravity upsweep and traversal on a second stream, overlapping the SPH loops that follow the
@@ -359,6 +362,7 @@ class HydroVeProp(Propagator):
         self.sync(domain, d)
         t.step("domain::sync")
         prep = self._gravity_prepare(domain, d)
+        self._prepared = False
         box = domain.box
         first, last = domain.start_index(), domain.end_index()
         # velocity halos are not read before the IAD loop: their exchange overlaps the search, XMass and Gradh
@@ -379,10 +383,12 @@ class HydroVeProp(Propagator):
             gradh(d, nl, box)
             H.compute_eos_ve(d, first, last)
 
-        done = self._neighbors(domain, d, first_loop=first_loops if chain else H.compute_xmass)
+        done = self._neighbors(domain, d, first_loop=first_loops if chain else H.compute_xmass, after_launch=prep)
         t.step("FindNeighbors")
         nl = self.nl
-        grav = self._gravity_start(domain, d, prepared=prep)
+        if prep is not None and not self._prepared:  # (a search path that did not call it)
+            prep()
+        grav = self._gravity_start(domain, d, prepared=prep is not None)
 
         if not done:
             H.compute_xmass(d, nl, box)

@@ -258,7 +258,7 @@ _PRED: dict = {}
 
 def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: bool = True,
                    nidx: torch.Tensor | None = None, prev: NeighborList | None = None,
-                   ride_along=None, speculate=None) -> NeighborList:
+                   ride_along=None, speculate=None, after_launch=None) -> NeighborList:
     """search neighbors of particles [first, last) within 2h, adjusting h towards ng0 neighbors.
 
     ``prev``: the previous step's lists; on the GPU its buffer is reused when it has the right size.
@@ -267,6 +267,8 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
     ``speculate`` (GPU): called with the provisional lists after the statistics copy is enqueued and before the host
     waits for it, to enqueue work that needs the lists (the first pair loop) while the host waits and books; the
     returned lists carry ``speculated`` = False if the search had to be repeated (the work must then be redone).
+    ``after_launch`` (GPU): called once right after the search kernels are enqueued (work for other streams whose host
+    time should overlap the search, models/propagators.py _gravity_prepare).
     """
     x, y, z, h, nc = d["x"], d["y"], d["z"], d["h"], d["nc"]
     n = last - first
@@ -315,6 +317,8 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               stats.data_ptr(),
                               scratch.data_ptr(), TEST_FRONT_CAP, _stream(), home=home, ov_stride=ov,
                               m=d["m"].data_ptr(), ntot=d.size, rec=rec.data_ptr(), **pkw)
+            if after_launch is not None and _attempt == 0:
+                after_launch()
             # per-stripe row demand of the five pool candidates of the next search (one kernel), the stripe
             # counters and the search statistics: one host copy
             # one packet for the host: [stats 0-7 | stripe counters | row demand | ride-along float64 words], written

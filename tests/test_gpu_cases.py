@@ -187,11 +187,11 @@ def test_speculative_xmass(gpu, small_glass):
     held = []
     orig = PR.Propagator._neighbors
 
-    def no_spec(self, domain, d, first_loop=None):
-        return orig(self, domain, d)
+    def no_spec(self, domain, d, first_loop=None, after_launch=None):
+        return orig(self, domain, d, after_launch=after_launch)
 
-    def watch(self, domain, d, first_loop=None):
-        r = orig(self, domain, d, first_loop)
+    def watch(self, domain, d, first_loop=None, after_launch=None):
+        r = orig(self, domain, d, first_loop, after_launch)
         held.append(r)
         return r
 
@@ -223,8 +223,8 @@ def test_speculation_rejected_redoes_chain(gpu, small_glass):
     spc = Simulation("evrard", n=32, prop="ve", device=gpu)
     orig, holds = PR.Propagator._neighbors, H.speculation_holds
 
-    def no_spec(self, domain, d, first_loop=None):
-        return orig(self, domain, d)
+    def no_spec(self, domain, d, first_loop=None, after_launch=None):
+        return orig(self, domain, d, after_launch=after_launch)
 
     try:
         for _ in range(3):
