@@ -15,7 +15,7 @@ def main():
     rx = re.compile(sys.argv[3]) if len(sys.argv) > 3 else None
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                  r["Kernel_Name"].split("(")[0].replace("void ", "").replace("sphx::hip::", "")[:60]) for r in rows)
-    starts = [s for s, e, n in ev if "computeKeysKernel" in n]
+    starts = [s for s, e, n in ev if "computeKeys" in n]
     t0, t1 = starts[step], starts[step + 1] if step + 1 < len(starts) and step != -1 else ev[-1][1] + 1
     cur = t0
     for s, e, n in ev:

@@ -107,6 +107,12 @@ PYBIND11_MODULE(_sphx_hip, m)
     // ---------------------------------------------------------------------------------------------- sfc / sort
     m.def("compute_keys", [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, int kind, Ptr keys, Ptr s)
           { computeKeys(n, P<double>(x), P<double>(y), P<double>(z), toBox(box), kind, P<KeyT>(keys), St(s)); });
+    m.def("compute_keys_devbox",
+          [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, Ptr ext, int kind, Ptr keys, Ptr s)
+          {
+              computeKeysDevBox(n, P<double>(x), P<double>(y), P<double>(z), toBox(box), P<double>(ext), kind,
+                                P<KeyT>(keys), St(s));
+          });
     m.def("sort_temp_bytes", [](int64_t n) { return sortPairsTempBytes(n); });
     m.def("sort_pairs_temp_bytes", [](int64_t n) { return sortPairsTempBytes(n); });
     m.def("sort_keys", [](int64_t n, Ptr kin, Ptr kout, Ptr perm, Ptr tmp, size_t tmpBytes, Ptr s)

@@ -45,6 +45,8 @@ struct PosArgs
 // sfc_sort.hip
 void computeKeys(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind, KeyT* keys,
                  hipStream_t s);
+void computeKeysDevBox(int64_t n, const double* x, const double* y, const double* z, const Box& box, const double* ext,
+                       int kind, KeyT* keys, hipStream_t s);
 size_t sortPairsTempBytes(int64_t n);
 void sortPairs(int64_t n, const KeyT* keysIn, KeyT* keysOut, const int32_t* valsIn, int32_t* valsOut, void* tmp,
                size_t tmpBytes, int beginBit, int endBit, hipStream_t s);

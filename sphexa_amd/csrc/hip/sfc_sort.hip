@@ -31,6 +31,32 @@ void computeKeys(int64_t n, const double* x, const double* y, const double* z, c
     SPHX_LAUNCH_CHECK();
 }
 
+/*! keys in a box whose open dimensions come from a device reduction ([min x, max x, min y, ...], the previous step's
+ *  prefetched extents): the host need not wait for the extents before the sort (parallel/domain.py sync). The
+ *  extents are used as Domain.update_box sets them (hi <= lo -> lo + 1e-10), so the keys are those of the host box. */
+__global__ void computeKeysDevBoxKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                                        const double* __restrict__ z, Box box, const double* __restrict__ ext, int kind,
+                                        KeyT* __restrict__ keys)
+{
+    for (int d = 0; d < 3; ++d)
+        if (box.bc[d] != kPeriodic)
+        {
+            const double lo = ext[2 * d], hi = ext[2 * d + 1];
+            box.lo[d]       = lo;
+            box.hi[d]       = hi <= lo ? lo + 1e-10 : hi;
+        }
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) keys[i] = particleKey(kind, x[i], y[i], z[i], box);
+}
+
+void computeKeysDevBox(int64_t n, const double* x, const double* y, const double* z, const Box& box, const double* ext,
+                       int kind, KeyT* keys, hipStream_t s)
+{
+    if (n == 0) return;
+    computeKeysDevBoxKernel<<<gridFor(n, 256), 256, 0, s>>>(n, x, y, z, box, ext, kind, keys);
+    SPHX_LAUNCH_CHECK();
+}
+
 __global__ void iotaKernel(int64_t n, int32_t* out)
 {
     int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;

@@ -35,6 +35,8 @@ MI355X-native design:
 
 from __future__ import annotations
 
+import os
+
 import math
 from typing import Dict, List, Optional, Sequence
 
@@ -69,6 +71,8 @@ def default_bucket_size_focus(gravity: bool, nranks: int = 1) -> int:
         return BUCKET_SIZE_FOCUS
     return BUCKET_SIZE_FOCUS_GRAVITY_1RANK if gravity else BUCKET_SIZE_FOCUS_HYDRO
 REORDER_BATCH = 3  # conserved fields reordered per gather launch in sync (bounds the transient memory)
+# one rank, GPU: SFC keys from the prefetched device extents, host box taken at the end of the sync
+DEVICE_BOX = os.environ.get("SPHX_DEVICE_BOX", "1") == "1"
 REORDER_ALL_BYTES = 1 << 30  # below this transient size all remaining fields are reordered together
 
 
@@ -141,19 +145,13 @@ class Domain:
         """recompute extents of non-periodic dimensions from the owned particles (global MIN/MAX allreduce)"""
         if all(b == PERIODIC for b in self.box.bc):
             return
-        pf, self._box_prefetch = getattr(self, "_box_prefetch", None), None
-        if pf is not None and pf[0] == self._box_key(x, y, z):
+        pf = self._take_box_prefetch(x, y, z)
+        if pf is not None:
             pf[2].synchronize()
             ext = self._box_ext(pf[1].tolist())
         else:
             ext = self._box_ext(self._box_reduce(x, y, z).cpu().tolist())
-        for d in range(3):
-            if self.box.bc[d] != PERIODIC:
-                lo, hi = ext[d], -ext[3 + d]
-                if hi <= lo:
-                    hi = lo + 1e-10
-                self.box.lo[d] = lo
-                self.box.hi[d] = hi
+        self._apply_box_ext(ext)
 
     def _box_key(self, x, y, z):
         # native kernels write through data_ptr without bumping _version: the sync counter ties a prefetch to the
@@ -195,7 +193,23 @@ class Domain:
         host.copy_(dev, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self._box_prefetch = (self._box_key(x, y, z), host, ev)
+        self._box_prefetch = (self._box_key(x, y, z), host, ev, dev)
+
+    def _take_box_prefetch(self, x, y, z):
+        """the valid prefetched extents (host copy, its event, device tensor) or None; consumes the prefetch"""
+        pf, self._box_prefetch = getattr(self, "_box_prefetch", None), None
+        if pf is not None and pf[0] == self._box_key(x, y, z):
+            return pf
+        return None
+
+    def _apply_box_ext(self, ext):
+        for d in range(3):
+            if self.box.bc[d] != PERIODIC:
+                lo, hi = ext[d], -ext[3 + d]
+                if hi <= lo:
+                    hi = lo + 1e-10
+                self.box.lo[d] = lo
+                self.box.hi[d] = hi
 
     # --------------------------------------------------------------------------------------------- the sync
     def sync(self, d, conserved: Sequence[str], dependent: Sequence[str] = (), gravity: bool = False):
@@ -212,9 +226,19 @@ class Domain:
         own = {f: d[f][s:e] for f in conserved}
         x, y, z = own["x"], own["y"], own["z"]
 
-        self.update_box(x, y, z)
-        PROF.mark("sync: box")
-        keys = sfc_ops.compute_keys(x, y, z, self.box, self.sfc_kind)
+        # one rank with the extents prefetched at the end of the previous step: the keys read them on the device and
+        # the host takes them only after the sort, gathers and octree are enqueued (nothing before needs the host
+        # box), so it waits for the previous step's GPU work with this sync's kernels queued behind it instead of
+        # launching them one by one into an idle GPU
+        pf = None
+        if DEVICE_BOX and self.size == 1 and not all(b == PERIODIC for b in self.box.bc):
+            pf = self._take_box_prefetch(x, y, z)
+        if pf is not None:
+            keys = sfc_ops.compute_keys_devbox(x, y, z, self.box, pf[3], self.sfc_kind)
+        else:
+            self.update_box(x, y, z)
+            PROF.mark("sync: box")
+            keys = sfc_ops.compute_keys(x, y, z, self.box, self.sfc_kind)
         PROF.mark("sync: keys")
 
         if self.size > 1:
@@ -309,6 +333,9 @@ class Domain:
         self.local_tree, counts = st.update(all_keys, self.bucket_size_focus)
         self.octree = st.build(self.local_tree, counts, all_keys, d["x"], d["y"], d["z"], 0)
         PROF.mark("sync: local octree")
+        if pf is not None:
+            pf[2].synchronize()
+            self._apply_box_ext(self._box_ext(pf[1].tolist()))
         self.stats["local_leaves"] = self.octree.num_leaves
         self.stats["halos"] = total - n_own
         self.sync_count += 1

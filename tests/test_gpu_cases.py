@@ -261,3 +261,22 @@ def test_gravity_overlap_matches_sequential(gpu, small_glass, monkeypatch):
     for k in a:
         assert torch.allclose(a[k], b[k], rtol=1e-5, atol=1e-6 * float(a[k].abs().max())), k
     assert dta == pytest.approx(dtb, rel=1e-6) and ea == pytest.approx(eb, rel=1e-6)
+
+
+def test_device_box_keys_match_host_box(gpu, monkeypatch):
+    """one rank: the sync's SFC keys from the prefetched device extents (parallel/domain.py DEVICE_BOX, host box taken
+    at the end of the sync) are the keys of the host box: the same steps bit for bit"""
+    from sphexa_amd.parallel import domain as Dm
+
+    out = {}
+    for dev_box in (False, True):
+        monkeypatch.setattr(Dm, "DEVICE_BOX", dev_box)
+        sim = Simulation("evrard", n=24, device=gpu)
+        sim.run(3)
+        torch.cuda.synchronize()
+        out[dev_box] = ({f: sim.d[f].clone() for f in ("keys", "x", "h", "vx")}, list(sim.domain.box.lo),
+                        list(sim.domain.box.hi))
+    (a, alo, ahi), (b, blo, bhi) = out[False], out[True]
+    assert alo == blo and ahi == bhi
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
