@@ -110,6 +110,8 @@ struct KernelFn
         s     = v > HT(0) ? sn * ix : HT(1);
         ds    = v > HT(0) ? halfPi * (cs - s) * ix : HT(0);
     }
+    //! s^n: integer exponents up to 15 (the kernel's n = 6 and the derivative's n - 1 = 5) by multiplication (n is
+    //! uniform: scalar branches), others through exp2/log2 (two quarter-rate transcendentals and range handling)
     SPHX_HD static HT powN(HT s, HT n)
     {
         if (n == HT(6))
@@ -117,6 +119,20 @@ struct KernelFn
             HT s3 = s * s * s;
             return s3 * s3;
         }
+#ifndef SPHX_POW_EXP2 // (A/B variant: every exponent but 6 through exp2/log2)
+        const int k = int(n);
+        if (HT(k) == n && k >= 1 && k <= 15)
+        {
+            HT r = (k & 1) ? s : HT(1);
+            HT p = s * s;
+            if (k & 2) r *= p;
+            p *= p;
+            if (k & 4) r *= p;
+            p *= p;
+            if (k & 8) r *= p;
+            return r;
+        }
+#endif
         return s > HT(0) ? exp2(n * log2(s)) : HT(0);
     }
     SPHX_HD HT w(HT v) const
