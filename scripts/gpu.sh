@@ -26,7 +26,7 @@ bench)
 busy)
     timeout -k 10 ${BENCH_TIMEOUT:-600} rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o run -- \
         python3 bench.py "$@" > "$O/kt.log" 2>&1 || { tail -20 "$O/kt.log"; exit 1; }
-    python3 scripts/gpu_busy.py "$O/kt/run_kernel_trace.csv" ${BUSY_STEPS:-3} > "$O/busy.txt" && head -40 "$O/busy.txt" ;;
+    python3 scripts/gpu_busy.py "$O/kt/run_kernel_trace.csv" ${BUSY_STEPS:-3} computeKeys > "$O/busy.txt" && head -40 "$O/busy.txt" ;;
 pmc)
     # PROG overrides the profiled program (default bench.py), e.g. PROG="python3 scripts/grav_micro.py"
     RX=$1; CTR=$2; shift 2
