@@ -527,19 +527,21 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("gravity_eval",
           [](int64_t first, int64_t last, Ptr child, Ptr n2l, Ptr ns, Ptr ne, Ptr centers, Ptr mp, Ptr x, Ptr y,
              Ptr z, Ptr h, Ptr mm, double G, Ptr ax, Ptr ay, Ptr az, Ptr ugrav, Ptr out, Ptr stats, Ptr scratch,
-             int capM, int capL, Ptr pacc, int64_t nsrc, int64_t numNodes, Ptr rec, Ptr minmax, Ptr s)
+             int capM, int capL, Ptr pacc, int64_t nsrc, int64_t numNodes, Ptr rec, Ptr minmax, Ptr s, int phase)
           {
               computeGravityEval(first, last, P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne),
                                  P<double>(centers), P<void>(mp), P<double>(x), P<double>(y), P<double>(z),
                                  P<float>(h), P<float>(mm), float(G), P<float>(ax), P<float>(ay), P<float>(az),
                                  P<double>(ugrav), P<double>(out), P<unsigned long long>(stats), P<void>(scratch),
-                                 capM, capL, P<void>(pacc), nsrc, numNodes, P<void>(rec), P<double>(minmax), St(s));
+                                 capM, capL, P<void>(pacc), nsrc, numNodes, P<void>(rec), P<double>(minmax), St(s),
+                                 phase);
           },
           py::arg("first"), py::arg("last"), py::arg("child"), py::arg("n2l"), py::arg("ns"), py::arg("ne"),
           py::arg("centers"), py::arg("mp"), py::arg("x"), py::arg("y"), py::arg("z"), py::arg("h"), py::arg("m"),
           py::arg("G"), py::arg("ax"), py::arg("ay"), py::arg("az"), py::arg("ugrav"), py::arg("out"),
           py::arg("stats"), py::arg("scratch"), py::arg("capM"), py::arg("capL"), py::arg("pacc"),
-          py::arg("nsrc"), py::arg("num_nodes"), py::arg("rec"), py::arg("mm"), py::arg("stream"));
+          py::arg("nsrc"), py::arg("num_nodes"), py::arg("rec"), py::arg("mm"), py::arg("stream"),
+          py::arg("phase") = 0);
     m.def("gravity_scratch_bytes", [](int64_t n, int capM, int capL) { return gravityScratchBytes(n, capM, capL); });
     m.def("device_checks_enabled", &deviceChecksEnabled);
     m.def("device_check_flags", []() { return dcheckHydro() | dcheckSfc() | dcheckGravity(); },

@@ -1877,22 +1877,31 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
                         const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
                         double* ugrav, double* out, unsigned long long* stats, void* scratch, int capM, int capL,
                         void* paccBuf, int64_t nsrc, int64_t numNodes, void* recBuf, const double* mm,
-                        hipStream_t s)
+                        hipStream_t s, int phase)
 {
     float4* pacc = static_cast<float4*>(paccBuf);
     int4* rec    = static_cast<int4*>(recBuf);
     int64_t n = last - first;
     if (n <= 0) return;
+    // phase 0: everything; split evaluation (models/propagators.py): 1 = node records + M2P (no smoothing lengths:
+    // it may run beside the neighbor search), 2 = particle records + P2P, 3 = P2P combine + spill groups (after 1, 2)
+    const bool all = phase == 0;
     // P2P source records of all particles of the tree and M2P node records (frame: mm = [min, max] per dimension,
     // on the device); the node records follow the particle records in the same buffer
-    gravityRecordsKernel<<<gridFor(nsrc, 256), 256, 0, s>>>(nsrc, x, y, z, h, mm, rec);
-    SPHX_LAUNCH_CHECK();
+    if (all || phase == 2)
+    {
+        gravityRecordsKernel<<<gridFor(nsrc, 256), 256, 0, s>>>(nsrc, x, y, z, h, mm, rec);
+        SPHX_LAUNCH_CHECK();
+    }
     float4* nra = reinterpret_cast<float4*>(rec + nsrc);
     float4* nrb = nra + numNodes;
     float2* nrc = reinterpret_cast<float2*>(nrb + numNodes);
-    gravityNodeRecordsKernel<<<gridFor(numNodes, 256), 256, 0, s>>>(numNodes, centers, (const Quadrupole*)mp, mm, nra,
-                                                                   nrb, nrc);
-    SPHX_LAUNCH_CHECK();
+    if (all || phase == 1)
+    {
+        gravityNodeRecordsKernel<<<gridFor(numNodes, 256), 256, 0, s>>>(numNodes, centers, (const Quadrupole*)mp, mm,
+                                                                       nra, nrb, nrc);
+        SPHX_LAUNCH_CHECK();
+    }
     const NodeRecs nrec{nra, nrb, nrc};
     GravTree t{child, n2l, ns, ne, centers, (const Quadrupole*)mp};
     int64_t groups = (n + 63) / 64;
@@ -1911,6 +1920,7 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
 #else
     const int32_t* orderM = nullptr;
 #endif
+    if (all || phase == 2)
     {
         SPHX_CHECK(hipMemsetAsync(c.hist, 0, 4 * kOrdBins * sizeof(int32_t), s));
         const unsigned og = unsigned(std::min<int64_t>((groups + 255) / 256, 1024));
@@ -1950,21 +1960,33 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
     if (!sideStream) SPHX_CHECK(hipStreamCreateWithFlags(&sideStream, hipStreamNonBlocking));
     side = sideStream;
 #endif
-    SPHX_CHECK(hipEventRecord(fork, s));
-    SPHX_CHECK(hipStreamWaitEvent(side, fork, 0));
-    gravityP2PKernel<<<gridP, 64 * kGWaves, 0, side>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
-                                                      stats, c.S, pacc, rec, mm, orderP, slotsP);
-    SPHX_LAUNCH_CHECK();
-    SPHX_CHECK(hipEventRecord(join, side));
-    gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
-                                                   c.S, orderM, groups, nrec, mm);
-    SPHX_LAUNCH_CHECK();
-    SPHX_CHECK(hipStreamWaitEvent(s, join, 0));
-    gravityCombineKernel<<<gridFor(n, 256), 256, 0, s>>>(first, last, pacc, m, G, ax, ay, az, ugrav);
-    SPHX_LAUNCH_CHECK();
-    gravitySpillKernel<<<kGSpillWaves, 64, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out, stats,
-                                                   c.spillList, c.spillMem, rec, mm);
-    SPHX_LAUNCH_CHECK();
+    if (all)
+    {
+        SPHX_CHECK(hipEventRecord(fork, s));
+        SPHX_CHECK(hipStreamWaitEvent(side, fork, 0));
+    }
+    if (all || phase == 2)
+    {
+        gravityP2PKernel<<<gridP, 64 * kGWaves, 0, side>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
+                                                          stats, c.S, pacc, rec, mm, orderP, slotsP);
+        SPHX_LAUNCH_CHECK();
+    }
+    if (all) SPHX_CHECK(hipEventRecord(join, side));
+    if (all || phase == 1)
+    {
+        gravityM2PKernel<<<grid, 64 * kGWaves, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
+                                                       stats, c.S, orderM, groups, nrec, mm);
+        SPHX_LAUNCH_CHECK();
+    }
+    if (all) SPHX_CHECK(hipStreamWaitEvent(s, join, 0));
+    if (all || phase == 3)
+    {
+        gravityCombineKernel<<<gridFor(n, 256), 256, 0, s>>>(first, last, pacc, m, G, ax, ay, az, ugrav);
+        SPHX_LAUNCH_CHECK();
+        gravitySpillKernel<<<kGSpillWaves, 64, 0, s>>>(first, last, t, x, y, z, h, m, G, ax, ay, az, ugrav, out,
+                                                       stats, c.spillList, c.spillMem, rec, mm);
+        SPHX_LAUNCH_CHECK();
+    }
 }
 
 // --------------------------------------------------------------------------------------------- direct sum

@@ -285,7 +285,7 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
                         const int32_t* ne, const double* centers, const void* mp, const double* x, const double* y,
                         const double* z, const float* h, const float* m, float G, float* ax, float* ay, float* az,
                         double* ugrav, double* out, unsigned long long* stats, void* scratch, int capM, int capL,
-                        void* pacc, int64_t nsrc, int64_t numNodes, void* rec, const double* mm, hipStream_t s);
+                        void* pacc, int64_t nsrc, int64_t numNodes, void* rec, const double* mm, hipStream_t s, int phase = 0);
 //! bytes of the record buffer of computeGravityEval (16 B per source particle, 40 B per tree node)
 inline size_t gravityRecordBytes(int64_t nsrc, int64_t numNodes) { return size_t(16 * nsrc + 40 * numNodes); }
 void directSum(int64_t first, int64_t last, int64_t n, const double* x, const double* y, const double* z,

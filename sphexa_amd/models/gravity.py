@@ -33,17 +33,25 @@ class MultipoleHolder:
         self.centers, self.multipoles = G.upsweep(ot, d["x"], d["y"], d["z"], d["m"], domain.box, domain.theta,
                                                   domain.sfc_kind)
 
-    def prepare(self, d, domain, scratch_key: str = ""):
+    def prepare(self, d, domain, scratch_key: str = "", m2p_out=None):
         """GPU: the upsweep and the interaction lists of the local tree (positions and masses only: they may run
-        before the neighbor search has settled h); traverse(prepared=True) evaluates them"""
+        before the neighbor search has settled h); traverse(prepared=True) evaluates them. ``m2p_out`` (ax, ay, az):
+        the M2P part of the evaluation runs here as well (it needs no smoothing lengths) and adds to those buffers;
+        ``lists_done`` is then recorded between the lists and the M2P kernel, for a P2P on another stream"""
         self.upsweep(d, domain)
         first, last = domain.start_index(), domain.end_index()
         self._lists = None
+        self.lists_done = None
         if last > first:
-            self._lists = G.gravity_lists(domain.octree, self.centers, self.multipoles, first, last, d["x"], d["y"],
-                                          d["z"], stats=self.stats, scratch_key=scratch_key)
+            gl = self._lists = G.gravity_lists(domain.octree, self.centers, self.multipoles, first, last, d["x"],
+                                               d["y"], d["z"], stats=self.stats, scratch_key=scratch_key)
+            if m2p_out is not None:
+                self.lists_done = torch.cuda.Event()
+                self.lists_done.record()
+                G.gravity_eval(gl, d["x"], d["y"], d["z"], d["h"], d["m"], d.g, *m2p_out, phase=1)
+                gl.m2p_done = True
 
-    def traverse(self, d, domain, out=None, scratch_key: str = "", prepared: bool = False):
+    def traverse(self, d, domain, out=None, scratch_key: str = "", prepared: bool = False, m2p_event=None):
         """accelerations now; on the GPU the energy and statistics stay on the device until the propagator's time
         step copies them to the host together with its own inputs (``pending`` / ``finish``). ``out``: (ax, ay, az)
         the gravitational accelerations are added to (default: the particle fields)"""
@@ -53,7 +61,15 @@ class MultipoleHolder:
         ax, ay, az = out if out is not None else (d["ax"], d["ay"], d["az"])
         if prepared:
             gl, self._lists = self._lists, None
-            parts = [G.gravity_eval(gl, d["x"], d["y"], d["z"], d["h"], d["m"], d.g, ax, ay, az)] if gl else [0.0]
+            self.last_lists = gl
+            if gl is not None and getattr(gl, "m2p_done", False):
+                # M2P ran in prepare (possibly on another stream: m2p_event); P2P here, then the combine after both
+                G.gravity_eval(gl, d["x"], d["y"], d["z"], d["h"], d["m"], d.g, ax, ay, az, phase=2)
+                if m2p_event is not None:
+                    torch.cuda.current_stream(d.device).wait_event(m2p_event)
+                parts = [G.gravity_eval(gl, d["x"], d["y"], d["z"], d["h"], d["m"], d.g, ax, ay, az, phase=3)]
+            else:
+                parts = [G.gravity_eval(gl, d["x"], d["y"], d["z"], d["h"], d["m"], d.g, ax, ay, az)] if gl else [0.0]
         else:
             parts = [G.compute_gravity(ot, self.centers, self.multipoles, first, last, d["x"], d["y"], d["z"],
                                        d["h"], d["m"], d.g, ax, ay, az, stats=self.stats, defer=True,

@@ -30,6 +30,9 @@ from ..parallel.comm import MIN
 GRAVITY_OVERLAP = os.environ.get("SPHX_GRAV_OVERLAP", "1") == "1"
 # upsweep + interaction lists forked right after the sync (overlapping the neighbor search), evaluation after it
 GRAVITY_PREPARE = os.environ.get("SPHX_GRAV_PREPARE", "1") == "1"
+# with it: the M2P part of the evaluation (no smoothing lengths) right after the lists, and the P2P part after the
+# search on a third stream, so M2P and P2P run concurrently beside the SPH loops
+GRAVITY_EARLY_M2P = os.environ.get("SPHX_GRAV_EARLY_M2P", "1") == "1"
 from ..utils.timer import Timer
 
 # XMass (STD: density) computed inside the GPU neighbor search instead of a separate pass over the lists. Off by
@@ -131,9 +134,21 @@ class Propagator:
         side = getattr(self, "_side_stream", None)
         if side is None:
             side = self._side_stream = torch.cuda.Stream(d.device)
+        self._gacc = None
         with torch.cuda.stream(side):
             side.wait_event(fork)
-            self.gravity.prepare(d, domain, scratch_key="overlap")
+            m2p_out = None
+            if GRAVITY_EARLY_M2P:
+                from ..ops.reduce import zero_
+
+                n = d.size
+                gacc = self._gacc = zero_(torch.empty(3 * n, dtype=torch.float32, device=d.device))
+                m2p_out = (gacc[:n], gacc[n:2 * n], gacc[2 * n:])
+            self.gravity.prepare(d, domain, scratch_key="overlap", m2p_out=m2p_out)
+            self._m2p_done = None
+            if m2p_out is not None:
+                self._m2p_done = torch.cuda.Event()
+                self._m2p_done.record(side)
         self._prepared = True
 
     def _gravity_start(self, domain, d, prepared=None):
@@ -155,19 +170,38 @@ class Propagator:
         if side is None:
             side = self._side_stream = torch.cuda.Stream(d.device)
         n = d.size
-        gacc = zero_(torch.empty(3 * n, dtype=torch.float32, device=d.device))  # (main stream)
+        early = prepared and getattr(self, "_gacc", None) is not None and self.gravity.lists_done is not None
+        if early:
+            # the M2P runs on the first side stream since the lists; the P2P goes to a second one, after the search
+            # (h) and the lists, and its combine waits for the M2P
+            gacc = self._gacc
+            gacc.record_stream(main)
+            side1, side = side, getattr(self, "_side_stream2", None)
+            if side is None:
+                side = self._side_stream2 = torch.cuda.Stream(d.device)
+            gacc.record_stream(side)
+        else:
+            gacc = zero_(torch.empty(3 * n, dtype=torch.float32, device=d.device))  # (main stream)
         fork = torch.cuda.Event()
         fork.record(main)
         with torch.cuda.stream(side):
             side.wait_event(fork)
+            if early:
+                side.wait_event(self.gravity.lists_done)
             if not prepared:
                 self.gravity.upsweep(d, domain)
                 self.timer.step("Upsweep")
             self.gravity.traverse(d, domain, out=(gacc[:n], gacc[n:2 * n], gacc[2 * n:]), scratch_key="overlap",
-                                  prepared=bool(prepared))
+                                  prepared=bool(prepared), m2p_event=self._m2p_done if early else None)
             joined = torch.cuda.Event()
             joined.record(side)
         gacc.record_stream(side)
+        gl = getattr(self.gravity, "last_lists", None)
+        if early and gl is not None:
+            # buffers allocated on the first side stream and used on the second
+            for t in (gl.zb, gl.pacc, gl.rec, gl.mm):
+                t.record_stream(side)
+        self._gacc = None
         for p in self.gravity.pending:
             p.dev.record_stream(main)  # (read by the time-step packet on the main stream after the join)
         return gacc, joined

@@ -148,28 +148,40 @@ def gravity_lists(tree: Octree, centers, mp, first: int, last: int, x, y, z, sta
     return gl
 
 
-def gravity_eval(gl: GravityLists, x, y, z, h, m, G: float, ax, ay, az, ugrav=None) -> "GravityPending":
-    """GPU phase 2 of compute_gravity on the lists of ``gl``: M2P + P2P, G a added to ax, ay, az"""
+def _eval_buffers(gl: GravityLists, x, y, z):
+    """P2P partials, the record buffer (16 B per source particle + 40 B per node, gravity.hip
+    gravityRecordsKernel/gravityNodeRecordsKernel) and the particles' extent of an evaluation (kept on ``gl``)"""
+    if getattr(gl, "rec", None) is None:
+        from .reduce import min_max
+
+        n, nsrc = gl.last - gl.first, x.numel()
+        gl.pacc = torch.empty(4 * n, dtype=torch.float32, device=x.device)  # P2P partials (phi, a) per target
+        gl.mm = min_max([x, y, z])
+        gl.rec = torch.empty(4 * nsrc + 10 * gl.tree.num_nodes, dtype=torch.int32, device=x.device)
+    return gl.pacc, gl.rec, gl.mm
+
+
+def gravity_eval(gl: GravityLists, x, y, z, h, m, G: float, ax, ay, az, ugrav=None, phase: int = 0):
+    """GPU phase 2 of compute_gravity on the lists of ``gl``: M2P + P2P, G a added to ax, ay, az. Returns the
+    GravityPending of the evaluation. ``phase`` splits it (gravity.hip computeGravityEval): 1 = M2P (needs no
+    smoothing lengths), 2 = P2P, 3 = P2P combine + spilled groups; the caller orders 1 and 2 before 3 and collects
+    the pending values after 3 (the earlier phases return None)"""
     hp = _lib.hip()
     first, last, tree = gl.first, gl.last, gl.tree
     n = last - first
     cap_m, cap_l = gl.caps
     zb = gl.zb
     st_dev, out = zb[:GravityPending.NSTATS], zb[GravityPending.NSTATS:].view(torch.float64)
-    pacc = torch.empty(4 * n, dtype=torch.float32, device=x.device)  # P2P partials (phi, a) per target
     # the P2P kernel generates its source indices from the opened-leaf lists: no index list, no host wait
-    # P2P source records (fixed point in a frame over the particles' extent, gravity.hip gravityRecordsKernel)
-    from .reduce import min_max
-    nsrc = x.numel()
-    mm = min_max([x, y, z])
-    # records: 16 B per source particle + 40 B per node (M2P), gravity.hip gravityNodeRecordsKernel
-    rec = torch.empty(4 * nsrc + 10 * tree.num_nodes, dtype=torch.int32, device=x.device)
+    pacc, rec, mm = _eval_buffers(gl, x, y, z)
     hp.gravity_eval(first, last, *gl.tree_args(), x.data_ptr(), y.data_ptr(), z.data_ptr(), h.data_ptr(),
                     m.data_ptr(), float(G), ax.data_ptr(), ay.data_ptr(), az.data_ptr(),
                     0 if ugrav is None else ugrav.data_ptr(), out.data_ptr(), st_dev.data_ptr(),
-                    gl.scratch.data_ptr(), cap_m, cap_l, pacc.data_ptr(), nsrc, tree.num_nodes, rec.data_ptr(),
-                    mm.data_ptr(), _stream())
-    return GravityPending(zb, (n + 63) // 64, (cap_m, cap_l), gl.stats, x.device)
+                    gl.scratch.data_ptr(), cap_m, cap_l, pacc.data_ptr(), x.numel(), tree.num_nodes, rec.data_ptr(),
+                    mm.data_ptr(), _stream(), phase=phase)
+    if phase in (0, 3):
+        return GravityPending(zb, (n + 63) // 64, (cap_m, cap_l), gl.stats, x.device)
+    return None
 
 
 def compute_gravity(tree: Octree, centers, mp, first: int, last: int, x, y, z, h, m, G: float, ax, ay, az,

@@ -16,10 +16,13 @@ _WORK: dict = {}
 
 
 def _work(device) -> torch.Tensor:
-    t = _WORK.get(device)
+    """[ticket | partials] workspace of the single-launch reductions, one per stream: the ticket re-arms itself at
+    the end of every launch, so launches on one stream can share it, but two streams running reductions at the same
+    time (gravity's extents on the side stream during the neighbor search's h reduction) must not"""
+    key = (device, _lib.stream())
+    t = _WORK.get(key)
     if t is None:
-        # [ticket | partials]; the ticket re-arms itself at the end of every launch
-        t = _WORK[device] = torch.zeros(_lib.hip().reduce_work_bytes(), dtype=torch.uint8, device=device)
+        t = _WORK[key] = torch.zeros(_lib.hip().reduce_work_bytes(), dtype=torch.uint8, device=device)
     return t
 
 

@@ -280,3 +280,21 @@ def test_device_box_keys_match_host_box(gpu, monkeypatch):
     assert alo == blo and ahi == bhi
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+def test_gravity_early_m2p_matches(gpu, monkeypatch):
+    """the M2P part of the gravity evaluation run beside the neighbor search and the P2P part on a third stream
+    (models/propagators.py GRAVITY_EARLY_M2P) give the accelerations of the single evaluation"""
+    from sphexa_amd.models import propagators as Pr
+
+    out = {}
+    for early in (False, True):
+        monkeypatch.setattr(Pr, "GRAVITY_EARLY_M2P", early)
+        sim = Simulation("evrard", n=32, device=gpu)
+        sim.run(3)
+        torch.cuda.synchronize()
+        out[early] = (_sorted_state(sim, ["ax", "ay", "az", "x", "h"]), sim.d.minDt, sim.conserved()["egrav"])
+    (a, dta, ea), (b, dtb, eb) = out[False], out[True]
+    for k in a:
+        assert torch.allclose(a[k], b[k], rtol=1e-5, atol=1e-6 * float(a[k].abs().max())), k
+    assert dta == pytest.approx(dtb, rel=1e-6) and ea == pytest.approx(eb, rel=1e-6)
