@@ -33,6 +33,8 @@ GRAVITY_PREPARE = os.environ.get("SPHX_GRAV_PREPARE", "1") == "1"
 # with it: the M2P part of the evaluation (no smoothing lengths) right after the lists, and the P2P part after the
 # search on a third stream, so M2P and P2P run concurrently beside the SPH loops
 GRAVITY_EARLY_M2P = os.environ.get("SPHX_GRAV_EARLY_M2P", "1") == "1"
+# priority of the gravity streams (torch: -1 high, 0 normal): the gravity chain is the longer one on Evrard
+GRAVITY_STREAM_PRIORITY = int(os.environ.get("SPHX_GRAV_PRIORITY", "0"))
 from ..utils.timer import Timer
 
 # XMass (STD: density) computed inside the GPU neighbor search instead of a separate pass over the lists. Off by
@@ -133,7 +135,7 @@ class Propagator:
             self.gravity = MultipoleHolder()
         side = getattr(self, "_side_stream", None)
         if side is None:
-            side = self._side_stream = torch.cuda.Stream(d.device)
+            side = self._side_stream = torch.cuda.Stream(d.device, priority=GRAVITY_STREAM_PRIORITY)
         self._gacc = None
         with torch.cuda.stream(side):
             side.wait_event(fork)
@@ -168,7 +170,7 @@ class Propagator:
         main = torch.cuda.current_stream(d.device)
         side = getattr(self, "_side_stream", None)
         if side is None:
-            side = self._side_stream = torch.cuda.Stream(d.device)
+            side = self._side_stream = torch.cuda.Stream(d.device, priority=GRAVITY_STREAM_PRIORITY)
         n = d.size
         early = prepared and getattr(self, "_gacc", None) is not None and self.gravity.lists_done is not None
         if early:
@@ -178,7 +180,7 @@ class Propagator:
             gacc.record_stream(main)
             side1, side = side, getattr(self, "_side_stream2", None)
             if side is None:
-                side = self._side_stream2 = torch.cuda.Stream(d.device)
+                side = self._side_stream2 = torch.cuda.Stream(d.device, priority=GRAVITY_STREAM_PRIORITY)
             gacc.record_stream(side)
         else:
             gacc = zero_(torch.empty(3 * n, dtype=torch.float32, device=d.device))  # (main stream)
