@@ -22,24 +22,14 @@
 namespace sphx::hip
 {
 
-/*! @brief one thread per (query box, destination): walk the own tree and flag the particles inside the box. Boxes
- *         of destination q are rows [q * nbPer, (q + 1) * nbPer) of (center[3], half[3]) doubles; empty slots have
- *         half < 0; destinations with enabled[q] == 0 (this rank, pruned peers) are skipped */
-__global__ void markHalosMultiKernel(int nbPer, const double* __restrict__ boxes, const uint8_t* __restrict__ enabled,
-                                     const int32_t* __restrict__ child, const int32_t* __restrict__ n2l,
-                                     const int32_t* __restrict__ ns, const int32_t* __restrict__ ne,
-                                     const double* __restrict__ center, const double* __restrict__ half,
-                                     const double* __restrict__ x, const double* __restrict__ y,
-                                     const double* __restrict__ z, int64_t n, Box box, uint8_t* __restrict__ flags)
+//! @brief the particles of the own tree inside one query box, walked by one thread (the fallback of the wave walk)
+__device__ void markBoxSerial(const double c[3], const double s[3], const int32_t* __restrict__ child,
+                              const int32_t* __restrict__ n2l, const int32_t* __restrict__ ns,
+                              const int32_t* __restrict__ ne, const double* __restrict__ center,
+                              const double* __restrict__ half, const double* __restrict__ x,
+                              const double* __restrict__ y, const double* __restrict__ z, const Box& box,
+                              uint8_t* __restrict__ f)
 {
-    const int q = blockIdx.y;
-    const int b = int(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (b >= nbPer || !enabled[q]) return;
-    const double* r = boxes + (int64_t(q) * nbPer + b) * 6;
-    const double c[3] = {r[0], r[1], r[2]};
-    const double s[3] = {r[3], r[4], r[5]};
-    if (!(s[0] >= 0.0)) return;
-    uint8_t* f  = flags + int64_t(q) * n;
     int32_t stack[192];
     int sp      = 0;
     stack[sp++] = 0;
@@ -64,28 +54,145 @@ __global__ void markHalosMultiKernel(int nbPer, const double* __restrict__ boxes
     }
 }
 
+constexpr int kMarkWaves = 4;    // boxes (waves) per block
+constexpr int kMarkStack = 2048; // LDS node stack per wave
+
+/*! @brief one wave per (query box, destination): the wave walks the own tree 64 nodes at a time (LDS stack, ballot
+ *         compaction) and tests the particles of every overlapping leaf 64 at a time, instead of one thread walking
+ *         the tree and looping over the leaves' particles (the round-4/5 form took 1.5-1.9 ms per sync on the 2-4 rank
+ *         rehearsals, profiles/r5/multirank). Boxes of destination q are rows [q * nbPer, (q + 1) * nbPer) of
+ *         (center[3], half[3]) doubles; empty slots have half < 0; destinations with enabled[q] == 0 (this rank,
+ *         pruned peers) are skipped. A box whose walk outgrows the stack is redone by one thread (markBoxSerial). */
+__global__ __launch_bounds__(64 * kMarkWaves) void markHalosMultiKernel(
+    int nbPer, const double* __restrict__ boxes, const uint8_t* __restrict__ enabled, const int32_t* __restrict__ child,
+    const int32_t* __restrict__ n2l, const int32_t* __restrict__ ns, const int32_t* __restrict__ ne,
+    const double* __restrict__ center, const double* __restrict__ half, const double* __restrict__ x,
+    const double* __restrict__ y, const double* __restrict__ z, int64_t n, Box box, uint8_t* __restrict__ flags)
+{
+    __shared__ int32_t stk[kMarkWaves][kMarkStack];
+    const int q    = blockIdx.y;
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int b    = int(blockIdx.x) * kMarkWaves + wave;
+    if (b >= nbPer || !enabled[q]) return; // (wave-uniform)
+    const double* r   = boxes + (int64_t(q) * nbPer + b) * 6;
+    const double c[3] = {r[0], r[1], r[2]};
+    const double s[3] = {r[3], r[4], r[5]};
+    if (!(s[0] >= 0.0)) return;
+    uint8_t* f  = flags + int64_t(q) * n;
+    int32_t* st = stk[wave];
+    if (lane == 0) st[0] = 0;
+    int top  = 1;
+    bool ovf = false;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    while (top > 0)
+    {
+        const int take     = min(top, 64);
+        const int base     = top - take;
+        const int32_t node = lane < take ? st[base + lane] : -1;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        top               = base;
+        const bool ov     = node >= 0 && boxesOverlap(c, s, center + 3 * node, half + 3 * node, box);
+        const bool leaf   = ov && n2l[node] >= 0;
+        const bool inner  = ov && !leaf;
+        const uint64_t mi = ballot(inner);
+        const int ni      = __popcll(mi);
+        if (top + 8 * ni > kMarkStack)
+        {
+            ovf = true;
+            break;
+        }
+        if (inner)
+        {
+            const int p      = top + 8 * __popcll(mi & lanemaskLt());
+            const int32_t co = child[node];
+            for (int k = 0; k < 8; ++k)
+                st[p + k] = co + k;
+        }
+        top += 8 * ni;
+        for (uint64_t ml = ballot(leaf); ml; ml &= ml - 1)
+        {
+            const int32_t nd = __builtin_amdgcn_readlane(node, __builtin_ctzll(ml));
+            const int32_t a = ns[nd], e = ne[nd];
+            for (int32_t j = a + lane; j < e; j += 64)
+            {
+                const double p[3] = {x[j], y[j], z[j]};
+                if (pointBoxDistSq(p, c, s, box) <= 0.0) f[j] = 1;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (ovf && lane == 0) markBoxSerial(c, s, child, n2l, ns, ne, center, half, x, y, z, box, f);
+}
+
 void markHalosMulti(int nDest, int nbPer, const double* boxes, const uint8_t* enabled, const int32_t* child,
                     const int32_t* n2l, const int32_t* ns, const int32_t* ne, const double* center, const double* half,
                     const double* x, const double* y, const double* z, int64_t n, const Box& box, uint8_t* flags,
                     hipStream_t s)
 {
     if (nDest == 0 || nbPer == 0) return;
-    markHalosMultiKernel<<<dim3(gridFor(nbPer, 64), nDest), 64, 0, s>>>(nbPer, boxes, enabled, child, n2l, ns, ne,
-                                                                        center, half, x, y, z, n, box, flags);
+    markHalosMultiKernel<<<dim3(unsigned((nbPer + kMarkWaves - 1) / kMarkWaves), nDest), 64 * kMarkWaves, 0, s>>>(
+        nbPer, boxes, enabled, child, n2l, ns, ne, center, half, x, y, z, n, box, flags);
     SPHX_LAUNCH_CHECK();
 }
 
-//! @brief LET marking of every destination (gravity.hpp markLetBox): failed[q][node]
-__global__ void markLetMultiKernel(int nbPer, const double* __restrict__ boxes, const uint8_t* __restrict__ enabled,
-                                   const int32_t* __restrict__ child, const int32_t* __restrict__ n2l,
-                                   const double* __restrict__ tc, const double* __restrict__ th,
-                                   const double* __restrict__ gc, int64_t N, Box box, uint8_t* __restrict__ failed)
+/*! @brief LET marking of every destination (gravity.hpp markLetBox: failed[q][node]), one wave per (query box,
+ *         destination): the wave walks the own tree 64 nodes at a time from an LDS stack (the per-thread walk of
+ *         markLetBox remains the fallback of a box whose walk outgrows the stack) */
+__global__ __launch_bounds__(64 * kMarkWaves) void markLetMultiKernel(
+    int nbPer, const double* __restrict__ boxes, const uint8_t* __restrict__ enabled, const int32_t* __restrict__ child,
+    const int32_t* __restrict__ n2l, const double* __restrict__ tc, const double* __restrict__ th,
+    const double* __restrict__ gc, int64_t N, Box box, uint8_t* __restrict__ failed)
 {
-    const int q = blockIdx.y;
-    const int b = int(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (b >= nbPer || !enabled[q]) return;
-    const double* r = boxes + (int64_t(q) * nbPer + b) * 6;
-    markLetBox(r, r + 3, child, n2l, tc, th, gc, box, failed + int64_t(q) * N);
+    __shared__ int32_t stk[kMarkWaves][kMarkStack];
+    const int q    = blockIdx.y;
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int b    = int(blockIdx.x) * kMarkWaves + wave;
+    if (b >= nbPer || !enabled[q]) return; // (wave-uniform)
+    const double* r   = boxes + (int64_t(q) * nbPer + b) * 6;
+    const double c[3] = {r[0], r[1], r[2]};
+    const double s[3] = {r[3], r[4], r[5]};
+    if (!(s[0] >= 0.0)) return;
+    uint8_t* f  = failed + int64_t(q) * N;
+    int32_t* st = stk[wave];
+    if (lane == 0) st[0] = 0;
+    int top  = 1;
+    bool ovf = false;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    while (top > 0)
+    {
+        const int take     = min(top, 64);
+        const int base     = top - take;
+        const int32_t node = lane < take ? st[base + lane] : -1;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        top       = base;
+        bool open = false;
+        if (node >= 0 && !(th[3 * node] < 0))
+        {
+            const double* g = gc + 4 * node;
+            open = boxesOverlap(c, s, tc + 3 * node, th + 3 * node, box) || pointBoxDistSq(g, c, s, box) < fabs(g[3]);
+        }
+        if (open) f[node] = 1;
+        const bool inner  = open && n2l[node] < 0;
+        const uint64_t mi = ballot(inner);
+        const int ni      = __popcll(mi);
+        if (top + 8 * ni > kMarkStack)
+        {
+            ovf = true;
+            break;
+        }
+        if (inner)
+        {
+            const int p      = top + 8 * __popcll(mi & lanemaskLt());
+            const int32_t co = child[node];
+            for (int k = 0; k < 8; ++k)
+                st[p + k] = co + k;
+        }
+        top += 8 * ni;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (ovf && lane == 0) markLetBox(c, s, child, n2l, tc, th, gc, box, f);
 }
 
 void markLetMulti(int nDest, int nbPer, const double* boxes, const uint8_t* enabled, const int32_t* child,
@@ -93,8 +200,8 @@ void markLetMulti(int nDest, int nbPer, const double* boxes, const uint8_t* enab
                   uint8_t* failed, hipStream_t s)
 {
     if (nDest == 0 || nbPer == 0) return;
-    markLetMultiKernel<<<dim3(gridFor(nbPer, 64), nDest), 64, 0, s>>>(nbPer, boxes, enabled, child, n2l, tc, th, gc,
-                                                                      N, box, failed);
+    markLetMultiKernel<<<dim3(unsigned((nbPer + kMarkWaves - 1) / kMarkWaves), nDest), 64 * kMarkWaves, 0, s>>>(
+        nbPer, boxes, enabled, child, n2l, tc, th, gc, N, box, failed);
     SPHX_LAUNCH_CHECK();
 }
 
