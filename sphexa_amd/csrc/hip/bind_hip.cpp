@@ -274,7 +274,8 @@ PYBIND11_MODULE(_sphx_hip, m)
           [](int64_t first, int64_t last, Ptr x, Ptr y, Ptr z, Ptr h, int64_t numNodes, Ptr child, Ptr n2l, Ptr ns,
              Ptr ne, Ptr center, Ptr half, const BoxArr& box, unsigned ng0, unsigned ngmax, Ptr nidx, Ptr nc,
              int iterateH, Ptr stats, Ptr scratch, int testFrontCap, Ptr s, int home, int ovStride, Ptr mm,
-             int64_t ntot, Ptr rec, Ptr keys, Ptr predIn, Ptr predOut, Ptr flags, int stamp, int predCap, Ptr plist)
+             int64_t ntot, Ptr rec, Ptr keys, Ptr predIn, Ptr predOut, Ptr flags, int stamp, int predCap, Ptr plist,
+             int predMark)
           {
               (void)numNodes;
               NsTree t{P<int32_t>(child), P<int32_t>(n2l), P<int32_t>(ns), P<int32_t>(ne), P<double>(center),
@@ -290,6 +291,7 @@ PYBIND11_MODULE(_sphx_hip, m)
                   sp.cap       = predCap;
                   sp.listCount = P<unsigned long long>(plist); // [count | int32 list]
                   sp.list      = reinterpret_cast<int32_t*>(sp.listCount + 1);
+                  sp.mark      = predMark;
               }
               findNeighbors(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(h), t, toBox(box), ng0,
                             ngmax, P<int32_t>(nidx), home, ovStride, P<int32_t>(nc), iterateH,
@@ -302,7 +304,7 @@ PYBIND11_MODULE(_sphx_hip, m)
           py::arg("iterateH"), py::arg("stats"), py::arg("scratch"), py::arg("testFrontCap"), py::arg("s"),
           py::arg("home") = 0, py::arg("ov_stride") = 1, py::arg("m") = 0, py::arg("ntot") = 0, py::arg("rec") = 0,
           py::arg("keys") = 0, py::arg("pred_in") = 0, py::arg("pred_out") = 0, py::arg("flags") = 0,
-          py::arg("stamp") = 0, py::arg("pred_cap") = 0, py::arg("plist") = 0);
+          py::arg("stamp") = 0, py::arg("pred_cap") = 0, py::arg("plist") = 0, py::arg("pred_mark") = 1);
     m.def("neighbor_row_stripes", []() { return neighborRowStripes(); });
     m.def("row_plan", [](int64_t groups, unsigned ngmax, Ptr tab, int home, Ptr over, Ptr s)
           { rowPlan(groups, ngmax, P<int32_t>(tab), home, P<unsigned long long>(over), St(s)); });

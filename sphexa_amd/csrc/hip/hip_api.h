@@ -164,6 +164,7 @@ struct SplitPredict
     int cap = 0;                                 // key pairs per record
     unsigned long long* listCount = nullptr;     // predicted groups: count + list (>= 3 cap entries)
     int32_t* list = nullptr;
+    int mark = 1; // 0: predIn is known to be empty (the previous search split no group): record only
 };
 void findNeighbors(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* h,
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int home,

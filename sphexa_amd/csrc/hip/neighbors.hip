@@ -1169,17 +1169,18 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
     const QFrame qf     = qframeOf(box);
     SrcPosQ* xq         = static_cast<SrcPosQ*>(rec);
     packPosQ(ntot, x, y, z, m, qf, xq, s);
-    const bool predict = sp.keys && sp.predIn && sp.predOut && sp.flags && sp.list && sp.cap > 0;
-    const PredOut pout{sp.keys, predict ? sp.predOut : nullptr, sp.cap, fc};
+    const bool record  = sp.keys && sp.predIn && sp.predOut && sp.flags && sp.list && sp.cap > 0;
+    const bool predict = record && sp.mark;
+    const PredOut pout{sp.keys, record ? sp.predOut : nullptr, sp.cap, fc};
     SideStream* side = predict ? &sideStream() : nullptr;
     auto launch = [&](auto capped)
     {
         constexpr bool kC = decltype(capped)::value;
         const int fcs = testFrontCap > 0 ? min(testFrontCap, kSplitFront) : kSplitFront;
+        if (record) SPHX_CHECK(hipMemsetAsync(sp.predOut, 0, sizeof(unsigned long long), s));
         if (predict)
         {
             // the predicted groups: listed on this stream, searched on the side stream while the main kernel runs
-            SPHX_CHECK(hipMemsetAsync(sp.predOut, 0, sizeof(unsigned long long), s));
             SPHX_CHECK(hipMemsetAsync(sp.listCount, 0, sizeof(unsigned long long), s));
             predMarkKernel<<<1, 256, 0, s>>>(sp.keys, first, last, sp.predIn, sp.cap, sp.flags, sp.stamp,
                                              sp.listCount, sp.list, stats);

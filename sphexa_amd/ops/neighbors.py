@@ -241,13 +241,17 @@ class _PredState:
         self.flags = None
         self.stamp = 0
         self.cur = 0
+        # the record read next holds groups (known from the statistics: the previous search split some group);
+        # when not, the marking and the second-stream launch are skipped (only the recording runs)
+        self.active = True
 
     def args(self, groups: int, device) -> dict:
         if self.flags is None or self.flags.numel() < groups:
             self.flags = zero_(torch.empty(max(groups, 1024) * 5 // 4, dtype=torch.int32, device=device))
         self.stamp = self.stamp % (2**31 - 2) + 1
         return dict(pred_in=self.rec[self.cur].data_ptr(), pred_out=self.rec[1 - self.cur].data_ptr(),
-                    flags=self.flags.data_ptr(), stamp=self.stamp, pred_cap=PRED_CAP, plist=self.plist.data_ptr())
+                    flags=self.flags.data_ptr(), stamp=self.stamp, pred_cap=PRED_CAP, plist=self.plist.data_ptr(),
+                    pred_mark=int(self.active))
 
     def swap(self):
         self.cur = 1 - self.cur
@@ -403,6 +407,9 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         d.nc_queued = int(st[2])
         d.nc_split = int(st[5]) & 0xFFFFFFFF
         d.nc_predicted = int(st[5]) >> 32  # groups the split kernel took on the second stream (predicted overflow)
+        if pred is not None:
+            # (a record can only hold groups the split kernel searched: queued by the main kernel or predicted)
+            pred.active = d.nc_queued + d.nc_predicted > 0
         d.nc_spilled = int(st[7])
         d.nc_spill_chunks = int(st[1]) >> 32
         d.nc_rounds = int(st[3]) / num_groups  # mean search rounds per group (h iteration)
