@@ -184,8 +184,14 @@ class Propagator:
             gacc.record_stream(side)
         else:
             gacc = zero_(torch.empty(3 * n, dtype=torch.float32, device=d.device))  # (main stream)
-        fork = torch.cuda.Event()
-        fork.record(main)
+        done = getattr(self.nl, "done", None) if self.nl is not None else None
+        if early and done is not None:
+            # the P2P needs the search's h only: fork at the search's end, not behind the first SPH loops the host
+            # has enqueued since (speculatively, while it waited for the search statistics)
+            fork = done
+        else:
+            fork = torch.cuda.Event()
+            fork.record(main)
         with torch.cuda.stream(side):
             side.wait_event(fork)
             if early:

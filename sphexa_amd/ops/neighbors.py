@@ -48,6 +48,7 @@ class NeighborList:
     hist: tuple = ()  # HIP: rows needed by recent searches (pool sizing)
     ride_along: list | None = None  # HIP: host values of find_neighbors' ride_along tensor
     speculated: bool = False  # HIP: find_neighbors' ``speculate`` ran on these lists (no repeated search)
+    done: object = None  # HIP: event recorded right after the (last) search's kernels: h and nc are final there
 
     @property
     def stride(self):
@@ -321,6 +322,8 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
                               stats.data_ptr(),
                               scratch.data_ptr(), TEST_FRONT_CAP, _stream(), home=home, ov_stride=ov,
                               m=d["m"].data_ptr(), ntot=d.size, rec=rec.data_ptr(), **pkw)
+            done_ev = torch.cuda.Event()
+            done_ev.record()
             if after_launch is not None and _attempt == 0:
                 after_launch()
             # per-stripe row demand of the five pool candidates of the next search (one kernel), the stripe
@@ -417,7 +420,7 @@ def find_neighbors(d, tree: Octree, box: Box, first: int, last: int, iterate_h: 
         if COLLECT_STATS:  # staged candidates and hits per group; candidates inside sub-group boxes (what-if)
             extra = stats[9:12].cpu().tolist()
             d.nc_hits, d.nc_staged, d.nc_subbox = (v / num_groups for v in extra)
-        return NeighborList(buf, first, last, ngmax, True, used, plan, hist, ride_host, speculated)
+        return NeighborList(buf, first, last, ngmax, True, used, plan, hist, ride_host, speculated, done_ev)
 
     need = max(n, 1) * ngmax
     if nidx is None or nidx.numel() < need:
