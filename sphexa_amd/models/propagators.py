@@ -35,6 +35,10 @@ GRAVITY_PREPARE = os.environ.get("SPHX_GRAV_PREPARE", "1") == "1"
 GRAVITY_EARLY_M2P = os.environ.get("SPHX_GRAV_EARLY_M2P", "1") == "1"
 # priority of the gravity streams (torch: -1 high, 0 normal): the gravity chain is the longer one on Evrard
 GRAVITY_STREAM_PRIORITY = int(os.environ.get("SPHX_GRAV_PRIORITY", "0"))
+# the upsweep and the interaction lists before the neighbor search (the search waits for them), the M2P beside it.
+# Off: measured Evrard -n 200 21.3-21.7 vs 20.9-21.5 ms, -n 100 3.61 vs 3.45 ms: the M2P's long waves then hold the
+# CU slots the search's unpredicted split groups need after the main kernel (a 5-ms tail at -n 200)
+GRAVITY_LISTS_FIRST = os.environ.get("SPHX_GRAV_LISTS_FIRST", "0") == "1"
 from ..utils.timer import Timer
 
 # XMass (STD: density) computed inside the GPU neighbor search instead of a separate pass over the lists. Off by
@@ -405,6 +409,15 @@ class HydroVeProp(Propagator):
         t.step("domain::sync")
         prep = self._gravity_prepare(domain, d)
         self._prepared = False
+        if prep is not None and GRAVITY_LISTS_FIRST:
+            # the upsweep and lists (short, latency-bound kernels that gate both evaluations) run before the search
+            # instead of beside it, where they were starved of CU slots; the M2P then overlaps the search
+            prep()
+            if self.gravity.lists_done is not None:
+                torch.cuda.current_stream(d.device).wait_event(self.gravity.lists_done)
+            prep = None
+            self._prepared = True
+            self._lists_first = True
         box = domain.box
         first, last = domain.start_index(), domain.end_index()
         # velocity halos are not read before the IAD loop: their exchange overlaps the search, XMass and Gradh
@@ -430,7 +443,7 @@ class HydroVeProp(Propagator):
         nl = self.nl
         if prep is not None and not self._prepared:  # (a search path that did not call it)
             prep()
-        grav = self._gravity_start(domain, d, prepared=prep is not None)
+        grav = self._gravity_start(domain, d, prepared=self._prepared)
 
         if not done:
             H.compute_xmass(d, nl, box)
