@@ -162,9 +162,19 @@ def _run_case(init: str, n: int, args, comm, device) -> dict:
     from sphexa_amd.utils.phase_prof import PROF as _PROF
 
     _PROF.reset()  # (profiled runs only: the attribution covers the timed steps)
+    # SPHX_HOST_PROFILE=<file>: Python profile of rank 0's timed steps (host-time analysis; slows the run)
+    hprof = None
+    if os.environ.get("SPHX_HOST_PROFILE") and rank == 0:
+        import cProfile
+
+        hprof = cProfile.Profile()
+        hprof.enable()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sim.step()
+    if hprof is not None:
+        hprof.disable()
+        hprof.dump_stats(os.environ["SPHX_HOST_PROFILE"])
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()

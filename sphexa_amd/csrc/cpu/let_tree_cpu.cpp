@@ -48,7 +48,7 @@ static void spanRange(KeyT a, KeyT b, std::vector<KeyT>& out)
 
 void markOutsideRange(int64_t N, const KeyT* prefixes, KeyT lo, KeyT hi, uint8_t* failed)
 {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(N > 16384)
     for (int64_t i = 0; i < N; ++i)
     {
         int l    = placeholderLevel(prefixes[i]);

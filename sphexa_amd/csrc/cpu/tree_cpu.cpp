@@ -18,9 +18,14 @@
 namespace sphx::cpu
 {
 
+//! loops over fewer elements run serially: the per-step host work of a multi-rank sync (global-tree rebalance and
+//! node properties over ~1e3 leaves) took ~1 ms in OpenMP fork/join alone on a many-core box
+constexpr int64_t kOmpMin = 16384;
+
+
 void computeKeys(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind, KeyT* keys)
 {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(n > kOmpMin)
     for (int64_t i = 0; i < n; ++i)
         keys[i] = particleKey(kind, x[i], y[i], z[i], box);
 }
@@ -28,11 +33,11 @@ void computeKeys(int64_t n, const double* x, const double* y, const double* z, c
 void sortKeys(int64_t n, KeyT* keys, int32_t* perm)
 {
     std::vector<std::pair<KeyT, int32_t>> kv(n);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(n > kOmpMin)
     for (int64_t i = 0; i < n; ++i)
         kv[i] = {keys[i], int32_t(i)};
     __gnu_parallel::sort(kv.begin(), kv.end());
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(n > kOmpMin)
     for (int64_t i = 0; i < n; ++i)
     {
         keys[i] = kv[i].first;
@@ -48,7 +53,7 @@ void gatherBytes(int64_t n, const int32_t* perm, const char* src, char* dst, int
         {
             auto s = reinterpret_cast<const uint32_t*>(src);
             auto d = reinterpret_cast<uint32_t*>(dst);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(n > kOmpMin)
             for (int64_t i = 0; i < n; ++i)
                 d[i] = s[perm[i]];
             break;
@@ -57,13 +62,13 @@ void gatherBytes(int64_t n, const int32_t* perm, const char* src, char* dst, int
         {
             auto s = reinterpret_cast<const uint64_t*>(src);
             auto d = reinterpret_cast<uint64_t*>(dst);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(n > kOmpMin)
             for (int64_t i = 0; i < n; ++i)
                 d[i] = s[perm[i]];
             break;
         }
         default:
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(n > kOmpMin)
             for (int64_t i = 0; i < n; ++i)
                 std::copy_n(src + int64_t(perm[i]) * elemSize, elemSize, dst + i * elemSize);
     }
@@ -71,7 +76,7 @@ void gatherBytes(int64_t n, const int32_t* perm, const char* src, char* dst, int
 
 void nodeCounts(const KeyT* tree, int64_t L, const KeyT* keys, int64_t n, uint32_t* counts)
 {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(L > kOmpMin)
     for (int64_t i = 0; i < L; ++i)
     {
         int64_t a = lowerBound(keys, n, tree[i]);
@@ -85,7 +90,7 @@ bool rebalance(std::vector<KeyT>& tree, const uint32_t* counts, uint32_t bucket)
     int64_t L = int64_t(tree.size()) - 1;
     std::vector<int64_t> ops(L + 1, 0);
     bool changed = false;
-#pragma omp parallel for schedule(static) reduction(|| : changed)
+#pragma omp parallel for schedule(static) reduction(|| : changed) if(L > kOmpMin)
     for (int64_t i = 0; i < L; ++i)
     {
         int op = leafRebalanceOp(i, tree.data(), counts, L, bucket);
@@ -95,7 +100,7 @@ bool rebalance(std::vector<KeyT>& tree, const uint32_t* counts, uint32_t bucket)
     if (!changed) return false;
     std::exclusive_scan(ops.begin(), ops.end(), ops.begin(), int64_t(0));
     std::vector<KeyT> out(ops[L] + 1);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(L > kOmpMin)
     for (int64_t i = 0; i < L; ++i)
     {
         int op = int(ops[i + 1] - ops[i]);
@@ -131,7 +136,7 @@ LinkedOctree linkOctree(const KeyT* tree, int64_t L)
     int64_t N  = Ni + L;
 
     std::vector<std::pair<KeyT, int64_t>> codes(N);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(L > kOmpMin)
     for (int64_t i = 0; i < L; ++i)
     {
         KeyT key    = tree[i];
@@ -164,7 +169,7 @@ LinkedOctree linkOctree(const KeyT* tree, int64_t L)
         KeyT c          = KeyT(1) << (3 * std::min(l, kMaxLevel));
         o.levelRange[l] = (l > kMaxLevel) ? N : lowerBound(o.prefixes.data(), N, c);
     }
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(N > kOmpMin)
     for (int64_t n = 0; n < N; ++n)
     {
         if (o.nodeToLeaf[n] >= 0) continue;
@@ -182,7 +187,7 @@ LinkedOctree linkOctree(const KeyT* tree, int64_t L)
 void nodeRanges(const LinkedOctree& o, const KeyT* keys, int64_t n, int64_t offset, int32_t* nodeStart,
                 int32_t* nodeEnd)
 {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(o.numNodes > kOmpMin)
     for (int64_t i = 0; i < o.numNodes; ++i)
     {
         KeyT code  = o.prefixes[i];
@@ -205,7 +210,7 @@ void boxesWithRadius(int64_t N, const int32_t* childOffsets, const int32_t* node
                      const double* z, const float* h, double factor, double* center, double* half)
 {
     std::vector<double> bmin(3 * N), bmax(3 * N);
-#pragma omp parallel for schedule(dynamic, 256)
+#pragma omp parallel for schedule(dynamic, 256) if(N > kOmpMin)
     for (int64_t i = 0; i < N; ++i)
     {
         if (nodeToLeaf[i] < 0) continue;
@@ -229,7 +234,7 @@ void boxesWithRadius(int64_t N, const int32_t* childOffsets, const int32_t* node
     for (int l = kMaxLevel; l >= 0; --l)
     {
         int64_t a = levelRange[l], b = levelRange[l + 1];
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(b - a > kOmpMin)
         for (int64_t i = a; i < b; ++i)
         {
             if (nodeToLeaf[i] >= 0) continue;
@@ -248,7 +253,7 @@ void boxesWithRadius(int64_t N, const int32_t* childOffsets, const int32_t* node
             }
         }
     }
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(N > kOmpMin)
     for (int64_t i = 0; i < N; ++i)
         for (int d = 0; d < 3; ++d)
         {
@@ -270,7 +275,7 @@ void boxesWithRadius(int64_t N, const int32_t* childOffsets, const int32_t* node
 void markInBoxes(int64_t numBoxes, const double* bc, const double* bh, const TreeView& t, const double* x,
                  const double* y, const double* z, const Box& box, uint8_t* flags)
 {
-#pragma omp parallel for schedule(dynamic, 4)
+#pragma omp parallel for schedule(dynamic, 4) if(numBoxes > 64)
     for (int64_t b = 0; b < numBoxes; ++b)
     {
         const double* c = bc + 3 * b;
