@@ -146,6 +146,12 @@ PYBIND11_MODULE(_sphx_hip, m)
                              P<int32_t>(ns), P<int32_t>(ne), P<double>(center), P<double>(half), P<double>(x),
                              P<double>(y), P<double>(z), n, toBox(box), P<uint8_t>(flags), St(s));
           });
+    m.def("remote_tree_scatter",
+          [](int64_t M, Ptr nodes, Ptr rc, Ptr rq, Ptr centers, Ptr mp, int forceAccept, double value, Ptr s)
+          {
+              remoteTreeScatter(M, P<int32_t>(nodes), P<double>(rc), P<float>(rq), P<double>(centers), P<float>(mp),
+                                forceAccept, value, St(s));
+          });
     m.def("mark_let_multi",
           [](int nDest, int nbPer, Ptr boxes, Ptr enabled, Ptr child, Ptr n2l, Ptr tc, Ptr th, Ptr gc, int64_t N,
              const BoxArr& box, Ptr failed, Ptr s)
@@ -182,7 +188,7 @@ PYBIND11_MODULE(_sphx_hip, m)
              int nSenders, int self, Ptr bad, Ptr s)
           {
               haloOwnerCheck(nLo, nHalo, end, P<uint64_t>(keys), P<uint64_t>(bounds), nBounds, P<int64_t>(recvStart),
-                             P<int32_t>(senders), nSenders, self, P<unsigned long long>(bad), St(s));
+                             P<int32_t>(senders), nSenders, self, P<double>(bad), St(s));
           });
     m.def("leaving_indices", [](int64_t nSend, Ptr perm, int64_t eSelf, int64_t nStay, Ptr out, Ptr s)
           { leavingIndices(nSend, P<int32_t>(perm), eSelf, nStay, P<int64_t>(out), St(s)); });
@@ -192,8 +198,11 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("unpack_rows", [](int64_t n, Ptr rows, const std::vector<uintptr_t>& dst, const std::vector<int>& sizes,
                             int64_t off, Ptr s) { unpackRows(n, P<void>(rows), dst, sizes, off, St(s)); });
     m.def("reduce_work_bytes", []() { return reduceWorkBytes(); });
-    m.def("multi_min_max", [](int64_t n, const std::vector<uintptr_t>& ptrs, const std::vector<int>& isDouble, Ptr out,
-                              Ptr work, Ptr s) { multiMinMax(n, ptrs, isDouble, P<double>(out), P<void>(work), St(s)); });
+    m.def("multi_min_max",
+          [](int64_t n, const std::vector<uintptr_t>& ptrs, const std::vector<int>& isDouble, Ptr out, Ptr work, Ptr s,
+             int layout) { multiMinMax(n, ptrs, isDouble, P<double>(out), P<void>(work), St(s), layout); },
+          py::arg("n"), py::arg("ptrs"), py::arg("is_double"), py::arg("out"), py::arg("work"), py::arg("s"),
+          py::arg("layout") = 0);
     m.def("max_norm2", [](int64_t first, int64_t last, Ptr ax, Ptr ay, Ptr az, Ptr out, Ptr work, Ptr s)
           { maxNorm2(first, last, P<float>(ax), P<float>(ay), P<float>(az), P<double>(out), P<void>(work), St(s)); });
     m.def("timestep_reduce",

@@ -502,4 +502,36 @@ void packMultipoleRows(int64_t n, const int64_t* idx, const double* gc, const vo
     SPHX_LAUNCH_CHECK();
 }
 
+/*! @brief remote LET tree assembly (ops/gravity.py remote_let_tree): the received multipole m goes to tree node
+ *         nodes[m] (centers: x y z | mass as the MAC slot before the upsweep, quadrupoles: 8 floats); the other rows
+ *         were zeroed. forceAccept: only write value into the MAC slot (w) of the received nodes (after the upsweep:
+ *         received leaves are always accepted) */
+__global__ void remoteTreeScatterKernel(int64_t M, const int32_t* __restrict__ nodes, const double* __restrict__ rc,
+                                        const float* __restrict__ rq, double* __restrict__ centers,
+                                        float* __restrict__ mp, int forceAccept, double value)
+{
+    const int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (k >= M) return;
+    const int64_t nd = nodes[k];
+    if (forceAccept)
+    {
+        centers[4 * nd + 3] = value;
+        return;
+    }
+    centers[4 * nd]     = rc[3 * k];
+    centers[4 * nd + 1] = rc[3 * k + 1];
+    centers[4 * nd + 2] = rc[3 * k + 2];
+    centers[4 * nd + 3] = double(rq[8 * k]);
+    for (int q = 0; q < 8; ++q)
+        mp[8 * nd + q] = rq[8 * k + q];
+}
+
+void remoteTreeScatter(int64_t M, const int32_t* nodes, const double* rc, const float* rq, double* centers, float* mp,
+                       int forceAccept, double value, hipStream_t s)
+{
+    if (M <= 0) return;
+    remoteTreeScatterKernel<<<gridFor(M, 256), 256, 0, s>>>(M, nodes, rc, rq, centers, mp, forceAccept, value);
+    SPHX_LAUNCH_CHECK();
+}
+
 } // namespace sphx::hip

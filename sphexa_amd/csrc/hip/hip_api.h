@@ -66,6 +66,8 @@ void markHalosMulti(int nDest, int nbPer, const double* boxes, const uint8_t* en
                     const int32_t* n2l, const int32_t* ns, const int32_t* ne, const double* center, const double* half,
                     const double* x, const double* y, const double* z, int64_t n, const Box& box, uint8_t* flags,
                     hipStream_t s);
+void remoteTreeScatter(int64_t M, const int32_t* nodes, const double* rc, const float* rq, double* centers, float* mp,
+                       int forceAccept, double value, hipStream_t s);
 void markLetMulti(int nDest, int nbPer, const double* boxes, const uint8_t* enabled, const int32_t* child,
                   const int32_t* n2l, const double* tc, const double* th, const double* gc, int64_t N, const Box& box,
                   uint8_t* failed, hipStream_t s);
@@ -83,7 +85,7 @@ void coarseCut(int64_t N, const int64_t* levelRange, int maxDepth, const int32_t
 void packMultipoleRows(int64_t n, const int64_t* idx, const double* gc, const void* mp, const uint64_t* prefixes,
                        double* rows, hipStream_t s);
 void haloOwnerCheck(int64_t nLo, int64_t nHalo, int64_t end, const uint64_t* keys, const uint64_t* bounds, int nBounds,
-                    const int64_t* recvStart, const int32_t* senders, int nSenders, int self, unsigned long long* bad,
+                    const int64_t* recvStart, const int32_t* senders, int nSenders, int self, double* bad,
                     hipStream_t s);
 void leavingIndices(int64_t nSend, const int32_t* perm, int64_t eSelf, int64_t nStay, int64_t* out, hipStream_t s);
 void gatherMulti(int64_t n, const int32_t* perm, const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,
@@ -106,7 +108,7 @@ void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, siz
 // reduce.hip: single-launch reductions (workspace: reduceWorkBytes(), zero-initialized once; one stream at a time)
 size_t reduceWorkBytes();
 void multiMinMax(int64_t n, const std::vector<uintptr_t>& ptrs, const std::vector<int>& isDouble, double* out,
-                 void* work, hipStream_t s);
+                 void* work, hipStream_t s, int layout = 0);
 void maxNorm2(int64_t first, int64_t last, const float* ax, const float* ay, const float* az, double* out, void* work,
               hipStream_t s);
 void timestepReduce(int64_t first, int64_t last, const float* ax, const float* ay, const float* az,

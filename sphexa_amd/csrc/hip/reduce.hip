@@ -79,9 +79,11 @@ __global__ __launch_bounds__(kRedBlock) void multiMinMaxKernel(int64_t n, Fields
 }
 
 //! one block: out[k] = min (k even) / max (k odd) over the `blocks` partials of value k
+/*! output layout: 0 = [min_0, max_0, min_1, ...]; 1 = the same with negated maxima; 2 = [min_0 .. min_c-1, -max_0 ..
+ *  -max_c-1] (the operands of one MIN all-reduce of mins and maxes, parallel/domain.py / ops/hydro.py) */
 __global__ __launch_bounds__(kRedBlock) void foldMinMaxKernel(int nvals, unsigned blocks,
                                                               const double* __restrict__ partials,
-                                                              double* __restrict__ out)
+                                                              double* __restrict__ out, int layout)
 {
     __shared__ double red[kRedBlock / 64];
     auto mn = [](double a, double b) { return nanMin(a, b); };
@@ -93,7 +95,12 @@ __global__ __launch_bounds__(kRedBlock) void foldMinMaxKernel(int nvals, unsigne
         for (unsigned b = threadIdx.x; b < blocks; b += kRedBlock)
             v = isMin ? nanMin(v, partials[k * blocks + b]) : nanMax(v, partials[k * blocks + b]);
         v = isMin ? blockReduce(v, red, mn) : blockReduce(v, red, mx);
-        if (threadIdx.x == 0) out[k] = v;
+        if (threadIdx.x == 0)
+        {
+            if (layout == 0) out[k] = v;
+            else if (layout == 1) out[k] = isMin ? v : -v;
+            else out[isMin ? (k >> 1) : (nvals >> 1) + (k >> 1)] = isMin ? v : -v;
+        }
     }
 }
 
@@ -195,7 +202,7 @@ unsigned blocksFor(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<in
 size_t reduceWorkBytes() { return size_t(8 * kRedBlocks) * sizeof(double) + 256; }
 
 void multiMinMax(int64_t n, const std::vector<uintptr_t>& ptrs, const std::vector<int>& isDouble, double* out,
-                 void* work, hipStream_t s)
+                 void* work, hipStream_t s, int layout)
 {
     if (ptrs.empty() || ptrs.size() > 4 || ptrs.size() != isDouble.size())
         throw std::runtime_error("multiMinMax: 1 to 4 fields");
@@ -211,7 +218,7 @@ void multiMinMax(int64_t n, const std::vector<uintptr_t>& ptrs, const std::vecto
     const unsigned blocks = blocksFor(n);
     multiMinMaxKernel<<<blocks, kRedBlock, 0, s>>>(n, f, partials);
     SPHX_LAUNCH_CHECK();
-    foldMinMaxKernel<<<1, kRedBlock, 0, s>>>(2 * f.count, blocks, partials, out);
+    foldMinMaxKernel<<<1, kRedBlock, 0, s>>>(2 * f.count, blocks, partials, out, layout);
     SPHX_LAUNCH_CHECK();
 }
 

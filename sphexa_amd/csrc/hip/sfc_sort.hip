@@ -328,7 +328,7 @@ void leavingIndices(int64_t nSend, const int32_t* perm, int64_t eSelf, int64_t n
 __global__ void haloOwnerCheckKernel(int64_t nLo, int64_t nHalo, int64_t end, const uint64_t* __restrict__ keys,
                                      const uint64_t* __restrict__ bounds, int nBounds,
                                      const int64_t* __restrict__ recvStart, const int32_t* __restrict__ senders,
-                                     int nSenders, int self, unsigned long long* __restrict__ bad)
+                                     int nSenders, int self, double* __restrict__ bad)
 {
     const int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     bool wrong      = false;
@@ -352,11 +352,13 @@ __global__ void haloOwnerCheckKernel(int64_t nLo, int64_t nHalo, int64_t end, co
         wrong = lo != senders[a] || lo == self;
     }
     const uint64_t m = __ballot(wrong);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, (unsigned long long)__popcll(m));
+    // (a float64 count: the deferred check rides in the propagator's float64 time-step packet without a conversion;
+    // counts are exact integers far below 2^53)
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, double(__popcll(m)));
 }
 
 void haloOwnerCheck(int64_t nLo, int64_t nHalo, int64_t end, const uint64_t* keys, const uint64_t* bounds, int nBounds,
-                    const int64_t* recvStart, const int32_t* senders, int nSenders, int self, unsigned long long* bad,
+                    const int64_t* recvStart, const int32_t* senders, int nSenders, int self, double* bad,
                     hipStream_t s)
 {
     if (nHalo <= 0) return;

@@ -115,7 +115,8 @@ class Propagator:
                                  ride_along=(lambda out: H.global_h_min_device(d, domain.comm, out)) if gpu else None,
                                  speculate=speculate, after_launch=after_launch)
         if gpu:
-            H.apply_global_h_min(d, self.nl.ride_along)
+            # (with several ranks the ride-along holds the maxima negated: global_h_min_device)
+            H.apply_global_h_min(d, self.nl.ride_along, neg_max=domain.size > 1 and d["h"].numel() > 0)
             # the previous step's time-step copy completed before the search statistics did (same stream)
             self.finish_host(d)
         return bool(spec) and self.nl.speculated and H.speculation_holds(d, domain.box, spec[0])

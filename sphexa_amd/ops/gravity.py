@@ -330,23 +330,32 @@ def remote_let_tree(codes: torch.Tensor, rcenters: torch.Tensor, rquads: torch.T
     nox = torch.empty(0, dtype=torch.float64)
     ot_h = build_octree(tree_h, torch.zeros(L, dtype=torch.int32), torch.empty(0, dtype=torch.int64), nox, nox, nox,
                         0)
+    # tree node of every received multipole (host: the tree is there)
+    nodes_h = torch.from_numpy(ot_h.leaf_to_node.numpy()[leaf_of].astype(np.int32))
     if dev.type == "cuda":
         def up(t):
             return t.pin_memory().to(dev, non_blocking=True)
 
         ot = dataclasses.replace(ot_h, **{f.name: up(getattr(ot_h, f.name)) for f in dataclasses.fields(ot_h)
                                           if isinstance(getattr(ot_h, f.name), torch.Tensor)})
-        leaf_idx = up(torch.from_numpy(leaf_of.astype(np.int64)))
+        nodes = up(nodes_h)
     else:
-        ot, leaf_idx = ot_h, torch.from_numpy(leaf_of.astype(np.int64))
+        ot, nodes = ot_h, nodes_h.long()
     N = ot.num_nodes
-    nodes = ot.leaf_to_node.long()[leaf_idx]
-    centers = torch.zeros(N, 4, dtype=torch.float64, device=dev)
-    mp = torch.zeros(N, 8, dtype=torch.float32, device=dev)
-    centers[:, :3].index_copy_(0, nodes, rcenters)
-    centers[:, 3].index_copy_(0, nodes, rquads[:, 0].double())
-    mp.index_copy_(0, nodes, rquads)
-    centers, mp = centers.view(-1), mp.view(-1)
+    if dev.type == "cuda":
+        # zeroed rows, the received multipoles scattered to their nodes: native launches (no torch kernels in a step)
+        centers = zero_(torch.empty(4 * N, dtype=torch.float64, device=dev))
+        mp = zero_(torch.empty(8 * N, dtype=torch.float32, device=dev))
+        _lib.hip().remote_tree_scatter(nodes.numel(), nodes.data_ptr(), rcenters.contiguous().data_ptr(),
+                                       rquads.contiguous().data_ptr(), centers.data_ptr(), mp.data_ptr(), 0, 0.0,
+                                       _stream())
+    else:
+        centers = torch.zeros(N, 4, dtype=torch.float64, device=dev)
+        mp = torch.zeros(N, 8, dtype=torch.float32, device=dev)
+        centers[:, :3].index_copy_(0, nodes, rcenters)
+        centers[:, 3].index_copy_(0, nodes, rquads[:, 0].double())
+        mp.index_copy_(0, nodes, rquads)
+        centers, mp = centers.view(-1), mp.view(-1)
     inv_theta = 1.0 / theta
     if dev.type == "cuda":
         h = _lib.hip()
@@ -362,7 +371,11 @@ def remote_let_tree(codes: torch.Tensor, rcenters: torch.Tensor, rquads: torch.T
                                    ot.prefixes.data_ptr(), ot.node_start.data_ptr(), ot.node_end.data_ptr(), 0, 0, 0, 0,
                                    box.to_array(), sfc_kind, inv_theta, centers.data_ptr(), mp.data_ptr(),
                                    leavesGiven=True)
-    centers.view(-1, 4)[:, 3].index_fill_(0, nodes, FORCE_ACCEPT_MAC2)
+    if dev.type == "cuda":
+        _lib.hip().remote_tree_scatter(nodes.numel(), nodes.data_ptr(), 0, 0, centers.data_ptr(), mp.data_ptr(), 1,
+                                       float(FORCE_ACCEPT_MAC2), _stream())
+    else:
+        centers.view(-1, 4)[:, 3].index_fill_(0, nodes, FORCE_ACCEPT_MAC2)
     return ot, centers, mp
 
 

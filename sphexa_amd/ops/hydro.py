@@ -219,6 +219,12 @@ def global_h_min_device(d, comm, out: torch.Tensor | None = None) -> torch.Tenso
     if h.numel():
         from .reduce import min_max
 
+        if multi and h.is_cuda and out is not None:
+            # [min h, -max h, min m, -max m] written by the reduction, reduced in place; the host flips the signs
+            # (apply_global_h_min(neg_max=True)): no elementwise torch kernels in the step
+            min_max([h, m], out=out, layout=1)
+            comm.allreduce(out, "min")
+            return out
         mm = min_max([h, m], out=None if multi else out)  # [min h, max h, min m, max m], one launch on the GPU
         if not multi:
             return mm
@@ -238,10 +244,13 @@ def global_h_min_device(d, comm, out: torch.Tensor | None = None) -> torch.Tenso
     return loc
 
 
-def apply_global_h_min(d, vals):
-    """store the host values of global_h_min_device ([min h, max h, min m, max m]): the per-step h extremes of the
-    fixed-point guard and frame, and the uniform-mass cache keyed on the current mass tensor"""
+def apply_global_h_min(d, vals, neg_max: bool = False):
+    """store the host values of global_h_min_device ([min h, max h, min m, max m]; ``neg_max``: the maxima negated, as
+    its multi-rank ride-along form leaves them): the per-step h extremes of the fixed-point guard and frame, and the
+    uniform-mass cache keyed on the current mass tensor"""
     hmin, hmax, mlo, mhi = (float(v) for v in vals)
+    if neg_max:
+        hmax, mhi = -hmax, -mhi
     m = d["m"][: d.size]
     d._h_min_global = hmin
     d._h_max_global = hmax

@@ -288,7 +288,8 @@ def _build_octree_hip(tree, counts, keys, x, y, z, offset) -> Octree:
     h.sort_pairs_i64_i32(N, codes.data_ptr(), codes_s.data_ptr(), vals.data_ptr(), vals_s.data_ptr(),
                          tmp.data_ptr(), tmp.numel(), 0, 64, s)
     child = torch.empty(N, dtype=torch.int32, device=dev)
-    parents = torch.full(((N - 1) // 8 + 1,), -1, dtype=torch.int32, device=dev)
+    parents = torch.empty(((N - 1) // 8 + 1,), dtype=torch.int32, device=dev)
+    h.fill32(parents.data_ptr(), 0xFFFFFFFF, parents.numel(), _stream())  # -1 (native fill, no torch kernel)
     leaf_to_node = torch.empty(L, dtype=torch.int32, device=dev)
     level_range = torch.empty(MAX_LEVEL + 2, dtype=torch.int64, device=dev)
     h.link_nodes(codes_s.data_ptr(), vals_s.data_ptr(), N, child.data_ptr(), parents.data_ptr(),

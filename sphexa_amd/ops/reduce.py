@@ -26,17 +26,20 @@ def _work(device) -> torch.Tensor:
     return t
 
 
-def min_max(tensors: Sequence[torch.Tensor], out: torch.Tensor | None = None) -> torch.Tensor:
+def min_max(tensors: Sequence[torch.Tensor], out: torch.Tensor | None = None, layout: int = 0) -> torch.Tensor:
     """float64 tensor [min_0, max_0, min_1, max_1, ...] of 1 to 4 equal-length float32/float64 tensors (empty:
-    +max / -max of float64); ``out`` (GPU): destination (2 x count float64 on the device)"""
+    +max / -max of float64); ``out`` (GPU): destination (2 x count float64 on the device). ``layout`` (GPU): 1 = the
+    maxima negated in place, 2 = [mins..., -maxes...] (operands of one MIN all-reduce, written by the kernel)"""
     dev = tensors[0].device
     if dev.type == "cuda":
         if out is None:
             out = torch.empty(2 * len(tensors), dtype=torch.float64, device=dev)
         n = tensors[0].numel()
         _lib.hip().multi_min_max(n, [t.data_ptr() for t in tensors], [int(t.dtype == torch.float64) for t in tensors],
-                                 out.data_ptr(), _work(dev).data_ptr(), _lib.stream())
+                                 out.data_ptr(), _work(dev).data_ptr(), _lib.stream(), layout)
         return out
+    if layout:
+        raise ValueError("min_max layout: GPU only")
     big = torch.finfo(torch.float64).max
     vals = []
     for t in tensors:

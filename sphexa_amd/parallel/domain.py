@@ -163,13 +163,15 @@ class Domain:
         kernels either), the allreduced [min x, min y, min z, -max x, -max y, -max z] on several"""
         from ..ops.reduce import min_max
 
-        mm = min_max([x, y, z])  # one launch on the GPU
         if self.size > 1:
-            mm = mm.view(3, 2)
-            ext = torch.cat([mm[:, 0], -mm[:, 1]])
+            if x.is_cuda:
+                ext = min_max([x, y, z], layout=2)  # [mins, -maxes] written by the reduction itself
+            else:
+                mm = min_max([x, y, z]).view(3, 2)
+                ext = torch.cat([mm[:, 0], -mm[:, 1]])
             self.comm.allreduce(ext, MIN)
             return ext
-        return mm
+        return min_max([x, y, z])  # one launch on the GPU
 
     def _box_ext(self, v):
         return v if self.size > 1 else [v[0], v[2], v[4], -v[1], -v[3], -v[5]]
@@ -311,15 +313,18 @@ class Domain:
                     sfc_ops.compute_keys(d["x"][sl], d["y"][sl], d["z"][sl], self.box, self.sfc_kind,
                                          out=d["keys"][sl])
             if self.check_halos:
-                bad = self._halo_ownership_bad(d["keys"])
-                if bad is not None:
-                    if bad.is_cuda and self.check_halos != "immediate":
-                        # deferred: the count reaches the host with the propagator's time-step copy (pending_checks),
-                        # i.e. the raise comes after the step's physics ran on the bad halos (the state is advanced
-                        # when it fires); check_halos="immediate" checks here, before any physics (one host copy)
-                        self._pending_bad = bad if self._pending_bad is None else self._pending_bad + bad
-                    else:
-                        self._raise_bad_halos(int(bad))
+                deferred = d["keys"].is_cuda and self.check_halos != "immediate"
+                if deferred and self._pending_bad is None and self.n_lo + self.n_hi:
+                    from ..ops.reduce import zero_
+
+                    self._pending_bad = zero_(torch.empty(1, dtype=torch.float64, device=d.device))
+                bad = self._halo_ownership_bad(d["keys"], acc=self._pending_bad if deferred else None)
+                if bad is not None and not deferred:
+                    # check_halos="immediate" (or the CPU path) checks here, before any physics (one host copy);
+                    # deferred, the count accumulates on the device and reaches the host with the propagator's
+                    # time-step copy (pending_checks), i.e. the raise comes after the step's physics ran on the bad
+                    # halos (the state is advanced when it fires)
+                    self._raise_bad_halos(int(bad.sum()))
             PROF.mark("sync: halo keys + ownership check")
         # native kernels write h in place (h iteration, h update) without bumping the tensor version: drop the
         # cached per-step reductions of h and m so the pair loops re-derive them for the new particle set
@@ -665,9 +670,10 @@ class Domain:
                 peers.add(q)
         return peers
 
-    def _halo_ownership_bad(self, keys: torch.Tensor):
-        """number of halos (device int64 scalar) not owned by the rank that sent them, or that fall into this rank's own
-        range (the push-based analog of the reference's checkHalos, halos/halos.hpp:73-105); None without halos"""
+    def _halo_ownership_bad(self, keys: torch.Tensor, acc: Optional[torch.Tensor] = None):
+        """number of halos not owned by the rank that sent them, or that fall into this rank's own range (the
+        push-based analog of the reference's checkHalos, halos/halos.hpp:73-105); None without halos. GPU: a float64
+        (1,) device tensor, ``acc`` if given (the count is added to it), so deferred counts accumulate natively"""
         if self.n_lo + self.n_hi == 0:
             return None
         dev = keys.device
@@ -683,11 +689,11 @@ class Domain:
             bnd = self._upload(np.array(self.assignment_keys[1:-1], dtype=np.uint64).view(np.int64), dev)
             rs = self._upload(starts, dev)
             sd = self._upload(np.array(senders, dtype=np.int32), dev)
-            bad = zero_(torch.empty(1, dtype=torch.int64, device=dev))
+            bad = acc if acc is not None else zero_(torch.empty(1, dtype=torch.float64, device=dev))
             _lib.hip().halo_owner_check(self.n_lo, self.n_lo + self.n_hi, self.end, keys.data_ptr(), bnd.data_ptr(),
                                         bnd.numel(), rs.data_ptr(), sd.data_ptr(), len(senders), self.rank,
                                         bad.data_ptr(), _stream())
-            return bad[0]
+            return bad
         bounds = torch.tensor([k if k < 2 ** 63 else 2 ** 63 - 1 for k in self.assignment_keys[1:-1]],
                               dtype=torch.int64).to(dev, non_blocking=True)
         halo_keys = torch.cat([keys[: self.start], keys[self.end:]])
@@ -706,14 +712,14 @@ class Domain:
         """immediate form of the ownership check (one host copy)"""
         bad = self._halo_ownership_bad(keys)
         if bad is not None:
-            self._raise_bad_halos(int(bad))
+            self._raise_bad_halos(int(bad.sum()))
 
     def pending_checks(self):
         """deferred device-side checks of the last sync (float64 device tensor) for the propagator's time-step copy,
         or None; the host values go to ``finish_checks``"""
         if self._pending_bad is None:
             return None
-        return self._pending_bad.to(torch.float64).reshape(1)
+        return self._pending_bad  # (float64 (1,), accumulated by the ownership-check kernel)
 
     def finish_checks(self, vals):
         self._pending_bad = None
