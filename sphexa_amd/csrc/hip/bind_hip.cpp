@@ -169,8 +169,10 @@ PYBIND11_MODULE(_sphx_hip, m)
           });
     m.def("flag_words", [](int nRows, int64_t n, Ptr flags, Ptr wcnt, Ptr count, int countStride, Ptr s)
           { flagWords(nRows, n, P<uint8_t>(flags), P<int64_t>(wcnt), P<int64_t>(count), countStride, St(s)); });
-    m.def("scatter_flag_indices", [](int nRows, int64_t n, Ptr flags, Ptr wpos, Ptr out, Ptr s)
-          { scatterFlagIndices(nRows, n, P<uint8_t>(flags), P<int64_t>(wpos), P<int64_t>(out), St(s)); });
+    m.def("scatter_flag_indices", [](int nRows, int64_t n, Ptr flags, Ptr wpos, Ptr out, Ptr s, int64_t offset)
+          { scatterFlagIndices(nRows, n, P<uint8_t>(flags), P<int64_t>(wpos), P<int64_t>(out), St(s), offset); },
+          py::arg("n_rows"), py::arg("n"), py::arg("flags"), py::arg("wpos"), py::arg("out"), py::arg("s"),
+          py::arg("offset") = 0);
     m.def("range_counts", [](int64_t n, Ptr keys, Ptr bounds, int nRanks, Ptr out, int outStride, Ptr s)
           { rangeCounts(n, P<uint64_t>(keys), P<uint64_t>(bounds), nRanks, P<int64_t>(out), outStride, St(s)); });
     m.def("coarse_cut",
@@ -231,6 +233,10 @@ PYBIND11_MODULE(_sphx_hip, m)
     // ---------------------------------------------------------------------------------------------- octree
     m.def("node_counts", [](Ptr tree, int64_t L, Ptr keys, int64_t n, Ptr counts, Ptr s)
           { nodeCounts(P<KeyT>(tree), L, P<KeyT>(keys), n, P<int32_t>(counts), St(s)); });
+    m.def("node_counts64", [](Ptr tree, int64_t L, Ptr keys, int64_t n, Ptr counts, Ptr s)
+          { nodeCounts64(P<KeyT>(tree), L, P<KeyT>(keys), n, P<int64_t>(counts), St(s)); });
+    m.def("split_multipole_rows", [](int64_t n, Ptr rows, Ptr centers, Ptr quads, Ptr codes, Ptr s)
+          { splitMultipoleRows(n, P<double>(rows), P<double>(centers), P<float>(quads), P<int64_t>(codes), St(s)); });
     m.def("rebalance_ops", [](Ptr tree, Ptr counts, int64_t L, uint32_t bucket, Ptr ops, Ptr flag, Ptr s)
           { rebalanceOps(P<KeyT>(tree), P<int32_t>(counts), L, bucket, P<int64_t>(ops), P<int>(flag), St(s)); });
     m.def("emit_leaves", [](Ptr tree, Ptr ops, int64_t L, Ptr out, int64_t newL, Ptr s)

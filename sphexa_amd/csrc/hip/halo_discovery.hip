@@ -299,7 +299,7 @@ void flagWords(int nRows, int64_t n, const uint8_t* flags, int64_t* wcnt, int64_
 /*! @brief out[wpos[q][w] + rank of i within its word] = i for every set flag i of row q (the rows' lists concatenate
  *         in row order: wpos is the exclusive scan of the word counts over all rows) */
 __global__ void scatterFlagIndicesKernel(int64_t n, int64_t nw, const uint8_t* __restrict__ flags,
-                                         const int64_t* __restrict__ wpos, int64_t* __restrict__ out)
+                                         const int64_t* __restrict__ wpos, int64_t* __restrict__ out, int64_t offset)
 {
     const int q       = blockIdx.y;
     const int64_t w   = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -309,14 +309,16 @@ __global__ void scatterFlagIndicesKernel(int64_t n, int64_t nw, const uint8_t* _
     const int64_t i0  = w * 64;
     const int64_t i1  = i0 + 64 < n ? i0 + 64 : n;
     for (int64_t i = i0; i < i1; ++i)
-        if (fq[i]) out[pos++] = i;
+        if (fq[i]) out[pos++] = i + offset;
 }
 
-void scatterFlagIndices(int nRows, int64_t n, const uint8_t* flags, const int64_t* wpos, int64_t* out, hipStream_t s)
+//! (offset: added to every index, e.g. the layout's lower-halo count for absolute send indices)
+void scatterFlagIndices(int nRows, int64_t n, const uint8_t* flags, const int64_t* wpos, int64_t* out, hipStream_t s,
+                        int64_t offset)
 {
     const int64_t nw = (n + 63) / 64;
     if (nw <= 0 || nRows == 0) return;
-    scatterFlagIndicesKernel<<<dim3(unsigned((nw + 255) / 256), nRows), 256, 0, s>>>(n, nw, flags, wpos, out);
+    scatterFlagIndicesKernel<<<dim3(unsigned((nw + 255) / 256), nRows), 256, 0, s>>>(n, nw, flags, wpos, out, offset);
     SPHX_LAUNCH_CHECK();
 }
 
@@ -499,6 +501,29 @@ void packMultipoleRows(int64_t n, const int64_t* idx, const double* gc, const vo
     if (n <= 0) return;
     packMultipoleRowsKernel<<<gridFor(n, 256), 256, 0, s>>>(n, idx, gc, static_cast<const Quadrupole*>(mp), prefixes,
                                                             rows);
+    SPHX_LAUNCH_CHECK();
+}
+
+//! @brief received multipole rows (packMultipoleRows layout) -> centers (n x 3 f64), quadrupoles (n x 8 f32), codes
+__global__ void splitMultipoleRowsKernel(int64_t n, const double* __restrict__ rows, double* __restrict__ centers,
+                                         float* __restrict__ quads, int64_t* __restrict__ codes)
+{
+    const int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const double* r = rows + 8 * k;
+    centers[3 * k]     = r[0];
+    centers[3 * k + 1] = r[1];
+    centers[3 * k + 2] = r[2];
+    const float* q     = reinterpret_cast<const float*>(r + 3);
+    for (int j = 0; j < 8; ++j)
+        quads[8 * k + j] = q[j];
+    codes[k] = __double_as_longlong(r[7]);
+}
+
+void splitMultipoleRows(int64_t n, const double* rows, double* centers, float* quads, int64_t* codes, hipStream_t s)
+{
+    if (n <= 0) return;
+    splitMultipoleRowsKernel<<<gridFor(n, 256), 256, 0, s>>>(n, rows, centers, quads, codes);
     SPHX_LAUNCH_CHECK();
 }
 

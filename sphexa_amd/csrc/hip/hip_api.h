@@ -77,7 +77,9 @@ void letSelectMulti(int nDest, int64_t N, int64_t L, int64_t np, const uint8_t* 
                     hipStream_t s);
 void flagWords(int nRows, int64_t n, const uint8_t* flags, int64_t* wcnt, int64_t* count, int countStride,
                hipStream_t s);
-void scatterFlagIndices(int nRows, int64_t n, const uint8_t* flags, const int64_t* wpos, int64_t* out, hipStream_t s);
+void scatterFlagIndices(int nRows, int64_t n, const uint8_t* flags, const int64_t* wpos, int64_t* out, hipStream_t s,
+                        int64_t offset = 0);
+void splitMultipoleRows(int64_t n, const double* rows, double* centers, float* quads, int64_t* codes, hipStream_t s);
 void rangeCounts(int64_t n, const uint64_t* keys, const uint64_t* bounds, int nRanks, int64_t* out, int outStride,
                  hipStream_t s);
 void coarseCut(int64_t N, const int64_t* levelRange, int maxDepth, const int32_t* n2l, const double* center,
@@ -128,6 +130,7 @@ void memsetAsync(void* p, int value, size_t bytes, hipStream_t s);
 
 // octree.hip
 void nodeCounts(const KeyT* tree, int64_t L, const KeyT* keys, int64_t n, int32_t* counts, hipStream_t s);
+void nodeCounts64(const KeyT* tree, int64_t L, const KeyT* keys, int64_t n, int64_t* counts, hipStream_t s);
 void rebalanceOps(const KeyT* tree, const int32_t* counts, int64_t L, uint32_t bucket, int64_t* ops, int* changed,
                   hipStream_t s);
 void emitLeavesLaunch(const KeyT* tree, const int64_t* ops, int64_t L, KeyT* out, int64_t newL, hipStream_t s);

@@ -16,17 +16,26 @@
 namespace sphx::hip
 {
 
+template<class C>
 __global__ void nodeCountsKernel(const KeyT* __restrict__ tree, int64_t L, const KeyT* __restrict__ keys, int64_t n,
-                                 int32_t* __restrict__ counts)
+                                 C* __restrict__ counts)
 {
     int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= L) return;
     int64_t a = lowerBound(keys, n, tree[i]);
     int64_t b = lowerBound(keys, n, tree[i + 1]);
-    counts[i] = int32_t(b - a);
+    counts[i] = C(b - a);
 }
 
 void nodeCounts(const KeyT* tree, int64_t L, const KeyT* keys, int64_t n, int32_t* counts, hipStream_t s)
+{
+    if (L == 0) return;
+    nodeCountsKernel<<<gridFor(L, 256), 256, 0, s>>>(tree, L, keys, n, counts);
+    SPHX_LAUNCH_CHECK();
+}
+
+//! int64 counts: the operand of the global-tree count all-reduce (parallel/domain.py), without a widening pass
+void nodeCounts64(const KeyT* tree, int64_t L, const KeyT* keys, int64_t n, int64_t* counts, hipStream_t s)
 {
     if (L == 0) return;
     nodeCountsKernel<<<gridFor(L, 256), 256, 0, s>>>(tree, L, keys, n, counts);

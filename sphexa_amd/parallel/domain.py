@@ -385,7 +385,12 @@ class Domain:
             tree = self._upload(tree_np.view(np.int64), dev)
         for _ in range(64):
             # local counts on the replicated tree -> global counts -> identical rebalance on every rank
-            gcounts = octree_ops.node_counts(tree, skeys).to(torch.int64)
+            if skeys.is_cuda:
+                gcounts = torch.empty(tree.numel() - 1, dtype=torch.int64, device=dev)
+                _lib.hip().node_counts64(tree.data_ptr(), tree.numel() - 1, skeys.data_ptr(), skeys.numel(),
+                                         gcounts.data_ptr(), _stream())
+            else:
+                gcounts = octree_ops.node_counts(tree, skeys).to(torch.int64)
             self.comm.allreduce(gcounts, SUM)
             c_np = gcounts.cpu().numpy()
             new_np, changed = _lib.cpu().rebalance(tree_np, c_np.clip(max=2**32 - 1).astype(np.uint32), bucket)
@@ -458,8 +463,14 @@ class Domain:
         # each run is SFC-sorted, so one merge gives the new order
         n_lo = sum(rc[:r])
         rkeys = outs[0]
-        kcat = torch.cat([rkeys[:n_lo], skeys[e_self:e_self + n_stay], rkeys[n_lo:]]) if n_recv else \
-            skeys[e_self:e_self + n_stay]
+        if n_recv:
+            # (three contiguous device copies instead of a cat kernel)
+            kcat = torch.empty(n_recv + n_stay, dtype=skeys.dtype, device=dev)
+            kcat[:n_lo].copy_(rkeys[:n_lo])
+            kcat[n_lo:n_lo + n_stay].copy_(skeys[e_self:e_self + n_stay])
+            kcat[n_lo + n_stay:].copy_(rkeys[n_lo:])
+        else:
+            kcat = skeys[e_self:e_self + n_stay]
         runs = rc[:r] + [n_stay] + rc[r + 1:]
         fkeys, pm = sfc_ops.merge_sorted_runs(kcat, runs)
         PROF.mark("distribute: unpack + merge")
@@ -613,16 +624,18 @@ class Domain:
         send_h, recv_h = host[: size], host[size:]
         PROF.mark("halos: count exchange")
 
-        def compact(flags, n, wcnt, col):
+        def compact(flags, n, wcnt, col, offset=0):
             total = int(send_h[:, col].sum())
             out = torch.empty(total + 1, dtype=torch.int64, device=dev)
             if total:
                 pos = sfc_ops.exclusive_scan(wcnt)
-                hp.scatter_flag_indices(size, n, flags.data_ptr(), pos.data_ptr(), out.data_ptr(), st)
+                hp.scatter_flag_indices(size, n, flags.data_ptr(), pos.data_ptr(), out.data_ptr(), st, offset)
             offs = np.cumsum([0] + [int(v) for v in send_h[:, col]])
             return out[:total], [out[offs[q]:offs[q + 1]] for q in range(size)]
 
-        cat_p, send_idx = compact(pflags, n_own, wcnt_p, 0)
+        # particle send lists as absolute indices of the new layout (the lower-halo count is added by the scatter)
+        n_lo_new = int(recv_h[: self.rank, 0].sum())
+        cat_abs, send_abs = compact(pflags, n_own, wcnt_p, 0, n_lo_new)
         if gravity:
             mp_cat, mp_send = compact(nflags, N, wcnt_n, 1)
             del nflags
@@ -632,15 +645,13 @@ class Domain:
             self._exchange_multipoles(mp_send, gcenters, gquads, ot.prefixes, [int(v) for v in recv_h[:, 1]],
                                       idx_cat=mp_cat)
             PROF.mark("halos: multipole exchange + remote LET tree")
-        self.halo_send_counts = [int(t.numel()) for t in send_idx]
+        self.halo_send_counts = [int(t.numel()) for t in send_abs]
         self.halo_recv_counts = [int(v) for v in recv_h[:, 0]]
         self.n_lo = sum(self.halo_recv_counts[: self.rank])
         self.n_hi = sum(self.halo_recv_counts[self.rank + 1:])
-        self._halo_send_rel = send_idx
-        # absolute indices: one add over the concatenated list; the per-destination lists are views of it
-        cat_abs = cat_p + self.n_lo
-        offs = np.cumsum([0] + self.halo_send_counts)
-        self.halo_send_idx = [cat_abs[offs[q]:offs[q + 1]] for q in range(size)]
+        assert self.n_lo == n_lo_new
+        # absolute indices (the scatter added n_lo); the per-destination lists are views of the concatenated one
+        self.halo_send_idx = send_abs
         self._halo_send_cat = cat_abs
 
     def _halo_peers(self, all_boxes, ot) -> set:
@@ -743,9 +754,17 @@ class Domain:
             rows = torch.cat([gcenters.view(-1, 4)[idx, :3], gquads.view(-1, 8)[idx].contiguous().view(torch.float64),
                               prefixes[idx].view(torch.float64).view(-1, 1)], dim=1)
         recv, _ = self.comm.alltoallv(rows, counts, recv_counts)
-        self.remote_centers = recv[:, :3].contiguous()
-        self.remote_quads = recv[:, 3:7].contiguous().view(torch.float32).view(-1, 8)
-        self.remote_codes = recv[:, 7].contiguous().view(torch.int64)
+        if recv.is_cuda:
+            M = recv.shape[0]
+            self.remote_centers = torch.empty((M, 3), dtype=torch.float64, device=recv.device)
+            self.remote_quads = torch.empty((M, 8), dtype=torch.float32, device=recv.device)
+            self.remote_codes = torch.empty(M, dtype=torch.int64, device=recv.device)
+            _lib.hip().split_multipole_rows(M, recv.data_ptr(), self.remote_centers.data_ptr(),
+                                            self.remote_quads.data_ptr(), self.remote_codes.data_ptr(), _stream())
+        else:
+            self.remote_centers = recv[:, :3].contiguous()
+            self.remote_quads = recv[:, 3:7].contiguous().view(torch.float32).view(-1, 8)
+            self.remote_codes = recv[:, 7].contiguous().view(torch.int64)
         self.stats["remote_multipoles"] = recv.shape[0]
         self._remote_tree = None
         self._remote_pending = None
