@@ -185,6 +185,14 @@ class Comm:
                 self._audit("allgather", src)
                 dist.all_gather_into_tensor(out, src, group=self.group)
             return out
+        if self._staged(t):
+            # gloo with a device tensor: stacked on the host, one copy up (no device concatenation kernel)
+            with timed_comm("allgather_fixed", t, True):
+                src = _stage_host(t)
+                outs = [torch.empty_like(src) for _ in range(self.size)]
+                self._audit("allgather", src)
+                dist.all_gather(outs, src, group=self.group)
+                return _stage_dev(torch.stack(outs), t.device)
         return torch.stack(self.allgather_fixed(t))
 
     def alltoallv(self, send: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int] | None = None,
