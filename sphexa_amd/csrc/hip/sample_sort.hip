@@ -511,7 +511,7 @@ __global__ void __launch_bounds__(kScanBlock) scanTilesKernel(T* in, T* out, int
             if (t0 + k < n) in[t0 + k] = T(0);
     }
     T total;
-    T run = blockExclusiveScan(s, total) + offs[blockIdx.x];
+    T run = blockExclusiveScan(s, total) + (offs ? offs[blockIdx.x] : T(0));
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k)
     {
@@ -526,6 +526,13 @@ template<class T>
 void exclusiveScanTiles(T* in, T* out, int64_t n, T* sums, bool zeroIn, hipStream_t s)
 {
     const int64_t tiles = (n + kScanTile - 1) / kScanTile;
+    if (tiles == 1)
+    {
+        // one tile (the bucket counts of sorts up to ~3.6 M keys): no tile sums, one launch instead of three
+        scanTilesKernel<T><<<1, kScanBlock, 0, s>>>(in, out, n, nullptr, zeroIn);
+        SPHX_LAUNCH_CHECK();
+        return;
+    }
     scanTileSumsKernel<T><<<unsigned(tiles), kScanBlock, 0, s>>>(in, n, sums);
     scanSumsKernel<T><<<1, 1024, 0, s>>>(sums, tiles);
     scanTilesKernel<T><<<unsigned(tiles), kScanBlock, 0, s>>>(in, out, n, sums, zeroIn);
@@ -535,9 +542,17 @@ void exclusiveScanTiles(T* in, T* out, int64_t n, T* sums, bool zeroIn, hipStrea
 //! buckets of a sort of n elements
 inline int64_t bucketsFor(int64_t n) { return (n + kTarget - 1) / kTarget; }
 
-/*! @brief the recursive sort; with base == nullptr only the workspace size is accumulated in bump.off */
+//! sample sorts of at most this many keys use buckets of kTargetSmall with 8 samples per bucket: their sample then
+//! fits one 512-pair wave sort and the bucket waves sort 4 items per lane (a latency chain: Evrard -n 100 sorts 8272
+//! samples, whose 10 buckets of ~830 keys took 32 us in one wave each)
+constexpr int64_t kSmallSort  = 14336;
+constexpr int kTargetSmall    = 224;
+constexpr int kOverSmall      = 8;
+
+/*! @brief the recursive sort; with base == nullptr only the workspace size is accumulated in bump.off. ``top``: the
+ *         caller's sort (the recursive calls sort samples) */
 void sortRec(int64_t n, const uint64_t* keysIn, const uint32_t* valsIn, uint64_t* keysOut, uint32_t* valsOut,
-             Bump& bump, hipStream_t s)
+             Bump& bump, hipStream_t s, bool top = true)
 {
     if (n <= 0) return;
     const bool run = bump.base != nullptr;
@@ -550,8 +565,9 @@ void sortRec(int64_t n, const uint64_t* keysIn, const uint32_t* valsIn, uint64_t
         }
         return;
     }
-    const int64_t B = bucketsFor(n);
-    const int64_t S = std::min<int64_t>(n, B * kOver);
+    const bool small = !top && n <= kSmallSort;
+    const int64_t B  = small ? (n + kTargetSmall - 1) / kTargetSmall : bucketsFor(n);
+    const int64_t S  = std::min<int64_t>(n, B * (small ? kOverSmall : kOver));
     uint64_t* sample  = bump.take<uint64_t>(S);
     uint64_t* sorted  = bump.take<uint64_t>(S);
     uint32_t* sortedV = bump.take<uint32_t>(S);
@@ -567,7 +583,7 @@ void sortRec(int64_t n, const uint64_t* keysIn, const uint32_t* valsIn, uint64_t
         sampleKernel<<<gridFor(S, 256), 256, 0, s>>>(n, keysIn, S, sample);
         SPHX_LAUNCH_CHECK();
     }
-    sortRec(S, sample, nullptr, sorted, sortedV, bump, s);
+    sortRec(S, sample, nullptr, sorted, sortedV, bump, s, false);
     if (!run) return;
     splitterKernel<<<gridFor(B, 256), 256, 0, s>>>(sorted, S, B, spl);
     const Splitters sp{spl, B};
