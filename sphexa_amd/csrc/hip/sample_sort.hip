@@ -542,12 +542,12 @@ void exclusiveScanTiles(T* in, T* out, int64_t n, T* sums, bool zeroIn, hipStrea
 //! buckets of a sort of n elements
 inline int64_t bucketsFor(int64_t n) { return (n + kTarget - 1) / kTarget; }
 
-//! sample sorts of at most this many keys use buckets of kTargetSmall with 8 samples per bucket: their sample then
-//! fits one 512-pair wave sort and the bucket waves sort 4 items per lane (a latency chain: Evrard -n 100 sorts 8272
-//! samples, whose 10 buckets of ~830 keys took 32 us in one wave each)
-constexpr int64_t kSmallSort  = 14336;
+//! sample sorts of at most this many keys use buckets of kTargetSmall with 8 samples per bucket (4 above half of it):
+//! their sample then fits one 512-pair wave sort and the bucket waves sort 4 items per lane (a latency chain: Evrard
+//! -n 100 sorts 8272 samples, whose 10 buckets of ~830 keys took 32 us in one wave each). The samples of a sample are
+//! as nearly sorted as the keys, so 4 per bucket still give buckets near their target
+constexpr int64_t kSmallSort  = 28672;
 constexpr int kTargetSmall    = 224;
-constexpr int kOverSmall      = 8;
 
 /*! @brief the recursive sort; with base == nullptr only the workspace size is accumulated in bump.off. ``top``: the
  *         caller's sort (the recursive calls sort samples) */
@@ -567,7 +567,7 @@ void sortRec(int64_t n, const uint64_t* keysIn, const uint32_t* valsIn, uint64_t
     }
     const bool small = !top && n <= kSmallSort;
     const int64_t B  = small ? (n + kTargetSmall - 1) / kTargetSmall : bucketsFor(n);
-    const int64_t S  = std::min<int64_t>(n, B * (small ? kOverSmall : kOver));
+    const int64_t S  = std::min<int64_t>(n, B * (small ? (2 * n <= kSmallSort ? 8 : 4) : kOver));
     uint64_t* sample  = bump.take<uint64_t>(S);
     uint64_t* sorted  = bump.take<uint64_t>(S);
     uint32_t* sortedV = bump.take<uint32_t>(S);

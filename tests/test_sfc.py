@@ -109,7 +109,7 @@ def _nearly_sorted(n, seed, far=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 7, 1000, 1024, 1025, 4097, 100_000, 463_277, 2_000_003])
+@pytest.mark.parametrize("n", [1, 7, 1000, 1024, 1025, 4097, 100_000, 463_277, 1_000_000, 2_000_003])
 def test_sample_sort_matches_stable_sort(gpu, n):
     """hand-written sample sort (csrc/hip/sample_sort.hip): keys and permutation equal to a stable sort on random,
     nearly sorted (+ far movers), and duplicate-heavy keys (buckets beyond 1024 take the global-memory path)"""
