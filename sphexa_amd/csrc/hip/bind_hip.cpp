@@ -358,6 +358,8 @@ PYBIND11_MODULE(_sphx_hip, m)
           py::arg("xm"), py::arg("kx"), py::arg("gradh"), py::arg("ntot"), py::arg("rec"), py::arg("s"),
           py::arg("mUniform"), py::arg("inDone") = 0, py::arg("out") = 0, py::arg("vx") = 0, py::arg("vy") = 0,
           py::arg("vz") = 0);
+    m.def("set_pair_block", [](int block) { setPairBlock(block); },
+          "threads per block of the fixed-point pair loops: 512 (8 target groups sharing a CU's L1) or 256");
     m.def("eos_ve", [](int64_t first, int64_t last, const ConstArr& c, Ptr temp, Ptr mm, Ptr kx, Ptr xm, Ptr gradh,
                        Ptr prho, Ptr cc, Ptr rho, Ptr p, Ptr s)
           {

@@ -175,6 +175,8 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
                    const NsTree& t, const Box& box, unsigned ng0, unsigned ngmax, int32_t* nidx, int home,
                    int ovStride, int32_t* nc, int iterateH, unsigned long long* stats, void* scratch,
                    int testFrontCap, const float* m, int64_t ntot, void* rec, hipStream_t s, const SplitPredict& sp = SplitPredict{});
+//! threads per block of the production pair loops (256 or 512, hydro.hip withPairBlock)
+void setPairBlock(int block);
 //! fixed-point {x, y, z, m} records (QFrame of the box) of particles [0, n): the search and the XMass loop read them
 void packPosQ(int64_t n, const double* x, const double* y, const double* z, const float* m, const QFrame& q,
               SrcPosQ* out, hipStream_t s);

@@ -35,11 +35,12 @@ constexpr int kBlock = SPHX_PAIR_BLOCK; // threads per block of the pair loops (
  *         last target stay alive with an empty list and a clamped index (the cooperative gathers need all 64 lanes of
  *         a wave); they store nothing. `n` is the neighbor count (excluding self, capped).
  */
+template<int B = kBlock>
 __device__ __forceinline__ bool targetOf(const NbrArgs& a, int64_t& i, PackedLane& pl, unsigned& n)
 {
-    __shared__ uint32_t ctabAll[kBlock / 64][kChunkCap];
+    __shared__ uint32_t ctabAll[B / 64][kChunkCap];
     unsigned lb     = xcdRemap(blockIdx.x, gridDim.x);
-    int64_t t       = int64_t(lb) * kBlock + threadIdx.x;
+    int64_t t       = int64_t(lb) * B + threadIdx.x;
     i               = a.first + t;
     const int64_t g = t >> 6;
     const int64_t G = (a.last - a.first + 63) / 64;
@@ -104,7 +105,22 @@ inline NbrArgs withTot(NbrArgs a, int64_t ntot)
     return a;
 }
 
-inline unsigned gridT(const NbrArgs& a) { return gridFor(a.last - a.first, kBlock); }
+inline unsigned gridT(const NbrArgs& a, int block = kBlock) { return gridFor(a.last - a.first, block); }
+
+/* Threads per block of the production (fixed-point) pair loops, set per run (setPairBlock): 512 = 8 consecutive
+ * target groups per block share their sources in the CU's L1 (Sedov -n 400 121.2 -> 118.5 ms/step); 256 where the
+ * loops share the GPU with the gravity streams (Evrard -n 200: 21.3 ms at 256, 22.4 at 512). */
+static int g_pairBlock = kBlock;
+
+void setPairBlock(int block) { g_pairBlock = block == 512 ? 512 : kBlock; }
+
+//! @brief f(std::integral_constant<int, B>) with the run's block size B
+template<class F>
+inline void withPairBlock(F&& f)
+{
+    if (g_pairBlock == 512) f(std::integral_constant<int, 512>{});
+    else f(std::integral_constant<int, kBlock>{});
+}
 
 // ------------------------------------------------------------------------------------------------- packing
 
@@ -400,15 +416,16 @@ __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, B
 }
 
 //! @brief XMass on fixed-point records (see SrcPosQ): same sum as xmassJLoop (sph_math.hpp), half the gathers
-__global__ __launch_bounds__(kBlock) void xmassQKernel(NbrArgs a, SphConsts sc, QFrame q, const float* __restrict__ h,
-                                                       const SrcPosQ* __restrict__ rec, const float* __restrict__ wh,
-                                                       float* __restrict__ xm, SrcXmQ* __restrict__ xmOut)
+template<int B = kBlock>
+__global__ __launch_bounds__(B) void xmassQKernel(NbrArgs a, SphConsts sc, QFrame q, const float* __restrict__ h,
+                                                  const SrcPosQ* __restrict__ rec, const float* __restrict__ wh,
+                                                  float* __restrict__ xm, SrcXmQ* __restrict__ xmOut)
 {
-    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcPosQ>::S];
+    __shared__ float4 tile[B / 64 * 64 * CoopLoader<SrcPosQ>::S];
     int64_t i;
     PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, pl, n);
+    const bool valid = targetOf<B>(a, i, pl, n);
     const auto ld    = coopOf(rec, tile, i, a);
     const KernelFn kf{wh, nullptr, sc.sincIndex, sc.kernelChoice};
     const SrcPosQ pi = ld(unsigned(i));
@@ -427,8 +444,8 @@ __global__ __launch_bounds__(kBlock) void xmassQKernel(NbrArgs a, SphConsts sc, 
     if (xmOut) xmOut[i] = SrcXmQ{pi.x, pi.y, pi.z, v}; // Gradh's record of this target
 }
 
-template<class R, class G>
-__global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts sc, G box,
+template<class R, class G, int B = kBlock>
+__global__ __launch_bounds__(B) void veDefGradhKernel(NbrArgs a, SphConsts sc, G box,
                                                            const float* __restrict__ h, const R* __restrict__ rec,
                                                            const float* __restrict__ wh, const float* __restrict__ whd,
                                                            float* __restrict__ kx, float* __restrict__ gradh,
@@ -436,11 +453,11 @@ __global__ __launch_bounds__(kBlock) void veDefGradhKernel(NbrArgs a, SphConsts 
                                                            const float* __restrict__ vy, const float* __restrict__ vz,
                                                            SrcIadQ* __restrict__ iadOut)
 {
-    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
+    __shared__ float4 tile[B / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
     PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, pl, n);
+    const bool valid = targetOf<B>(a, i, pl, n);
     float k, g;
     veDefGradhJLoop(unsigned(i), sc.K, box, &pl, 0, n, h[i], coopOf(rec, tile, i, a),
                     KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice}, k, g, mUniform);
@@ -531,8 +548,8 @@ __global__ __launch_bounds__(kBlock) void iadKernel(NbrArgs a, SphConsts sc, Box
 }
 
 //! @brief IAD matrix, then divv/curlv (+ velocity gradient) in the same kernel over the same neighbor list
-template<bool kAvS, class R, class G>
-__global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConsts sc, G box,
+template<bool kAvS, class R, class G, int B = kBlock>
+__global__ __launch_bounds__(B) void iadDivvCurlvKernel(NbrArgs a, SphConsts sc, G box,
                                                              const float* __restrict__ h,
                                                              const float* __restrict__ kx,
                                                              const R* __restrict__ rec,
@@ -543,11 +560,11 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConst
                                                              const float* __restrict__ cs, const float* __restrict__ mm,
                                                              const float* __restrict__ prho)
 {
-    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<R>::S];
+    __shared__ float4 tile[B / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
     PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, pl, n);
+    const bool valid = targetOf<B>(a, i, pl, n);
     float c[6], g[6], dvi, cvi, S[3];
     iadDivvCurlvJLoop<kAvS>(unsigned(i), sc.K, box, &pl, 0, n, h[i], kx[i], coopOf(rec, tile, i, a),
                             KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, g, S);
@@ -569,7 +586,7 @@ __global__ __launch_bounds__(kBlock) void iadDivvCurlvKernel(NbrArgs a, SphConst
         // stride; staged through LDS, the wave writes its 64 contiguous records as whole 1-KiB rows instead.
         if ((avOut || momOut) && ballot(valid))
         {
-            __shared__ float4 stage[kBlock / 64][64 * 5];
+            __shared__ float4 stage[B / 64][64 * 5];
             float4* w       = stage[threadIdx.x >> 6];
             const int lane  = threadIdx.x & 63;
             const int64_t i0 = int64_t(__builtin_amdgcn_readfirstlane(int(i - a.first))) + a.first; // lane 0 is valid
@@ -673,7 +690,8 @@ __global__ __launch_bounds__(kBlock) void avSwitchesQKernel(NbrArgs a, SphConsts
 }
 
 //! @brief AV switches on SrcAvV records (vd = vol divv) with the IAD loop's S_i (avSwitchesVJLoop, sph_math.hpp)
-__global__ __launch_bounds__(kBlock) void avSwitchesVKernel(NbrArgs a, SphConsts sc, QFrame q,
+template<int B = kBlock>
+__global__ __launch_bounds__(B) void avSwitchesVKernel(NbrArgs a, SphConsts sc, QFrame q,
                                                             const float* __restrict__ h, Six cij,
                                                             const SrcAvV* __restrict__ rec,
                                                             const float* __restrict__ divv,
@@ -683,11 +701,11 @@ __global__ __launch_bounds__(kBlock) void avSwitchesVKernel(NbrArgs a, SphConsts
                                                             float* __restrict__ alphaOut, const double* dtDev,
                                                             SrcMomQ* __restrict__ momOut)
 {
-    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcAvV>::S];
+    __shared__ float4 tile[B / 64 * 64 * CoopLoader<SrcAvV>::S];
     int64_t i;
     PackedLane pl;
     unsigned n;
-    const bool valid = targetOf(a, i, pl, n);
+    const bool valid = targetOf<B>(a, i, pl, n);
     if (dtDev) dt = *dtDev;
     float ci[6]    = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
     const float4 s = avS[i - a.first];
@@ -701,9 +719,10 @@ __global__ __launch_bounds__(kBlock) void avSwitchesVKernel(NbrArgs a, SphConsts
 }
 
 //! @brief block min of the Courant time step, then one atomic per block
+template<int B = kBlock>
 __device__ inline void reduceMinDt(float dti, float* minDt)
 {
-    __shared__ float red[kBlock / 64];
+    __shared__ float red[B / 64];
     float v = waveMin(dti);
     int w   = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) red[w] = v;
@@ -711,7 +730,7 @@ __device__ inline void reduceMinDt(float dti, float* minDt)
     if (threadIdx.x == 0)
     {
         float r = red[0];
-        for (int k = 1; k < kBlock / 64; ++k)
+        for (int k = 1; k < B / 64; ++k)
             r = fminf(r, red[k]);
         atomicMinPosFloat(minDt, r);
     }
@@ -781,16 +800,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 }
 
 //! @brief the split-record instance (uniform mass, SrcMomQ64 + SrcMomSide), 4 waves per SIMD as above
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void momentumEnergyVeQ64Kernel(
+template<int B = kBlock>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void momentumEnergyVeQ64Kernel(
     NbrArgs a, SphConsts sc, QFrame box, const SrcMomQ64* __restrict__ rec, const SrcMomSide* __restrict__ side,
     float mU, const float* __restrict__ wh, float* __restrict__ ax, float* __restrict__ ay, float* __restrict__ az,
     double* __restrict__ du, float* __restrict__ minDt)
 {
-    __shared__ float4 tile[kBlock / 64 * 64 * CoopLoader<SrcMomQ64>::S];
+    __shared__ float4 tile[B / 64 * 64 * CoopLoader<SrcMomQ64>::S];
     int64_t i;
     PackedLane pl;
     unsigned n;
-    bool valid = targetOf(a, i, pl, n);
+    bool valid = targetOf<B>(a, i, pl, n);
     float dti  = FLT_MAX;
     float mvs, axi, ayi, azi;
     double dui;
@@ -806,7 +826,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         const SrcMomQ64 ri = rec[i];
         dti                = tsKCourant(mvs, 1.0f / ri.ih, ri.c, float(sc.Kcour));
     }
-    reduceMinDt(dti, minDt);
+    reduceMinDt<B>(dti, minDt);
 }
 
 __global__ __launch_bounds__(kBlock) void momentumEnergyStdKernel(NbrArgs a, SphConsts sc, Box box,
@@ -975,8 +995,12 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
         const QFrame q = qframeOf(box, sc.fixedPoint);
         packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    { packPosQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, m, q, (SrcPosQ*)rec); });
-        xmassQKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec, wh, xm,
-                                                 (SrcXmQ*)xmOut);
+        withPairBlock([&](auto bc)
+                      {
+                          constexpr int B = decltype(bc)::value;
+                          xmassQKernel<B><<<gridT(a, B), B, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec,
+                                                                    wh, xm, (SrcXmQ*)xmOut);
+                      });
     }
     SPHX_LAUNCH_CHECK();
 }
@@ -992,8 +1016,13 @@ void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
         const QFrame q = qframeOf(box, sc.fixedPoint);
         packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    { packXmQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, xm, q, (SrcXmQ*)rec); });
-        veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcXmQ*)rec, wh, whd, kx,
-                                                     gradh, mUniform, vx, vy, vz, (SrcIadQ*)iadOut);
+        withPairBlock([&](auto bc)
+                      {
+                          constexpr int B = decltype(bc)::value;
+                          veDefGradhKernel<SrcXmQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
+                              withTot(a, ntot), sc, q, h, (const SrcXmQ*)rec, wh, whd, kx, gradh, mUniform, vx, vy, vz,
+                              (SrcIadQ*)iadOut);
+                      });
     }
     else
     {
@@ -1065,14 +1094,18 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
                    });
         // fixed-point path: also the S_i of the AV loop (avSwitchesVJLoop) when a workspace is given, and the next
         // loops' own records (avOut / momOut)
-        if (avS)
-            iadDivvCurlvKernel<true><<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh,
-                                                                 c, divv, curlv, g, dV[0] != nullptr, (float4*)avS,
-                                                                 (SrcAvV*)avOut, (SrcMomQ*)momOut, cs, m, prho);
-        else
-            iadDivvCurlvKernel<false><<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec,
-                                                                  wh, c, divv, curlv, g, dV[0] != nullptr, nullptr,
-                                                                  nullptr, (SrcMomQ*)momOut, cs, m, prho);
+        withPairBlock([&](auto bc)
+                      {
+                          constexpr int B = decltype(bc)::value;
+                          if (avS)
+                              iadDivvCurlvKernel<true, SrcIadQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
+                                  withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv, curlv, g,
+                                  dV[0] != nullptr, (float4*)avS, (SrcAvV*)avOut, (SrcMomQ*)momOut, cs, m, prho);
+                          else
+                              iadDivvCurlvKernel<false, SrcIadQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
+                                  withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv, curlv, g,
+                                  dV[0] != nullptr, nullptr, nullptr, (SrcMomQ*)momOut, cs, m, prho);
+                      });
     }
     SPHX_LAUNCH_CHECK();
 }
@@ -1104,9 +1137,14 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                        packAvVKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, kx, vx, vy, vz, xm, c, divv,
                                                                            q, (SrcAvV*)rec);
                    });
-        avSwitchesVKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, h, cc, (const SrcAvV*)rec, divv,
-                                                      (const float4*)avS, wh, dt, alpha, alphaOut, dtDev,
-                                                      (SrcMomQ*)momOut);
+        withPairBlock([&](auto bc)
+                      {
+                          constexpr int B = decltype(bc)::value;
+                          avSwitchesVKernel<B><<<gridT(a, B), B, 0, s>>>(withTot(a, ntot), sc, q, h, cc,
+                                                                         (const SrcAvV*)rec, divv, (const float4*)avS,
+                                                                         wh, dt, alpha, alphaOut, dtDev,
+                                                                         (SrcMomQ*)momOut);
+                      });
     }
     else
     {
@@ -1135,8 +1173,12 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
         auto* side      = reinterpret_cast<SrcMomSide*>(static_cast<char*>(rec) + momSideOffset(ntot));
         packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    { packMomQ64Kernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, f, q, main, side); });
-        momentumEnergyVeQ64Kernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, q, main, side, mUniform, wh, ax,
-                                                              ay, az, du, minDt);
+        withPairBlock([&](auto bc)
+                      {
+                          constexpr int B = decltype(bc)::value;
+                          momentumEnergyVeQ64Kernel<B><<<gridT(a, B), B, 0, s>>>(withTot(a, ntot), sc, q, main, side,
+                                                                                 mUniform, wh, ax, ay, az, du, minDt);
+                      });
         SPHX_LAUNCH_CHECK();
         return;
     }

@@ -406,6 +406,7 @@ class HydroVeProp(Propagator):
     def compute_forces(self, domain, d):
         t = self.timer
         t.start()
+        H.select_pair_block(d)
         self.sync(domain, d)
         t.step("domain::sync")
         prep = self._gravity_prepare(domain, d)

@@ -60,6 +60,23 @@ def _is_gpu(d):
     return d.device.type == "cuda"
 
 
+# threads per block of the fixed-point pair loops (csrc/hip/hydro.hip withPairBlock): 512 puts 8 consecutive target
+# groups on one CU, where they share their sources in L1 (Sedov -n 400 121.2 -> 118.5 ms/step); 256 when self-gravity
+# runs on the side streams beside the loops (Evrard -n 200 21.3 ms at 256, 22.4 at 512). SPHX_PAIR_BLOCK overrides.
+PAIR_BLOCK = int(os.environ.get("SPHX_PAIR_BLOCK", "0"))
+_pair_block_set = [None]
+
+
+def select_pair_block(d):
+    """GPU: set the pair loops' block size for this run's step (one binding call when it changes)"""
+    if d.device.type != "cuda":
+        return
+    b = PAIR_BLOCK or (256 if d.g != 0.0 else 512)
+    if _pair_block_set[0] != b:
+        _lib.hip().set_pair_block(b)
+        _pair_block_set[0] = b
+
+
 def release_workspaces(d):
     """drop the record workspaces (re-allocated by the next loop; the caching allocator hands the blocks back)"""
     d._rec0 = None
