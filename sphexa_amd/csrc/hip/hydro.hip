@@ -16,6 +16,7 @@
  * The pair math is sphx/sph_math.hpp, shared with the OpenMP path.
  */
 #include <cfloat>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -111,14 +112,20 @@ inline unsigned gridT(const NbrArgs& a, int block = kBlock) { return gridFor(a.l
  * target groups per block share their sources in the CU's L1 (Sedov -n 400 121.2 -> 118.5 ms/step); 256 where the
  * loops share the GPU with the gravity streams (Evrard -n 200: 21.3 ms at 256, 22.4 at 512). */
 static int g_pairBlock = kBlock;
+// loops that take the larger block (bit 0 XMass, 1 Gradh, 2 IAD, 3 AV, 4 momentum); experiment knob SPHX_PAIR_MASK
+static const unsigned kPairMask = []
+{
+    const char* e = std::getenv("SPHX_PAIR_MASK");
+    return e ? unsigned(std::strtoul(e, nullptr, 0)) : 31u;
+}();
 
 void setPairBlock(int block) { g_pairBlock = block == 512 ? 512 : kBlock; }
 
-//! @brief f(std::integral_constant<int, B>) with the run's block size B
+//! @brief f(std::integral_constant<int, B>) with the run's block size B for loop `loop` (bit of kPairMask)
 template<class F>
-inline void withPairBlock(F&& f)
+inline void withPairBlock(F&& f, int loop = 0)
 {
-    if (g_pairBlock == 512) f(std::integral_constant<int, 512>{});
+    if (g_pairBlock == 512 && ((kPairMask >> loop) & 1u)) f(std::integral_constant<int, 512>{});
     else f(std::integral_constant<int, kBlock>{});
 }
 
@@ -1000,7 +1007,7 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
                           constexpr int B = decltype(bc)::value;
                           xmassQKernel<B><<<gridT(a, B), B, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec,
                                                                     wh, xm, (SrcXmQ*)xmOut);
-                      });
+                      }, 0);
     }
     SPHX_LAUNCH_CHECK();
 }
@@ -1022,7 +1029,7 @@ void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                           veDefGradhKernel<SrcXmQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
                               withTot(a, ntot), sc, q, h, (const SrcXmQ*)rec, wh, whd, kx, gradh, mUniform, vx, vy, vz,
                               (SrcIadQ*)iadOut);
-                      });
+                      }, 1);
     }
     else
     {
@@ -1105,7 +1112,7 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
                               iadDivvCurlvKernel<false, SrcIadQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
                                   withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv, curlv, g,
                                   dV[0] != nullptr, nullptr, nullptr, (SrcMomQ*)momOut, cs, m, prho);
-                      });
+                      }, 2);
     }
     SPHX_LAUNCH_CHECK();
 }
@@ -1144,7 +1151,7 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                                                                          (const SrcAvV*)rec, divv, (const float4*)avS,
                                                                          wh, dt, alpha, alphaOut, dtDev,
                                                                          (SrcMomQ*)momOut);
-                      });
+                      }, 3);
     }
     else
     {
@@ -1178,7 +1185,7 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
                           constexpr int B = decltype(bc)::value;
                           momentumEnergyVeQ64Kernel<B><<<gridT(a, B), B, 0, s>>>(withTot(a, ntot), sc, q, main, side,
                                                                                  mUniform, wh, ax, ay, az, du, minDt);
-                      });
+                      }, 4);
         SPHX_LAUNCH_CHECK();
         return;
     }
