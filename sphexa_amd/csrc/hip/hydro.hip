@@ -112,6 +112,14 @@ inline unsigned gridT(const NbrArgs& a, int block = kBlock) { return gridFor(a.l
  * target groups per block share their sources in the CU's L1 (Sedov -n 400 121.2 -> 118.5 ms/step); 256 where the
  * loops share the GPU with the gravity streams (Evrard -n 200: 21.3 ms at 256, 22.4 at 512). */
 static int g_pairBlock = kBlock;
+// the AV loop (92 VGPRs, 5 waves per SIMD) in blocks of 10 waves: two per CU keep its occupancy (Sedov -n 200 AV
+// 1.814 -> 1.705 ms); Gradh measured 1.119 (512) / 1.171 (448) / 1.354 ms (896), XMass slower at 1024
+#ifndef SPHX_AV_BLOCK
+#define SPHX_AV_BLOCK 640
+#endif
+#ifndef SPHX_GRADH_BLOCK
+#define SPHX_GRADH_BLOCK 512
+#endif
 // loops that take the larger block (bit 0 XMass, 1 Gradh, 2 IAD, 3 AV, 4 momentum); experiment knob SPHX_PAIR_MASK
 static const unsigned kPairMask = []
 {
@@ -126,6 +134,14 @@ template<class F>
 inline void withPairBlock(F&& f, int loop = 0)
 {
     if (g_pairBlock == 512 && ((kPairMask >> loop) & 1u)) f(std::integral_constant<int, 512>{});
+    else f(std::integral_constant<int, kBlock>{});
+}
+
+//! @brief as withPairBlock, with block size L instead of 512 (a loop whose occupancy fits other multiples of 64)
+template<int L, class F>
+inline void withPairBlockL(F&& f, int loop)
+{
+    if (g_pairBlock == 512 && ((kPairMask >> loop) & 1u)) f(std::integral_constant<int, L>{});
     else f(std::integral_constant<int, kBlock>{});
 }
 
@@ -1023,7 +1039,7 @@ void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
         const QFrame q = qframeOf(box, sc.fixedPoint);
         packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    { packXmQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, xm, q, (SrcXmQ*)rec); });
-        withPairBlock([&](auto bc)
+        withPairBlockL<SPHX_GRADH_BLOCK>([&](auto bc)
                       {
                           constexpr int B = decltype(bc)::value;
                           veDefGradhKernel<SrcXmQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
@@ -1144,7 +1160,7 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                        packAvVKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, kx, vx, vy, vz, xm, c, divv,
                                                                            q, (SrcAvV*)rec);
                    });
-        withPairBlock([&](auto bc)
+        withPairBlockL<SPHX_AV_BLOCK>([&](auto bc)
                       {
                           constexpr int B = decltype(bc)::value;
                           avSwitchesVKernel<B><<<gridT(a, B), B, 0, s>>>(withTot(a, ntot), sc, q, h, cc,
