@@ -1916,6 +1916,8 @@ void computeGravityEval(int64_t first, int64_t last, const int32_t* child, const
     // M2P keeps the SFC order by default: heaviest-first dispatch scatters the node lists of concurrently running
     // groups over the tree (A/B on Evrard -n 200: P2P 10.14 -> 9.29 ms, M2P 8.10 -> 8.60 ms with both ordered)
 #ifdef SPHX_GRAV_M2P_ORDER
+    // the order is built with the P2P phase (2): a split evaluation would run the M2P (phase 1) before it exists
+    if (!all) throw std::runtime_error("SPHX_GRAV_M2P_ORDER builds evaluate gravity in one phase (phase 0) only");
     const int32_t* orderM = c.order;
 #else
     const int32_t* orderM = nullptr;

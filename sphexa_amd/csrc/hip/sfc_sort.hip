@@ -2,12 +2,9 @@
  *
  * Parity: reference sfc/sfc_gpu.cu:38-54 (computeSfcKeysKernel), primitives/primitives_gpu.cu:85-91,270-338
  * (gatherGpu, sortByKeyGpu with CUB radix sort, exclusiveScanGpu), primitives/gather.cuh:44-113 (GpuSfcSorter).
- * Sorts and scans are the hand-written sample sort / tile scans of sample_sort.hip (the hipCUB radix sort stays as
- * the A/B variant SPHX_SORT_HIPCUB).
+ * Sorts and scans are the hand-written sample sort / tile scans of sample_sort.hip (hipCUB measured ~6 ms for 64 M
+ * keys against ~2.2 ms: scripts/micro_bench.py; no library sort is built).
  */
-#ifdef SPHX_SORT_HIPCUB
-#include <hipcub/hipcub.hpp>
-#endif
 
 #include "common.h"
 #include "hip_api.h"
@@ -57,43 +54,6 @@ void computeKeysDevBox(int64_t n, const double* x, const double* y, const double
     SPHX_LAUNCH_CHECK();
 }
 
-__global__ void iotaKernel(int64_t n, int32_t* out)
-{
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = int32_t(i);
-}
-
-#ifdef SPHX_SORT_HIPCUB
-// library sorts (A/B variant: build_native --variant hipcub -DSPHX_SORT_HIPCUB)
-size_t sortPairsTempBytes(int64_t n)
-{
-    size_t bytes = 0;
-    SPHX_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const KeyT*)nullptr, (KeyT*)nullptr,
-                                                  (const int32_t*)nullptr, (int32_t*)nullptr, int(n), 0, 64));
-    // room for the iota value array used by sortKeys
-    return bytes + size_t(n) * sizeof(int32_t) + 256;
-}
-
-void sortPairs(int64_t n, const KeyT* keysIn, KeyT* keysOut, const int32_t* valsIn, int32_t* valsOut, void* tmp,
-               size_t tmpBytes, int beginBit, int endBit, hipStream_t s)
-{
-    if (n == 0) return;
-    size_t bytes = tmpBytes;
-    SPHX_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, keysIn, keysOut, valsIn, valsOut, int(n), beginBit,
-                                                  endBit, s));
-}
-
-void sortKeys(int64_t n, const KeyT* keysIn, KeyT* keysOut, int32_t* perm, void* tmp, size_t tmpBytes,
-              hipStream_t s)
-{
-    if (n == 0) return;
-    // carve the iota array off the front of the workspace, hipCUB temp storage follows (256-B aligned)
-    size_t iotaBytes = (size_t(n) * sizeof(int32_t) + 255) & ~size_t(255);
-    int32_t* iota    = static_cast<int32_t*>(tmp);
-    iotaKernel<<<gridFor(n, 256), 256, 0, s>>>(n, iota);
-    sortPairs(n, keysIn, keysOut, iota, perm, static_cast<char*>(tmp) + iotaBytes, tmpBytes - iotaBytes, 0, 63, s);
-}
-#else
 // hand-written sample sort (sample_sort.hip): (key, value) ascending, keys compared on all 64 bits (the SFC keys and
 // octree codes leave the bits past endBit zero, so the bit range needs no handling)
 size_t sortPairsTempBytes(int64_t n) { return sampleSortTempBytes(n); }
@@ -109,7 +69,6 @@ void sortKeys(int64_t n, const KeyT* keysIn, KeyT* keysOut, int32_t* perm, void*
 {
     sampleSortPairs(n, keysIn, nullptr, keysOut, reinterpret_cast<uint32_t*>(perm), tmp, tmpBytes, s);
 }
-#endif
 
 /*! @brief stable merge of k sorted runs (the particles received from k ranks after a migration, each source's
  *         part already SFC-sorted by the sender): element i of run a lands at
@@ -460,28 +419,12 @@ void unpackRows(int64_t n, const void* rows, const std::vector<uintptr_t>& dst, 
     SPHX_LAUNCH_CHECK();
 }
 
-#ifdef SPHX_SORT_HIPCUB
-size_t scanTempBytes(int64_t n)
-{
-    size_t bytes = 0;
-    SPHX_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int64_t*)nullptr, (int64_t*)nullptr, int(n)));
-    return bytes + 256;
-}
-
-void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s)
-{
-    if (n == 0) return;
-    size_t bytes = tmpBytes;
-    SPHX_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, int(n), s));
-}
-#else
 size_t scanTempBytes(int64_t n) { return exclusiveScanTempBytes(n); }
 
 void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s)
 {
     exclusiveScanI64Hip(in, out, n, tmp, tmpBytes, s);
 }
-#endif
 
 SPHX_DCHECK_READER(dcheckSfc)
 bool deviceChecksEnabled() { return SPHX_DCHECK_ENABLED != 0; }

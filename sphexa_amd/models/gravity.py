@@ -46,6 +46,10 @@ class MultipoleHolder:
             gl = self._lists = G.gravity_lists(domain.octree, self.centers, self.multipoles, first, last, d["x"],
                                                d["y"], d["z"], stats=self.stats, scratch_key=scratch_key)
             if m2p_out is not None:
+                # the evaluation buffers and the particles' extent (min_max into gl.mm) are enqueued here, before
+                # lists_done: the P2P phase on the second side stream quantizes its source records with gl.mm and
+                # waits only on lists_done (advisor r5: reading gl.mm unordered after the min_max raced)
+                G._eval_buffers(gl, d["x"], d["y"], d["z"])
                 self.lists_done = torch.cuda.Event()
                 self.lists_done.record()
                 G.gravity_eval(gl, d["x"], d["y"], d["z"], d["h"], d["m"], d.g, *m2p_out, phase=1)

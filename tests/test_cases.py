@@ -207,3 +207,17 @@ def test_turbulence_rng_checkpoint_roundtrip():
     a.update_noise(2e-3)
     b.update_noise(2e-3)
     assert np.array_equal(a.phases, b.phases)
+
+
+def test_sphexa_executable(tmp_path):
+    """bin/sphexa is the reference's `sphexa` binary (main/src/sphexa/CMakeLists.txt:24-30): same flags, runs a case"""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHON=sys.executable, OMP_NUM_THREADS="2")
+    r = subprocess.run([os.path.join(root, "bin", "sphexa"), "--init", "sedov", "-n", "20", "-s", "2", "--device",
+                        "cpu"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "### Check ###" in r.stdout
