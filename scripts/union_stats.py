@@ -65,7 +65,7 @@ def main():
     newv &= srt != big
     uexact = newv.sum(dim=1)
     # per-chunk offset ranges: chunk id = j >> 6 in aligned terms is not the search's chunk; use the table's chunks:
-    nch = (tab[:kk, 1] & 0xFFFF).long()
+    nch = (tab[:kk, 1] & 0x3FF).long()
     nblk = tab[:kk, 0].long()
     # range union by 64-aligned blocks of the source index (an upper bound proxy of per-chunk ranges)
     blk = torch.where(srt != big, srt >> 6, -1)

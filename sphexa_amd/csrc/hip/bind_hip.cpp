@@ -358,6 +358,9 @@ PYBIND11_MODULE(_sphx_hip, m)
           py::arg("xm"), py::arg("kx"), py::arg("gradh"), py::arg("ntot"), py::arg("rec"), py::arg("s"),
           py::arg("mUniform"), py::arg("inDone") = 0, py::arg("out") = 0, py::arg("vx") = 0, py::arg("vy") = 0,
           py::arg("vz") = 0);
+    m.def("set_staged", [](unsigned mask) { setStaged(mask); },
+          "pair loops that run LDS-staged: bit 0 XMass, 1 Gradh, 2 IAD, 3 AV, 4 momentum (hydro.hip, staged.h)");
+    m.def("staged_mask", []() { return stagedMask(); });
     m.def("set_pair_block", [](int block) { setPairBlock(block); },
           "threads per block of the fixed-point pair loops: 512 (8 target groups sharing a CU's L1) or 256");
     m.def("eos_ve", [](int64_t first, int64_t last, const ConstArr& c, Ptr temp, Ptr mm, Ptr kx, Ptr xm, Ptr gradh,

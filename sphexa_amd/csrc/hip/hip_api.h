@@ -177,6 +177,9 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
                    int testFrontCap, const float* m, int64_t ntot, void* rec, hipStream_t s, const SplitPredict& sp = SplitPredict{});
 //! threads per block of the production pair loops (256 or 512, hydro.hip withPairBlock)
 void setPairBlock(int block);
+//! pair loops that run LDS-staged (hydro.hip g_staged: bit 0 XMass, 1 Gradh, 2 IAD, 3 AV, 4 momentum)
+void setStaged(unsigned mask);
+unsigned stagedMask();
 //! fixed-point {x, y, z, m} records (QFrame of the box) of particles [0, n): the search and the XMass loop read them
 void packPosQ(int64_t n, const double* x, const double* y, const double* z, const float* m, const QFrame& q,
               SrcPosQ* out, hipStream_t s);

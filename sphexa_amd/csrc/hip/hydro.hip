@@ -22,6 +22,7 @@
 #include "common.h"
 #include "hip_api.h"
 #include "sphx/sph_math.hpp"
+#include "staged.h"
 
 namespace sphx::hip
 {
@@ -55,8 +56,8 @@ __device__ __forceinline__ bool targetOf(const NbrArgs& a, int64_t& i, PackedLan
     {
         pl.nblk          = unsigned(*(const __attribute__((address_space(4))) int32_t*)(tab));
         const unsigned w = unsigned(*(const __attribute__((address_space(4))) int32_t*)(tab + 1));
-        nch              = min(w & 0xFFFFu, kChunkCap);
-        T                = w >> 16;
+        nch              = min(tableWordNch(w), kChunkCap);
+        T                = tableWordT(w);
     }
     pl.tab  = tab + 2 + T;
     pl.rows = reinterpret_cast<const int4*>(rowsInt) + lane;
@@ -128,6 +129,20 @@ static const unsigned kPairMask = []
 }();
 
 void setPairBlock(int block) { g_pairBlock = block == 512 ? 512 : kBlock; }
+
+/* Loops that run LDS-staged (staged.h; bit 0 XMass, 1 Gradh, 2 IAD, 3 AV, 4 momentum), fixed-point path only.
+ * SPHX_STAGED overrides the default; setStaged (tests, A/B) at run time. */
+static unsigned g_staged = []
+{
+    const char* e = std::getenv("SPHX_STAGED");
+    return e ? unsigned(std::strtoul(e, nullptr, 0)) : 0u;
+}();
+
+void setStaged(unsigned mask) { g_staged = mask; }
+unsigned stagedMask() { return g_staged; }
+
+//! grid of a staged loop: one workgroup per target group
+inline unsigned gridStaged(const NbrArgs& a) { return unsigned((a.last - a.first + 63) / 64); }
 
 //! @brief f(std::integral_constant<int, B>) with the run's block size B for loop `loop` (bit of kPairMask)
 template<class F>
@@ -466,6 +481,49 @@ __global__ __launch_bounds__(B) void xmassQKernel(NbrArgs a, SphConsts sc, QFram
     xm[i]         = v;
     if (xmOut) xmOut[i] = SrcXmQ{pi.x, pi.y, pi.z, v}; // Gradh's record of this target
 }
+
+/*! @brief XMass, LDS-staged (staged.h): W waves per group, the group's SrcPosQ union in LDS. Same sum as xmassQKernel
+ *         (summed in W partial sums, the target's own term last). */
+template<int W, int UCAP>
+__global__ __launch_bounds__(64 * W) void xmassQStagedKernel(NbrArgs a, SphConsts sc, QFrame q,
+                                                             const float* __restrict__ h,
+                                                             const SrcPosQ* __restrict__ rec,
+                                                             const float* __restrict__ wh, float* __restrict__ xm,
+                                                             SrcXmQ* __restrict__ xmOut)
+{
+    using Ld = StagedLoader<SrcPosQ, W, UCAP>;
+    __shared__ typename Ld::Shared sh;
+    int64_t i;
+    StagedLane sl;
+    unsigned n;
+    const bool valid = stagedTargetOf<W>(a, i, sl, n);
+    const Ld ld{rec, nullptr, 0.f, &sh};
+    const KernelFn kf{wh, nullptr, sc.sincIndex, sc.kernelChoice};
+    const SrcPosQ pi = ld(unsigned(i));
+    const float hi = h[i], hInv = 1.f / hi, h3Inv = hInv * hInv * hInv;
+    float rho0 = 0.f;
+    forEachNeighbor<SPHX_BATCH_POS>(&sl, 0, n, ld, [&](unsigned, const SrcPosQ& pj) {
+        const float rx   = float(int32_t(pi.x - pj.x)) * q.inv[0];
+        const float ry   = float(int32_t(pi.y - pj.y)) * q.inv[1];
+        const float rz   = float(int32_t(pi.z - pj.z)) * q.inv[2];
+        const float dist = sqrtF(rx * rx + ry * ry + rz * rz);
+        rho0 += kf.w(dist * hInv) * pj.m;
+    });
+    reduceAcross(ld, rho0);
+    rho0 += pi.m;
+    if (!valid || threadIdx.x >= 64) return;
+    const float v = pi.m / (rho0 * float(sc.K) * h3Inv);
+    xm[i]         = v;
+    if (xmOut) xmOut[i] = SrcXmQ{pi.x, pi.y, pi.z, v};
+}
+
+// staged shapes (waves per group, union capacity in records), per loop
+#ifndef SPHX_ST_XMASS_W
+#define SPHX_ST_XMASS_W 4
+#endif
+#ifndef SPHX_ST_XMASS_U
+#define SPHX_ST_XMASS_U 1024
+#endif
 
 template<class R, class G, int B = kBlock>
 __global__ __launch_bounds__(B) void veDefGradhKernel(NbrArgs a, SphConsts sc, G box,
@@ -1018,6 +1076,13 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
         const QFrame q = qframeOf(box, sc.fixedPoint);
         packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    { packPosQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, m, q, (SrcPosQ*)rec); });
+        if (g_staged & 1u)
+        {
+            xmassQStagedKernel<SPHX_ST_XMASS_W, SPHX_ST_XMASS_U><<<gridStaged(a), 64 * SPHX_ST_XMASS_W, 0, s>>>(
+                withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec, wh, xm, (SrcXmQ*)xmOut);
+            SPHX_LAUNCH_CHECK();
+            return;
+        }
         withPairBlock([&](auto bc)
                       {
                           constexpr int B = decltype(bc)::value;

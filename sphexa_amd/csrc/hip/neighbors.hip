@@ -242,7 +242,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     const uint32_t padCode = chunkCode(0, valid ? lane : unsigned(last - 1 - (first + g * 64)));
 
     RowAlloc ra;
-    unsigned ncSph = 1, cnt = 0, fb = 0, T = 0, slot = 1, nT = 0, nTall = 0;
+    unsigned ncSph = 1, cnt = 0, fb = 0, T = 0, Tc = 0, slot = 1, nT = 0, nTall = 0;
     unsigned long long nStagedLast = 0, nSubLast = 0;
     uint32_t selfCode = padCode;
     int round = 0;
@@ -266,6 +266,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         slot      = 1;
         selfCode  = padCode;
         T         = 0;
+        Tc        = 0;
         nTall     = 0;
         chunkOvf  = false;
         didSplit  = len0 < 64;
@@ -504,7 +505,8 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     // table rows: exact for a single pass, the capacity once the group is split (later passes add
                     // slots after list blocks have been stored at ordinals T + b)
                     const bool single = !kSplit || (pos == 0 && len == 64);
-                    T = single ? chunkTabRows(min(1 + nch, kChunkCap)) : kChunkTabRowsMax;
+                    Tc = single ? chunkTabRows(min(1 + nch, kChunkCap)) : kChunkTabRowsMax;
+                    T  = Tc + (single ? maskTabRows(min(1 + nch, kChunkCap)) : kMaskTabRowsMax);
                     ra.ensure(min(po.home, po.rowsMax), g, po);
                     ra.ensure(T, g, po);
                 }
@@ -748,6 +750,14 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                         if (rw < po.poolRows) rowsInt[size_t(rw) * 256 + (s & 255)] = c0;
                         cbase[s & (kCbase - 1)] = c0;
                     }
+                    // the slot's staged-source mask (packed_list.hpp): the union of the group's sources for the
+                    // LDS-staged pair loops (two lanes: a vector store of the {lo, hi} pair)
+                    if (lane < 2)
+                    {
+                        const unsigned rw = ra.rowU(Tc + (s >> 7));
+                        if (rw < po.poolRows)
+                            rowsInt[size_t(rw) * 256 + 2 * (s & 127) + lane] = int32_t(lane ? uint32_t(m >> 32) : uint32_t(m));
+                    }
                     if (int64_t(c0) <= i && i < int64_t(c0) + 64) selfCode = chunkCode(s, unsigned(i - c0));
                     // compact the in-box sources into the staging pairs (source order kept: deterministic lists)
                     if (inBox) stagePut(sTail + unsigned(__popcll(m & lanemaskLt())), xr, yr, zr, chunkCode(s, lane));
@@ -850,7 +860,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
     const unsigned rwo = ra.row(ord);
     if (lane < po.tabInts)
         tab[lane] = lane == 0   ? int32_t(nblk)
-                    : lane == 1 ? int32_t(slot | (T << 16))
+                    : lane == 1 ? int32_t(tableWord(slot, Tc, T))
                                 : (ord < T + nblk && rwo < po.poolRows ? int32_t(rwo) : 0);
     if (lane == 0)
     {

@@ -18,11 +18,15 @@
  *
  * Layout of one search's list buffer (int32):
  *   [ group tables: G x packedTableInts ints, padded to 256 ints ][ rows: 1 KiB each = 64 lanes x int4 ]
- *   group table: [0] = list blocks nblk (wave-uniform trip count of the pair loops), [1] = nch | T << 16 with nch the
- *                chunk-table entries and T its rows, [2 + r] = row of ordinal r. Ordinals 0 .. T-1 hold the chunk
- *                table (256 ints per row; the search reserves T from an upper bound of nch), ordinals T .. T+nblk-1
- *                the list blocks (row of 64 lanes x 8 codes). Entries past them name row 0 (valid memory: the pair
- *                loops prefetch a block ahead).
+ *   group table: [0] = list blocks nblk (wave-uniform trip count of the pair loops), [1] = nch | Tc << 10 | T << 16
+ *                (tableWord) with nch the chunk-table entries, Tc the rows of chunk bases and T all table rows,
+ *                [2 + r] = row of ordinal r. Ordinals 0 .. Tc-1 hold the chunk bases (256 ints per row), ordinals
+ *                Tc .. T-1 the chunk masks (bit k of slot s: source c0 + k was staged for the group, i.e. lies in the
+ *                group's search box; 128 {lo, hi} int pairs per row; the search reserves Tc and T from an upper bound
+ *                of nch), ordinals T .. T+nblk-1 the list blocks (row of 64 lanes x 8 codes). Entries past them name
+ *                row 0 (valid memory: the pair loops prefetch a block ahead). Every code (s, k) of a list has bit k of
+ *                mask s set (s >= 1), so the union of a group's sources is known from the table alone: the LDS-staged
+ *                pair loops (hydro.hip StagedGroup) load it once per group.
  * Rows: group g owns `home` rows (g*home ..), chosen by the host from the previous search's row counts; rows past
  * those come from one of 64 overflow stripes through an atomic counter per stripe (neighbors.hip). The host reads
  * the counters and repeats the search with more overflow rows if a stripe ran out.
@@ -43,10 +47,14 @@ constexpr unsigned kChunkSlotBits = 10;
 constexpr unsigned kChunkSlotMask = (1u << kChunkSlotBits) - 1;
 //! rows of a chunk table at capacity
 constexpr unsigned kChunkTabRowsMax = (kChunkCap + 255) / 256;
+//! rows of the chunk masks at capacity (64-bit mask of the staged sources per slot, 128 per row)
+constexpr unsigned kMaskTabRowsMax = (kChunkCap + 127) / 128;
+//! table rows (chunk bases + masks) at capacity
+constexpr unsigned kTableRowsMax = kChunkTabRowsMax + kMaskTabRowsMax;
 //! list blocks a lane may fill: ngmax neighbors + the target itself
 SPHX_HD constexpr unsigned listBlocksMax(unsigned ngmax) { return (ngmax + 1 + 7) / 8; }
-//! rows a group may use (chunk table + list blocks)
-SPHX_HD constexpr unsigned packedRowsMax(unsigned ngmax) { return listBlocksMax(ngmax) + kChunkTabRowsMax; }
+//! rows a group may use (chunk table + masks + list blocks)
+SPHX_HD constexpr unsigned packedRowsMax(unsigned ngmax) { return listBlocksMax(ngmax) + kTableRowsMax; }
 //! ints per group table: counts + rows + 2 prefetch entries, rounded to 4 (16-B aligned tables)
 SPHX_HD constexpr unsigned packedTableInts(unsigned ngmax) { return (2 + packedRowsMax(ngmax) + 2 + 3) & ~3u; }
 //! ints of the table region of a list buffer for `groups` target groups (rows start 1-KiB aligned)
@@ -56,6 +64,13 @@ SPHX_HD constexpr int64_t packedTableRegion(int64_t groups, unsigned ngmax)
 }
 //! rows of a chunk table with nch entries
 SPHX_HD constexpr unsigned chunkTabRows(unsigned nch) { return (nch + 255) / 256; }
+//! rows of the chunk masks of nch entries
+SPHX_HD constexpr unsigned maskTabRows(unsigned nch) { return (nch + 127) / 128; }
+//! group-table word 1: chunk-table entries | chunk-base rows << 10 | table rows << 16
+SPHX_HD constexpr uint32_t tableWord(unsigned nch, unsigned Tc, unsigned T) { return nch | Tc << 10 | T << 16; }
+SPHX_HD constexpr unsigned tableWordNch(uint32_t w) { return w & 0x3FFu; }
+SPHX_HD constexpr unsigned tableWordTc(uint32_t w) { return (w >> 10) & 0x3Fu; }
+SPHX_HD constexpr unsigned tableWordT(uint32_t w) { return w >> 16; }
 //! code of particle c0 + k of chunk slot s
 SPHX_HD constexpr uint32_t chunkCode(unsigned s, unsigned k) { return s | (k << kChunkSlotBits); }
 

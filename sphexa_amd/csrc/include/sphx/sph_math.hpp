@@ -1020,6 +1020,22 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const MomS
 }
 #endif
 
+/*! @brief cross-wave reductions of the LDS-staged loops (csrc/hip/staged.h: W waves split one group's neighbor
+ *         lists and add their partial sums after the loop). Every other loader: nothing to do. The J-loops start
+ *         their sums at zero and add the target's own term after the reduction, so it is counted once. */
+template<class Ld, class... T>
+SPHX_HD void reduceAcross(const Ld&, T&...)
+{
+}
+template<class Ld, class... T>
+SPHX_HD void reduceAcrossMax(const Ld&, T&...)
+{
+}
+template<class Ld>
+SPHX_HD void reduceAcrossN(const Ld&, HT*, int)
+{
+}
+
 //! @brief xm_i = m_i / rho0_i, rho0_i = K h^-3 sum_j W_ij m_j including self (reference xmass_kern.hpp)
 template<class Idx, class Ld>
 SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
@@ -1047,9 +1063,9 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const G& box, const Idx* nbr,
     HT mi = massOf(pi, mUniform), xmi = pi.xm;
     HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv;
 
-    HT kxi      = xmi;
-    HT whomegai = -HT(3) * xmi;
-    HT wrho0i   = -HT(3) * mi;
+    HT kxi      = 0;
+    HT whomegai = 0;
+    HT wrho0i   = 0;
     forEachNeighbor<SPHX_BATCH_POS>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
         pairSep(box, pi, pj, hi, rx, ry, rz);
@@ -1063,6 +1079,11 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const G& box, const Idx* nbr,
         whomegai += dterh * xmj;
         wrho0i += dterh * massOf(pj, mUniform);
     });
+    reduceAcross(ld, kxi, whomegai, wrho0i);
+    // the target's own terms: W(0) = 1, dW(0) = 0
+    kxi += xmi;
+    whomegai += -HT(3) * xmi;
+    wrho0i += -HT(3) * mi;
     HT Kf = HT(K);
     kxi *= Kf * h3Inv;
     whomegai *= Kf * h3Inv * hInv;
@@ -1210,6 +1231,9 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nb
         M[2][1] += az * ry;
         M[2][2] += az * rz;
     });
+    reduceAcrossN(ld, tau, 6);
+    reduceAcrossN(ld, &M[0][0], 9);
+    if constexpr (kAvS) reduceAcrossN(ld, S, 3);
     invertTau(tau, hi, K, c);
     if constexpr (kAvS)
     {
@@ -1354,6 +1378,8 @@ SPHX_HD HT avSwitchesVJLoop(unsigned i, double K, const G& box, const Idx* nbr, 
         T[1] += wd * ry;
         T[2] += wd * rz;
     });
+    reduceAcross(ld, T[0], T[1], T[2]);
+    reduceAcrossMax(ld, vsig);
     const HT D[3] = {divvi * Si[0] - T[0], divvi * Si[1] - T[1], divvi * Si[2] - T[2]};
     const HT s    = -HT(K) * hInv3;
     HT gx = s * (ci6[0] * D[0] + ci6[1] * D[1] + ci6[2] * D[2]);
@@ -1496,6 +1522,8 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, 
         e1 += mja * Wi * vui;
         e2 += av * Wi * vui + bv * Wj * vuj;
     });
+    reduceAcross(ld, mx, my, mz, e1, e2);
+    reduceAcrossMax(ld, maxvs);
     HT aviscE     = smax(HT(0), HT(-0.5) * e2);
     HT Kf         = HT(sc.K);
     duOut         = double(Kf * (-prhoi * e1 + HT(0.5) * aviscE));

@@ -61,6 +61,13 @@ class NeighborList:
 CHUNK_CAP = 512
 CHUNK_SLOT_BITS = 10
 CHUNK_TAB_ROWS_MAX = (CHUNK_CAP + 255) // 256
+MASK_TAB_ROWS_MAX = (CHUNK_CAP + 127) // 128  # 64-bit staged-source mask per slot, 128 per row
+TABLE_ROWS_MAX = CHUNK_TAB_ROWS_MAX + MASK_TAB_ROWS_MAX
+
+
+def table_word(nch: int, tc: int, t: int) -> int:
+    """group-table word 1 (packed_list.hpp tableWord)"""
+    return nch | tc << 10 | t << 16
 
 
 def list_blocks_max(ngmax: int) -> int:
@@ -68,7 +75,7 @@ def list_blocks_max(ngmax: int) -> int:
 
 
 def packed_rows_max(ngmax: int) -> int:
-    return list_blocks_max(ngmax) + CHUNK_TAB_ROWS_MAX
+    return list_blocks_max(ngmax) + TABLE_ROWS_MAX
 
 
 def packed_table_ints(ngmax: int) -> int:
@@ -102,22 +109,31 @@ def pack_lists(lists, first: int, ngmax: int, device=None) -> NeighborList:
         table = [first + g * GROUP] + bases
         slot = {b: s + 1 for s, b in enumerate(bases)}
         codes = [[slot[j & ~63] | ((j & 63) << CHUNK_SLOT_BITS) for j in lst] for lst in glists]
+        # staged-source masks: every source a code names (slot 0, the padding slot, has none)
+        masks = [0] * len(table)
+        for lst in glists:
+            for j in lst:
+                masks[slot[j & ~63]] |= 1 << (j & 63)
         nblk = max([(len(c) + 7) // 8 for c in codes] + [0])
-        per_group.append((table, codes, nblk))
-    nrows = [-(-len(tb) // 256) + nb for tb, _, nb in per_group]
+        per_group.append((table, masks, codes, nblk))
+    nrows = [-(-len(tb) // 256) + -(-len(tb) // 128) + nb for tb, _, _, nb in per_group]
     total = max(sum(nrows), 1)
     buf = np.zeros(region + total * 256, dtype=np.int32)
     tab = buf[:groups * T_I].reshape(groups, T_I)
     rows = buf[region:].reshape(total, 256)
     rows16 = buf[region:].view(np.uint16).reshape(total, GROUP, 8)
     r0 = 0
-    for g, (table, codes, nblk) in enumerate(per_group):
-        T = -(-len(table) // 256)
+    for g, (table, masks, codes, nblk) in enumerate(per_group):
+        Tc = -(-len(table) // 256)
+        T = Tc + -(-len(table) // 128)
         tab[g, 0] = nblk
-        tab[g, 1] = len(table) | (T << 16)
+        tab[g, 1] = table_word(len(table), Tc, T)
         tab[g, 2:2 + T + nblk] = np.arange(r0, r0 + T + nblk)
         for e, v in enumerate(table):
             rows[r0 + e // 256, e % 256] = v
+        for e, mk in enumerate(masks):
+            rows[r0 + Tc + e // 128, 2 * (e % 128)] = np.uint32(mk & 0xFFFFFFFF).view(np.int32)
+            rows[r0 + Tc + e // 128, 2 * (e % 128) + 1] = np.uint32(mk >> 32).view(np.int32)
         for lane in range(GROUP):
             c = codes[lane] if lane < len(codes) else []
             # padding decodes to the target itself; lanes past the last target to the last target (a valid record)
@@ -139,7 +155,7 @@ def decode_packed(nl: NeighborList):
     T_I, region = packed_table_ints(nl.ngmax), packed_table_region(groups, nl.ngmax)
     tab = buf[:groups * T_I].view(groups, T_I).long()
     nblk = tab[:, 0]
-    nch = tab[:, 1] & 0xFFFF
+    nch = tab[:, 1] & 0x3FF
     T = tab[:, 1] >> 16
     R = max(int(nblk.max()), 1)
     data = buf[region:].view(-1, 256)
