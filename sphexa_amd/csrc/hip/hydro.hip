@@ -468,14 +468,16 @@ __global__ __launch_bounds__(B) void xmassQKernel(NbrArgs a, SphConsts sc, QFram
     const KernelFn kf{wh, nullptr, sc.sincIndex, sc.kernelChoice};
     const SrcPosQ pi = ld(unsigned(i));
     const float hi = h[i], hInv = 1.f / hi, h3Inv = hInv * hInv * hInv;
-    float rho0 = pi.m;
+    // quarter arguments u = r / (4h): the quantum and 1/(4h) folded into one scale per dimension (KernelFn::wq)
+    const float sx = q.inv[0] * 0.25f * hInv, sy = q.inv[1] * 0.25f * hInv, sz = q.inv[2] * 0.25f * hInv;
+    float rho0 = 0.f;
     forEachNeighbor<SPHX_BATCH_POS>(&pl, 0, n, ld, [&](unsigned, const SrcPosQ& pj) {
-        const float rx   = float(int32_t(pi.x - pj.x)) * q.inv[0];
-        const float ry   = float(int32_t(pi.y - pj.y)) * q.inv[1];
-        const float rz   = float(int32_t(pi.z - pj.z)) * q.inv[2];
-        const float dist = sqrtF(rx * rx + ry * ry + rz * rz);
-        rho0 += kf.w(dist * hInv) * pj.m;
+        const float ux = float(int32_t(pi.x - pj.x)) * sx;
+        const float uy = float(int32_t(pi.y - pj.y)) * sy;
+        const float uz = float(int32_t(pi.z - pj.z)) * sz;
+        rho0 += kf.wq(sqrtF(ux * ux + uy * uy + uz * uz)) * pj.m;
     });
+    rho0 = pi.m + rho0 / kf.wqScale();
     if (!valid) return;
     const float v = pi.m / (rho0 * float(sc.K) * h3Inv);
     xm[i]         = v;
@@ -501,16 +503,16 @@ __global__ __launch_bounds__(64 * W) void xmassQStagedKernel(NbrArgs a, SphConst
     const KernelFn kf{wh, nullptr, sc.sincIndex, sc.kernelChoice};
     const SrcPosQ pi = ld(unsigned(i));
     const float hi = h[i], hInv = 1.f / hi, h3Inv = hInv * hInv * hInv;
+    const float sx = q.inv[0] * 0.25f * hInv, sy = q.inv[1] * 0.25f * hInv, sz = q.inv[2] * 0.25f * hInv;
     float rho0 = 0.f;
     forEachNeighbor<SPHX_BATCH_POS>(&sl, 0, n, ld, [&](unsigned, const SrcPosQ& pj) {
-        const float rx   = float(int32_t(pi.x - pj.x)) * q.inv[0];
-        const float ry   = float(int32_t(pi.y - pj.y)) * q.inv[1];
-        const float rz   = float(int32_t(pi.z - pj.z)) * q.inv[2];
-        const float dist = sqrtF(rx * rx + ry * ry + rz * rz);
-        rho0 += kf.w(dist * hInv) * pj.m;
+        const float ux = float(int32_t(pi.x - pj.x)) * sx;
+        const float uy = float(int32_t(pi.y - pj.y)) * sy;
+        const float uz = float(int32_t(pi.z - pj.z)) * sz;
+        rho0 += kf.wq(sqrtF(ux * ux + uy * uy + uz * uz)) * pj.m;
     });
     reduceAcross(ld, rho0);
-    rho0 += pi.m;
+    rho0 = pi.m + rho0 / kf.wqScale();
     if (!valid || threadIdx.x >= 64) return;
     const float v = pi.m / (rho0 * float(sc.K) * h3Inv);
     xm[i]         = v;

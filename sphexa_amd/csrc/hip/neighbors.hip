@@ -854,12 +854,15 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
         const unsigned rw = ra.rowU(0);
         if (rw < po.poolRows) rowsInt[size_t(rw) * 256] = int32_t(first + g * 64);
     }
-    // group table: block count, chunk entries | table rows << 16, row of every ordinal
+    // group table: block count, chunk entries | table rows << 16, row of every ordinal. A group whose rows ran past
+    // its overflow stripe (the host repeats the search with a larger pool) gets no list blocks: a pair loop enqueued
+    // speculatively on these lists (models/propagators.py) must not decode the borrowed row 0 as this group's codes
+    const bool rowsLost = ballot(lane < T + nblk && (lane >= ra.n || ra.reg >= po.poolRows)) != 0;
     int32_t* tab = po.tab + g * int64_t(po.tabInts);
     const unsigned ord = lane >= 2 ? lane - 2 : 0u;
     const unsigned rwo = ra.row(ord);
     if (lane < po.tabInts)
-        tab[lane] = lane == 0   ? int32_t(nblk)
+        tab[lane] = lane == 0   ? int32_t(rowsLost ? 0u : nblk)
                     : lane == 1 ? int32_t(tableWord(slot, Tc, T))
                                 : (ord < T + nblk && rwo < po.poolRows ? int32_t(rwo) : 0);
     if (lane == 0)

@@ -153,9 +153,55 @@ struct KernelFn
         HT s2 = s * s, s3 = s2 * s, s8 = (s2 * s2) * (s2 * s2);
         return (HT(0.9) * HT(4) * s3 + HT(0.1) * HT(9) * s8) * ds;
     }
+    /* Quarter-argument forms of the pair loops: u = v / 4, so the hardware sine (v_sin_f32 takes revolutions,
+     * sin(2 pi u) = sin(pi v / 2)) needs no argument scaling and sinc * 2 pi = sin(2 pi u) / u needs no division by
+     * pi/2. For choice 0 the constant (2 pi)^n is left in every term: wq(u) = S w(4u), S = wqScale(), and the loops
+     * divide their sums by S once per target (every term of a sum carries exactly one kernel value). v dW/dv needs no
+     * division either: v d(sinc^n)/dv = n sinc^(n-1) (cos x - sinc). Choice 1 (the sinc^4 / sinc^9 mix): S = 1. */
+    SPHX_HD HT wqScale() const
+    {
+        // (in double: once per target, and the fp32 exp2 would add its ulp to every sum)
+        constexpr double log2TwoPi = 2.651496129472318798043279295;
+        return choice == 0 ? HT(exp2(double(n) * log2TwoPi)) : HT(1);
+    }
+    SPHX_HD HT wq(HT u) const
+    {
+        if (choice != 0) return w(HT(4) * u);
+        constexpr HT twoPi = HT(6.283185307179586);
+        HT sq = __builtin_amdgcn_sinf(u) * rcpF(u);
+        sq    = u > HT(0) ? sq : twoPi; // (r = 0: sinc = 1)
+        const HT r = powN(sq, n);
+        return u < HT(0.5) ? r : HT(0);
+    }
+    //! @brief S w(4u) and S v dW/dv at v = 4u (see wq)
+    SPHX_HD void wdq(HT u, HT& wS, HT& vdwS) const
+    {
+        if (choice != 0)
+        {
+            wS   = w(HT(4) * u);
+            vdwS = HT(4) * u * dw(HT(4) * u);
+            return;
+        }
+        constexpr HT twoPi = HT(6.283185307179586);
+        HT sq = __builtin_amdgcn_sinf(u) * rcpF(u);
+        sq    = u > HT(0) ? sq : twoPi;
+        const HT cs = __builtin_amdgcn_cosf(u);
+        const HT p  = powN(sq, n - HT(1));
+        const bool in = u < HT(0.5);
+        wS   = in ? p * sq : HT(0);
+        vdwS = in ? n * p * (twoPi * cs - sq) : HT(0);
+    }
 #else
     SPHX_HD HT w(HT v) const { return tableLookup(wh, v); }
     SPHX_HD HT dw(HT v) const { return tableLookup(whd, v); }
+    //! host forms of the quarter-argument interface (no scaling: S = 1)
+    SPHX_HD HT wqScale() const { return HT(1); }
+    SPHX_HD HT wq(HT u) const { return w(HT(4) * u); }
+    SPHX_HD void wdq(HT u, HT& wS, HT& vdwS) const
+    {
+        wS   = w(HT(4) * u);
+        vdwS = HT(4) * u * dw(HT(4) * u);
+    }
 #endif
 };
 
@@ -1042,14 +1088,15 @@ SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
                       const Ld& ld, const KernelFn& kf)
 {
     SrcPos pi = ld(i);
-    HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv;
-    HT rho0 = pi.m;
+    HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv, hq = HT(0.25) * hInv;
+    HT rho0 = 0;
     forEachNeighbor<SPHX_BATCH_POS>(nbr, stride, nc, ld, [&](unsigned j, const SrcPos& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
-        rho0 += kf.w(dist * hInv) * pj.m;
+        rho0 += kf.wq(dist * hq) * pj.m;
     });
+    rho0 = pi.m + rho0 / kf.wqScale(); // (kernel scale, KernelFn::wq; the target's own term W(0) m_i)
     return pi.m / (rho0 * HT(K) * h3Inv);
 }
 
@@ -1061,7 +1108,7 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const G& box, const Idx* nbr,
 {
     const auto pi = ld(i);
     HT mi = massOf(pi, mUniform), xmi = pi.xm;
-    HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv;
+    HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv, hq = HT(0.25) * hInv;
 
     HT kxi      = 0;
     HT whomegai = 0;
@@ -1070,20 +1117,20 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const G& box, const Idx* nbr,
         HT rx, ry, rz;
         pairSep(box, pi, pj, hi, rx, ry, rz);
         HT dist  = sqrtF(rx * rx + ry * ry + rz * rz);
-        HT v     = dist * hInv;
-        HT w     = kf.w(v);
-        HT dw    = kf.dw(v);
-        HT dterh = -(HT(3) * w + v * dw);
+        HT w, vdw; // (S-scaled, KernelFn::wdq)
+        kf.wdq(dist * hq, w, vdw);
+        HT dterh = -(HT(3) * w + vdw);
         HT xmj   = pj.xm;
         kxi += w * xmj;
         whomegai += dterh * xmj;
         wrho0i += dterh * massOf(pj, mUniform);
     });
     reduceAcross(ld, kxi, whomegai, wrho0i);
-    // the target's own terms: W(0) = 1, dW(0) = 0
-    kxi += xmi;
-    whomegai += -HT(3) * xmi;
-    wrho0i += -HT(3) * mi;
+    // the kernel scale, then the target's own terms: W(0) = 1, dW(0) = 0
+    const HT invS = HT(1) / kf.wqScale();
+    kxi      = xmi + kxi * invS;
+    whomegai = -HT(3) * xmi + whomegai * invS;
+    wrho0i   = -HT(3) * mi + wrho0i * invS;
     HT Kf = HT(K);
     kxi *= Kf * h3Inv;
     whomegai *= Kf * h3Inv * hInv;
@@ -1122,12 +1169,12 @@ SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
 {
     HT tau[6] = {0, 0, 0, 0, 0, 0};
     SrcIad pi = ld(i);
-    HT hInv   = HT(1) / hi;
+    HT hq     = HT(0.25) / hi;
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
-        HT w    = kf.w(dist * hInv);
+        HT w    = kf.wq(dist * hq);
         HT vw   = pj.vol * w;
         tau[0] += rx * rx * vw;
         tau[1] += rx * ry * vw;
@@ -1136,6 +1183,9 @@ SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
         tau[4] += ry * rz * vw;
         tau[5] += rz * rz * vw;
     });
+    const HT invS = HT(1) / kf.wqScale();
+    for (int k = 0; k < 6; ++k)
+        tau[k] *= invS;
     invertTau(tau, hi, K, c);
 }
 
@@ -1145,7 +1195,7 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
                             HT kxi, const HT ci[6], const Ld& ld, const KernelFn& kf, HT& divvOut, HT& curlvOut, HT* dV)
 {
     SrcIad pi = ld(i);
-    HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
+    HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv, hq = HT(0.25) * hInv;
     HT c11 = ci[0], c12 = ci[1], c13 = ci[2], c22 = ci[3], c23 = ci[4], c33 = ci[5];
     HT dVx[3] = {0, 0, 0}, dVy[3] = {0, 0, 0}, dVz[3] = {0, 0, 0};
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const SrcIad& pj) {
@@ -1153,7 +1203,7 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
         HT vxji = pj.vx - pi.vx, vyji = pj.vy - pi.vy, vzji = pj.vz - pi.vz;
-        HT W    = kf.w(dist * hInv);
+        HT W    = kf.wq(dist * hq);
         HT tA0  = -(c11 * rx + c12 * ry + c13 * rz) * W;
         HT tA1  = -(c12 * rx + c22 * ry + c23 * rz) * W;
         HT tA2  = -(c13 * rx + c23 * ry + c33 * rz) * W;
@@ -1169,7 +1219,7 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
         dVz[1] += az * tA1;
         dVz[2] += az * tA2;
     });
-    HT nk   = HT(K) * hInv3 / kxi;
+    HT nk   = HT(K) * hInv3 / (kxi * kf.wqScale());
     divvOut = nk * (dVx[0] + dVy[1] + dVz[2]);
     HT cx = dVz[1] - dVy[2], cy = dVx[2] - dVz[0], cz = dVy[0] - dVx[1];
     curlvOut = nk * sqrt(cx * cx + cy * cy + cz * cz);
@@ -1200,12 +1250,12 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nb
     HT M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
     HT S[3]    = {0, 0, 0};
     const auto pi = ld(i);
-    HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv;
+    HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv, hq = HT(0.25) * hInv;
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
         pairSep(box, pi, pj, hi, rx, ry, rz);
         HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
-        HT w    = kf.w(dist * hInv);
+        HT w    = kf.wq(dist * hq);
         HT vw   = pj.vol * w;
         tau[0] += rx * rx * vw;
         tau[1] += rx * ry * vw;
@@ -1234,6 +1284,18 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nb
     reduceAcrossN(ld, tau, 6);
     reduceAcrossN(ld, &M[0][0], 9);
     if constexpr (kAvS) reduceAcrossN(ld, S, 3);
+    {
+        // the kernel scale (KernelFn::wq)
+        const HT invS = HT(1) / kf.wqScale();
+        for (int k = 0; k < 6; ++k)
+            tau[k] *= invS;
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b)
+                M[a][b] *= invS;
+        if constexpr (kAvS)
+            for (int k = 0; k < 3; ++k)
+                S[k] *= invS;
+    }
     invertTau(tau, hi, K, c);
     if constexpr (kAvS)
     {
@@ -1274,9 +1336,10 @@ SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const G& box, const Idx* nbr, i
     HT ci     = pi.c;
     HT c11 = ci6[0], c12 = ci6[1], c13 = ci6[2], c22 = ci6[3], c23 = ci6[4], c33 = ci6[5];
     HT vsig  = HT(1.e-40) * ci;
-    HT hInv  = HT(1) / hi, hInv3 = hInv * hInv * hInv;
+    HT hInv  = HT(1) / hi, hInv3 = hInv * hInv * hInv, hq = HT(0.25) * hInv;
     HT divvi = pi.divv;
     HT gx = 0, gy = 0, gz = 0;
+    const HT KhS = HT(K) * hInv3 / kf.wqScale();
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
         pairSep(box, pi, pj, hi, rx, ry, rz);
@@ -1290,7 +1353,7 @@ SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const G& box, const Idx* nbr, i
         HT vst  = ci + pj.c - HT(3) * rv * invDist;
         HT vsij = rv < HT(0) ? vst : HT(0);
         vsig   = smax(vsig, vsij);
-        HT W   = HT(K) * hInv3 * kf.w(dist * hInv);
+        HT W   = KhS * kf.wq(dist * hq);
         HT tA0 = -(c11 * rx + c12 * ry + c13 * rz) * W;
         HT tA1 = -(c12 * rx + c22 * ry + c23 * rz) * W;
         HT tA2 = -(c13 * rx + c23 * ry + c33 * rz) * W;
@@ -1358,7 +1421,7 @@ SPHX_HD HT avSwitchesVJLoop(unsigned i, double K, const G& box, const Idx* nbr, 
     const auto pi = ld(i);
     HT ci    = pi.c;
     HT vsig  = HT(1.e-40) * ci;
-    HT hInv  = HT(1) / hi, hInv3 = hInv * hInv * hInv;
+    HT hInv  = HT(1) / hi, hInv3 = hInv * hInv * hInv, hq = HT(0.25) * hInv;
     HT T[3]  = {0, 0, 0};
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
@@ -1373,13 +1436,19 @@ SPHX_HD HT avSwitchesVJLoop(unsigned i, double K, const G& box, const Idx* nbr, 
         HT vst  = ci + pj.c - HT(3) * rv * invDist;
         HT vsij = rv < HT(0) ? vst : HT(0);
         vsig  = smax(vsig, vsij);
-        HT wd = kf.w(dist * hInv) * pj.vd;
+        HT wd = kf.wq(dist * hq) * pj.vd;
         T[0] += wd * rx;
         T[1] += wd * ry;
         T[2] += wd * rz;
     });
     reduceAcross(ld, T[0], T[1], T[2]);
     reduceAcrossMax(ld, vsig);
+    {
+        const HT invS = HT(1) / kf.wqScale(); // (KernelFn::wq)
+        T[0] *= invS;
+        T[1] *= invS;
+        T[2] *= invS;
+    }
     const HT D[3] = {divvi * Si[0] - T[0], divvi * Si[1] - T[1], divvi * Si[2] - T[2]};
     const HT s    = -HT(K) * hInv3;
     HT gx = s * (ci6[0] * D[0] + ci6[1] * D[1] + ci6[2] * D[2]);
@@ -1462,9 +1531,11 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, 
         HT dist    = r2 * invDist;
         HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
         HT hjInv = pj.ih;
-        HT v1 = dist * hInv, v2 = dist * hjInv;
-        HT Wi = hInv3 * kf.w(v1);
-        HT Wj = hjInv * hjInv * hjInv * kf.w(v2);
+        // quarter arguments and S-scaled kernel values (KernelFn::wq; the sums are rescaled once after the loop)
+        HT dq = HT(0.25) * dist;
+        HT u1 = dq * hInv, u2 = dq * hjInv;
+        HT Wi = hInv3 * kf.wq(u1);
+        HT Wj = hjInv * hjInv * hjInv * kf.wq(u2);
 
         // u = C r for the target and the neighbor
         HT uix = pi.c11 * rx + pi.c12 * ry + pi.c13 * rz;
@@ -1480,7 +1551,7 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, 
         if (avClean)
         {
             SrcGradV gj = ldg(j);
-            rv += avRvCorrection(rx, ry, rz, smin(v1, v2), etaCrit, gVi, gj.dV);
+            rv += avRvCorrection(rx, ry, rz, HT(4) * smin(u1, u2), etaCrit, gVi, gj.dV);
         }
         HT wij  = rv * invDist;
         HT visc = artificialViscosity(alphai, pj.alpha, ci, cj, wij);
@@ -1525,7 +1596,7 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, 
     reduceAcross(ld, mx, my, mz, e1, e2);
     reduceAcrossMax(ld, maxvs);
     HT aviscE     = smax(HT(0), HT(-0.5) * e2);
-    HT Kf         = HT(sc.K);
+    HT Kf         = HT(sc.K) / kf.wqScale(); // (every summed term carries one S-scaled kernel value)
     duOut         = double(Kf * (-prhoi * e1 + HT(0.5) * aviscE));
     axOut         = Kf * mx;
     ayOut         = Kf * my;
@@ -1552,10 +1623,11 @@ SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const 
         HT dist    = r2 * invDist;
         HT vxij = pi.vx - pj.vx, vyij = pi.vy - pj.vy, vzij = pi.vz - pj.vz;
         HT hjInv = pj.ih;
-        HT v1 = dist * hInv, v2 = dist * hjInv;
+        HT dq = HT(0.25) * dist;
+        HT u1 = dq * hInv, u2 = dq * hjInv;
         HT rv = rx * vxij + ry * vyij + rz * vzij;
-        HT Wi = hInv3 * kf.w(v1);
-        HT Wj = hjInv * hjInv * hjInv * kf.w(v2);
+        HT Wi = hInv3 * kf.wq(u1); // (S-scaled: KernelFn::wq)
+        HT Wj = hjInv * hjInv * hjInv * kf.wq(u2);
         HT tAi0 = pi.c11 * rx + pi.c12 * ry + pi.c13 * rz;
         HT tAi1 = pi.c12 * rx + pi.c22 * ry + pi.c23 * rz;
         HT tAi2 = pi.c13 * rx + pi.c23 * ry + pi.c33 * rz;
@@ -1583,7 +1655,7 @@ SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const 
             energy += vxij * (a * tAi0 + b * tAj0) + vyij * (a * tAi1 + b * tAj1) + vzij * (a * tAi2 + b * tAj2);
         }
     });
-    HT Kf         = HT(K);
+    HT Kf         = HT(K) / kf.wqScale();
     duOut         = double(-Kf * HT(0.5) * energy);
     axOut         = Kf * mx;
     ayOut         = Kf * my;

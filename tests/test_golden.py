@@ -307,8 +307,12 @@ def _check_std(dev, f):
     for k, c in enumerate(("c11", "c12", "c13", "c22", "c23", "c33")):
         d[c] = c6[k]
     H.compute_momentum_energy_std(d, nl, B)
-    for got, (w, _) in zip([float(d[c][0]) for c in ("ax", "ay", "az", "du")], STD_MOM):
-        assert got == pytest.approx(w, rel=2e-6, abs=1e-7)
+    # acceleration components against the largest one (ay = -1.24 is a sum of terms of ~15 that nearly cancel: fp32
+    # rounding of the analytic GPU kernel, ~1e-7 per term, is ~3e-6 of ay alone), du relative to itself
+    amax = max(abs(w) for w, _ in STD_MOM[:3])
+    for got, (w, _) in zip([float(d[c][0]) for c in ("ax", "ay", "az")], STD_MOM[:3]):
+        assert abs(got - w) <= 5e-7 * amax
+    assert float(d["du"][0]) == pytest.approx(STD_MOM[3][0], rel=2e-6, abs=1e-7)
 
 
 def test_production_cpu_xmass_gradh(fx):
