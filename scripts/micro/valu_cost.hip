@@ -94,6 +94,9 @@ DEF_K(kCvtU, "v_cvt_f32_u32 %0, %1", float, unsigned)
 DEF_K(kExp, "v_exp_f32 %0, %0", float, float)
 DEF_K(kCmpOnly, "v_cmp_gt_f32 vcc, %0, %1", float, float)
 DEF_K(kMad24, "v_mad_u32_u24 %0, %0, %1, 3", unsigned, unsigned)
+DEF_K(kMulLit, "v_mul_f32 %0, 0x3f9df3b6, %0", float, float)
+DEF_K(kMulInl, "v_mul_f32 %0, 2.0, %0", float, float)
+DEF_K(kCnd, "v_cndmask_b32 %0, %0, %1, s[0:1]", float, float)
 DEF_S(kFmaS, "v_fma_f32 %0, %0, %1, 1.0")
 DEF_S(kMulS, "v_mul_f32 %0, %1, %0")
 DEF_S(kAddS, "v_add_f32 %0, %1, %0")
@@ -154,6 +157,9 @@ int main()
     run("v_exp_f32", kExp, out, f, 1);
     run("v_cmp_gt_f32 (vcc)", kCmpOnly, out, f, 1);
     run("v_mad_u32_u24", kMad24, out, f, 1);
+    run("v_mul_f32 literal", kMulLit, out, f, 1);
+    run("v_mul_f32 inline 2.0", kMulInl, out, f, 1);
+    run("v_cndmask_b32 s[0:1]", kCnd, out, f, 1);
     run("v_fma_f32 sgpr", kFmaS, out, f, 1, 0.999f);
     run("v_mul_f32 sgpr", kMulS, out, f, 1, 0.999f);
     run("v_add_f32 sgpr", kAddS, out, f, 1, 0.5f);

@@ -493,6 +493,27 @@ SPHX_HD void pairSep(const QFrame& q, const R& pi, const R& pj, HT, HT& rx, HT& 
     rz = HT(int32_t(pi.z - pj.z)) * q.inv[2];
 }
 
+/*! @brief v held in a vector register from here on (GPU). On gfx950 VALU instructions that read an SGPR operand issue
+ *         at ~60 % of the rate of their all-VGPR forms (fma/mul/add: ~1.7x slower, scripts/micro/valu_cost.hip), so
+ *         the pair loops copy their loop-invariant uniform constants to VGPRs once. Host: identity. */
+template<class T>
+SPHX_HD T inVgpr(T v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(v));
+#endif
+    return v;
+}
+
+//! @brief the frame of a pair loop with its inverse quanta in VGPRs (inVgpr); fp64 boxes unchanged
+SPHX_HD QFrame vgprFrame(QFrame q)
+{
+    for (int k = 0; k < 3; ++k)
+        q.inv[k] = inVgpr(q.inv[k]);
+    return q;
+}
+SPHX_HD const Box& vgprFrame(const Box& b) { return b; }
+
 //! @brief 1/sqrt(x) in hydro precision (annotation.hpp rsqrtF)
 SPHX_HD HT rsqrtH(HT x) { return rsqrtF(x); }
 
@@ -1113,9 +1134,10 @@ SPHX_HD void veDefGradhJLoop(unsigned i, double K, const G& box, const Idx* nbr,
     HT kxi      = 0;
     HT whomegai = 0;
     HT wrho0i   = 0;
+    const auto bx = vgprFrame(box);
     forEachNeighbor<SPHX_BATCH_POS>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
-        pairSep(box, pi, pj, hi, rx, ry, rz);
+        pairSep(bx, pi, pj, hi, rx, ry, rz);
         HT dist  = sqrtF(rx * rx + ry * ry + rz * rz);
         HT w, vdw; // (S-scaled, KernelFn::wdq)
         kf.wdq(dist * hq, w, vdw);
@@ -1251,9 +1273,10 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nb
     HT S[3]    = {0, 0, 0};
     const auto pi = ld(i);
     HT hInv = HT(1) / hi, hInv3 = hInv * hInv * hInv, hq = HT(0.25) * hInv;
+    const auto bx = vgprFrame(box);
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
-        pairSep(box, pi, pj, hi, rx, ry, rz);
+        pairSep(bx, pi, pj, hi, rx, ry, rz);
         HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
         HT w    = kf.wq(dist * hq);
         HT vw   = pj.vol * w;
@@ -1423,9 +1446,10 @@ SPHX_HD HT avSwitchesVJLoop(unsigned i, double K, const G& box, const Idx* nbr, 
     HT vsig  = HT(1.e-40) * ci;
     HT hInv  = HT(1) / hi, hInv3 = hInv * hInv * hInv, hq = HT(0.25) * hInv;
     HT T[3]  = {0, 0, 0};
+    const auto bx = vgprFrame(box);
     forEachNeighbor<SPHX_BATCH_IAD>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
-        pairSep(box, pi, pj, hi, rx, ry, rz);
+        pairSep(bx, pi, pj, hi, rx, ry, rz);
         HT r2      = rx * rx + ry * ry + rz * rz;
         HT invDist = rsqrtH(r2);
         HT dist    = r2 * invDist;
@@ -1520,12 +1544,13 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, 
     //   du_i = K (prho_i sum -m_j a_mom W_i v.(C_i r) + 1/2 max(0, -1/2 sum av W_i v.(C_i r) + bv W_j v.(C_j r)))
     // so the six tA components are never formed (profiles/r3_perf_log.md: 144 -> ~100 VALU per pair)
     HT maxvs = 0, mx = 0, my = 0, mz = 0, e1 = 0, e2 = 0;
-    const HT Atmin = sc.Atmin, Atmax = sc.Atmax, ramp = sc.ramp;
+    const HT Atmin = inVgpr(HT(sc.Atmin)), Atmax = inVgpr(HT(sc.Atmax)), ramp = inVgpr(HT(sc.ramp));
     const HT xmi2 = xmi * xmi;
+    const auto bx = vgprFrame(box);
 
     forEachNeighbor<SPHX_BATCH_MOM>(nbr, stride, nc, ld, [&](unsigned j, const auto& pj) {
         HT rx, ry, rz;
-        pairSep(box, pi, pj, hi, rx, ry, rz);
+        pairSep(bx, pi, pj, hi, rx, ry, rz);
         HT r2      = rx * rx + ry * ry + rz * rz;
         HT invDist = rsqrtH(r2);
         HT dist    = r2 * invDist;
