@@ -107,7 +107,8 @@ size_t exclusiveScanTempBytes(int64_t n);
 void exclusiveScanI64Hip(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s);
 void exclusiveScanI64(const int64_t* in, int64_t* out, int64_t n, void* tmp, size_t tmpBytes, hipStream_t s);
 
-// reduce.hip: single-launch reductions (workspace: reduceWorkBytes(), zero-initialized once; one stream at a time)
+// reduce.hip: device reductions in two launches (block partials + one fold kernel; workspace: reduceWorkBytes() of
+// partials, one per concurrently reducing stream)
 size_t reduceWorkBytes();
 void multiMinMax(int64_t n, const std::vector<uintptr_t>& ptrs, const std::vector<int>& isDouble, double* out,
                  void* work, hipStream_t s, int layout = 0);

@@ -1,4 +1,4 @@
-"""Per-step scalar reductions in one launch each on the GPU (csrc/hip/reduce.hip), torch on the host.
+"""Per-step scalar reductions in two native launches each on the GPU (csrc/hip/reduce.hip), torch on the host.
 
 Parity: the reference's per-step extrema (sfc/box_mpi.hpp:83-118 global bounding box, the time-step inputs of
 sph/timestep.hpp) — here as device tensors that ride along in the step's few host copies.
@@ -16,9 +16,10 @@ _WORK: dict = {}
 
 
 def _work(device) -> torch.Tensor:
-    """[ticket | partials] workspace of the single-launch reductions, one per stream: the ticket re-arms itself at
-    the end of every launch, so launches on one stream can share it, but two streams running reductions at the same
-    time (gravity's extents on the side stream during the neighbor search's h reduction) must not"""
+    """partials workspace of the device reductions (reduce.hip: every block writes a partial, one fold kernel reduces
+    them; two launches, no ticket), one per stream: launches on one stream are ordered and can share it, but two
+    streams reducing at the same time (gravity's extents on a side stream during the neighbor search's h reduction)
+    must not (tests/test_gpu_reduce.py::test_reductions_on_two_streams_match_serial)"""
     key = (device, _lib.stream())
     t = _WORK.get(key)
     if t is None:

@@ -73,6 +73,9 @@ def default_bucket_size_focus(gravity: bool, nranks: int = 1) -> int:
 REORDER_BATCH = 3  # conserved fields reordered per gather launch in sync (bounds the transient memory)
 # one rank, GPU: SFC keys from the prefetched device extents, host box taken at the end of the sync
 DEVICE_BOX = os.environ.get("SPHX_DEVICE_BOX", "1") == "1"
+# ranks up to which the global-tree step gathers every rank's leaf counts (size x leaves int64, ~100 leaves per rank):
+# the migration counts then come from the same host copy (Domain._distribute)
+GATHER_COUNTS_MAX_RANKS = int(os.environ.get("SPHX_GATHER_COUNTS_MAX_RANKS", "32"))
 REORDER_ALL_BYTES = 1 << 30  # below this transient size all remaining fields are reordered together
 
 
@@ -383,23 +386,33 @@ class Domain:
         if tree_np is None or tree is None:
             tree_np = np.array([0, octree_ops.KEY_END], dtype=np.uint64)
             tree = self._upload(tree_np.view(np.int64), dev)
+        # every rank's local counts on the replicated tree, gathered (not only summed): one host copy then gives the
+        # global counts for the rebalance AND, when the rank boundaries fall on leaf boundaries of this tree (every
+        # step whose tree did not change), every send and receive count of the migration, so the migration needs no
+        # count exchange and no second host copy (rank-count^2 leaf counts: up to GATHER_COUNTS_MAX_RANKS ranks)
+        gather_all = self.size <= GATHER_COUNTS_MAX_RANKS
+        all_np = None
         for _ in range(64):
             # local counts on the replicated tree -> global counts -> identical rebalance on every rank
             if skeys.is_cuda:
-                gcounts = torch.empty(tree.numel() - 1, dtype=torch.int64, device=dev)
+                lcounts = torch.empty(tree.numel() - 1, dtype=torch.int64, device=dev)
                 _lib.hip().node_counts64(tree.data_ptr(), tree.numel() - 1, skeys.data_ptr(), skeys.numel(),
-                                         gcounts.data_ptr(), _stream())
+                                         lcounts.data_ptr(), _stream())
             else:
-                gcounts = octree_ops.node_counts(tree, skeys).to(torch.int64)
-            self.comm.allreduce(gcounts, SUM)
-            c_np = gcounts.cpu().numpy()
+                lcounts = octree_ops.node_counts(tree, skeys).to(torch.int64)
+            if gather_all:
+                all_np = self.comm.allgather_stacked(lcounts).cpu().numpy().reshape(self.size, -1)
+                c_np = all_np.sum(axis=0)
+            else:
+                self.comm.allreduce(lcounts, SUM)
+                c_np = lcounts.cpu().numpy()
             new_np, changed = _lib.cpu().rebalance(tree_np, c_np.clip(max=2**32 - 1).astype(np.uint32), bucket)
             if not changed:
                 break
             tree_np = new_np
             tree = self._upload(tree_np.view(np.int64), dev)
         L = tree_np.size - 1
-        self.global_tree, self.global_counts, self._tree_np = tree, gcounts, tree_np
+        self.global_tree, self.global_counts, self._tree_np = tree, c_np, tree_np
         PROF.mark("distribute: global tree counts + rebalance")
         n_global = int(c_np.sum())
         self._n_global = n_global
@@ -420,10 +433,19 @@ class Domain:
             for r in range(1, self.size):
                 keys_b[r] = min(max(keys_b[r], old[r - 1]), old[r + 1])
         self.assignment_keys = keys_b
+        # boundaries on leaf boundaries of the counted tree: send/receive counts from the gathered leaf counts
+        lb = np.searchsorted(tree_np, np.array(keys_b, dtype=np.uint64))
+        on_leaves = all_np is not None and bool((tree_np[np.minimum(lb, L)] == np.array(keys_b, dtype=np.uint64)).all())
+        if on_leaves:
+            csum_all = np.concatenate([np.zeros((self.size, 1), dtype=np.int64), np.cumsum(all_np, axis=1)], axis=1)
+            mine = csum_all[self.rank]
+            send_counts = [int(mine[lb[q + 1]] - mine[lb[q]]) for q in range(self.size)]
+            recv_counts = [int(csum_all[q][lb[self.rank + 1]] - csum_all[q][lb[self.rank]]) for q in range(self.size)]
+            self.stats["migration_counts"] = "gathered"
         # send ranges: lower_bound of the boundary keys in the sorted local keys, on the device; send and receive
         # counts come to the host in one copy
-        bkeys = self._upload(np.array(keys_b[1:-1], dtype=np.uint64).view(np.int64), dev)
-        if skeys.is_cuda:
+        elif skeys.is_cuda:
+            bkeys = self._upload(np.array(keys_b[1:-1], dtype=np.uint64).view(np.int64), dev)
             # send counts by one native launch (lower bounds of the boundary keys), received into the second half of
             # the same buffer: one host copy for both
             sr = torch.empty((2 * self.size, 1), dtype=torch.int64, device=dev)
@@ -431,14 +453,18 @@ class Domain:
                                     _stream())
             self.comm.exchange_counts_dev(sr[: self.size], out=sr[self.size:])
             counts = sr.view(-1).cpu().tolist()
+            send_counts, recv_counts = counts[: self.size], counts[self.size:]
+            self.stats["migration_counts"] = "exchanged"
         else:
+            bkeys = self._upload(np.array(keys_b[1:-1], dtype=np.uint64).view(np.int64), dev)
             pos = torch.searchsorted(skeys, bkeys)
             edges = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), pos,
                                torch.full((1,), skeys.numel(), dtype=torch.int64, device=dev)])
             send_dev = (edges[1:] - edges[:-1]).view(-1, 1)
             recv_dev = self.comm.exchange_counts_dev(send_dev)
             counts = torch.cat([send_dev, recv_dev]).view(-1).cpu().tolist()
-        send_counts, recv_counts = counts[: self.size], counts[self.size:]
+            send_counts, recv_counts = counts[: self.size], counts[self.size:]
+            self.stats["migration_counts"] = "exchanged"
         PROF.mark("distribute: assignment + send/recv counts")
 
         # only the particles that change rank travel: one packed all-to-all of keys + every conserved field (rows of

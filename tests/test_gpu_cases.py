@@ -298,3 +298,34 @@ def test_gravity_early_m2p_matches(gpu, monkeypatch):
     for k in a:
         assert torch.allclose(a[k], b[k], rtol=1e-5, atol=1e-6 * float(a[k].abs().max())), k
     assert dta == pytest.approx(dtb, rel=1e-6) and ea == pytest.approx(eb, rel=1e-6)
+
+
+def test_gravity_early_m2p_ordering_under_delay(gpu, monkeypatch):
+    """advisor r5: the P2P phase (third stream) quantizes its source records with the particles' extent computed on
+    the side stream. A slow side stream (a busy kernel enqueued right after the interaction lists) must not let the
+    P2P read the extent before it exists: the accelerations still equal the single-stream evaluation"""
+    from sphexa_amd.models import propagators as Pr
+    from sphexa_amd.ops import gravity as G
+
+    orig = G.gravity_lists
+
+    def slow_lists(*args, **kw):
+        gl = orig(*args, **kw)
+        a = torch.randn(3072, 3072, device=gpu)
+        for _ in range(6):
+            a = a @ a
+            a = a / a.abs().max()
+        return gl
+
+    out = {}
+    for early in (False, True):
+        monkeypatch.setattr(Pr, "GRAVITY_EARLY_M2P", early)
+        monkeypatch.setattr(G, "gravity_lists", slow_lists if early else orig)
+        sim = Simulation("evrard", n=32, device=gpu)
+        sim.run(2)
+        torch.cuda.synchronize()
+        out[early] = (_sorted_state(sim, ["ax", "ay", "az", "x", "h"]), sim.conserved()["egrav"])
+    (a, ea), (b, eb) = out[False], out[True]
+    for k in a:
+        assert torch.allclose(a[k], b[k], rtol=1e-5, atol=1e-6 * float(a[k].abs().max())), k
+    assert ea == pytest.approx(eb, rel=1e-6)

@@ -104,3 +104,80 @@ def test_pack_bits_native_matches_torch(gpu, n):
     assert torch.equal(_unpack_bits(got, n).cpu(), flags)
     # bool flags take the same path
     assert torch.equal(_pack_bits(flags.bool().to(gpu)).cpu(), ref)
+
+
+def test_reductions_on_two_streams_match_serial(gpu):
+    """two streams reducing at once (gravity's particle extents on a side stream during the search's h reduction,
+    models/propagators.py): every stream has its own partials workspace (ops/reduce.py _work), so the results equal
+    the serial ones. Many repetitions with large inputs keep the two streams' kernels overlapping."""
+    n = 4_000_003
+    g = torch.Generator(device="cpu").manual_seed(31)
+    a = [torch.randn(n, generator=g, dtype=torch.float64).to(gpu) for _ in range(3)]
+    b = [torch.randn(n, generator=g).to(gpu) for _ in range(2)]
+    f = torch.randn(n, generator=g).to(gpu)
+    ref_a = R.min_max(a).cpu()
+    ref_b = R.min_max(b).cpu()
+    ref_f = float(R.field_max(f, 7, n))
+    s1, s2 = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(20):
+        with torch.cuda.stream(s1):
+            oa = R.min_max(a)
+            of = R.field_max(f, 7, n)
+        with torch.cuda.stream(s2):
+            ob = R.min_max(b)
+        outs.append((oa, ob, of))
+    torch.cuda.synchronize()
+    for oa, ob, of in outs:
+        assert torch.equal(oa.cpu(), ref_a)
+        assert torch.equal(ob.cpu(), ref_b)
+        assert float(of) == ref_f
+
+
+def test_search_beside_gravity_matches_serial(gpu):
+    """the neighbor search on the main stream while the gravity upsweep, interaction lists and M2P run on a side
+    stream (the overlapped Evrard step, models/propagators.py _gravity_prepare): both results equal their serial runs
+    (the two use disjoint workspaces: search scratch key '' vs 'overlap', per-stream reduction partials)"""
+    from sphexa_amd.app.simulation import Simulation
+    from sphexa_amd.models.gravity import MultipoleHolder
+    from sphexa_amd.ops import gravity as G
+    from sphexa_amd.ops.neighbors import find_neighbors
+
+    sim = Simulation("evrard", n=40, device=gpu)
+    sim.run(1)
+    d, dom = sim.d, sim.domain
+    first, last = dom.start_index(), dom.end_index()
+    h0 = d["h"].clone()
+
+    def search():
+        d["h"].copy_(h0)
+        nl = find_neighbors(d, dom.octree, dom.box, first, last)
+        return d["h"].clone(), d["nc"][first:last].clone(), nl
+
+    def gravity():
+        mh = MultipoleHolder()
+        mh.upsweep(d, dom)
+        gl = G.gravity_lists(dom.octree, mh.centers, mh.multipoles, first, last, d["x"], d["y"], d["z"],
+                             scratch_key="overlap")
+        acc = torch.zeros(3 * d.size, dtype=torch.float32, device=gpu)
+        G.gravity_eval(gl, d["x"], d["y"], d["z"], h0, d["m"], d.g, acc[:d.size], acc[d.size:2 * d.size],
+                       acc[2 * d.size:], phase=1)
+        return acc
+
+    torch.cuda.synchronize()
+    h_ref, nc_ref, _ = search()
+    acc_ref = gravity()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream(gpu)
+    for _ in range(3):
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(side):
+            side.wait_event(ev)
+            acc = gravity()
+        h1, nc1, _ = search()
+        torch.cuda.synchronize()
+        assert torch.equal(nc1, nc_ref)
+        assert torch.equal(h1, h_ref)
+        assert torch.equal(acc, acc_ref)

@@ -24,7 +24,7 @@ def test_syncs_one_rank(gpu, init, ceiling):
 
 
 @pytest.mark.parametrize("ranks", [2, 8])
-@pytest.mark.parametrize("init,ceiling", [("sedov", 5), ("evrard", 7)])
+@pytest.mark.parametrize("init,ceiling", [("sedov", 4), ("evrard", 6)])
 def test_syncs_multi_rank(gpu, ranks, init, ceiling):
     import sync_inventory as S
 
