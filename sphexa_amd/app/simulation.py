@@ -49,8 +49,8 @@ class Simulation:
         # (tuning: SPHX_BUCKET_FOCUS overrides the local octree's leaf capacity, reference bucketSizeFocus = 64)
         # (an explicit argument wins over the environment)
         if bucket_size_focus is None:
-            bucket_size_focus = int(os.environ.get("SPHX_BUCKET_FOCUS", default_bucket_size_focus(self.d.g != 0.0,
-                                                                                                    size)))
+            bucket_size_focus = int(os.environ.get("SPHX_BUCKET_FOCUS", default_bucket_size_focus(
+                self.d.g != 0.0, size, init.split(":")[0] if isinstance(init, str) else None)))
         bucket = max(bucket_size_focus, int(self.d.numParticlesGlobal) // (100 * size))
         self.domain = Domain(self.comm, box, bucket_size_focus=bucket_size_focus, bucket_size=bucket, theta=theta)
         self.propagator.sync(self.domain, self.d)

@@ -136,7 +136,8 @@ def main(argv=None) -> int:
 
     from ..parallel.domain import default_bucket_size_focus
 
-    bucket_focus = int(os.environ.get("SPHX_BUCKET_FOCUS", default_bucket_size_focus(have_grav, num_ranks)))
+    bucket_focus = int(os.environ.get("SPHX_BUCKET_FOCUS", default_bucket_size_focus(
+        have_grav, num_ranks, init_cond.split(":")[0] if init_cond else None)))
     bucket = max(bucket_focus, d.numParticlesGlobal // (100 * num_ranks))
     domain = Domain(comm, box, bucket_size_focus=bucket_focus, bucket_size=bucket, theta=theta)
     propagator.sync(domain, d)

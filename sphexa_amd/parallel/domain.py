@@ -61,14 +61,17 @@ HALO_FIELDS = ("x", "y", "z", "h", "m")
 BUCKET_SIZE_FOCUS = 64
 BUCKET_SIZE_FOCUS_HYDRO = 512
 BUCKET_SIZE_FOCUS_GRAVITY_1RANK = 128
+BUCKET_SIZE_FOCUS_TURB_MULTIRANK = 128
 
 
-def default_bucket_size_focus(gravity: bool, nranks: int = 1) -> int:
-    """leaf capacity of the local octree. The larger capacities were measured on one rank only; on several ranks the
-    leaves also set the halo search boxes (one per own-tree leaf) and opened LET leaves travel whole, so multi-rank
-    runs keep the reference's 64 (bucketSizeFocus)"""
+def default_bucket_size_focus(gravity: bool, nranks: int = 1, case: str | None = None) -> int:
+    """leaf capacity of the local octree. On several ranks the leaves also set the halo search boxes (one per own-tree
+    leaf) and opened LET leaves travel whole. Measured on 2 and 4 ranks sharing one GPU
+    (profiles/r6/multirank/leaf_capacity_glass.md, r5 multirank/leaf_capacity_multirank.md): the turbulence glass runs
+    fastest at 128 (64 costs 4-5 %), Noh at 64 (512 costs 10 % at 4 ranks), the Sedov lattice is flat and Evrard
+    (gravity) is 7 % slower at 128, so multi-rank runs keep the reference's 64 (bucketSizeFocus) except turbulence"""
     if nranks > 1:
-        return BUCKET_SIZE_FOCUS
+        return BUCKET_SIZE_FOCUS_TURB_MULTIRANK if (case == "turbulence" and not gravity) else BUCKET_SIZE_FOCUS
     return BUCKET_SIZE_FOCUS_GRAVITY_1RANK if gravity else BUCKET_SIZE_FOCUS_HYDRO
 REORDER_BATCH = 3  # conserved fields reordered per gather launch in sync (bounds the transient memory)
 # one rank, GPU: SFC keys from the prefetched device extents, host box taken at the end of the sync
