@@ -475,7 +475,7 @@ __global__ __launch_bounds__(B) void xmassQKernel(NbrArgs a, SphConsts sc, QFram
         const float ux = float(int32_t(pi.x - pj.x)) * sx;
         const float uy = float(int32_t(pi.y - pj.y)) * sy;
         const float uz = float(int32_t(pi.z - pj.z)) * sz;
-        rho0 += kf.wq(sqrtF(ux * ux + uy * uy + uz * uz)) * pj.m;
+        rho0 += kf.wqIn(sqrtF(ux * ux + uy * uy + uz * uz)) * pj.m;
     });
     rho0 = pi.m + rho0 / kf.wqScale();
     if (!valid) return;
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(64 * W) void xmassQStagedKernel(NbrArgs a, SphConst
         const float ux = float(int32_t(pi.x - pj.x)) * sx;
         const float uy = float(int32_t(pi.y - pj.y)) * sy;
         const float uz = float(int32_t(pi.z - pj.z)) * sz;
-        rho0 += kf.wq(sqrtF(ux * ux + uy * uy + uz * uz)) * pj.m;
+        rho0 += kf.wqIn(sqrtF(ux * ux + uy * uy + uz * uz)) * pj.m;
     });
     reduceAcross(ld, rho0);
     rho0 = pi.m + rho0 / kf.wqScale();

@@ -173,7 +173,18 @@ struct KernelFn
         const HT r = powN(sq, n);
         return u < HT(0.5) ? r : HT(0);
     }
-    //! @brief S w(4u) and S v dW/dv at v = 4u (see wq)
+    /*! @brief wq for a neighbor of the list of the target whose h defines u: the search's exact fp64 test put it
+     *         inside 2h, so u < 1/2 up to the fp32 rounding of u. No support test: at u = 1/2 (1 + eps) the sine is
+     *         ~1e-7 and its n-th power below 1e-40, which is the kernel value there. (u = 0 keeps sinc = 1.) */
+    SPHX_HD HT wqIn(HT u) const
+    {
+        if (choice != 0) return w(HT(4) * u);
+        constexpr HT twoPi = HT(6.283185307179586);
+        HT sq = __builtin_amdgcn_sinf(u) * rcpF(u);
+        sq    = u > HT(0) ? sq : twoPi;
+        return powN(sq, n);
+    }
+    //! @brief S w(4u) and S v dW/dv at v = 4u for a list neighbor (see wq, wqIn: no support test)
     SPHX_HD void wdq(HT u, HT& wS, HT& vdwS) const
     {
         if (choice != 0)
@@ -187,9 +198,8 @@ struct KernelFn
         sq    = u > HT(0) ? sq : twoPi;
         const HT cs = __builtin_amdgcn_cosf(u);
         const HT p  = powN(sq, n - HT(1));
-        const bool in = u < HT(0.5);
-        wS   = in ? p * sq : HT(0);
-        vdwS = in ? n * p * (twoPi * cs - sq) : HT(0);
+        wS   = p * sq;
+        vdwS = n * p * (twoPi * cs - sq);
     }
 #else
     SPHX_HD HT w(HT v) const { return tableLookup(wh, v); }
@@ -197,6 +207,7 @@ struct KernelFn
     //! host forms of the quarter-argument interface (no scaling: S = 1)
     SPHX_HD HT wqScale() const { return HT(1); }
     SPHX_HD HT wq(HT u) const { return w(HT(4) * u); }
+    SPHX_HD HT wqIn(HT u) const { return w(HT(4) * u); }
     SPHX_HD void wdq(HT u, HT& wS, HT& vdwS) const
     {
         wS   = w(HT(4) * u);
@@ -1115,7 +1126,7 @@ SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
-        rho0 += kf.wq(dist * hq) * pj.m;
+        rho0 += kf.wqIn(dist * hq) * pj.m;
     });
     rho0 = pi.m + rho0 / kf.wqScale(); // (kernel scale, KernelFn::wq; the target's own term W(0) m_i)
     return pi.m / (rho0 * HT(K) * h3Inv);
@@ -1196,7 +1207,7 @@ SPHX_HD void iadJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
         HT rx, ry, rz;
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
-        HT w    = kf.wq(dist * hq);
+        HT w    = kf.wqIn(dist * hq);
         HT vw   = pj.vol * w;
         tau[0] += rx * rx * vw;
         tau[1] += rx * ry * vw;
@@ -1225,7 +1236,7 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
         pairDelta(pi.x, pi.y, pi.z, pj.x, pj.y, pj.z, hi, box, rx, ry, rz);
         HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
         HT vxji = pj.vx - pi.vx, vyji = pj.vy - pi.vy, vzji = pj.vz - pi.vz;
-        HT W    = kf.wq(dist * hq);
+        HT W    = kf.wqIn(dist * hq);
         HT tA0  = -(c11 * rx + c12 * ry + c13 * rz) * W;
         HT tA1  = -(c12 * rx + c22 * ry + c23 * rz) * W;
         HT tA2  = -(c13 * rx + c23 * ry + c33 * rz) * W;
@@ -1278,7 +1289,7 @@ SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nb
         HT rx, ry, rz;
         pairSep(bx, pi, pj, hi, rx, ry, rz);
         HT dist = sqrtF(rx * rx + ry * ry + rz * rz);
-        HT w    = kf.wq(dist * hq);
+        HT w    = kf.wqIn(dist * hq);
         HT vw   = pj.vol * w;
         tau[0] += rx * rx * vw;
         tau[1] += rx * ry * vw;
@@ -1376,7 +1387,7 @@ SPHX_HD HT avSwitchesJLoop(unsigned i, double K, const G& box, const Idx* nbr, i
         HT vst  = ci + pj.c - HT(3) * rv * invDist;
         HT vsij = rv < HT(0) ? vst : HT(0);
         vsig   = smax(vsig, vsij);
-        HT W   = KhS * kf.wq(dist * hq);
+        HT W   = KhS * kf.wqIn(dist * hq);
         HT tA0 = -(c11 * rx + c12 * ry + c13 * rz) * W;
         HT tA1 = -(c12 * rx + c22 * ry + c23 * rz) * W;
         HT tA2 = -(c13 * rx + c23 * ry + c33 * rz) * W;
@@ -1460,7 +1471,7 @@ SPHX_HD HT avSwitchesVJLoop(unsigned i, double K, const G& box, const Idx* nbr, 
         HT vst  = ci + pj.c - HT(3) * rv * invDist;
         HT vsij = rv < HT(0) ? vst : HT(0);
         vsig  = smax(vsig, vsij);
-        HT wd = kf.wq(dist * hq) * pj.vd;
+        HT wd = kf.wqIn(dist * hq) * pj.vd;
         T[0] += wd * rx;
         T[1] += wd * ry;
         T[2] += wd * rz;
@@ -1559,7 +1570,7 @@ SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, 
         // quarter arguments and S-scaled kernel values (KernelFn::wq; the sums are rescaled once after the loop)
         HT dq = HT(0.25) * dist;
         HT u1 = dq * hInv, u2 = dq * hjInv;
-        HT Wi = hInv3 * kf.wq(u1);
+        HT Wi = hInv3 * kf.wqIn(u1); // (u1 from the target's h: inside the support, KernelFn::wqIn)
         HT Wj = hjInv * hjInv * hjInv * kf.wq(u2);
 
         // u = C r for the target and the neighbor
@@ -1651,7 +1662,7 @@ SPHX_HD void momentumEnergyStdJLoop(unsigned i, double K, const Box& box, const 
         HT dq = HT(0.25) * dist;
         HT u1 = dq * hInv, u2 = dq * hjInv;
         HT rv = rx * vxij + ry * vyij + rz * vzij;
-        HT Wi = hInv3 * kf.wq(u1); // (S-scaled: KernelFn::wq)
+        HT Wi = hInv3 * kf.wqIn(u1); // (S-scaled: KernelFn::wq; inside the support: wqIn)
         HT Wj = hjInv * hjInv * hjInv * kf.wq(u2);
         HT tAi0 = pi.c11 * rx + pi.c12 * ry + pi.c13 * rz;
         HT tAi1 = pi.c12 * rx + pi.c22 * ry + pi.c23 * rz;
