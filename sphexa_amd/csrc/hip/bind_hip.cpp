@@ -361,6 +361,8 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("set_staged", [](unsigned mask) { setStaged(mask); },
           "pair loops that run LDS-staged: bit 0 XMass, 1 Gradh, 2 IAD, 3 AV, 4 momentum (hydro.hip, staged.h)");
     m.def("staged_mask", []() { return stagedMask(); });
+    m.def("set_list_masks", [](bool on) { setListMasks(on); },
+          "store the per-slot staged-source masks in the list tables even without a staged loop (tests)");
     m.def("set_pair_block", [](int block) { setPairBlock(block); },
           "threads per block of the fixed-point pair loops: 512 (8 target groups sharing a CU's L1) or 256");
     m.def("eos_ve", [](int64_t first, int64_t last, const ConstArr& c, Ptr temp, Ptr mm, Ptr kx, Ptr xm, Ptr gradh,

@@ -181,6 +181,9 @@ void setPairBlock(int block);
 //! pair loops that run LDS-staged (hydro.hip g_staged: bit 0 XMass, 1 Gradh, 2 IAD, 3 AV, 4 momentum)
 void setStaged(unsigned mask);
 unsigned stagedMask();
+//! the search stores its per-slot staged-source masks (packed_list.hpp) also when no staged loop is enabled (tests)
+void setListMasks(bool on);
+bool listMasksForced();
 //! fixed-point {x, y, z, m} records (QFrame of the box) of particles [0, n): the search and the XMass loop read them
 void packPosQ(int64_t n, const double* x, const double* y, const double* z, const float* m, const QFrame& q,
               SrcPosQ* out, hipStream_t s);

@@ -141,6 +141,11 @@ static unsigned g_staged = []
 void setStaged(unsigned mask) { g_staged = mask; }
 unsigned stagedMask() { return g_staged; }
 
+// tests: the search stores the slot masks even when no staged loop runs (packed-list format checks)
+static bool g_listMasks = false;
+void setListMasks(bool on) { g_listMasks = on; }
+bool listMasksForced() { return g_listMasks; }
+
 //! grid of a staged loop: one workgroup per target group
 inline unsigned gridStaged(const NbrArgs& a) { return unsigned((a.last - a.first + 63) / 64); }
 

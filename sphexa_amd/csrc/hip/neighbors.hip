@@ -120,6 +120,7 @@ struct PackedOut
     unsigned long long ovBase;   // first overflow row (groups * home)
     unsigned long long poolRows; // rows in the buffer
     unsigned long long* ctr;     // stripe counters
+    int masks;                   // store the staged-source masks of the chunk slots (the LDS-staged pair loops)
 };
 
 //! @brief rows of one group, allocated on demand by the whole wave: ordinal r's row sits in lane r of `reg`
@@ -506,7 +507,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     // slots after list blocks have been stored at ordinals T + b)
                     const bool single = !kSplit || (pos == 0 && len == 64);
                     Tc = single ? chunkTabRows(min(1 + nch, kChunkCap)) : kChunkTabRowsMax;
-                    T  = Tc + (single ? maskTabRows(min(1 + nch, kChunkCap)) : kMaskTabRowsMax);
+                    T  = Tc + (!po.masks ? 0u : single ? maskTabRows(min(1 + nch, kChunkCap)) : kMaskTabRowsMax);
                     ra.ensure(min(po.home, po.rowsMax), g, po);
                     ra.ensure(T, g, po);
                 }
@@ -752,7 +753,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     }
                     // the slot's staged-source mask (packed_list.hpp): the union of the group's sources for the
                     // LDS-staged pair loops (two lanes: a vector store of the {lo, hi} pair)
-                    if (lane < 2)
+                    if (po.masks && lane < 2)
                     {
                         const unsigned rw = ra.rowU(Tc + (s >> 7));
                         if (rw < po.poolRows)
@@ -1170,7 +1171,9 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
                        unsigned(ovStride),
                        ovBase,
                        ovBase + (unsigned long long)kRowStripes * ovStride,
-                       stats + 8};
+                       stats + 8,
+                       // the slot masks cost a table row per group (16 B/particle): only while a staged loop reads them
+                       stagedMask() != 0u || listMasksForced() ? 1 : 0};
     int64_t spillMemOff, total;
     scratchLayout(n, spillMemOff, total);
     int32_t* splitList = static_cast<int32_t*>(scratch);

@@ -57,6 +57,7 @@ struct StagedLane
     unsigned b0, b1; // list blocks walked by this wave
     unsigned self;   // target index
     unsigned gfirst; // first particle of the group
+    unsigned ntot;   // source records
 
     //! row of table ordinal o (uniform: scalar load)
     __device__ __forceinline__ int32_t rowOf(unsigned o) const
@@ -94,6 +95,7 @@ __device__ __forceinline__ bool stagedTargetOf(const NbrArgs& a, int64_t& i, Sta
     sl.b0     = wave * sl.nblk / W;
     sl.b1     = (wave + 1) * sl.nblk / W;
     sl.gfirst = unsigned(a.first + int64_t(g) * 64);
+    sl.ntot   = a.ntot;
     i         = a.first + int64_t(g) * 64 + lane;
     if (i >= a.last)
     {
@@ -176,13 +178,25 @@ __device__ unsigned stageWindow(const StagedLane& sl, const StagedLoader<R, W, U
     {
         const unsigned s = s0 + lane;
         const bool in    = lane < kStRows - 1 && s < sl.nch;
+        // (lists searched without the slot masks, T == Tc: every source of the chunk below ntot is staged)
+        const bool masks = sl.T >= sl.Tc + maskTabRows(sl.nch);
         uint32_t cb = 0, lo = 0, hi = 0;
         if (in)
         {
-            cb                 = uint32_t(sl.rowsInt[size_t(sl.rowOf(s >> 8)) * 256 + (s & 255)]);
-            const int32_t* mr  = sl.rowsInt + size_t(sl.rowOf(sl.Tc + (s >> 7))) * 256 + 2 * (s & 127);
-            lo                 = uint32_t(mr[0]);
-            hi                 = uint32_t(mr[1]);
+            cb = uint32_t(sl.rowsInt[size_t(sl.rowOf(s >> 8)) * 256 + (s & 255)]);
+            if (masks)
+            {
+                const int32_t* mr = sl.rowsInt + size_t(sl.rowOf(sl.Tc + (s >> 7))) * 256 + 2 * (s & 127);
+                lo                = uint32_t(mr[0]);
+                hi                = uint32_t(mr[1]);
+            }
+            else
+            {
+                const unsigned avail = cb < sl.ntot ? min(sl.ntot - cb, 64u) : 0u;
+                const uint64_t m     = avail >= 64u ? ~0ull : ((1ull << avail) - 1ull);
+                lo                   = uint32_t(m);
+                hi                   = uint32_t(m >> 32);
+            }
         }
         const unsigned cnt = unsigned(__popc(lo) + __popc(hi));
         unsigned incl      = cnt;

@@ -23,7 +23,7 @@
  *                [2 + r] = row of ordinal r. Ordinals 0 .. Tc-1 hold the chunk bases (256 ints per row), ordinals
  *                Tc .. T-1 the chunk masks (bit k of slot s: source c0 + k was staged for the group, i.e. lies in the
  *                group's search box; 128 {lo, hi} int pairs per row; the search reserves Tc and T from an upper bound
- *                of nch), ordinals T .. T+nblk-1 the list blocks (row of 64 lanes x 8 codes). Entries past them name
+ *                of nch; written only while an LDS-staged pair loop is enabled, else T = Tc), ordinals T .. T+nblk-1 the list blocks (row of 64 lanes x 8 codes). Entries past them name
  *                row 0 (valid memory: the pair loops prefetch a block ahead). Every code (s, k) of a list has bit k of
  *                mask s set (s >= 1), so the union of a group's sources is known from the table alone: the LDS-staged
  *                pair loops (hydro.hip StagedGroup) load it once per group.

@@ -222,11 +222,13 @@ def _scratch(nbytes: int, device, key: str = "") -> torch.Tensor:
 
 def _pool_plan(prev: NeighborList | None, groups: int, ng0: int, stripes: int):
     """(home rows per group, rows per overflow stripe) of the list-row pool: the previous search's choice for this
-    group count, else ng0/8 + 2 home rows (list blocks + one chunk-table row + one mask row) and 0.35 ng0/8 overflow
-    rows per group (on lattices the neighbor count jumps to ~1.3 ng0 at shell steps)"""
+    group count, else ng0/8 + 1 home rows (list blocks + one chunk-table row; + one mask row while an LDS-staged pair
+    loop is enabled, packed_list.hpp) and 0.35 ng0/8 overflow rows per group (on lattices the neighbor count jumps to
+    ~1.3 ng0 at shell steps)"""
     if prev is not None and prev.grouped and prev.plan is not None and prev.plan[0] == groups:
         return prev.plan[1], prev.plan[2]
-    return max(1, round(ng0 / 8) + 2), max(8, -(-int(0.35 * ng0 / 8 * groups + 0.5) // stripes))
+    masks = 1 if _lib.hip().staged_mask() else 0
+    return max(1, round(ng0 / 8) + 1 + masks), max(8, -(-int(0.35 * ng0 / 8 * groups + 0.5) // stripes))
 
 
 _STATS_IDX: dict = {}

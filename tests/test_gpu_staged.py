@@ -65,3 +65,41 @@ def test_staged_windows_match_gathered(gpu):
     b = _run(gpu, "sedov", 20, 31, steps=1, ng=(300, 400))
     assert float(a["nc"].mean()) > 250
     _compare(a, b, 2e-5)
+
+
+def test_search_masks_cover_every_code(gpu):
+    """the search's per-slot staged-source masks (packed_list.hpp; stored while a staged loop is enabled or
+    set_list_masks) have the bit of every list entry: the union the staged loops copy into LDS holds every neighbor"""
+    import numpy as np
+
+    from sphexa_amd.ops.neighbors import GROUP, packed_table_ints, packed_table_region
+
+    hp = _lib.hip()
+    hp.set_list_masks(True)
+    try:
+        sim = Simulation("evrard", n=24, device=gpu)
+        sim.run(1)
+    finally:
+        hp.set_list_masks(False)
+    nl = sim.propagator.nl
+    n = nl.last - nl.first
+    G = (n + GROUP - 1) // GROUP
+    buf = nl.nidx.cpu().numpy()
+    Ti = packed_table_ints(nl.ngmax)
+    tab = buf[:G * Ti].reshape(G, Ti)
+    rows = buf[packed_table_region(G, nl.ngmax):].reshape(-1, 256)
+    rows16 = rows.view(np.uint16).reshape(-1, 64, 8)
+    checked = 0
+    for g in range(0, G, max(1, G // 64)):
+        nblk, w = int(tab[g, 0]), int(tab[g, 1])
+        nch, tc, T = w & 0x3FF, (w >> 10) & 0x3F, w >> 16
+        assert T >= tc + (nch + 127) // 128
+        r = tab[g, 2:]
+        masks = [int(np.uint32(rows[r[tc + s // 128], 2 * (s % 128)])) |
+                 int(np.uint32(rows[r[tc + s // 128], 2 * (s % 128) + 1])) << 32 for s in range(nch)]
+        codes = rows16[r[T:T + nblk]].reshape(-1)
+        slot, k = codes & 0x3FF, codes >> 10
+        real = slot > 0
+        assert all((masks[s] >> kk) & 1 for s, kk in zip(slot[real].tolist(), k[real].tolist()))
+        checked += int(real.sum())
+    assert checked > 1000
