@@ -1,6 +1,7 @@
 // pybind11 bindings of the gfx950 module. Buffers are raw device addresses of torch HIP tensors; every launcher
 // takes the caller's stream (torch.cuda.current_stream()) so kernels are ordered with torch ops and RCCL.
 #include <array>
+#include <stdexcept>
 #include <vector>
 
 #include <pybind11/pybind11.h>
@@ -151,6 +152,24 @@ PYBIND11_MODULE(_sphx_hip, m)
           {
               remoteTreeScatter(M, P<int32_t>(nodes), P<double>(rc), P<float>(rq), P<double>(centers), P<float>(mp),
                                 forceAccept, value, St(s));
+          });
+    m.def("remote_let_work_bytes", [](int64_t M) { return remoteLetWorkBytes(M); });
+    m.def("remote_let_plan", [](int64_t M, Ptr codes, Ptr work, Ptr plan, Ptr s)
+          { remoteLetPlan(M, P<KeyT>(codes), P<void>(work), P<uint64_t>(plan), St(s)); });
+    m.def("remote_let_emit", [](int64_t M, Ptr codes, Ptr work, Ptr tree, Ptr s)
+          { remoteLetEmit(M, P<KeyT>(codes), P<void>(work), P<KeyT>(tree), St(s)); });
+    m.def("remote_let_scatter",
+          [](int64_t M, Ptr work, Ptr leafToNode, Ptr rc, Ptr rq, Ptr centers, Ptr mp, int mode, double value, Ptr s)
+          {
+              remoteLetScatter(M, P<void>(work), P<int32_t>(leafToNode), P<double>(rc), P<float>(rq),
+                               P<double>(centers), P<float>(mp), mode, value, St(s));
+          });
+    m.def("remote_let_upsweep",
+          [](const std::vector<int64_t>& levelRange, Ptr n2l, Ptr child, Ptr centers, Ptr mp, Ptr s)
+          {
+              if (levelRange.size() != size_t(kMaxLevel + 2)) throw std::invalid_argument("level ranges");
+              remoteLetUpsweep(levelRange.data(), P<int32_t>(n2l), P<int32_t>(child), P<double>(centers),
+                               P<void>(mp), St(s));
           });
     m.def("mark_let_multi",
           [](int nDest, int nbPer, Ptr boxes, Ptr enabled, Ptr child, Ptr n2l, Ptr tc, Ptr th, Ptr gc, int64_t N,

@@ -315,6 +315,15 @@ void markOutsideRange(int64_t N, const KeyT* prefixes, KeyT lo, KeyT hi, uint8_t
 void letSelect(int64_t N, int64_t L, int64_t np, const uint8_t* failed, const uint8_t* outside,
                const int32_t* leafToNode, const int32_t* ns, const int32_t* ne, int64_t offset, const void* mp,
                const int32_t* parents, uint8_t* pflags, uint8_t* send, hipStream_t s);
+// let_tree.hip: the remote LET tree on the device (plan in the sync, build at the gravity phase)
+size_t remoteLetWorkBytes(int64_t M);
+//! plan words (uint64, kLetPlanWords = 24): [0] leaf-array entries L + 1, [1] overlapping nodes, [2 + l] leaves at level l
+void remoteLetPlan(int64_t M, const KeyT* codes, void* work, uint64_t* plan, hipStream_t s);
+void remoteLetEmit(int64_t M, const KeyT* codes, const void* work, KeyT* tree, hipStream_t s);
+void remoteLetScatter(int64_t M, const void* work, const int32_t* leafToNode, const double* rc, const float* rq,
+                      double* centers, float* mp, int mode, double value, hipStream_t s);
+void remoteLetUpsweep(const int64_t* levelRange, const int32_t* n2l, const int32_t* child, double* centers, void* mp,
+                      hipStream_t s);
 void m2pFlat(int64_t first, int64_t last, const double* x, const double* y, const double* z, const float* m,
              int64_t M, const double* mc, const void* mp, float G, float* ax, float* ay, float* az, double* ugrav,
              double* out, hipStream_t s);

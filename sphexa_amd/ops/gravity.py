@@ -379,6 +379,116 @@ def remote_let_tree(codes: torch.Tensor, rcenters: torch.Tensor, rquads: torch.T
     return ot, centers, mp
 
 
+LET_PLAN_WORDS = 2 + MAX_LEVEL + 1  # csrc/hip/let_tree.hip kLetPlanWords
+
+
+class RemoteLetPlan:
+    """device plan of a remote LET tree (csrc/hip/let_tree.hip remoteLetPlan): the received codes sorted by key, the
+    leaf-array positions of every gap, and the plan words [L + 1, overlaps, leaves per level], whose copy to pinned
+    host memory is in flight until ``remote_let_tree_device`` collects it"""
+
+    def __init__(self, codes, work, plan, host, event):
+        self.codes, self.work, self.plan, self.host, self.event = codes, work, plan, host, event
+
+
+def remote_let_plan(codes: torch.Tensor) -> RemoteLetPlan:
+    """GPU, in the sync right after the multipole exchange: sort the M received placeholder codes and size the remote
+    leaf array on the device; only the plan words go to the host (asynchronously)"""
+    hp = _lib.hip()
+    M = codes.numel()
+    codes = codes.contiguous()
+    work = torch.empty(hp.remote_let_work_bytes(M), dtype=torch.uint8, device=codes.device)
+    plan = torch.empty(LET_PLAN_WORDS, dtype=torch.int64, device=codes.device)
+    hp.remote_let_plan(M, codes.data_ptr(), work.data_ptr(), plan.data_ptr(), _stream())
+    host = torch.empty(LET_PLAN_WORDS, dtype=torch.int64, pin_memory=True)
+    host.copy_(plan, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return RemoteLetPlan(codes, work, plan, host, ev)
+
+
+def let_level_ranges(leaves_per_level) -> tuple:
+    """(node count, level ranges) of the cornerstone octree with these leaves per level: every internal node has eight
+    children, so the internal nodes of level l - 1 are the nodes of level l over eight (deepest level first)"""
+    nodes = [0] * (MAX_LEVEL + 1)
+    internal = 0
+    for lv in range(MAX_LEVEL, -1, -1):
+        nodes[lv] = int(leaves_per_level[lv]) + internal
+        if lv > 0:
+            if nodes[lv] % 8:
+                raise RuntimeError(f"remote LET leaf histogram is not a cornerstone octree (level {lv}: {nodes[lv]})")
+            internal = nodes[lv] // 8
+    if nodes[0] != 1:
+        raise RuntimeError(f"remote LET leaf histogram is not a cornerstone octree ({nodes[0]} roots)")
+    lr = [0]
+    for lv in range(MAX_LEVEL + 1):
+        lr.append(lr[-1] + nodes[lv])
+    return lr[-1], lr
+
+
+def remote_let_tree_device(plan: RemoteLetPlan, rcenters: torch.Tensor, rquads: torch.Tensor, box: Box,
+                           theta: float, sfc_kind: int = 0):
+    """GPU form of ``remote_let_tree`` from a ``remote_let_plan``: the leaf keys are emitted, linked and upswept on the
+    device (no code or tree array crosses to the host; sizes and level ranges come from the plan words). The tree's
+    particle ranges are empty and its tight boxes are not computed (zero): the gravity kernels read the multipole
+    centers, MAC radii and quadrupoles only."""
+    plan.event.synchronize()  # (recorded in the sync: complete long before the gravity phase)
+    words = [int(v) for v in plan.host.tolist()]
+    if words[1]:
+        raise RuntimeError(f"remote LET nodes overlap ({words[1]} received nodes)")
+    hp, s, dev = _lib.hip(), _stream(), rcenters.device
+    M = plan.codes.numel()
+    L = words[0] - 1
+    N, lr = let_level_ranges(words[2:])
+    if N != L + (L - 1) // 7:
+        raise RuntimeError(f"remote LET plan inconsistent: {L} leaves, {N} nodes")
+    tree = torch.empty(L + 1, dtype=torch.int64, device=dev)
+    hp.remote_let_emit(M, plan.codes.data_ptr(), plan.work.data_ptr(), tree.data_ptr(), s)
+    # link (octree.py _build_octree_hip, with the level ranges known on the host and no particles)
+    Ni = (L - 1) // 7
+    icount = torch.empty(L + 1, dtype=torch.int64, device=dev)
+    hp.internal_counts(tree.data_ptr(), L, icount.data_ptr(), s)
+    tmp = torch.empty(max(hp.scan_temp_bytes(L + 1), hp.sort_pairs_temp_bytes(N)), dtype=torch.uint8, device=dev)
+    hp.exclusive_scan_i64(icount.data_ptr(), icount.data_ptr(), L + 1, tmp.data_ptr(), tmp.numel(), s)
+    codes = torch.empty(N, dtype=torch.int64, device=dev)
+    vals = torch.empty(N, dtype=torch.int32, device=dev)
+    hp.make_codes(tree.data_ptr(), L, icount.data_ptr(), Ni, codes.data_ptr(), vals.data_ptr(), s)
+    codes_s = torch.empty_like(codes)
+    vals_s = torch.empty_like(vals)
+    hp.sort_pairs_i64_i32(N, codes.data_ptr(), codes_s.data_ptr(), vals.data_ptr(), vals_s.data_ptr(), tmp.data_ptr(),
+                          tmp.numel(), 0, 64, s)
+    child = torch.empty(N, dtype=torch.int32, device=dev)
+    parents = torch.empty(((N - 1) // 8 + 1,), dtype=torch.int32, device=dev)
+    hp.fill32(parents.data_ptr(), 0xFFFFFFFF, parents.numel(), s)
+    leaf_to_node = torch.empty(L, dtype=torch.int32, device=dev)
+    level_range_dev = torch.empty(MAX_LEVEL + 2, dtype=torch.int64, device=dev)
+    hp.link_nodes(codes_s.data_ptr(), vals_s.data_ptr(), N, child.data_ptr(), parents.data_ptr(),
+                  leaf_to_node.data_ptr(), level_range_dev.data_ptr(), s)
+    ns = torch.empty(N, dtype=torch.int32, device=dev)
+    ne = torch.empty(N, dtype=torch.int32, device=dev)
+    hp.node_ranges(codes_s.data_ptr(), N, 0, 0, 0, ns.data_ptr(), ne.data_ptr(), s)
+    center = torch.empty(3 * N, dtype=torch.float64, device=dev)
+    half = torch.empty(3 * N, dtype=torch.float64, device=dev)
+    hp.memset(center.data_ptr(), 0, 8 * 3 * N, s)
+    hp.memset(half.data_ptr(), 0, 8 * 3 * N, s)
+    counts = zero_(torch.empty(L, dtype=torch.int32, device=dev))
+    ot = Octree(tree=tree, counts=counts, num_nodes=N, num_leaves=L, prefixes=codes_s, child_offsets=child,
+                parents=parents, node_to_leaf=vals_s, leaf_to_node=leaf_to_node, level_range=lr, node_start=ns,
+                node_end=ne, center=center, half=half, offset=0)
+    # multipoles: received rows into their leaves, one launch for every level, MAC radii, received leaves accepted
+    centers = zero_(torch.empty(4 * N, dtype=torch.float64, device=dev))
+    mp = zero_(torch.empty(8 * N, dtype=torch.float32, device=dev))
+    rc, rq = rcenters.contiguous(), rquads.contiguous()
+    hp.remote_let_scatter(M, plan.work.data_ptr(), leaf_to_node.data_ptr(), rc.data_ptr(), rq.data_ptr(),
+                          centers.data_ptr(), mp.data_ptr(), 0, 0.0, s)
+    hp.remote_let_upsweep(lr, vals_s.data_ptr(), child.data_ptr(), centers.data_ptr(), mp.data_ptr(), s)
+    hp.gravity_set_mac(N, codes_s.data_ptr(), box.to_array(), sfc_kind, 1.0 / theta, centers.data_ptr(), s)
+    hp.remote_let_scatter(M, plan.work.data_ptr(), leaf_to_node.data_ptr(), 0, 0, centers.data_ptr(), mp.data_ptr(),
+                          1, float(FORCE_ACCEPT_MAC2), s)
+    ot.level_range_dev = level_range_dev  # (the linker's own ranges: tests compare them with ``lr``)
+    return ot, centers, mp
+
+
 def m2p_flat(first: int, last: int, x, y, z, m, mcenters: torch.Tensor, mquads: torch.Tensor, G: float, ax, ay, az,
              ugrav=None) -> float:
     """apply M remote multipoles (centers (M,3) f64, quadrupoles (M,8) f32) to every target in [first, last)"""

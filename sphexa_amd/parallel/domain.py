@@ -74,6 +74,9 @@ def default_bucket_size_focus(gravity: bool, nranks: int = 1, case: str | None =
         return BUCKET_SIZE_FOCUS_TURB_MULTIRANK if (case == "turbulence" and not gravity) else BUCKET_SIZE_FOCUS
     return BUCKET_SIZE_FOCUS_GRAVITY_1RANK if gravity else BUCKET_SIZE_FOCUS_HYDRO
 REORDER_BATCH = 3  # conserved fields reordered per gather launch in sync (bounds the transient memory)
+# GPU: the remote LET tree planned in the sync and built on the device (csrc/hip/let_tree.hip); 0: built on the host
+# from a copy of the received codes (cpu/let_tree_cpu.cpp, the CPU path's construction)
+LET_TREE_DEVICE = os.environ.get("SPHX_LET_DEVICE", "1") == "1"
 # one rank, GPU: SFC keys from the prefetched device extents, host box taken at the end of the sync
 DEVICE_BOX = os.environ.get("SPHX_DEVICE_BOX", "1") == "1"
 # ranks up to which the global-tree step gathers every rank's leaf counts (size x leaves int64, ~100 leaves per rank):
@@ -797,12 +800,17 @@ class Domain:
         self.stats["remote_multipoles"] = recv.shape[0]
         self._remote_tree = None
         self._remote_pending = None
+        self._remote_plan = None
         if recv.shape[0] > 0:
-            if self.remote_codes.is_cuda:
-                # the tree over the received nodes is built on the host from their codes; it is first needed by the
-                # gravity traversal after the SPH loops, so the codes' copy is only started here and collected there
-                # (remote_tree): the host then waits for a copy the GPU finished long before, instead of draining
-                # the stream in the sync
+            if self.remote_codes.is_cuda and LET_TREE_DEVICE:
+                # the tree over the received nodes is planned on the device here (codes sorted, leaf array sized:
+                # csrc/hip/let_tree.hip) and built there at the gravity phase (remote_tree) from the plan words, whose
+                # small copy is in flight meanwhile: no code or tree array crosses to the host
+                self._remote_plan = (grav_ops.remote_let_plan(self.remote_codes), self.box.copy())
+            elif self.remote_codes.is_cuda:
+                # (host build, SPHX_LET_DEVICE=0) the tree over the received nodes is built on the host from their
+                # codes; it is first needed by the gravity traversal after the SPH loops, so the codes' copy is only
+                # started here and collected there (remote_tree)
                 host = torch.empty(self.remote_codes.numel(), dtype=torch.int64, pin_memory=True)
                 host.copy_(self.remote_codes, non_blocking=True)
                 ev = torch.cuda.Event()
@@ -816,6 +824,13 @@ class Domain:
     def remote_tree(self):
         """(octree, centers, quadrupoles) of the received remote multipoles (ops.gravity.remote_let_tree), built on
         first use from the codes copied to the host during the sync; None without remote multipoles"""
+        plan = getattr(self, "_remote_plan", None)
+        if plan is not None:
+            from ..ops import gravity as grav_ops
+
+            self._remote_plan = None
+            self._remote_tree = grav_ops.remote_let_tree_device(plan[0], self.remote_centers, self.remote_quads,
+                                                                plan[1], self.theta, self.sfc_kind)
         p = getattr(self, "_remote_pending", None)
         if p is not None:
             from ..ops import gravity as grav_ops
@@ -830,6 +845,7 @@ class Domain:
     @remote_tree.setter
     def remote_tree(self, value):
         self._remote_pending = None
+        self._remote_plan = None
         self._remote_tree = value
 
     def exchange_halos(self, d, fields: Sequence[str]):

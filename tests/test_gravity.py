@@ -245,3 +245,64 @@ def test_fused_upsweep_matches_levels(gpu, monkeypatch, n):
         small = _setup(40, gpu)
         G.upsweep(small[1], *small[2:6], small[0], 0.5)
     assert int(G._arrival_counters(1, x.device).abs().sum()) == 0
+
+
+def _disjoint_remote_nodes(n_particles=20000, seed=3, keep=0.6, merge=0.3):
+    """(placeholder codes, centers, quadrupoles) of a random set of disjoint octree nodes: a subset of the leaves of a
+    Plummer octree, some runs of eight sibling leaves replaced by their parent (received nodes at several levels)"""
+    rng = np.random.default_rng(seed)
+    box, ot, *_ = _setup(n_particles, "cpu", seed=seed, bucket=16)
+    t = ot.tree.numpy().view(np.uint64).astype(object)
+    nodes = []
+    i, L = 0, len(t) - 1
+    while i < L:
+        rng_ = int(t[i + 1] - t[i])
+        lev = 21 - (rng_.bit_length() - 1) // 3
+        if lev > 0 and i + 8 <= L and rng.random() < merge:
+            span = 1 << (3 * (21 - lev + 1))
+            if int(t[i]) % span == 0 and int(t[i + 8]) - int(t[i]) == span:
+                if rng.random() < keep:
+                    nodes.append((int(t[i]), lev - 1))
+                i += 8
+                continue
+        if rng.random() < keep:
+            nodes.append((int(t[i]), lev))
+        i += 1
+    rng.shuffle(nodes)
+    codes = np.array([(1 << (3 * lv)) | (k >> (3 * (21 - lv))) for k, lv in nodes], dtype=np.uint64)
+    M = len(nodes)
+    rc = torch.from_numpy(rng.normal(size=(M, 3)))
+    rq = torch.from_numpy(rng.normal(scale=1e-3, size=(M, 8)).astype(np.float32))
+    rq[:, 0] = torch.from_numpy(rng.uniform(0.5, 1.5, M).astype(np.float32))
+    return box, torch.from_numpy(codes.view(np.int64)), rc, rq
+
+
+def test_let_level_ranges_cpu():
+    """node count and level ranges from the leaves per level equal the linked octree's (the device LET build sizes
+    its arrays this way, without a host copy of the linker's ranges)"""
+    for seed in (0, 1, 2):
+        box, codes, rc, rq = _disjoint_remote_nodes(5000, seed=seed)
+        ot, _, _ = G.remote_let_tree(codes, rc, rq, box, 0.5)
+        t = ot.tree.numpy().view(np.uint64)
+        lv = [21 - (int(r).bit_length() - 1) // 3 for r in (t[1:] - t[:-1])]
+        hist = np.bincount(lv, minlength=22)
+        N, lr = G.let_level_ranges(hist)
+        assert N == ot.num_nodes and lr == list(ot.level_range)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 1])
+def test_remote_let_tree_device_matches_host(gpu, seed):
+    """the device LET build (csrc/hip/let_tree.hip: plan in the sync, build at the gravity phase) gives the host
+    build's tree (leaf keys, linked structure, level ranges) and its upswept multipoles and MAC radii"""
+    box, codes, rc, rq = _disjoint_remote_nodes(30000, seed=seed)
+    ot_h, c_h, mp_h = G.remote_let_tree(codes, rc, rq, box, 0.5)
+    plan = G.remote_let_plan(codes.to(gpu))
+    ot_d, c_d, mp_d = G.remote_let_tree_device(plan, rc.to(gpu), rq.to(gpu), box, 0.5)
+    assert torch.equal(ot_d.tree.cpu(), ot_h.tree)
+    assert ot_d.num_nodes == ot_h.num_nodes and list(ot_d.level_range) == list(ot_h.level_range)
+    assert ot_d.level_range_dev.cpu().tolist() == list(ot_h.level_range)
+    for f in ("prefixes", "child_offsets", "node_to_leaf", "leaf_to_node"):
+        assert torch.equal(getattr(ot_d, f).cpu().to(getattr(ot_h, f).dtype), getattr(ot_h, f)), f
+    assert torch.allclose(c_d.cpu(), c_h.view(-1), rtol=1e-10, atol=1e-12)
+    assert torch.allclose(mp_d.cpu(), mp_h.view(-1), rtol=1e-4, atol=1e-7)
