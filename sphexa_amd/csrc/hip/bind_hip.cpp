@@ -109,11 +109,13 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("compute_keys", [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, int kind, Ptr keys, Ptr s)
           { computeKeys(n, P<double>(x), P<double>(y), P<double>(z), toBox(box), kind, P<KeyT>(keys), St(s)); });
     m.def("compute_keys_devbox",
-          [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, Ptr ext, int kind, Ptr keys, Ptr s)
+          [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, Ptr ext, int kind, Ptr keys, Ptr s, int layout)
           {
               computeKeysDevBox(n, P<double>(x), P<double>(y), P<double>(z), toBox(box), P<double>(ext), kind,
-                                P<KeyT>(keys), St(s));
-          });
+                                P<KeyT>(keys), St(s), layout);
+          },
+          py::arg("n"), py::arg("x"), py::arg("y"), py::arg("z"), py::arg("box"), py::arg("ext"), py::arg("kind"),
+          py::arg("keys"), py::arg("s"), py::arg("layout") = 0);
     m.def("sort_temp_bytes", [](int64_t n) { return sortPairsTempBytes(n); });
     m.def("sort_pairs_temp_bytes", [](int64_t n) { return sortPairsTempBytes(n); });
     m.def("sort_keys", [](int64_t n, Ptr kin, Ptr kout, Ptr perm, Ptr tmp, size_t tmpBytes, Ptr s)

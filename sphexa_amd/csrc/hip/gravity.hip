@@ -308,6 +308,12 @@ void gravitySetMac(int64_t N, const KeyT* prefixes, const Box& box, int kind, do
 #ifndef SPHX_M2P_WAVES
 #define SPHX_M2P_WAVES 3 // twelve MFMA result tiles in flight per 16-node block (4 waves spill)
 #endif
+#ifndef SPHX_M2P_TBCHUNK
+// target blocks of an M2P tile pass (evalM2PMfma): 2 = two passes over the node rows, half the MFMA result registers
+// in flight (166 VGPRs, no spills at 3 waves/SIMD; 4: 168 + 8 spilled). Evrard -n 200 alone 6.25 -> 5.99 ms
+// (profiles/r6/gravity/README.md)
+#define SPHX_M2P_TBCHUNK 2
+#endif
 #ifndef SPHX_M2P_UNROLL
 #define SPHX_M2P_UNROLL 2 // unroll of the per-node M2P loop
 #endif
@@ -659,9 +665,17 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const NodeRecs& R
             const float4 Z4 = reinterpret_cast<const float4*>(sC + 128)[4 * tile + kq];
             const float4 M4 = reinterpret_cast<const float4*>(sC + 192)[4 * tile + kq];
             const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+            // (SPHX_M2P_TBCHUNK target blocks per pass: 4 = every block's tiles in flight at once, 2 = two passes
+            // with half the MFMA result registers)
+            constexpr int kChunk = SPHX_M2P_TBCHUNK < kTb1 - kTb0 ? SPHX_M2P_TBCHUNK : kTb1 - kTb0;
+            const f32x2 Cx[2] = {{X4.x, X4.y}, {X4.z, X4.w}}, Cy[2] = {{Y4.x, Y4.y}, {Y4.z, Y4.w}};
+            const f32x2 Cz[2] = {{Z4.x, Z4.y}, {Z4.z, Z4.w}}, Cm[2] = {{M4.x, M4.y}, {M4.z, M4.w}};
+#pragma unroll
+            for (int tc = kTb0; tc < kTb1; tc += kChunk)
+            {
             f32x4 Qx[4], Qy[4], Qz[4];
 #pragma unroll
-            for (int tb = kTb0; tb < kTb1; ++tb)
+            for (int tb = tc; tb < tc + kChunk; ++tb)
             {
                 Qx[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.x, T.bT[tb], zero, 0, 0, 0);
                 Qy[tb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A.y, T.bT[tb], zero, 0, 0, 0);
@@ -672,13 +686,11 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const NodeRecs& R
 #endif
             // pair arithmetic on pairs of node rows (r, r + 1): one v_pk_*_f32 per two pairs (13 VALU per pair
             // instead of ~20; the M2P loop keeps the SIMD's VALU ~70 % busy, profiles/r4/pmc_grav.txt)
-            const f32x2 Cx[2] = {{X4.x, X4.y}, {X4.z, X4.w}}, Cy[2] = {{Y4.x, Y4.y}, {Y4.z, Y4.w}};
-            const f32x2 Cz[2] = {{Z4.x, Z4.y}, {Z4.z, Z4.w}}, Cm[2] = {{M4.x, M4.y}, {M4.z, M4.w}};
 #pragma unroll
             for (int rp = 0; rp < 2; ++rp)
             {
 #pragma unroll
-                for (int tb = kTb0; tb < kTb1; ++tb)
+                for (int tb = tc; tb < tc + kChunk; ++tb)
                 {
                     const f32x2 rx  = T.tx[tb] - Cx[rp], ry = T.ty[tb] - Cy[rp], rz = T.tz[tb] - Cz[rp];
                     const f32x2 r2  = rx * rx + ry * ry + rz * rz;
@@ -697,6 +709,7 @@ __device__ inline void evalM2PMfma(const int32_t* list, int n, const NodeRecs& R
                     T.ay[tb]        = (T.ay[tb] + ir5 * qy) + cmb * ry;
                     T.az[tb]        = (T.az[tb] + ir5 * qz) + cmb * rz;
                 }
+            }
             }
         }
     }

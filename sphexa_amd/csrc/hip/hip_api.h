@@ -46,7 +46,7 @@ struct PosArgs
 void computeKeys(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind, KeyT* keys,
                  hipStream_t s);
 void computeKeysDevBox(int64_t n, const double* x, const double* y, const double* z, const Box& box, const double* ext,
-                       int kind, KeyT* keys, hipStream_t s);
+                       int kind, KeyT* keys, hipStream_t s, int layout = 0);
 size_t sortPairsTempBytes(int64_t n);
 void sortPairs(int64_t n, const KeyT* keysIn, KeyT* keysOut, const int32_t* valsIn, int32_t* valsOut, void* tmp,
                size_t tmpBytes, int beginBit, int endBit, hipStream_t s);

@@ -33,12 +33,14 @@ void computeKeys(int64_t n, const double* x, const double* y, const double* z, c
  *  extents are used as Domain.update_box sets them (hi <= lo -> lo + 1e-10), so the keys are those of the host box. */
 __global__ void computeKeysDevBoxKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
                                         const double* __restrict__ z, Box box, const double* __restrict__ ext, int kind,
-                                        KeyT* __restrict__ keys)
+                                        KeyT* __restrict__ keys, int layout)
 {
     for (int d = 0; d < 3; ++d)
         if (box.bc[d] != kPeriodic)
         {
-            const double lo = ext[2 * d], hi = ext[2 * d + 1];
+            // layout 0: [min x, max x, min y, ...] (one rank); 1: [min x, min y, min z, -max x, -max y, -max z] (the
+            // MIN-allreduced extents of several ranks)
+            const double lo = layout ? ext[d] : ext[2 * d], hi = layout ? -ext[3 + d] : ext[2 * d + 1];
             box.lo[d]       = lo;
             box.hi[d]       = hi <= lo ? lo + 1e-10 : hi;
         }
@@ -47,10 +49,10 @@ __global__ void computeKeysDevBoxKernel(int64_t n, const double* __restrict__ x,
 }
 
 void computeKeysDevBox(int64_t n, const double* x, const double* y, const double* z, const Box& box, const double* ext,
-                       int kind, KeyT* keys, hipStream_t s)
+                       int kind, KeyT* keys, hipStream_t s, int layout)
 {
     if (n == 0) return;
-    computeKeysDevBoxKernel<<<gridFor(n, 256), 256, 0, s>>>(n, x, y, z, box, ext, kind, keys);
+    computeKeysDevBoxKernel<<<gridFor(n, 256), 256, 0, s>>>(n, x, y, z, box, ext, kind, keys, layout);
     SPHX_LAUNCH_CHECK();
 }
 

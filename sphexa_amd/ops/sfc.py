@@ -40,15 +40,16 @@ def compute_keys(x: torch.Tensor, y: torch.Tensor, z: torch.Tensor, box: Box, ki
 
 
 def compute_keys_devbox(x: torch.Tensor, y: torch.Tensor, z: torch.Tensor, box: Box, ext: torch.Tensor,
-                        kind: int = HILBERT, out: torch.Tensor | None = None) -> torch.Tensor:
+                        kind: int = HILBERT, out: torch.Tensor | None = None, layout: int = 0) -> torch.Tensor:
     """GPU keys with the open dimensions' extents read from the device (``ext`` = [min x, max x, min y, max y, min z,
-    max z] float64, e.g. the prefetched reduction of parallel/domain.py); periodic dimensions from ``box``"""
+    max z] float64, e.g. the prefetched reduction of parallel/domain.py; ``layout`` 1: [min x, min y, min z, -max x,
+    -max y, -max z], the MIN-allreduced extents of several ranks); periodic dimensions from ``box``"""
     n = x.numel()
     if out is None:
         out = torch.empty(n, dtype=torch.int64, device=x.device)
     if n:
         _lib.hip().compute_keys_devbox(n, x.data_ptr(), y.data_ptr(), z.data_ptr(), box.to_array(), ext.data_ptr(),
-                                       kind, out.data_ptr(), _stream())
+                                       kind, out.data_ptr(), _stream(), layout)
     return out
 
 

@@ -242,10 +242,23 @@ class Domain:
         # box), so it waits for the previous step's GPU work with this sync's kernels queued behind it instead of
         # launching them one by one into an idle GPU
         pf = None
-        if DEVICE_BOX and self.size == 1 and not all(b == PERIODIC for b in self.box.bc):
+        multi_box = None
+        open_box = not all(b == PERIODIC for b in self.box.bc)
+        if DEVICE_BOX and self.size == 1 and open_box:
             pf = self._take_box_prefetch(x, y, z)
         if pf is not None:
             keys = sfc_ops.compute_keys_devbox(x, y, z, self.box, pf[3], self.sfc_kind)
+        elif DEVICE_BOX and self.size > 1 and open_box and x.is_cuda:
+            # several ranks: the MIN-allreduced extents stay on the device for the keys; their host copy is collected
+            # after the migration's leaf-count copy (a synchronization anyway), before anything on the host reads the
+            # box (halo discovery): no host wait of its own
+            ext = self._box_reduce(x, y, z)
+            host = torch.empty(ext.numel(), dtype=torch.float64, pin_memory=True)
+            host.copy_(ext, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            multi_box = (host, ev, ext)
+            keys = sfc_ops.compute_keys_devbox(x, y, z, self.box, ext, self.sfc_kind, layout=1)
         else:
             self.update_box(x, y, z)
             PROF.mark("sync: box")
@@ -256,6 +269,10 @@ class Domain:
             # the staying particles are not moved: skeys is the new SFC order, src reads it from the own fields and the
             # received rows (sfc_ops.MergedSource)
             skeys, src = self._distribute(keys, own, conserved)
+            if multi_box is not None:
+                multi_box[1].synchronize()
+                self._apply_box_ext(self._box_ext(multi_box[0].tolist()))
+                PROF.mark("sync: box (device extents)")
         else:
             skeys, perm = sfc_ops.sort_keys(keys)
             src = None
