@@ -21,16 +21,19 @@
 typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr int kIters = 4096;
 
-// kind 0: 8 independent v_fma_f32 chains; 1: 8 independent v_pk_fma_f32 chains; 2: 4 fma + 4 v_exp_f32
+// kind 0: 8 independent v_fma_f32 chains; 1: 8 independent v_pk_fma_f32 chains; 2: 4 fma + 4 v_exp_f32;
+// 3: 8 independent v_add_u32 chains; 4: 8 v_and_b32/v_lshl_or chains (bit ops); 5: v_cndmask_b32 chains
 template<int kind>
 __global__ __launch_bounds__(64) void valuKernel(float* out, float s, long long* clk)
 {
     float a[8];
     f2 p[8];
+    unsigned ia[8];
     for (int k = 0; k < 8; ++k)
     {
         a[k] = float(threadIdx.x + k);
         p[k] = f2{a[k], a[k] + 1.f};
+        ia[k] = threadIdx.x * 7u + k;
     }
     const f2 s2 = f2{s, s};
     const long long t0 = __builtin_amdgcn_s_memtime();
@@ -41,17 +44,23 @@ __global__ __launch_bounds__(64) void valuKernel(float* out, float s, long long*
         {
             if constexpr (kind == 0) a[k] = __builtin_fmaf(a[k], s, 0.5f);
             else if constexpr (kind == 1) p[k] = __builtin_elementwise_fma(p[k], s2, f2{0.5f, 0.25f});
-            else
+            else if constexpr (kind == 2)
             {
                 if (k & 1) a[k] = __builtin_amdgcn_exp2f(a[k]);
                 else a[k] = __builtin_fmaf(a[k], s, 0.5f);
             }
+            else if constexpr (kind == 3)
+                asm volatile("v_add_u32 %0, %0, %1" : "+v"(ia[k]) : "v"(ia[(k + 1) & 7]));
+            else if constexpr (kind == 4)
+                asm volatile("v_lshl_or_b32 %0, %0, 1, %1" : "+v"(ia[k]) : "v"(ia[(k + 3) & 7]));
+            else
+                asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(ia[k]) : "v"(ia[(k + 5) & 7]));
         }
     }
     const long long t1 = __builtin_amdgcn_s_memtime();
     float r = 0.f;
     for (int k = 0; k < 8; ++k)
-        r += a[k] + p[k].x + p[k].y;
+        r += a[k] + p[k].x + p[k].y + float(ia[k]);
     out[blockIdx.x * 64 + threadIdx.x] = r;
     if (threadIdx.x == 0) clk[blockIdx.x] = t1 - t0;
 }
@@ -97,5 +106,8 @@ int main()
     if (run<0>("v_fma_f32", out, clk, hclk)) return 1;
     if (run<1>("v_pk_fma", out, clk, hclk)) return 1;
     if (run<2>("fma+exp", out, clk, hclk)) return 1;
+    if (run<3>("v_add_u32", out, clk, hclk)) return 1;
+    if (run<4>("v_lshl_or", out, clk, hclk)) return 1;
+    if (run<5>("v_cndmask", out, clk, hclk)) return 1;
     return 0;
 }
