@@ -437,6 +437,11 @@ def remote_let_tree_device(plan: RemoteLetPlan, rcenters: torch.Tensor, rquads: 
     if words[1]:
         raise RuntimeError(f"remote LET nodes overlap ({words[1]} received nodes)")
     hp, s, dev = _lib.hip(), _stream(), rcenters.device
+    # the plan's buffers come from the sync's stream; the build may run on a gravity side stream: without this the
+    # caching allocator could hand them to the sync stream's next allocation while these kernels still read them
+    cur = torch.cuda.current_stream(dev)
+    plan.work.record_stream(cur)
+    plan.codes.record_stream(cur)
     M = plan.codes.numel()
     L = words[0] - 1
     N, lr = let_level_ranges(words[2:])
@@ -486,6 +491,7 @@ def remote_let_tree_device(plan: RemoteLetPlan, rcenters: torch.Tensor, rquads: 
     hp.remote_let_scatter(M, plan.work.data_ptr(), leaf_to_node.data_ptr(), 0, 0, centers.data_ptr(), mp.data_ptr(),
                           1, float(FORCE_ACCEPT_MAC2), s)
     ot.level_range_dev = level_range_dev  # (the linker's own ranges: tests compare them with ``lr``)
+    ot.let_plan = plan  # (held with the tree: its lifetime is the step's)
     return ot, centers, mp
 
 
