@@ -413,7 +413,7 @@ PYBIND11_MODULE(_sphx_hip, m)
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
              Ptr curlv, const std::array<Ptr, 6>& dV, int64_t ntot, Ptr rec, Ptr s, Ptr avS, int inDone, Ptr avOut,
-             Ptr momOut, Ptr cs, Ptr mm, Ptr prho)
+             Ptr momOut, Ptr cs, Ptr mm, Ptr prho, int momSplit)
           {
               auto sc = toConsts(c);
               auto cp = six(cij);
@@ -422,31 +422,33 @@ PYBIND11_MODULE(_sphx_hip, m)
                            P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(wh),
                            P<float>(kx), P<float>(xm), P<void>(rec), cp.data(), P<float>(divv), P<float>(curlv),
                            g.data(), P<void>(avS), St(s), inDone, P<void>(avOut), P<void>(momOut), P<float>(cs),
-                           P<float>(mm), P<float>(prho));
+                           P<float>(mm), P<float>(prho), momSplit);
           },
           py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
           py::arg("x"), py::arg("y"), py::arg("z"), py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("h"),
           py::arg("cij"), py::arg("wh"), py::arg("kx"), py::arg("xm"), py::arg("divv"), py::arg("curlv"),
           py::arg("dV"), py::arg("ntot"), py::arg("rec"), py::arg("s"), py::arg("avS") = 0, py::arg("inDone") = 0,
-          py::arg("avOut") = 0, py::arg("momOut") = 0, py::arg("cs") = 0, py::arg("mm") = 0, py::arg("prho") = 0);
+          py::arg("avOut") = 0, py::arg("momOut") = 0, py::arg("cs") = 0, py::arg("mm") = 0, py::arg("prho") = 0,
+          py::arg("momSplit") = 0);
     m.def("av_switches",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr cs, const std::array<Ptr, 6>& cij, Ptr wh, Ptr kx, Ptr xm, Ptr divv,
              double dt, Ptr alpha, int64_t ntot, Ptr rec, Ptr s, Ptr avS, int inDone, Ptr momOut, Ptr alphaOut,
-             Ptr dtDev)
+             Ptr dtDev, int momSplit)
           {
               auto sc = toConsts(c);
               auto cp = six(cij);
               avSwitches(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
                          P<double>(z), P<float>(vx), P<float>(vy), P<float>(vz), P<float>(h), P<float>(cs), cp.data(),
                          P<float>(wh), P<float>(kx), P<float>(xm), P<float>(divv), dt, P<void>(rec), P<void>(avS),
-                         P<float>(alpha), St(s), inDone, P<void>(momOut), P<float>(alphaOut), P<double>(dtDev));
+                         P<float>(alpha), St(s), inDone, P<void>(momOut), P<float>(alphaOut), P<double>(dtDev),
+                         momSplit);
           },
           py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
           py::arg("x"), py::arg("y"), py::arg("z"), py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("h"),
           py::arg("cs"), py::arg("cij"), py::arg("wh"), py::arg("kx"), py::arg("xm"), py::arg("divv"), py::arg("dt"),
           py::arg("alpha"), py::arg("ntot"), py::arg("rec"), py::arg("s"), py::arg("avS") = 0, py::arg("inDone") = 0,
-          py::arg("momOut") = 0, py::arg("alphaOut") = 0, py::arg("dtDev") = 0);
+          py::arg("momOut") = 0, py::arg("alphaOut") = 0, py::arg("dtDev") = 0, py::arg("momSplit") = 0);
     m.def("momentum_energy_ve",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr vx, Ptr vy, Ptr vz, Ptr h, Ptr mm, Ptr prho, Ptr cs, const std::array<Ptr, 6>& cij, Ptr kx, Ptr xm,

@@ -234,12 +234,12 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
                   const float* wh, const float* kx, const float* xm, void* rec, float* const cij[6], float* divv,
                   float* curlv, float* const dV[6], void* avS, hipStream_t s, int inDone = 0, void* avOut = nullptr,
                   void* momOut = nullptr, const float* cs = nullptr, const float* m = nullptr,
-                  const float* prho = nullptr);
+                  const float* prho = nullptr, int momSplit = 0);
 void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                 const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                 const float* c, float* const cij[6], const float* wh, const float* kx, const float* xm,
                 const float* divv, double dt, void* rec, const void* avS, float* alpha, hipStream_t s, int inDone = 0,
-                void* momOut = nullptr, float* alphaOut = nullptr, const double* dtDev = nullptr);
+                void* momOut = nullptr, float* alphaOut = nullptr, const double* dtDev = nullptr, int momSplit = 0);
 void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const MomFields& f,
                       bool avClean, const float* wh, void* rec, void* recGradV, float* ax, float* ay, float* az,
                       double* du, float* minDt, hipStream_t s, int inDone = 0, float mUniform = 0.f);

@@ -646,7 +646,8 @@ __global__ __launch_bounds__(B) void iadDivvCurlvKernel(NbrArgs a, SphConsts sc,
                                                              Six dV, int doGrad, float4* __restrict__ avS,
                                                              SrcAvV* __restrict__ avOut, SrcMomQ* __restrict__ momOut,
                                                              const float* __restrict__ cs, const float* __restrict__ mm,
-                                                             const float* __restrict__ prho)
+                                                             const float* __restrict__ prho,
+                                                             SrcMomSide* __restrict__ momSide = nullptr)
 {
     __shared__ float4 tile[B / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
@@ -695,7 +696,35 @@ __global__ __launch_bounds__(B) void iadDivvCurlvKernel(NbrArgs a, SphConsts sc,
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             };
-            if (momOut)
+            if (momOut && momSide)
+            {
+                // split records (SrcMomQ64 + SrcMomSide, uniform mass: momOut is the SrcMomQ64 array): the 64-B main
+                // record as whole 1-KiB rows, the side record {rho, alpha = 0} per lane (alpha by the AV loop)
+                SrcMomQ64 r;
+                r.x    = pi.x;
+                r.y    = pi.y;
+                r.z    = pi.z;
+                r.vx   = pi.vx;
+                r.vy   = pi.vy;
+                r.vz   = pi.vz;
+                r.ih   = 1.0f / h[i];
+                r.c11  = c[0];
+                r.c12  = c[1];
+                r.c13  = c[2];
+                r.c22  = c[3];
+                r.c23  = c[4];
+                r.c33  = c[5];
+                r.c    = ci;
+                r.xm   = pi.xm;
+                r.prho = prho[i];
+                const float4* rp = reinterpret_cast<const float4*>(&r);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    w[lane * 4 + k] = rp[k];
+                flush(reinterpret_cast<float4*>(reinterpret_cast<SrcMomQ64*>(momOut) + i0), 4);
+                if (valid) momSide[i] = SrcMomSide{kx[i] * mm[i] / pi.xm, 0.f};
+            }
+            else if (momOut)
             {
                 SrcMomQ r;
                 r.x     = pi.x;
@@ -787,7 +816,8 @@ __global__ __launch_bounds__(B) void avSwitchesVKernel(NbrArgs a, SphConsts sc, 
                                                             const float* __restrict__ wh, double dt,
                                                             const float* __restrict__ alpha,
                                                             float* __restrict__ alphaOut, const double* dtDev,
-                                                            SrcMomQ* __restrict__ momOut)
+                                                            SrcMomQ* __restrict__ momOut,
+                                                            SrcMomSide* __restrict__ momSide = nullptr)
 {
     __shared__ float4 tile[B / 64 * 64 * CoopLoader<SrcAvV>::S];
     int64_t i;
@@ -803,7 +833,8 @@ __global__ __launch_bounds__(B) void avSwitchesVKernel(NbrArgs a, SphConsts sc, 
                                 sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
     if (!valid) return;
     alphaOut[i] = al;
-    if (momOut) momOut[i].alpha = al;
+    if (momSide) momSide[i].alpha = al;
+    else if (momOut) momOut[i].alpha = al;
 }
 
 //! @brief block min of the Courant time step, then one atomic per block
@@ -1158,13 +1189,25 @@ void iad(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, co
     SPHX_LAUNCH_CHECK();
 }
 
+//! byte offset of the side records in a split momentum workspace of ntot records (256-B aligned after the main ones)
+inline size_t momSideOffset(int64_t ntot) { return (size_t(ntot) * sizeof(SrcMomQ64) + 255) & ~size_t(255); }
+
+//! side records of a split momentum workspace (null: 80-B SrcMomQ records or none)
+static SrcMomSide* momSideOf(void* momOut, int64_t ntot, int momSplit)
+{
+    if (!momOut || !momSplit) return nullptr;
+    if (reinterpret_cast<uintptr_t>(momOut) & 63) throw std::invalid_argument("momentum records: 64-B alignment");
+    return reinterpret_cast<SrcMomSide*>(static_cast<char*>(momOut) + momSideOffset(ntot));
+}
+
 void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                   const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                   const float* wh, const float* kx, const float* xm, void* rec, float* const cij[6], float* divv,
                   float* curlv, float* const dV[6], void* avS, hipStream_t s, int inDone, void* avOut, void* momOut,
-                  const float* cs, const float* m, const float* prho)
+                  const float* cs, const float* m, const float* prho, int momSplit)
 {
     if (a.last <= a.first) return;
+    SrcMomSide* momSide = momSideOf(momOut, ntot, momSplit);
     Six c, g;
     for (int k = 0; k < 6; ++k)
     {
@@ -1195,11 +1238,12 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
                           if (avS)
                               iadDivvCurlvKernel<true, SrcIadQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
                                   withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv, curlv, g,
-                                  dV[0] != nullptr, (float4*)avS, (SrcAvV*)avOut, (SrcMomQ*)momOut, cs, m, prho);
+                                  dV[0] != nullptr, (float4*)avS, (SrcAvV*)avOut, (SrcMomQ*)momOut, cs, m, prho,
+                                  momSide);
                           else
                               iadDivvCurlvKernel<false, SrcIadQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
                                   withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv, curlv, g,
-                                  dV[0] != nullptr, nullptr, nullptr, (SrcMomQ*)momOut, cs, m, prho);
+                                  dV[0] != nullptr, nullptr, nullptr, (SrcMomQ*)momOut, cs, m, prho, momSide);
                       }, 2);
     }
     SPHX_LAUNCH_CHECK();
@@ -1209,7 +1253,7 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                 const double* y, const double* z, const float* vx, const float* vy, const float* vz, const float* h,
                 const float* c, float* const cij[6], const float* wh, const float* kx, const float* xm,
                 const float* divv, double dt, void* rec, const void* avS, float* alpha, hipStream_t s, int inDone,
-                void* momOut, float* alphaOut, const double* dtDev)
+                void* momOut, float* alphaOut, const double* dtDev, int momSplit)
 {
     // alpha_i is read by its own target only: the new values may go to another buffer (alphaOut), so that a step
     // enqueued speculatively can be redone from the old ones (models/propagators.py)
@@ -1238,7 +1282,8 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                           avSwitchesVKernel<B><<<gridT(a, B), B, 0, s>>>(withTot(a, ntot), sc, q, h, cc,
                                                                          (const SrcAvV*)rec, divv, (const float4*)avS,
                                                                          wh, dt, alpha, alphaOut, dtDev,
-                                                                         (SrcMomQ*)momOut);
+                                                                         (SrcMomQ*)momOut,
+                                                                         momSideOf(momOut, ntot, momSplit));
                       }, 3);
     }
     else
@@ -1250,9 +1295,6 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
     }
     SPHX_LAUNCH_CHECK();
 }
-
-//! byte offset of the side records in a split momentum workspace of ntot records (256-B aligned after the main ones)
-inline size_t momSideOffset(int64_t ntot) { return (size_t(ntot) * sizeof(SrcMomQ64) + 255) & ~size_t(255); }
 
 void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const MomFields& f,
                       bool avClean, const float* wh, void* rec, void* recGradV, float* ax, float* ay, float* az,

@@ -34,12 +34,12 @@ DV = ("dV11", "dV12", "dV13", "dV22", "dV23", "dV33")
 REC_BYTES = {"xmass": (32, 32), "gradh": (32, 32), "iad": (48, 48), "iadq": (32, 32), "av": (48, 48),
              "mom": (96, 96), "std": (80, 80)}
 
-# fixed-point VE chain: the IAD and AV loops also write the momentum loop's own SrcMomQ records (workspace M, 80 B per
-# particle) so that the momentum loop packs only its halos. That holds workspace M from the IAD loop on, at the
-# step's memory high-water mark (IAD: lists + fields + workspaces 0, B, 1 and M). Off: the momentum loop packs its
-# records itself and the peak drops by 80 B per particle (Sedov -n 400: 622 -> ~540 B/particle) for one more
-# record pass (profiles/r4/memory.md).
-MOM_HANDOFF = os.environ.get("SPHX_MOM_HANDOFF") == "1"
+# fixed-point VE chain: the IAD and AV loops also write the momentum loop's own records (workspace M: the split
+# SrcMomQ64 rows + SrcMomSide {rho, alpha}, 72 B per particle; or SrcMomQ, 80 B) so that the momentum loop packs only
+# its halos. That holds workspace M from the IAD loop on, at the step's memory high-water mark (IAD: lists + fields +
+# workspaces 0, B, 1 and M): Sedov -n 400 115.9 / 116.2 -> 115.0 / 114.9 ms per step for a peak of 30.9 -> 35.4 GiB
+# (519 -> 595 B/particle; profiles/r6/handoff.md). 0: the momentum loop packs its records itself.
+MOM_HANDOFF = os.environ.get("SPHX_MOM_HANDOFF", "1") == "1"
 # split momentum records (SrcMomQ64 + SrcMomSide) on the fixed-point uniform-mass path; 0: the 80-B SrcMomQ (A/B)
 MOM_SPLIT = os.environ.get("SPHX_MOM_SPLIT", "1") == "1"
 
@@ -499,11 +499,13 @@ def compute_iad_divv_curlv(d, nl: NeighborList, box: Box, av_clean: bool = False
             ho = _handoff(d)
             done = 1 if handoff_take(d, "iadq_own") else 0
             ho.clear()
-            mom = _recM(d).data_ptr() if (MOM_HANDOFF and not av_clean and not mom_split(d, av_clean)) else 0
+            split = mom_split(d, av_clean)
+            mom = _recM(d, split).data_ptr() if (MOM_HANDOFF and not av_clean) else 0
             _lib.hip().iad_divv_curlv(*args, d.size, _rec(d, 0, "iadq").data_ptr(), _stream(),
                                       _rec(d, 1, "av").data_ptr(), inDone=done, avOut=_recB(d).data_ptr(),
                                       momOut=mom, cs=d["c"].data_ptr(), mm=d["m"].data_ptr(),
-                                      prho=d["prho"].data_ptr())
+                                      prho=d["prho"].data_ptr(), momSplit=int(split))
+            d._mom_split_handoff = split
             handoff_mark(d, "avv_own")
             if mom:
                 handoff_mark(d, "momq_iad")
@@ -533,10 +535,11 @@ def compute_av_switches(d, nl: NeighborList, box: Box, alpha_out: torch.Tensor |
             # SrcAvV records in workspace B (own range from the IAD loop); alpha also into the momentum records
             ho = _handoff(d)
             done = 1 if handoff_take(d, "avv_own") else 0
-            mom = _recM(d).data_ptr() if handoff_take(d, "momq_iad") else 0
+            split = bool(getattr(d, "_mom_split_handoff", False))
+            mom = _recM(d, split).data_ptr() if handoff_take(d, "momq_iad") else 0
             ho.clear()
             _lib.hip().av_switches(*args, d.size, _recB(d).data_ptr(), _stream(), avs, inDone=done, momOut=mom,
-                                   **extra)
+                                   momSplit=int(split), **extra)
             if mom:
                 handoff_mark(d, "momq_own")
         else:
@@ -571,8 +574,10 @@ def compute_momentum_energy_ve(d, nl: NeighborList, box: Box, av_clean: bool = F
             d._recB = None  # the AV records are dead: their block serves the momentum records (B is re-created by XMass)
         split = mom_split(d, av_clean)
         rec = _recM(d, split) if d.fixedPoint else _rec(d, 0, "mom")
+        # (a hand-off of the other record form is not used: the records are packed here)
+        same = bool(getattr(d, "_mom_split_handoff", False)) == split
         _lib.hip().momentum_energy_ve(*common, dt.data_ptr(), d.size, rec.data_ptr(), gv, _stream(),
-                                      inDone=0 if split else done, mUniform=uniform_mass(d) if split else 0.0)
+                                      inDone=done if same else 0, mUniform=uniform_mass(d) if split else 0.0)
         d.minDtCourant_dev = dt
         d.minDtCourant = None
     else:

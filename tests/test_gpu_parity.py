@@ -390,3 +390,27 @@ def test_packed_list_overflow_rows_and_repeat(gpu, monkeypatch):
     assert neighbor_lists_as_sets(nl, dg["nc"]) == sets_ref
     H.compute_xmass(dg, nl, domg.box)
     assert torch.equal(dg["xm"], xm_ref)
+
+
+@pytest.mark.parametrize("n", [16, 24])
+def test_ve_step_momentum_handoff_identical(gpu, monkeypatch, n):
+    """the momentum records written by the IAD / AV epilogues (ops/hydro.py MOM_HANDOFF: SrcMomQ64 rows + SrcMomSide
+    {rho, alpha}) equal the ones packMomQ64Kernel packs: the step's fields are bit-identical with and without the
+    hand-off"""
+    results = []
+    for handoff in (False, True):
+        monkeypatch.setattr(H, "MOM_HANDOFF", handoff)
+        d = P.ParticlesData(gpu)
+        prop = HydroVeProp(None, 0)
+        prop.activate_fields(d)
+        box = SedovGrid().init(0, 1, n, d)
+        dom = Domain(Comm(), box)
+        prop.sync(dom, d)
+        for _ in range(3):
+            prop.step(dom, d)
+            d.iteration += 1
+        assert H.mom_split(d, False), "the split momentum records are the path under test"
+        results.append({f: d[f].clone().cpu() for f in ("x", "y", "z", "vx", "vy", "vz", "temp", "du", "ax", "ay",
+                                                         "az", "alpha")})
+    for f in results[0]:
+        assert torch.equal(results[0][f], results[1][f]), f

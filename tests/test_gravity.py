@@ -306,3 +306,30 @@ def test_remote_let_tree_device_matches_host(gpu, seed):
         assert torch.equal(getattr(ot_d, f).cpu().to(getattr(ot_h, f).dtype), getattr(ot_h, f)), f
     assert torch.allclose(c_d.cpu(), c_h.view(-1), rtol=1e-10, atol=1e-12)
     assert torch.allclose(mp_d.cpu(), mp_h.view(-1), rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_remote_let_build_on_delayed_side_stream(gpu):
+    """the plan is made on the sync's stream and the build runs on a gravity side stream (models/propagators.py):
+    with the side stream held back and the main stream allocating and overwriting memory after the plan object is
+    dropped, the tree still equals the host build (the plan's buffers may not return to the main stream's pool while
+    the build reads them)"""
+    box, codes, rc, rq = _disjoint_remote_nodes(30000, seed=1)
+    ot_h, c_h, mp_h = G.remote_let_tree(codes, rc, rq, box, 0.5)
+    codes_d, rc_d, rq_d = codes.to(gpu), rc.to(gpu), rq.to(gpu)
+    plan = G.remote_let_plan(codes_d)
+    nbytes = plan.work.numel()
+    side = torch.cuda.Stream(gpu)
+    side.wait_stream(torch.cuda.current_stream(gpu))
+    with torch.cuda.stream(side):
+        busy = torch.ones(1 << 24, device=gpu)
+        for _ in range(40):  # ~ms of work ahead of the build on the side stream
+            busy = busy * 1.0001
+        ot_d, c_d, mp_d = G.remote_let_tree_device(plan, rc_d, rq_d, box, 0.5)
+    del plan
+    junk = [torch.full((nbytes // 4 + 4096,), -1, dtype=torch.int32, device=gpu) for _ in range(4)]
+    torch.cuda.synchronize(gpu)
+    del junk
+    assert torch.equal(ot_d.tree.cpu(), ot_h.tree)
+    assert torch.allclose(c_d.cpu(), c_h.view(-1), rtol=1e-10, atol=1e-12)
+    assert torch.allclose(mp_d.cpu(), mp_h.view(-1), rtol=1e-4, atol=1e-7)
