@@ -636,6 +636,13 @@ PYBIND11_MODULE(_sphx_hip, m)
               computeStirring(first, last, P<double>(x), P<double>(y), P<double>(z), P<float>(ax), P<float>(ay),
                               P<float>(az), numModes, P<void>(modes), float(norm), St(s));
           });
+    m.def("turbulence_phases",
+          [](int numModes, Ptr phases, Ptr noise, Ptr kvec, Ptr amps, Ptr dtDev, double decayTime, double variance,
+             double solWeight, Ptr table, Ptr s)
+          {
+              turbulencePhases(numModes, P<double>(phases), P<double>(noise), P<double>(kvec), P<double>(amps),
+                               P<double>(dtDev), decayTime, variance, solWeight, P<void>(table), St(s));
+          });
 
     m.def("mark_let",
           [](int64_t nb, Ptr bc, Ptr bh, Ptr child, Ptr n2l, Ptr tc, Ptr th, Ptr gc, const BoxArr& box, Ptr failed,

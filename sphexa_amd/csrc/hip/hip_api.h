@@ -331,5 +331,9 @@ void m2pFlat(int64_t first, int64_t last, const double* x, const double* y, cons
 // turbulence.hip: modes = numModes records of 10 floats {kx, ky, kz, pad, amp*Re[3], amp*Im[3]}
 void computeStirring(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* ax,
                      float* ay, float* az, int numModes, const void* modes, float norm, hipStream_t s);
+//! OU update of the phases (6 per mode, fp64, dt from the device) and the stirring table rows, one launch
+void turbulencePhases(int numModes, double* phases, const double* noise, const double* kvec, const double* amps,
+                      const double* dtDev, double decayTime, double variance, double solWeight, void* table,
+                      hipStream_t s);
 
 } // namespace sphx::hip

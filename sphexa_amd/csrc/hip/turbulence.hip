@@ -54,7 +54,59 @@ __global__ __launch_bounds__(kStirBlock) void stirKernel(int64_t first, int64_t 
     }
 }
 
+/*! @brief one thread per mode: the Ornstein-Uhlenbeck update of its six phases (reference driver.hpp updateNoise:
+ *         phases = phases * a + variance * b * N(0,1), a = exp(-dt / decayTime), b = sqrt(1 - a^2), in fp64 with dt
+ *         read on the device) and its row of the stirring table from the Helmholtz projection (phases.hpp
+ *         computePhases; models/turbulence.py compute_phases): {k, 0, amp Re(3), amp Im(3)} */
+__global__ void turbPhasesKernel(int numModes, double* __restrict__ phases, const double* __restrict__ noise,
+                                 const double* __restrict__ kvec, const double* __restrict__ amps,
+                                 const double* __restrict__ dtDev, double decayTime, double variance, double solWeight,
+                                 StirMode* __restrict__ table)
+{
+    const int m = int(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (m >= numModes) return;
+    const double dt = dtDev[0];
+    const double a  = exp(-dt / decayTime);
+    const double b  = sqrt(1.0 - a * a);
+    double P[3][2];
+    for (int d = 0; d < 3; ++d)
+        for (int c = 0; c < 2; ++c)
+        {
+            const int q = 6 * m + 2 * d + c;
+            P[d][c]     = phases[q] * a + variance * b * noise[q];
+            phases[q]   = P[d][c];
+        }
+    const double k[3] = {kvec[3 * m], kvec[3 * m + 1], kvec[3 * m + 2]};
+    const double kk   = k[0] * k[0] + k[1] * k[1] + k[2] * k[2];
+    const double ka   = k[0] * P[0][1] + k[1] * P[1][1] + k[2] * P[2][1];
+    const double kb   = k[0] * P[0][0] + k[1] * P[1][0] + k[2] * P[2][0];
+    const double amp  = amps[m];
+    StirMode r;
+    r.kx  = float(k[0]);
+    r.ky  = float(k[1]);
+    r.kz  = float(k[2]);
+    r.pad = 0.f;
+    for (int d = 0; d < 3; ++d)
+    {
+        const double diva = k[d] * (ka / kk), divb = k[d] * (kb / kk);
+        const double curla = P[d][0] - divb, curlb = P[d][1] - diva;
+        r.re[d] = float((solWeight * curla + (1.0 - solWeight) * divb) * amp);
+        r.im[d] = float((solWeight * curlb + (1.0 - solWeight) * diva) * amp);
+    }
+    table[m] = r;
+}
+
 } // namespace
+
+void turbulencePhases(int numModes, double* phases, const double* noise, const double* kvec, const double* amps,
+                      const double* dtDev, double decayTime, double variance, double solWeight, void* table,
+                      hipStream_t s)
+{
+    if (numModes <= 0) return;
+    turbPhasesKernel<<<gridFor(numModes, 64), 64, 0, s>>>(numModes, phases, noise, kvec, amps, dtDev, decayTime,
+                                                          variance, solWeight, static_cast<StirMode*>(table));
+    SPHX_LAUNCH_CHECK();
+}
 
 void computeStirring(int64_t first, int64_t last, const double* x, const double* y, const double* z, float* ax,
                      float* ay, float* az, int numModes, const void* modes, float norm, hipStream_t s)

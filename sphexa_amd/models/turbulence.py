@@ -132,7 +132,38 @@ class TurbulenceData:
         t[:, 7:10] = im * self.amplitudes[:, None]
         return t, re, im
 
+    def _pull_device_phases(self):
+        """the device's phases (drive_device) back into the host state"""
+        if getattr(self, "_dev_valid", False):
+            self.phases = self._phases_dev.cpu().numpy().copy()
+            self._dev_valid = False
+
+    def drive_device(self, d, first, last, dt_dev):
+        """GPU: the same update with dt read on the device (``dt_dev``, float64 [dt, ...] of the deferred time step,
+        Propagator.defer_host): the host draws the step's normals (same engine, same order as update_noise: the RNG
+        state and checkpoints are unchanged), one launch updates the phases in fp64 and writes the stirring table
+        (csrc/hip/turbulence.hip turbPhasesKernel), then the stirring kernel. No host synchronization on dt."""
+        dev = d.device
+        if not getattr(self, "_dev_valid", False):
+            self._phases_dev = torch.from_numpy(np.ascontiguousarray(self.phases, dtype=np.float64)).to(dev)
+            self._kvec_dev = torch.from_numpy(np.ascontiguousarray(self.modes, dtype=np.float64)).to(dev)
+            self._amps_dev = torch.from_numpy(np.ascontiguousarray(self.amplitudes, dtype=np.float64)).to(dev)
+            self._table_dev = torch.empty(self.num_modes * 10, dtype=torch.float32, device=dev)
+            self._dev_valid = True
+        noise = torch.from_numpy(self.rng.normal(self.phases.size)).pin_memory()
+        noise_dev = noise.to(dev, non_blocking=True)
+        s = _lib.stream()
+        _lib.hip().turbulence_phases(self.num_modes, self._phases_dev.data_ptr(), noise_dev.data_ptr(),
+                                     self._kvec_dev.data_ptr(), self._amps_dev.data_ptr(), dt_dev.data_ptr(),
+                                     self.decay_time, self.variance, self.sol_weight, self._table_dev.data_ptr(), s)
+        self._dev_noise = noise  # (pinned source of the in-flight copy: kept until the next step)
+        x, y, z, ax, ay, az = (d[f] for f in ("x", "y", "z", "ax", "ay", "az"))
+        _lib.hip().compute_stirring(first, last, x.data_ptr(), y.data_ptr(), z.data_ptr(), ax.data_ptr(),
+                                    ay.data_ptr(), az.data_ptr(), self.num_modes, self._table_dev.data_ptr(),
+                                    self.sol_weight_norm, s)
+
     def drive(self, d, first, last, dt):
+        self._pull_device_phases()
         self.update_noise(dt)
         table, re, im = self.mode_table()
         x, y, z, ax, ay, az = (d[f] for f in ("x", "y", "z", "ax", "ay", "az"))
@@ -151,6 +182,7 @@ class TurbulenceData:
 
     # ----------------------------------------------------------------------------------------- checkpointing
     def store(self, writer):
+        self._pull_device_phases()
         p = self.PREFIX
         writer.step_attribute(p + "variance", self.variance)
         writer.step_attribute(p + "decayTime", self.decay_time)
@@ -173,13 +205,16 @@ class TurbulenceData:
         self.modes = g("modes").reshape(nm, 3)
         self.amplitudes = g("amplitudes")
         self.phases = g("phases")
+        self._dev_valid = False  # (a device copy is re-made from these on the next device drive)
         if "rngEngineState" in attrs:
             raw = np.asarray(attrs["rngEngineState"]).ravel().astype(np.int8).tobytes()
             self.rng.set_state_text(raw.split(b"\0")[0].decode())
 
 
 class TurbVeProp(HydroVeProp):
-    needs_host_dt = True  # the new dt is used on the host within the step (Propagator.defer_host)
+    # the stirring reads the new dt on the device when the host copy is deferred (TurbulenceData.drive_device), so
+    # the step does not wait for it (Propagator.defer_host)
+    needs_host_dt = False
 
     def __init__(self, out=sys.stdout, rank=0, av_clean=False, quiet=False, settings=None):
         super().__init__(out, rank, av_clean, quiet)
@@ -196,7 +231,11 @@ class TurbVeProp(HydroVeProp):
         first, last = domain.start_index(), domain.end_index()
         self.compute_timestep(domain, d)
         self.timer.step("Timestep")
-        self.turb.drive(d, first, last, d.minDt)
+        dt_dev = getattr(d, "_dt_dev", None)
+        if d.device.type == "cuda" and dt_dev is not None:
+            self.turb.drive_device(d, first, last, dt_dev)
+        else:
+            self.turb.drive(d, first, last, d.minDt)
         self.timer.step("Turbulence Stirring")
         H.compute_positions(d, first, last, domain.box)
         H.update_smoothing_length(d, first, last)

@@ -61,6 +61,27 @@ def test_turbulence_gpu(gpu, small_glass):
         assert float((a[k] - b[k]).abs().max()) / float(a[k].abs().max()) < 1e-3
 
 
+def test_turbulence_device_drive_matches_host(gpu, small_glass):
+    """the deferred GPU step (bench.py / CLI: dt stays on the device) stirs with the phases updated on the device
+    (TurbulenceData.drive_device); the same run with host dt and the host update agrees, and the RNG state and the
+    phases the checkpoint stores are the same"""
+    runs = []
+    for defer in (False, True):
+        sim = Simulation("turbulence", n=32, prop="turbulence", device=gpu)
+        sim.propagator.defer_host = defer
+        sim.run(3)
+        sim.propagator.finish_host(sim.d)
+        t = sim.propagator.turb
+        t._pull_device_phases()
+        runs.append((_sorted_state(sim, ["vx", "vy", "vz", "x"]), t.phases.copy(), t.rng.state_text(), sim.d.ttot))
+    (a, pa, ra, ta), (b, pb, rb, tb) = runs
+    assert ra == rb
+    assert math.isclose(ta, tb, rel_tol=1e-12)
+    assert np.allclose(pa, pb, rtol=1e-12, atol=1e-14)
+    for k in a:
+        assert float((a[k] - b[k]).abs().max()) <= 1e-6 * float(a[k].abs().max()), k
+
+
 @pytest.mark.slow
 def test_sedov_ci_accuracy(gpu, tmp_path):
     """sedov grid -n 50 (VE) L1 errors vs the self-similar solution, in the reference's comparison convention
