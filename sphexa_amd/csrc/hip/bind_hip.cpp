@@ -615,6 +615,22 @@ PYBIND11_MODULE(_sphx_hip, m)
           py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("xm1"), py::arg("ym1"), py::arg("zm1"), py::arg("ax"),
           py::arg("ay"), py::arg("az"), py::arg("h"), py::arg("temp"), py::arg("u"), py::arg("du"), py::arg("dum1"),
           py::arg("cv"), py::arg("box"), py::arg("stream"), py::arg("dtDev") = 0);
+    m.def("update_step",
+          [](int64_t first, int64_t last, double dt, double dtm1, Ptr x, Ptr y, Ptr z, Ptr vx, Ptr vy, Ptr vz,
+             Ptr xm1, Ptr ym1, Ptr zm1, Ptr ax, Ptr ay, Ptr az, Ptr h, Ptr temp, Ptr u, Ptr du, Ptr dum1, double cv,
+             const BoxArr& box, Ptr s, Ptr dtDev, unsigned ng0, Ptr nc, Ptr mm, Ptr cons, Ptr eg0, Ptr eg1)
+          {
+              PosArgs p{P<double>(x),  P<double>(y),  P<double>(z),  P<float>(vx), P<float>(vy), P<float>(vz),
+                        P<float>(xm1), P<float>(ym1), P<float>(zm1), P<float>(ax), P<float>(ay), P<float>(az),
+                        P<float>(h),   P<double>(temp), P<double>(u), P<double>(du), P<float>(dum1)};
+              updateStep(first, last, dt, dtm1, p, cv, toBox(box), St(s), P<double>(dtDev), ng0, P<int32_t>(nc),
+                         P<float>(h), P<float>(mm), P<double>(cons), P<double>(eg0), P<double>(eg1));
+          },
+          py::arg("first"), py::arg("last"), py::arg("dt"), py::arg("dtm1"), py::arg("x"), py::arg("y"), py::arg("z"),
+          py::arg("vx"), py::arg("vy"), py::arg("vz"), py::arg("xm1"), py::arg("ym1"), py::arg("zm1"), py::arg("ax"),
+          py::arg("ay"), py::arg("az"), py::arg("h"), py::arg("temp"), py::arg("u"), py::arg("du"), py::arg("dum1"),
+          py::arg("cv"), py::arg("box"), py::arg("stream"), py::arg("dtDev") = 0, py::arg("ng0") = 100,
+          py::arg("nc") = 0, py::arg("m") = 0, py::arg("cons") = 0, py::arg("eg0") = 0, py::arg("eg1") = 0);
     m.def("update_h", [](int64_t first, int64_t last, unsigned ng0, Ptr nc, Ptr h, Ptr s)
           { updateH(first, last, ng0, P<int32_t>(nc), P<float>(h), St(s)); });
     m.def("conserved_quantities",

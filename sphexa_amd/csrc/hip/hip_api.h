@@ -249,6 +249,10 @@ void momentumEnergyStd(const NbrArgs& a, const SphConsts& sc, const Box& box, in
 void updatePositions(int64_t first, int64_t last, double dt, double dt_m1, const PosArgs& p, double cv,
                      const Box& box, hipStream_t s, const double* dtDev = nullptr);
 void updateH(int64_t first, int64_t last, unsigned ng0, const int32_t* nc, float* h, hipStream_t s);
+//! updatePositions + updateH (+ conservedQuantities into cons when given, over the updated values) in one pass
+void updateStep(int64_t first, int64_t last, double dt, double dt_m1, const PosArgs& p, double cv, const Box& box,
+                hipStream_t s, const double* dtDev, unsigned ng0, const int32_t* nc, float* h, const float* m,
+                double* cons, const double* eg0, const double* eg1);
 void conservedQuantities(int64_t first, int64_t last, const double* x, const double* y, const double* z,
                          const float* vx, const float* vy, const float* vz, const float* m, const double* temp,
                          const double* u, const int32_t* nc, double cv, double* out, hipStream_t s,

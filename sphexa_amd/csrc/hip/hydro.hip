@@ -1036,6 +1036,120 @@ __global__ void updatePositionsKernel(int64_t first, int64_t last, double dt, do
     }
 }
 
+/*! @brief the end of a step in one pass (the separate updatePositionsKernel + updateHKernel + conservedKernel): the
+ *         position/velocity/energy update of updatePositionsKernel, the smoothing-length update of updateHKernel (the
+ *         fixed-boundary test reads the old h, as there) and, with cons, the conserved-quantity sums of conservedKernel
+ *         over the updated values (the fields the separate reduction would read after the step). Grid-stride, a block
+ *         reduction and 10 atomics per block. */
+template<bool kCons>
+__global__ __launch_bounds__(256) void updateStepKernel(int64_t first, int64_t last, double dt, double dt_m1, PosArgs p,
+                                                        double cv, Box box, const double* __restrict__ dtDev,
+                                                        unsigned ng0, const int32_t* __restrict__ nc,
+                                                        float* hOut, const float* __restrict__ m,
+                                                        double* __restrict__ cons, const double* __restrict__ eg0,
+                                                        const double* __restrict__ eg1)
+{
+    if (dtDev)
+    {
+        dt    = dtDev[0];
+        dt_m1 = dtDev[1];
+    }
+    const bool fbc[3] = {box.bc[0] == kFixed, box.bc[1] == kFixed, box.bc[2] == kFixed};
+    const bool anyFixed = fbc[0] || fbc[1] || fbc[2];
+    double q[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (kCons && blockIdx.x == 0 && threadIdx.x == 0) q[2] = (eg0 ? *eg0 : 0.0) + (eg1 ? *eg1 : 0.0);
+    for (int64_t i = first + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < last;
+         i += int64_t(gridDim.x) * blockDim.x)
+    {
+        const float hOld = p.h[i];
+        double X[3] = {p.x[i], p.y[i], p.z[i]};
+        float Vf[3];
+        bool frozen = false;
+        if (anyFixed)
+        {
+            Vf[0] = p.vx[i], Vf[1] = p.vy[i], Vf[2] = p.vz[i];
+            if (Vf[0] == 0.f && Vf[1] == 0.f && Vf[2] == 0.f)
+                for (int d = 0; d < 3; ++d)
+                    if (fbc[d] && (fabs(box.hi[d] - X[d]) < 2.0 * hOld || fabs(box.lo[d] - X[d]) < 2.0 * hOld))
+                        frozen = true;
+        }
+        if (!frozen)
+        {
+            const double dA  = dt + 0.5 * dt_m1;
+            const double dB  = 0.5 * (dt + dt_m1);
+            const double A[3]  = {p.ax[i], p.ay[i], p.az[i]};
+            const double Xm[3] = {p.xm1[i], p.ym1[i], p.zm1[i]};
+            double dX[3];
+            for (int d = 0; d < 3; ++d)
+            {
+                const double val = Xm[d] * (1.0 / dt_m1);
+                Vf[d]            = float(val + A[d] * dA);
+                dX[d]            = dt * val + A[d] * dB * dt;
+                X[d] += dX[d];
+            }
+            putInBox(X[0], X[1], X[2], box);
+            p.x[i]   = X[0];
+            p.y[i]   = X[1];
+            p.z[i]   = X[2];
+            p.xm1[i] = float(dX[0]);
+            p.ym1[i] = float(dX[1]);
+            p.zm1[i] = float(dX[2]);
+            p.vx[i]  = Vf[0];
+            p.vy[i]  = Vf[1];
+            p.vz[i]  = Vf[2];
+        }
+        double eNew = 0;
+        if (p.temp)
+        {
+            const double uOld = cv * p.temp[i];
+            const double tNew = energyUpdate(uOld, dt, dt_m1, p.du[i], p.dum1[i]) / cv;
+            p.temp[i]         = tNew;
+            p.dum1[i]         = float(p.du[i]);
+            eNew              = cv * tNew;
+        }
+        else if (p.u)
+        {
+            eNew      = energyUpdate(p.u[i], dt, dt_m1, p.du[i], p.dum1[i]);
+            p.u[i]    = eNew;
+            p.dum1[i] = float(p.du[i]);
+        }
+        const int32_t nci = nc[i];
+        hOut[i]           = sphx::updateH<float>(ng0, unsigned(nci), hOld);
+        if constexpr (kCons)
+        {
+            const double mi   = m[i];
+            const double V[3] = {Vf[0], Vf[1], Vf[2]};
+            q[0] += 0.5 * mi * (V[0] * V[0] + V[1] * V[1] + V[2] * V[2]);
+            q[1] += eNew * mi;
+            q[3] += mi * V[0];
+            q[4] += mi * V[1];
+            q[5] += mi * V[2];
+            q[6] += mi * (X[1] * V[2] - X[2] * V[1]);
+            q[7] += mi * (X[2] * V[0] - X[0] * V[2]);
+            q[8] += mi * (X[0] * V[1] - X[1] * V[0]);
+            q[9] += double(nci);
+        }
+    }
+    if constexpr (kCons)
+    {
+        __shared__ double red[4][10];
+        const int w = threadIdx.x >> 6;
+        for (int k = 0; k < 10; ++k)
+        {
+            const double v = waveSum(q[k]);
+            if ((threadIdx.x & 63) == 0) red[w][k] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < 10)
+        {
+            double s = 0;
+            for (int ww = 0; ww < int(blockDim.x >> 6); ++ww)
+                s += red[ww][threadIdx.x];
+            atomicAdd(&cons[threadIdx.x], s);
+        }
+    }
+}
+
 __global__ void updateHKernel(int64_t first, int64_t last, unsigned ng0, const int32_t* __restrict__ nc,
                               float* __restrict__ h)
 {
@@ -1361,6 +1475,28 @@ void updatePositions(int64_t first, int64_t last, double dt, double dt_m1, const
 {
     if (last <= first) return;
     updatePositionsKernel<<<gridFor(last - first, 256), 256, 0, s>>>(first, last, dt, dt_m1, p, cv, box, dtDev);
+    SPHX_LAUNCH_CHECK();
+}
+
+void updateStep(int64_t first, int64_t last, double dt, double dt_m1, const PosArgs& p, double cv, const Box& box,
+                hipStream_t s, const double* dtDev, unsigned ng0, const int32_t* nc, float* h, const float* m,
+                double* cons, const double* eg0, const double* eg1)
+{
+    if (cons) SPHX_CHECK(hipMemsetAsync(cons, 0, 10 * sizeof(double), s)); // the sums accumulate atomically
+    if (last <= first)
+    {
+        if (cons && (eg0 || eg1)) // (no particles: the gravity energy slot only)
+            updateStepKernel<true><<<1, 256, 0, s>>>(first, first, dt, dt_m1, p, cv, box, dtDev, ng0, nc, h, m, cons,
+                                                     eg0, eg1);
+        return;
+    }
+    const unsigned grid = std::max<unsigned>(1, std::min<unsigned>(gridFor(last - first, 256), 8192));
+    if (cons)
+        updateStepKernel<true><<<grid, 256, 0, s>>>(first, last, dt, dt_m1, p, cv, box, dtDev, ng0, nc, h, m, cons,
+                                                    eg0, eg1);
+    else
+        updateStepKernel<false><<<grid, 256, 0, s>>>(first, last, dt, dt_m1, p, cv, box, dtDev, ng0, nc, h, m,
+                                                     nullptr, nullptr, nullptr);
     SPHX_LAUNCH_CHECK();
 }
 

@@ -85,6 +85,17 @@ class DeferredConserved:
         self._ev.record()
         self.pending = True
 
+    def enqueue_sums(self, d, q, comm):
+        """as enqueue, with the rank's sums already formed on the device (Propagator.update_quantities)"""
+        comm.allreduce(q, SUM)
+        if self._host is None:
+            self._host = torch.empty(10, dtype=torch.float64, pin_memory=True)
+            self._ev = torch.cuda.Event()
+        self.finish(d)  # (a previous copy is collected before its buffer is reused)
+        self._host.copy_(q, non_blocking=True)
+        self._ev.record()
+        self.pending = True
+
     def finish(self, d):
         if not self.pending:
             return

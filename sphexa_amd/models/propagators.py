@@ -39,6 +39,9 @@ GRAVITY_STREAM_PRIORITY = int(os.environ.get("SPHX_GRAV_PRIORITY", "0"))
 # Off: measured Evrard -n 200 21.3-21.7 vs 20.9-21.5 ms, -n 100 3.61 vs 3.45 ms: the M2P's long waves then hold the
 # CU slots the search's unpredicted split groups need after the main kernel (a 5-ms tail at -n 200)
 GRAVITY_LISTS_FIRST = os.environ.get("SPHX_GRAV_LISTS_FIRST", "0") == "1"
+# GPU with deferred host values: the position/energy/h update and the conserved-quantity sums of observe() in one
+# native pass (ops/hydro.py update_step, hydro.hip updateStepKernel); 0: three launches
+FUSED_UPDATE = os.environ.get("SPHX_FUSED_UPDATE", "1") == "1"
 from ..utils.timer import Timer
 
 # XMass (STD: density) computed inside the GPU neighbor search instead of a separate pass over the lists. Off by
@@ -65,6 +68,7 @@ class Propagator:
         self.gravity = None
         self._host_pending = None
         self._observed = None
+        self._cons_fused = None
 
     # --------------------------------------------------------------------------------------------- interface
     def conserved_fields(self) -> List[str]:
@@ -329,6 +333,34 @@ class Propagator:
         if self._observed is not None:
             self._observed.finish(d)
 
+    def _egrav_device(self, d):
+        """the rank's gravitational energy for a device reduction: a list of float64 device scalars (the pending
+        gravity evaluations' energies, or the host value uploaded), or None when pending evaluations mix host and
+        device energies (observe() then collects them first)"""
+        grav = self.gravity
+        pend = list(getattr(grav, "pending", None) or [])
+        if pend:
+            return None if grav._host_energy else [p.energy_dev() for p in pend]
+        e = float(getattr(d, "egrav_local", 0.0))
+        if e == 0.0:
+            return []
+        return [torch.tensor([e], dtype=torch.float64).pin_memory().to(d.device, non_blocking=True)]
+
+    def update_quantities(self, domain, d):
+        """positions, velocities, energy and h of the owned particles (reference updateQuantities). GPU with deferred
+        host values: one native pass that also forms this step's conserved-quantity sums, which observe() then only
+        reduces over ranks (hydro.hip updateStepKernel)"""
+        first, last = domain.start_index(), domain.end_index()
+        self._cons_fused = None
+        if d.device.type == "cuda" and self.defer_host and FUSED_UPDATE:
+            eg = self._egrav_device(d)
+            cons = torch.empty(10, dtype=torch.float64, device=d.device) if eg is not None else None
+            H.update_step(d, first, last, domain.box, cons, eg or ())
+            self._cons_fused = cons
+            return
+        H.compute_positions(d, first, last, domain.box)
+        H.update_smoothing_length(d, first, last)
+
     def observe(self, domain, d):
         """the per-iteration conserved quantities of the time loop (reference sphexa.cpp:150: energies, momenta and
         the neighbor sum, globally reduced). With defer_host on the GPU the reduction is enqueued and its host copy is
@@ -341,6 +373,11 @@ class Propagator:
         if d.device.type == "cuda" and self.defer_host:
             if self._observed is None:
                 self._observed = DeferredConserved()
+            cons, self._cons_fused = self._cons_fused, None
+            if cons is not None:
+                # the sums were formed by the step's update pass (update_quantities): reduce and copy only
+                self._observed.enqueue_sums(d, cons, domain.comm)
+                return
             # the gravity energy of this step is still on the device (GravityPending): the kernel reads it there
             grav = self.gravity
             pend = list(getattr(grav, "pending", None) or [])
@@ -499,8 +536,7 @@ class HydroVeProp(Propagator):
         first, last = domain.start_index(), domain.end_index()
         self.compute_timestep(domain, d)
         self.timer.step("Timestep")
-        H.compute_positions(d, first, last, domain.box)
-        H.update_smoothing_length(d, first, last)
+        self.update_quantities(domain, d)
         self.timer.step("UpdateQuantities")
         self.timer.stop()
 
@@ -575,8 +611,7 @@ class HydroProp(Propagator):
         first, last = domain.start_index(), domain.end_index()
         self.compute_timestep(domain, d)
         self.timer.step("Timestep")
-        H.compute_positions(d, first, last, domain.box)
-        H.update_smoothing_length(d, first, last)
+        self.update_quantities(domain, d)
         self.timer.step("UpdateQuantities")
         self.timer.stop()
 

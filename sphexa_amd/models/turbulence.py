@@ -225,8 +225,6 @@ class TurbVeProp(HydroVeProp):
             self.turb = TurbulenceData(settings, self.out is not None)
 
     def step(self, domain, d):
-        from ..ops import hydro as H
-
         self.compute_forces(domain, d)
         first, last = domain.start_index(), domain.end_index()
         self.compute_timestep(domain, d)
@@ -237,8 +235,7 @@ class TurbVeProp(HydroVeProp):
         else:
             self.turb.drive(d, first, last, d.minDt)
         self.timer.step("Turbulence Stirring")
-        H.compute_positions(d, first, last, domain.box)
-        H.update_smoothing_length(d, first, last)
+        self.update_quantities(domain, d)
         self.timer.step("UpdateQuantities")
         self.timer.stop()
 

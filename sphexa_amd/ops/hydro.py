@@ -620,6 +620,27 @@ def compute_positions(d, first: int, last: int, box: Box):
         _lib.cpu().update_positions(*args)
 
 
+def update_step(d, first: int, last: int, box: Box, cons: torch.Tensor | None = None, egrav_dev=()):
+    """GPU: compute_positions + update_smoothing_length in one native pass (hydro.hip updateStepKernel); with
+    ``cons`` (float64 (10,) device tensor) also the rank's conserved-quantity sums of models/observables.py over the
+    updated fields, the gravitational energy read from ``egrav_dev`` (<= 2 float64 device scalars)"""
+    from .hydro_consts import ideal_gas_cv
+
+    temp = d["temp"] if d.is_allocated("temp") else None
+    u = d["u"] if (temp is None and d.is_allocated("u")) else None
+    cv = ideal_gas_cv(d.muiConst, d.gamma)
+    dt_dev = getattr(d, "_dt_dev", None)
+    eg = [t.data_ptr() for t in egrav_dev] + [0, 0]
+    _lib.hip().update_step(first, last, float(d.minDt), float(d.minDt_m1), d["x"].data_ptr(), d["y"].data_ptr(),
+                           d["z"].data_ptr(), d["vx"].data_ptr(), d["vy"].data_ptr(), d["vz"].data_ptr(),
+                           d["x_m1"].data_ptr(), d["y_m1"].data_ptr(), d["z_m1"].data_ptr(), d["ax"].data_ptr(),
+                           d["ay"].data_ptr(), d["az"].data_ptr(), d["h"].data_ptr(), _p(temp), _p(u),
+                           d["du"].data_ptr(), d["du_m1"].data_ptr(), cv, box.to_array(), _stream(),
+                           dtDev=0 if dt_dev is None else dt_dev.data_ptr(), ng0=int(d.ng0), nc=d["nc"].data_ptr(),
+                           m=d["m"].data_ptr(), cons=_p(cons), eg0=eg[0], eg1=eg[1])
+    invalidate_h_cache(d)
+
+
 def update_smoothing_length(d, first: int, last: int):
     args = (first, last, int(d.ng0), d["nc"].data_ptr(), d["h"].data_ptr())
     if _is_gpu(d):

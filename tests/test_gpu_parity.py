@@ -414,3 +414,29 @@ def test_ve_step_momentum_handoff_identical(gpu, monkeypatch, n):
                                                          "az", "alpha")})
     for f in results[0]:
         assert torch.equal(results[0][f], results[1][f]), f
+
+
+@pytest.mark.parametrize("case", ["sedov", "evrard"])
+def test_fused_update_matches_separate_passes(gpu, monkeypatch, case):
+    """the end of a deferred GPU step in one pass (hydro.hip updateStepKernel: positions, energy, h and the
+    conserved-quantity sums) against the three separate launches: fields bit-identical, conserved sums to fp64
+    summation order"""
+    from sphexa_amd.app.simulation import Simulation
+    from sphexa_amd.models import propagators as PR
+
+    out = []
+    for fused in (False, True):
+        monkeypatch.setattr(PR, "FUSED_UPDATE", fused)
+        sim = Simulation(case, n=20, prop="ve", device=gpu)
+        sim.propagator.defer_host = True
+        sim.run(3)
+        sim.propagator.finish_host(sim.d)
+        d = sim.d
+        out.append(({f: sim.local(f).clone().cpu() for f in ("x", "y", "z", "vx", "vy", "vz", "h", "temp")},
+                    (d.ecin, d.eint, d.egrav, d.linmom, d.angmom, d.totalNeighbors)))
+    (fa, ca), (fb, cb) = out
+    for f in fa:
+        assert torch.equal(fa[f], fb[f]), f
+    assert ca[5] == cb[5]
+    for a, b in zip(ca[:5], cb[:5]):
+        assert math.isclose(a, b, rel_tol=1e-12, abs_tol=1e-14), (ca, cb)
