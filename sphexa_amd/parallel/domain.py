@@ -82,7 +82,11 @@ DEVICE_BOX = os.environ.get("SPHX_DEVICE_BOX", "1") == "1"
 # ranks up to which the global-tree step gathers every rank's leaf counts (size x leaves int64, ~100 leaves per rank):
 # the migration counts then come from the same host copy (Domain._distribute)
 GATHER_COUNTS_MAX_RANKS = int(os.environ.get("SPHX_GATHER_COUNTS_MAX_RANKS", "32"))
-REORDER_ALL_BYTES = 1 << 30  # below this transient size all remaining fields are reordered together
+# below this transient size (new buffers of every remaining field) all remaining fields are reordered together: one
+# launch per element size, the permutation read once. The sync's transient stays under the step's peak (the IAD loop):
+# Sedov -n 400 (4.6 GB) 113.4 / 113.2 -> 112.8 / 112.8 ms per step at an unchanged 35.4 GiB peak
+# (profiles/r6/reorder_batch.md). SPHX_REORDER_ALL_GB overrides (1: the round-5 batches of 3 fields)
+REORDER_ALL_BYTES = int(float(os.environ.get("SPHX_REORDER_ALL_GB", "32")) * (1 << 30))
 
 
 class HaloOwnershipError(RuntimeError):
