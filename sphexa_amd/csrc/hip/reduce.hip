@@ -9,6 +9,7 @@
  * torch's per-field min/max/aminmax/stack/cat cost ~15 launches per query.
  */
 #include <cfloat>
+#include <limits>
 
 #include "common.h"
 #include "hip_api.h"
@@ -19,7 +20,9 @@ namespace sphx::hip
 namespace
 {
 constexpr int kRedBlock  = 256;
-constexpr int kRedBlocks = 512;
+// 2048 blocks (8 per CU, 32 waves) and 16-byte loads: the reductions are streaming reads (Sedov -n 400: h and m,
+// 512 MB, 536 -> ~90 us with 512 blocks of scalar fp64-converted loads, profiles/r6/reductions.md)
+constexpr int kRedBlocks = 2048;
 
 struct Fields4
 {
@@ -36,6 +39,58 @@ __device__ __forceinline__ double nanMax(double a, double b) { return a != a ? a
 __device__ __forceinline__ double loadAs(const void* p, int isD, int64_t i)
 {
     return isD ? static_cast<const double*>(p)[i] : double(static_cast<const float*>(p)[i]);
+}
+
+__device__ __forceinline__ float nanMinF(float a, float b) { return a != a ? a : (b != b ? b : fminf(a, b)); }
+__device__ __forceinline__ float nanMaxF(float a, float b) { return a != a ? a : (b != b ? b : fmaxf(a, b)); }
+
+//! @brief this thread's share of min/max over p[0, n) (grid-stride): 16-byte loads when p is 16-B aligned, the
+//!        float comparisons in fp32 (exact: the conversion to double is monotone)
+template<class T>
+__device__ __forceinline__ void minMaxShare(const T* __restrict__ p, int64_t n, double& lo, double& hi)
+{
+    constexpr int V = 16 / sizeof(T);
+    const int64_t t0 = int64_t(blockIdx.x) * kRedBlock + threadIdx.x, stride = int64_t(gridDim.x) * kRedBlock;
+    int64_t nv = (reinterpret_cast<uintptr_t>(p) & 15) == 0 ? n / V : 0;
+    T l = std::numeric_limits<T>::max(), h = -std::numeric_limits<T>::max();
+    if constexpr (V == 4)
+    {
+        const float4* p4 = reinterpret_cast<const float4*>(p);
+#pragma unroll 2
+        for (int64_t j = t0; j < nv; j += stride)
+        {
+            const float4 v = p4[j];
+            l = nanMinF(nanMinF(l, v.x), nanMinF(nanMinF(v.y, v.z), v.w));
+            h = nanMaxF(nanMaxF(h, v.x), nanMaxF(nanMaxF(v.y, v.z), v.w));
+        }
+    }
+    else
+    {
+        const double2* p2 = reinterpret_cast<const double2*>(p);
+#pragma unroll 2
+        for (int64_t j = t0; j < nv; j += stride)
+        {
+            const double2 v = p2[j];
+            l = nanMin(l, nanMin(v.x, v.y));
+            h = nanMax(h, nanMax(v.x, v.y));
+        }
+    }
+    for (int64_t i = nv * V + t0; i < n; i += stride)
+    {
+        const T v = p[i];
+        if constexpr (V == 4)
+        {
+            l = nanMinF(l, v);
+            h = nanMaxF(h, v);
+        }
+        else
+        {
+            l = nanMin(l, v);
+            h = nanMax(h, v);
+        }
+    }
+    lo = nanMin(lo, double(l));
+    hi = nanMax(hi, double(h));
 }
 
 //! block min of v over the block's threads (kRedBlock)
@@ -62,12 +117,8 @@ __global__ __launch_bounds__(kRedBlock) void multiMinMaxKernel(int64_t n, Fields
     for (int k = 0; k < f.count; ++k)
     {
         double lo = DBL_MAX, hi = -DBL_MAX;
-        for (int64_t i = int64_t(blockIdx.x) * kRedBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kRedBlock)
-        {
-            const double v = loadAs(f.p[k], f.isDouble[k], i);
-            lo             = nanMin(lo, v);
-            hi             = nanMax(hi, v);
-        }
+        if (f.isDouble[k]) minMaxShare(static_cast<const double*>(f.p[k]), n, lo, hi);
+        else minMaxShare(static_cast<const float*>(f.p[k]), n, lo, hi);
         lo = blockReduce(lo, red, mn);
         hi = blockReduce(hi, red, mx);
         if (threadIdx.x == 0)
@@ -114,8 +165,34 @@ __global__ __launch_bounds__(kRedBlock) void maxNorm2Kernel(int64_t first, int64
     __shared__ double red[kRedBlock / 64];
     auto mx = [](double a, double b) { return nanMax(a, b); };
     double m = 0.0, fm = -DBL_MAX;
-    for (int64_t i = first + int64_t(blockIdx.x) * kRedBlock + threadIdx.x; i < last;
-         i += int64_t(gridDim.x) * kRedBlock)
+    const int64_t t0 = int64_t(blockIdx.x) * kRedBlock + threadIdx.x, stride = int64_t(gridDim.x) * kRedBlock;
+    auto al = [&](const float* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q + first) & 15) == 0; };
+    const int64_t nv = (al(ax) && al(ay) && al(az) && al(f)) ? (last - first) / 4 : 0;
+    // 16-byte loads over the aligned part (|a|^2 in fp64 per element as below, the field max in fp32: exact)
+    float fmF = -FLT_MAX;
+    for (int64_t j = t0; j < nv; j += stride)
+    {
+        if (ax)
+        {
+            const float4 x = reinterpret_cast<const float4*>(ax + first)[j];
+            const float4 y = reinterpret_cast<const float4*>(ay + first)[j];
+            const float4 z = reinterpret_cast<const float4*>(az + first)[j];
+            const float xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w}, zs[4] = {z.x, z.y, z.z, z.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+            {
+                const double a = xs[u], b = ys[u], c = zs[u];
+                m              = nanMax(m, a * a + b * b + c * c);
+            }
+        }
+        if (f)
+        {
+            const float4 v = reinterpret_cast<const float4*>(f + first)[j];
+            fmF = nanMaxF(nanMaxF(fmF, v.x), nanMaxF(nanMaxF(v.y, v.z), v.w));
+        }
+    }
+    if (f) fm = nanMax(fm, double(fmF));
+    for (int64_t i = first + 4 * nv + t0; i < last; i += stride)
     {
         if (ax)
         {

@@ -26,6 +26,23 @@ def test_min_max_and_norm(gpu, n):
     assert R.max_norm2(ax, ay, az, first, last).item() == pytest.approx(ref.item(), rel=1e-15)
 
 
+@pytest.mark.parametrize("off", [0, 1, 3, 5])
+def test_min_max_vector_loads_any_alignment(gpu, off):
+    """the 16-byte load path of the reductions (aligned share + scalar tail, or scalar when the slice is not 16-B
+    aligned): slices starting at every alignment, extremes planted in the tail and the head"""
+    n = 1_000_003
+    g = torch.Generator(device="cpu").manual_seed(off)
+    a = torch.randn(n + off, generator=g, dtype=torch.float64).to(gpu)
+    b = torch.randn(n + off, generator=g).to(gpu)
+    a[-1], b[off] = 1e6, -1e6
+    av, bv = a[off:], b[off:]
+    out = R.min_max([av, bv]).cpu().tolist()
+    assert out == [av.min().item(), av.max().item(), float(bv.min()), float(bv.max())]
+    f = torch.randn(n + off, generator=g).to(gpu)
+    f[n + off - 2] = 7e5
+    assert R.field_max(f, off, n + off).item() == pytest.approx(float(f[off:].max()), rel=0)
+
+
 @pytest.mark.parametrize("grav,dev_inputs,n", [(True, True, 200_001), (False, True, 5000), (True, False, 777),
                                                (False, False, 1)])
 def test_timestep_kernel(gpu, grav, dev_inputs, n):
