@@ -366,19 +366,21 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("ve_def_gradh",
           [](int64_t first, int64_t last, const ConstArr& c, const BoxArr& box, Ptr nidx, Ptr nc, Ptr x, Ptr y, Ptr z,
              Ptr h, Ptr mm, Ptr wh, Ptr whd, Ptr xm, Ptr kx, Ptr gradh, int64_t ntot, Ptr rec, Ptr s, double mUniform,
-             int inDone, Ptr out, Ptr vx, Ptr vy, Ptr vz)
+             int inDone, Ptr out, Ptr vx, Ptr vy, Ptr vz, Ptr eosTemp, Ptr eosPrho, Ptr eosC, Ptr eosRho, Ptr eosP)
           {
               auto sc = toConsts(c);
               veDefGradh(nbr(first, last, nidx, nc, sc), sc, toBox(box), ntot, P<double>(x), P<double>(y),
                          P<double>(z), P<float>(h), P<float>(mm), P<float>(wh), P<float>(whd), P<float>(xm),
                          P<void>(rec), P<float>(kx), P<float>(gradh), float(mUniform), St(s), inDone, P<void>(out),
-                         P<float>(vx), P<float>(vy), P<float>(vz));
+                         P<float>(vx), P<float>(vy), P<float>(vz), P<double>(eosTemp), P<float>(eosPrho),
+                         P<float>(eosC), P<float>(eosRho), P<float>(eosP));
           },
           py::arg("first"), py::arg("last"), py::arg("c"), py::arg("box"), py::arg("nidx"), py::arg("nc"),
           py::arg("x"), py::arg("y"), py::arg("z"), py::arg("h"), py::arg("mm"), py::arg("wh"), py::arg("whd"),
           py::arg("xm"), py::arg("kx"), py::arg("gradh"), py::arg("ntot"), py::arg("rec"), py::arg("s"),
           py::arg("mUniform"), py::arg("inDone") = 0, py::arg("out") = 0, py::arg("vx") = 0, py::arg("vy") = 0,
-          py::arg("vz") = 0);
+          py::arg("vz") = 0, py::arg("eosTemp") = 0, py::arg("eosPrho") = 0, py::arg("eosC") = 0,
+          py::arg("eosRho") = 0, py::arg("eosP") = 0);
     m.def("set_staged", [](unsigned mask) { setStaged(mask); },
           "pair loops that run LDS-staged: bit 0 XMass, 1 Gradh, 2 IAD, 3 AV, 4 momentum (hydro.hip, staged.h)");
     m.def("staged_mask", []() { return stagedMask(); });

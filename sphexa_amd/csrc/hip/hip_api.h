@@ -219,7 +219,8 @@ void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                 const double* y, const double* z, const float* h, const float* m, const float* wh, const float* whd,
                 const float* xm, void* rec, float* kx, float* gradh, float mUniform, hipStream_t s, int inDone = 0,
                 void* iadOut = nullptr, const float* vx = nullptr, const float* vy = nullptr,
-                const float* vz = nullptr);
+                const float* vz = nullptr, const double* eosTemp = nullptr, float* eosPrho = nullptr,
+                float* eosC = nullptr, float* eosRho = nullptr, float* eosP = nullptr);
 void eosPolytropic(int64_t first, int64_t last, const float* kx, const float* xm, const float* m, float* p, float* c,
                    hipStream_t s);
 void eosVe(int64_t first, int64_t last, const SphConsts& sc, const double* temp, const float* m, const float* kx,

@@ -532,6 +532,13 @@ __global__ __launch_bounds__(64 * W) void xmassQStagedKernel(NbrArgs a, SphConst
 #define SPHX_ST_XMASS_U 1024
 #endif
 
+//! VE equation of state fused into the Gradh loop's epilogue (eosVeKernel per target; temp == nullptr: not fused)
+struct EosOut
+{
+    const double* temp = nullptr;
+    float *prho = nullptr, *c = nullptr, *rho = nullptr, *p = nullptr;
+};
+
 template<class R, class G, int B = kBlock>
 __global__ __launch_bounds__(B) void veDefGradhKernel(NbrArgs a, SphConsts sc, G box,
                                                            const float* __restrict__ h, const R* __restrict__ rec,
@@ -539,7 +546,7 @@ __global__ __launch_bounds__(B) void veDefGradhKernel(NbrArgs a, SphConsts sc, G
                                                            float* __restrict__ kx, float* __restrict__ gradh,
                                                            float mUniform, const float* __restrict__ vx,
                                                            const float* __restrict__ vy, const float* __restrict__ vz,
-                                                           SrcIadQ* __restrict__ iadOut)
+                                                           SrcIadQ* __restrict__ iadOut, EosOut eos = EosOut{})
 {
     __shared__ float4 tile[B / 64 * 64 * CoopLoader<R>::S];
     int64_t i;
@@ -559,6 +566,18 @@ __global__ __launch_bounds__(B) void veDefGradhKernel(NbrArgs a, SphConsts sc, G
             // the IAD loop's record of this target: vol = xm / kx (as packIadQKernel)
             const SrcXmQ pi = rec[i];
             iadOut[i]       = SrcIadQ{pi.x, pi.y, pi.z, pi.xm / k, vx[i], vy[i], vz[i], pi.xm};
+        }
+        if (eos.temp)
+        {
+            // eosVeKernel for this target (m uniform, xm from its own record)
+            const float xmi   = rec[i].xm;
+            const double rhoi = double(k) * mUniform / xmi;
+            double pi, ci;
+            idealGasEOS(eos.temp[i], rhoi, sc.muiConst, sc.gamma, pi, ci);
+            eos.prho[i] = float(pi / (double(k) * mUniform * mUniform * g));
+            eos.c[i]    = float(ci);
+            if (eos.rho) eos.rho[i] = float(rhoi);
+            if (eos.p) eos.p[i] = float(pi);
         }
     }
 }
@@ -1248,11 +1267,13 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
 void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, const double* x,
                 const double* y, const double* z, const float* h, const float* m, const float* wh, const float* whd,
                 const float* xm, void* rec, float* kx, float* gradh, float mUniform, hipStream_t s, int inDone,
-                void* iadOut, const float* vx, const float* vy, const float* vz)
+                void* iadOut, const float* vx, const float* vy, const float* vz, const double* eosTemp,
+                float* eosPrho, float* eosC, float* eosRho, float* eosP)
 {
     if (a.last <= a.first) return;
     if (mUniform > 0.f && sc.fixedPoint)
     {
+        const EosOut eos{eosTemp, eosPrho, eosC, eosRho, eosP};
         const QFrame q = qframeOf(box, sc.fixedPoint);
         packRanges(inDone, a, ntot, [&](int64_t lo, int64_t hi)
                    { packXmQKernel<<<gridFor(hi - lo, 256), 256, 0, s>>>(lo, hi, x, y, z, xm, q, (SrcXmQ*)rec); });
@@ -1261,7 +1282,7 @@ void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
                           constexpr int B = decltype(bc)::value;
                           veDefGradhKernel<SrcXmQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
                               withTot(a, ntot), sc, q, h, (const SrcXmQ*)rec, wh, whd, kx, gradh, mUniform, vx, vy, vz,
-                              (SrcIadQ*)iadOut);
+                              (SrcIadQ*)iadOut, eos);
                       }, 1);
     }
     else
@@ -1269,6 +1290,8 @@ void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
         packPosKernel<<<gridFor(ntot, 256), 256, 0, s>>>(ntot, x, y, z, m, xm, (SrcPos*)rec);
         veDefGradhKernel<<<gridT(a), kBlock, 0, s>>>(withTot(a, ntot), sc, box, h, (const SrcPos*)rec, wh, whd, kx,
                                                      gradh, 0.f, vx, vy, vz, nullptr);
+        SPHX_LAUNCH_CHECK();
+        if (eosTemp) eosVe(a.first, a.last, sc, eosTemp, m, kx, xm, gradh, eosPrho, eosC, eosRho, eosP, s);
     }
     SPHX_LAUNCH_CHECK();
 }

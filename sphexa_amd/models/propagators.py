@@ -42,6 +42,8 @@ GRAVITY_LISTS_FIRST = os.environ.get("SPHX_GRAV_LISTS_FIRST", "0") == "1"
 # GPU with deferred host values: the position/energy/h update and the conserved-quantity sums of observe() in one
 # native pass (ops/hydro.py update_step, hydro.hip updateStepKernel); 0: three launches
 FUSED_UPDATE = os.environ.get("SPHX_FUSED_UPDATE", "1") == "1"
+# the VE equation of state in the Gradh loop's epilogue (GPU fixed-point path; ops/hydro.py compute_ve_def_gradh)
+FUSED_EOS = os.environ.get("SPHX_FUSED_EOS", "1") == "1"
 from ..utils.timer import Timer
 
 # XMass (STD: density) computed inside the GPU neighbor search instead of a separate pass over the lists. Off by
@@ -467,15 +469,16 @@ class HydroVeProp(Propagator):
         chain = domain.size == 1 and d.device.type == "cuda"
 
         def gradh(d, nl, box):
+            """Gradh and (fused into its epilogue where the GPU path supports it, else after it) the EOS"""
             if d.is_allocated("ay"):
                 d.release("ay")
                 d.acquire("gradh")
-            H.compute_ve_def_gradh(d, nl, box)
+            if not H.compute_ve_def_gradh(d, nl, box, eos=FUSED_EOS):
+                H.compute_eos_ve(d, first, last)
 
         def first_loops(d, nl, box):
             H.compute_xmass(d, nl, box)
             gradh(d, nl, box)
-            H.compute_eos_ve(d, first, last)
 
         done = self._neighbors(domain, d, first_loop=first_loops if chain else H.compute_xmass, after_launch=prep)
         t.step("FindNeighbors")
@@ -494,8 +497,6 @@ class HydroVeProp(Propagator):
         if redo:
             gradh(d, nl, box)
         t.step("Normalization & Gradh")
-        if redo:
-            H.compute_eos_ve(d, first, last)
         t.step("EquationOfState")
         domain.exchange_halos(d, ["prho", "c", "kx"])
         domain.exchange_halos_finish(vel_halos)

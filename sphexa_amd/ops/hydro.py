@@ -417,7 +417,10 @@ def uniform_mass(d) -> float:
     return val
 
 
-def compute_ve_def_gradh(d, nl: NeighborList, box: Box):
+def compute_ve_def_gradh(d, nl: NeighborList, box: Box, eos: bool = False) -> bool:
+    """kx and gradh. ``eos``: also the VE equation of state of the targets (compute_eos_ve) in the same kernel where
+    the loop supports it (GPU fixed-point uniform-mass path: the Gradh epilogue); returns True if it did, the caller
+    runs compute_eos_ve otherwise"""
     nidx, nc = _nl_args(nl, d)
     args = (nl.first, nl.last, _consts(d, box), box.to_array(), nidx, nc, d["x"].data_ptr(), d["y"].data_ptr(),
             d["z"].data_ptr(), d["h"].data_ptr(), d["m"].data_ptr(), d.wh.data_ptr(), d.whd.data_ptr(),
@@ -431,13 +434,19 @@ def compute_ve_def_gradh(d, nl: NeighborList, box: Box):
             done = 1 if handoff_take(d, "xmq_own") else 0
             ho.clear()
             w0 = _rec(d, 0, "iadq").data_ptr()
+            ek = {}
+            if eos:
+                ek = dict(eosTemp=d["temp"].data_ptr(), eosPrho=d["prho"].data_ptr(), eosC=d["c"].data_ptr(),
+                          eosRho=_p(d["rho"] if d.is_allocated("rho") else None),
+                          eosP=_p(d["p"] if d.is_allocated("p") else None))
             _lib.hip().ve_def_gradh(*args, d.size, _recB(d).data_ptr(), _stream(), mu, inDone=done, out=w0,
-                                    vx=d["vx"].data_ptr(), vy=d["vy"].data_ptr(), vz=d["vz"].data_ptr())
+                                    vx=d["vx"].data_ptr(), vy=d["vy"].data_ptr(), vz=d["vz"].data_ptr(), **ek)
             handoff_mark(d, "iadq_own")
-        else:
-            _lib.hip().ve_def_gradh(*args, *_gpu_tail(d, "gradh"), mu)
+            return eos
+        _lib.hip().ve_def_gradh(*args, *_gpu_tail(d, "gradh"), mu)
     else:
         _lib.cpu().ve_def_gradh(*args)
+    return False
 
 
 def compute_eos_ve(d, first: int, last: int):

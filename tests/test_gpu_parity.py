@@ -440,3 +440,25 @@ def test_fused_update_matches_separate_passes(gpu, monkeypatch, case):
     assert ca[5] == cb[5]
     for a, b in zip(ca[:5], cb[:5]):
         assert math.isclose(a, b, rel_tol=1e-12, abs_tol=1e-14), (ca, cb)
+
+
+def test_fused_eos_identical(gpu, monkeypatch):
+    """the VE EOS in the Gradh loop's epilogue (hydro.hip veDefGradhKernel, EosOut) equals the separate eosVeKernel:
+    fields after three steps bit-identical"""
+    from sphexa_amd.models import propagators as PR
+
+    out = []
+    for fused in (False, True):
+        monkeypatch.setattr(PR, "FUSED_EOS", fused)
+        d = P.ParticlesData(gpu)
+        prop = HydroVeProp(None, 0)
+        prop.activate_fields(d)
+        box = SedovGrid().init(0, 1, 20, d)
+        dom = Domain(Comm(), box)
+        prop.sync(dom, d)
+        for _ in range(3):
+            prop.step(dom, d)
+            d.iteration += 1
+        out.append({f: d[f].clone().cpu() for f in ("x", "vx", "temp", "c", "prho", "du", "ax")})
+    for f in out[0]:
+        assert torch.equal(out[0][f], out[1][f]), f
