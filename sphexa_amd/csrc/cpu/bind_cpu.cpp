@@ -10,6 +10,7 @@
 #include <pybind11/stl.h>
 
 #include "cpu_api.hpp"
+#include "sphx/hilbert_fsm.hpp"
 
 namespace py = pybind11;
 using namespace sphx;
@@ -152,6 +153,31 @@ PYBIND11_MODULE(_sphx_cpu, m)
                   sfcDecode(kind, k[i], u, v, w);
                   a[i] = int32_t(u), b[i] = int32_t(v), c[i] = int32_t(w);
               }
+          });
+
+    m.def("hilbert_fsm_check",
+          [](int64_t n, uint64_t seed)
+          {
+              // (states, mismatches of the table walk against hilbertKey over n hashed points and the grid corners)
+              const HilbertFsm f = buildHilbertFsm();
+              int64_t bad        = 0;
+              const uint32_t M   = kGridMax - 1;
+              const uint32_t corners[3] = {0u, M / 2u, M};
+              for (uint32_t a : corners)
+                  for (uint32_t b : corners)
+                      for (uint32_t c : corners)
+                          bad += hilbertKeyFsm(f, a, b, c) != hilbertKey(a, b, c);
+#pragma omp parallel for reduction(+ : bad) schedule(static)
+              for (int64_t i = 0; i < n; ++i)
+              {
+                  uint64_t h = (uint64_t(i) + 1) * 0x9E3779B97F4A7C15ull ^ seed;
+                  h ^= h >> 31;
+                  h *= 0xBF58476D1CE4E5B9ull;
+                  h ^= h >> 29;
+                  const uint32_t x = uint32_t(h) & M, y = uint32_t(h >> 21) & M, z = uint32_t(h >> 42) & M;
+                  bad += hilbertKeyFsm(f, x, y, z) != hilbertKey(x, y, z);
+              }
+              return py::make_tuple(f.nStates, bad);
           });
 
     m.def("sort_keys", [](int64_t n, Ptr keys, Ptr perm) { cpu::sortKeys(n, P<KeyT>(keys), P<int32_t>(perm)); });

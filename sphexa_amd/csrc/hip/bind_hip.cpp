@@ -108,6 +108,9 @@ PYBIND11_MODULE(_sphx_hip, m)
     // ---------------------------------------------------------------------------------------------- sfc / sort
     m.def("compute_keys", [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, int kind, Ptr keys, Ptr s)
           { computeKeys(n, P<double>(x), P<double>(y), P<double>(z), toBox(box), kind, P<KeyT>(keys), St(s)); });
+    m.def("compute_keys_serial", [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, int kind, Ptr keys, Ptr s)
+          { computeKeysSerial(n, P<double>(x), P<double>(y), P<double>(z), toBox(box), kind, P<KeyT>(keys), St(s)); });
+    m.def("hilbert_table_states", []() { return hilbertTableStates(); });
     m.def("compute_keys_devbox",
           [](int64_t n, Ptr x, Ptr y, Ptr z, const BoxArr& box, Ptr ext, int kind, Ptr keys, Ptr s, int layout)
           {

@@ -45,6 +45,11 @@ struct PosArgs
 // sfc_sort.hip
 void computeKeys(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind, KeyT* keys,
                  hipStream_t s);
+//! the bit-serial reference form of computeKeys (sfc.hpp hilbertKey; computeKeys walks a table: identical keys)
+void computeKeysSerial(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind,
+                       KeyT* keys, hipStream_t s);
+//! states of the Hilbert key table (built on first use; a consistency failure throws)
+int hilbertTableStates();
 void computeKeysDevBox(int64_t n, const double* x, const double* y, const double* z, const Box& box, const double* ext,
                        int kind, KeyT* keys, hipStream_t s, int layout = 0);
 size_t sortPairsTempBytes(int64_t n);

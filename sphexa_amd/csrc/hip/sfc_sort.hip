@@ -6,54 +6,153 @@
  * keys against ~2.2 ms: scripts/micro_bench.py; no library sort is built).
  */
 
+#include <mutex>
+
 #include "common.h"
 #include "hip_api.h"
 #include "sphx/box.hpp"
+#include "sphx/hilbert_fsm.hpp"
 
 namespace sphx::hip
 {
 
-__global__ void computeKeysKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
-                                  const double* __restrict__ z, Box box, int kind, KeyT* __restrict__ keys)
+/* Hilbert keys by table (gfx950). The bit-serial transform of sfc.hpp hilbertKey (~20 conditional XOR rounds, a Gray
+ * code pass and three 64-bit bit spreads per key) made the key kernel compute-bound: 0.88 ms for 64 M keys, 3.4x its
+ * memory time. The same curve as a finite-state machine: a cell's orientation (state) maps the octant of each child to
+ * its key digit and to the child's state. The machine is derived once on the host from hilbertKey itself (the
+ * octant -> digit permutation of a cell identifies its state; every transition is checked against hilbertKey on a
+ * second cell of the same state), and the kernel walks it two levels per step from a table in LDS: 11 lookups per key.
+ * Keys are identical to hilbertKey (tests/test_gpu_parity.py::test_keys_and_sort, test_hilbert_table_keys). */
+constexpr int kHMaxStates = 64;
+
+//! device copies of the tables (built and uploaded on first use; never freed)
+struct HilbertLutDev
+{
+    const uint8_t* t1  = nullptr;
+    const uint16_t* t2 = nullptr;
+    int nStates        = 0;
+};
+
+static HilbertLutDev hilbertLut()
+{
+    static std::once_flag once;
+    static HilbertLutDev dev;
+    std::call_once(once,
+                   []()
+                   {
+                       const HilbertFsm f = buildHilbertFsm();
+                       void *p1 = nullptr, *p2 = nullptr;
+                       SPHX_CHECK(hipMalloc(&p1, f.t1.size()));
+                       SPHX_CHECK(hipMalloc(&p2, f.t2.size() * sizeof(uint16_t)));
+                       SPHX_CHECK(hipMemcpy(p1, f.t1.data(), f.t1.size(), hipMemcpyHostToDevice));
+                       SPHX_CHECK(hipMemcpy(p2, f.t2.data(), f.t2.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+                       dev = HilbertLutDev{static_cast<const uint8_t*>(p1), static_cast<const uint16_t*>(p2),
+                                           f.nStates};
+                   });
+    return dev;
+}
+
+int hilbertTableStates() { return hilbertLut().nStates; }
+
+__device__ __forceinline__ uint32_t octantAt(uint32_t ix, uint32_t iy, uint32_t iz, int b)
+{
+    return (((ix >> b) & 1u) << 2) | (((iy >> b) & 1u) << 1) | ((iz >> b) & 1u);
+}
+
+//! @brief the Hilbert key of integer coordinates from the tables in LDS (the top level, then ten levels of two)
+__device__ __forceinline__ KeyT hilbertKeyLut(uint32_t ix, uint32_t iy, uint32_t iz, const uint8_t* s1,
+                                              const uint16_t* s2)
+{
+    uint32_t e  = s1[octantAt(ix, iy, iz, kMaxLevel - 1)];
+    KeyT key    = e & 7u;
+    uint32_t st = e >> 3;
+#pragma unroll
+    for (int b = kMaxLevel - 2; b >= 1; b -= 2)
+    {
+        const uint32_t o2 = (octantAt(ix, iy, iz, b) << 3) | octantAt(ix, iy, iz, b - 1);
+        const uint32_t f  = s2[st * 64 + o2];
+        key               = (key << 6) | (f & 63u);
+        st                = f >> 6;
+    }
+    return key;
+}
+
+//! @brief keys of n particles: Hilbert by table, Morton (bit spreading, already cheap) directly. ext: open-dimension
+//!        extents read on the device (computeKeysDevBox; layout 0: [min x, max x, ...], 1: [mins, -maxes])
+__global__ __launch_bounds__(256) void computeKeysKernel(int64_t n, const double* __restrict__ x,
+                                                         const double* __restrict__ y, const double* __restrict__ z,
+                                                         Box box, int kind, KeyT* __restrict__ keys,
+                                                         const double* __restrict__ ext, int layout,
+                                                         const uint8_t* __restrict__ t1,
+                                                         const uint16_t* __restrict__ t2, int nStates)
+{
+    __shared__ uint16_t s2[kHMaxStates * 64];
+    __shared__ uint8_t s1[kHMaxStates * 8];
+    const bool lut = kind == kHilbert && t2 != nullptr;
+    if (lut)
+    {
+        for (int k = threadIdx.x; k < nStates * 64; k += blockDim.x)
+            s2[k] = t2[k];
+        for (int k = threadIdx.x; k < nStates * 8; k += blockDim.x)
+            s1[k] = t1[k];
+        __syncthreads();
+    }
+    if (ext)
+        for (int d = 0; d < 3; ++d)
+            if (box.bc[d] != kPeriodic)
+            {
+                const double lo = layout ? ext[d] : ext[2 * d], hi = layout ? -ext[3 + d] : ext[2 * d + 1];
+                box.lo[d]       = lo;
+                box.hi[d]       = hi <= lo ? lo + 1e-10 : hi;
+            }
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t ix = toGridInt(x[i], box.lo[0], box.ilen(0));
+    const uint32_t iy = toGridInt(y[i], box.lo[1], box.ilen(1));
+    const uint32_t iz = toGridInt(z[i], box.lo[2], box.ilen(2));
+    keys[i]           = lut ? hilbertKeyLut(ix, iy, iz, s1, s2) : sfcKey(kind, ix, iy, iz);
+}
+
+//! @brief keys by the bit-serial sfcKey (reference form; tests compare the table keys with it)
+__global__ void computeKeysSerialKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
+                                        const double* __restrict__ z, Box box, int kind, KeyT* __restrict__ keys)
 {
     int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i < n) keys[i] = particleKey(kind, x[i], y[i], z[i], box);
+}
+
+static void launchKeys(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind,
+                       KeyT* keys, const double* ext, int layout, hipStream_t s)
+{
+    const HilbertLutDev t = kind == kHilbert ? hilbertLut() : HilbertLutDev{};
+    computeKeysKernel<<<gridFor(n, 256), 256, 0, s>>>(n, x, y, z, box, kind, keys, ext, layout, t.t1, t.t2,
+                                                      t.nStates);
+    SPHX_LAUNCH_CHECK();
 }
 
 void computeKeys(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind, KeyT* keys,
                  hipStream_t s)
 {
     if (n == 0) return;
-    computeKeysKernel<<<gridFor(n, 256), 256, 0, s>>>(n, x, y, z, box, kind, keys);
+    launchKeys(n, x, y, z, box, kind, keys, nullptr, 0, s);
+}
+
+void computeKeysSerial(int64_t n, const double* x, const double* y, const double* z, const Box& box, int kind,
+                       KeyT* keys, hipStream_t s)
+{
+    if (n == 0) return;
+    computeKeysSerialKernel<<<gridFor(n, 256), 256, 0, s>>>(n, x, y, z, box, kind, keys);
     SPHX_LAUNCH_CHECK();
 }
 
 /*! keys in a box whose open dimensions come from a device reduction ([min x, max x, min y, ...], the previous step's
  *  prefetched extents): the host need not wait for the extents before the sort (parallel/domain.py sync). The
  *  extents are used as Domain.update_box sets them (hi <= lo -> lo + 1e-10), so the keys are those of the host box. */
-__global__ void computeKeysDevBoxKernel(int64_t n, const double* __restrict__ x, const double* __restrict__ y,
-                                        const double* __restrict__ z, Box box, const double* __restrict__ ext, int kind,
-                                        KeyT* __restrict__ keys, int layout)
-{
-    for (int d = 0; d < 3; ++d)
-        if (box.bc[d] != kPeriodic)
-        {
-            // layout 0: [min x, max x, min y, ...] (one rank); 1: [min x, min y, min z, -max x, -max y, -max z] (the
-            // MIN-allreduced extents of several ranks)
-            const double lo = layout ? ext[d] : ext[2 * d], hi = layout ? -ext[3 + d] : ext[2 * d + 1];
-            box.lo[d]       = lo;
-            box.hi[d]       = hi <= lo ? lo + 1e-10 : hi;
-        }
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i < n) keys[i] = particleKey(kind, x[i], y[i], z[i], box);
-}
-
 void computeKeysDevBox(int64_t n, const double* x, const double* y, const double* z, const Box& box, const double* ext,
                        int kind, KeyT* keys, hipStream_t s, int layout)
 {
     if (n == 0) return;
-    computeKeysDevBoxKernel<<<gridFor(n, 256), 256, 0, s>>>(n, x, y, z, box, ext, kind, keys, layout);
-    SPHX_LAUNCH_CHECK();
+    launchKeys(n, x, y, z, box, kind, keys, ext, layout, s);
 }
 
 // hand-written sample sort (sample_sort.hip): (key, value) ascending, keys compared on all 64 bits (the SFC keys and

@@ -462,3 +462,27 @@ def test_fused_eos_identical(gpu, monkeypatch):
         out.append({f: d[f].clone().cpu() for f in ("x", "vx", "temp", "c", "prho", "du", "ax")})
     for f in out[0]:
         assert torch.equal(out[0][f], out[1][f]), f
+
+
+def test_hilbert_table_keys(gpu):
+    """the GPU key kernel's table walk equals the bit-serial hilbertKey kernel on 4 M random points (open and
+    periodic boxes, points on the box faces included)"""
+    from sphexa_amd.ops import _lib
+
+    n = 4_000_000
+    g = torch.Generator().manual_seed(5)
+    for box in (Box.cube(-1.0, 2.0, OPEN), Box([0.0, -0.5, 0.25], [1.0, 0.7, 0.6], [PERIODIC] * 3)):
+        lo, hi = torch.tensor(box.lo, dtype=torch.float64), torch.tensor(box.hi, dtype=torch.float64)
+        p = lo + torch.rand(n, 3, generator=g, dtype=torch.float64) * (hi - lo)
+        p[:1000] = lo
+        p[1000:2000] = hi
+        x, y, z = (p[:, k].contiguous().to(gpu) for k in range(3))
+        a = torch.empty(n, dtype=torch.int64, device=gpu)
+        b = torch.empty(n, dtype=torch.int64, device=gpu)
+        s = _lib.stream()
+        _lib.hip().compute_keys(n, x.data_ptr(), y.data_ptr(), z.data_ptr(), box.to_array(), sfc.HILBERT,
+                                a.data_ptr(), s)
+        _lib.hip().compute_keys_serial(n, x.data_ptr(), y.data_ptr(), z.data_ptr(), box.to_array(), sfc.HILBERT,
+                                       b.data_ptr(), s)
+        assert torch.equal(a, b)
+    assert _lib.hip().hilbert_table_states() == 24

@@ -147,3 +147,12 @@ def test_sample_sort_pairs_and_scan(gpu):
         h.exclusive_scan_i64(x.data_ptr(), x.data_ptr(), m, t.data_ptr(), t.numel(),
                              torch.cuda.current_stream().cuda_stream)
         assert torch.equal(x.cpu(), ref)
+
+
+def test_hilbert_fsm_matches_bit_serial_keys():
+    """the 24-state machine of the Hilbert curve (sphx/hilbert_fsm.hpp, walked by the GPU key kernel two levels per
+    lookup) gives hilbertKey's key for 4 M hashed grid points and the grid corners"""
+    from sphexa_amd.ops import _lib
+
+    states, bad = _lib.cpu().hilbert_fsm_check(4_000_000, 11)
+    assert states == 24 and bad == 0
