@@ -60,6 +60,9 @@ constexpr int kFrontCap      = 512;
 #ifndef SPHX_NS_WAVES_EU
 #define SPHX_NS_WAVES_EU 5
 #endif
+#ifndef SPHX_NS_PREFETCH // candidate chunks with one chunk of look-ahead (searchGroup, step 4)
+#define SPHX_NS_PREFETCH 1
+#endif
 constexpr int kLeafCap = SPHX_NS_LEAFCAP; // LDS candidate-leaf list per wave (overflowing groups take the spill path)
 constexpr int kRing          = 16;  // hit-ring entries per lane (two list blocks)
 constexpr int kStagePairs    = 64;  // staged candidate pairs (128 candidates)
@@ -478,6 +481,9 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                 const float rt2 = act ? rt * rt : -1.0f;
                 unsigned nch    = 0;
                 nT              = 0;
+#ifdef SPHX_NS_TIMING_NOTOUCH // timing experiments only (no usable lists)
+                nLeaves = 0;
+#endif
                 for (int l = 0; l < nLeaves; ++l)
                 {
                     const int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + l));
@@ -606,7 +612,6 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                                  : [wp] "+v"(wp), [st] "=&v"(step)
                                  : [m] "s"(hm), [code] "v"(code)
                                  : "memory");
-#endif
                 }
             };
             // the four appends of a test step in one asm statement: the compiler pads every inline-asm statement
@@ -638,6 +643,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                                  : [m0] "s"(hm[0]), [m1] "s"(hm[1]), [m2] "s"(hm[2]), [m3] "s"(hm[3]),
                                    [c0] "v"(code[0]), [c1] "v"(code[1]), [c2] "v"(code[2]), [c3] "v"(code[3])
                                  : "memory");
+#endif
                 }
             };
             /* Test `count` (a multiple of 4, <= 64) staged candidates against every lane: four candidates (five
@@ -698,6 +704,54 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
 #ifdef SPHX_NS_TIMING_NOCAND // timing experiments only (no usable lists)
             nT = 0;
 #endif
+#if SPHX_NS_PREFETCH
+            /* the touched leaves' 64-source chunks as one sequence with one chunk of look-ahead: the next chunk's
+             * records are in flight while this one is staged and tested (one dependent global-load latency per chunk
+             * before; counters at Sedov -n 400: waves waited on data ~52 % of their lifetime, profiles/r6/search.md) */
+            unsigned lc  = 0;
+            int32_t nc0  = 0, nb = 0;
+            auto leafAt = [&](unsigned k)
+            {
+                const int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + k));
+                nc0              = ldConst(t.ns + nd);
+                nb               = ldConst(t.ne + nd);
+            };
+            auto skipDone = [&]()
+            {
+                while (nc0 >= nb && ++lc < nT)
+                    leafAt(lc);
+            };
+            if (nT > 0)
+            {
+                leafAt(0);
+                skipDone();
+            }
+            uint32_t px = 0, py = 0, pz = 0;
+            auto fetch = [&]()
+            {
+                if (lc < nT && nc0 + int32_t(lane) < nb)
+                {
+                    const SrcPosQ r = xq[nc0 + int32_t(lane)];
+                    px              = r.x;
+                    py              = r.y;
+                    pz              = r.z;
+                }
+            };
+            fetch();
+            while (lc < nT)
+            {
+                const int32_t c0 = nc0, b = nb;
+                const SrcPosQ rj{px, py, pz, 0.0f};
+                nc0 += 64;
+                skipDone();
+                fetch();
+                {
+                    const int32_t j = c0 + int32_t(lane);
+                    float xr = 0, yr = 0, zr = 0;
+                    bool inBox = false;
+                    if (j < b)
+                    {
+#else
             for (unsigned l = 0; l < nT; ++l)
             {
                 const int32_t nd = __builtin_amdgcn_readfirstlane(ldList<kSpill>(leaves + l));
@@ -711,6 +765,7 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
                     if (j < b)
                     {
                         const SrcPosQ rj = xq[j];
+#endif
                         xr               = float(int32_t(rj.x - gq[0])) * qf.inv[0];
                         yr               = float(int32_t(rj.y - gq[1])) * qf.inv[1];
                         zr               = float(int32_t(rj.z - gq[2])) * qf.inv[2];
