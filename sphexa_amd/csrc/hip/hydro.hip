@@ -94,6 +94,13 @@ __device__ __forceinline__ float4* waveTile(float4* blockTile)
     return blockTile + (threadIdx.x >> 6) * 64 * CoopLoader<R>::S;
 }
 
+//! descriptor word 3 of the raw buffer loads on gfx9 (32-bit data format; the num-format fields are unused by
+//! untyped loads)
+constexpr int kBufferFormatWord = 0x00020000;
+#ifndef SPHX_MOM_BUF // momentum loop gathers as 32-bit-offset buffer loads (momentumEnergyVeQ64Kernel kBuf)
+#define SPHX_MOM_BUF 1
+#endif
+
 template<class R>
 __device__ __forceinline__ CoopLoader<R> coopOf(const R* rec, float4* blockTile, int64_t self, const NbrArgs& a)
 {
@@ -938,7 +945,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 }
 
 //! @brief the split-record instance (uniform mass, SrcMomQ64 + SrcMomSide), 4 waves per SIMD as above
-template<int B = kBlock>
+//! (kBuf: neighbor gathers as raw buffer loads with 32-bit offsets, MomSplitLoaderT; the launcher takes it while the
+//! records fit 4 GiB)
+template<int B = kBlock, bool kBuf = false>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void momentumEnergyVeQ64Kernel(
     NbrArgs a, SphConsts sc, QFrame box, const SrcMomQ64* __restrict__ rec, const SrcMomSide* __restrict__ side,
     float mU, const float* __restrict__ wh, float* __restrict__ ax, float* __restrict__ ay, float* __restrict__ az,
@@ -952,7 +961,11 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void mom
     float dti  = FLT_MAX;
     float mvs, axi, ayi, azi;
     double dui;
-    const MomSplitLoader ld{coopOf(rec, tile, i, a), side, mU};
+    // (buffer descriptors: base, no stride, byte range, gfx9 raw-buffer format word; unused without kBuf)
+    const MomSplitLoaderT<kBuf> ld{
+        coopOf(rec, tile, i, a), side, mU,
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<SrcMomQ64*>(rec), 0, int(a.ntot * 64u), kBufferFormatWord),
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<SrcMomSide*>(side), 0, int(a.ntot * 8u), kBufferFormatWord)};
     momentumEnergyJLoop<false>(unsigned(i), sc, box, &pl, 0, n, ld, GradVLoader{nullptr},
                                KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui, mvs);
     if (valid)
@@ -1450,8 +1463,13 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
         withPairBlock([&](auto bc)
                       {
                           constexpr int B = decltype(bc)::value;
-                          momentumEnergyVeQ64Kernel<B><<<gridT(a, B), B, 0, s>>>(withTot(a, ntot), sc, q, main, side,
-                                                                                 mUniform, wh, ax, ay, az, du, minDt);
+                          // 32-bit buffer offsets while the 64-B records fit 4 GiB (Sedov -n 400: 4.1 GB)
+                          if (SPHX_MOM_BUF && uint64_t(ntot) * sizeof(SrcMomQ64) < (uint64_t(1) << 32))
+                              momentumEnergyVeQ64Kernel<B, true><<<gridT(a, B), B, 0, s>>>(
+                                  withTot(a, ntot), sc, q, main, side, mUniform, wh, ax, ay, az, du, minDt);
+                          else
+                              momentumEnergyVeQ64Kernel<B, false><<<gridT(a, B), B, 0, s>>>(
+                                  withTot(a, ntot), sc, q, main, side, mUniform, wh, ax, ay, az, du, minDt);
                       }, 4);
         SPHX_LAUNCH_CHECK();
         return;

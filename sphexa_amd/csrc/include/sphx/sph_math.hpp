@@ -1001,19 +1001,56 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const Coop
 
 /*! @brief loader of the split momentum records (SrcMomQ64 cooperative + SrcMomSide per lane, uniform mass): returns
  *         the assembled SrcMomQ, so momentumEnergyJLoop runs unchanged on it */
-struct MomSplitLoader
+template<bool kBuf = false>
+struct MomSplitLoaderT
 {
     CoopLoader<SrcMomQ64> main;
     const SrcMomSide* side;
     HT m;
+    // kBuf: the neighbor gathers as raw buffer loads with 32-bit byte offsets (both arrays < 4 GiB; the launcher
+    // checks): one 32-bit shift-or per load instead of the two 64-bit address instructions of a global load
+    // (v_lshlrev_b64 + v_lshl_add_u64, ~6.5 cycles each per wave on gfx950, profiles/r6/valu_cost_micro.txt) and the
+    // moves that build their register pairs: 2055 -> 1984 VALU per 8-neighbor iteration. Measured on the 16/32-B
+    // direct-gather loops (XMass, Gradh, IAD, AV) the same change was neutral or slower (profiles/r6/buffer_loads.md).
+    __amdgpu_buffer_rsrc_t rsMain, rsSide;
+
     __device__ SrcMomQ operator()(unsigned j) const { return momOfSplit(main.r[j], side[j], m); }
+
+    //! @brief chunk q of the cooperative gather (CoopLoader::issue)
+    __device__ __forceinline__ float4 issue(unsigned jr, int q) const
+    {
+        if constexpr (!kBuf) return main.issue(jr, q);
+        else
+        {
+            // chunk of this lane: (q * 64 + lane) mod 4 = lane mod 4 (64-B records, 4 chunks)
+            static_assert(sizeof(SrcMomQ64) == 64, "four 16-B chunks");
+            const unsigned off = (jr << 6) | ((threadIdx.x & 3u) << 4);
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v v = __builtin_amdgcn_raw_buffer_load_b128(rsMain, off, 0, 0);
+            return make_float4(v.x, v.y, v.z, v.w);
+        }
+    }
+    __device__ __forceinline__ SrcMomSide sideAt(unsigned j) const
+    {
+        if constexpr (!kBuf) return side[j];
+        else
+        {
+            static_assert(sizeof(SrcMomSide) == 8, "one 8-B load");
+            typedef float f2v __attribute__((ext_vector_type(2)));
+            const f2v v = __builtin_amdgcn_raw_buffer_load_b64(rsSide, j << 3, 0, 0);
+            SrcMomSide r;
+            __builtin_memcpy(&r, &v, 8);
+            return r;
+        }
+    }
 };
+using MomSplitLoader = MomSplitLoaderT<false>;
 
 /*! @brief the cooperative loop of forEachNeighbor(CoopLoader) for the split momentum records: the 64-B main records
  *         move as 4 chunks per record (16 records per wave instruction, one 64-B segment each), and each lane gathers
  *         its own 8-B side record with the same one-step-ahead schedule */
-template<int B, class F>
-__device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const MomSplitLoader& ldm, F&& f)
+template<int B, bool kBuf, class F>
+__device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const MomSplitLoaderT<kBuf>& ldm, F&& f)
 {
     using R            = SrcMomQ64;
     const auto& ld     = ldm.main;
@@ -1053,10 +1090,10 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const MomS
 #pragma unroll
     for (int q = 0; q < C; ++q)
     {
-        A[q]  = ld.issue(ld.spread(D[0], q), q);
+        A[q]  = ldm.issue(ld.spread(D[0], q), q);
         I1[q] = ld.spread(D[1], q);
     }
-    As = ldm.side[D[0]];
+    As = ldm.sideAt(D[0]);
     for (unsigned b = 0; b < nblk; ++b)
     {
         const int4 W    = pl.block(b + 1);
@@ -1080,17 +1117,17 @@ __device__ void forEachNeighbor(const PackedLane* plp, int, unsigned, const MomS
             for (int q = 0; q < C; ++q)
             {
                 I2[q] = ld.spread(jA, q);
-                Bf[q] = ld.issue(I1[q], q);
+                Bf[q] = ldm.issue(I1[q], q);
             }
-            Bs = ldm.side[D[u + 1]];
+            Bs = ldm.sideAt(D[u + 1]);
             consume(A, As, D[u]);
 #pragma unroll
             for (int q = 0; q < C; ++q)
             {
                 I1[q] = ld.spread(jB, q);
-                A[q]  = ld.issue(I2[q], q);
+                A[q]  = ldm.issue(I2[q], q);
             }
-            As = ldm.side[jA];
+            As = ldm.sideAt(jA);
             consume(Bf, Bs, D[u + 1]);
         }
         decodeChecked(W, more);
