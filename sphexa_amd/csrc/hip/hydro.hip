@@ -94,6 +94,27 @@ __device__ __forceinline__ float4* waveTile(float4* blockTile)
     return blockTile + (threadIdx.x >> 6) * 64 * CoopLoader<R>::S;
 }
 
+/*! @brief f(kf) with the pair loops' kernel function of a kernel instance: kKf = 6, the default sinc^6 fixed at
+ *         compile time (KernelFnSinc6: no per-neighbor scalar branches on the kernel choice and exponent), or 0, the
+ *         runtime form. The launchers pick the instance (withKf); each has its own registers. */
+template<int kKf, class F>
+__device__ __forceinline__ void withKernelFn(const SphConsts& sc, const float* wh, const float* whd, F&& f)
+{
+    if constexpr (kKf == 6) f(KernelFnSinc6{wh, whd, 6.0f, 0});
+    else f(KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice});
+}
+
+#ifndef SPHX_KERNEL_FIXED // 0: every pair loop on the runtime kernel function (A/B)
+#define SPHX_KERNEL_FIXED 1
+#endif
+//! f(std::integral_constant<int, kKf>) for the kernel function of these constants (withKernelFn)
+template<class F>
+inline void withKf(const SphConsts& sc, F&& f)
+{
+    if (SPHX_KERNEL_FIXED && sc.kernelChoice == 0 && sc.sincIndex == 6.0f) f(std::integral_constant<int, 6>{});
+    else f(std::integral_constant<int, 0>{});
+}
+
 //! descriptor word 3 of the raw buffer loads on gfx9 (32-bit data format; the num-format fields are unused by
 //! untyped loads)
 constexpr int kBufferFormatWord = 0x00020000;
@@ -466,7 +487,7 @@ __global__ __launch_bounds__(kBlock) void xmassKernel(NbrArgs a, SphConsts sc, B
 }
 
 //! @brief XMass on fixed-point records (see SrcPosQ): same sum as xmassJLoop (sph_math.hpp), half the gathers
-template<int B = kBlock>
+template<int B = kBlock, int kKf = 0>
 __global__ __launch_bounds__(B) void xmassQKernel(NbrArgs a, SphConsts sc, QFrame q, const float* __restrict__ h,
                                                   const SrcPosQ* __restrict__ rec, const float* __restrict__ wh,
                                                   float* __restrict__ xm, SrcXmQ* __restrict__ xmOut)
@@ -477,19 +498,21 @@ __global__ __launch_bounds__(B) void xmassQKernel(NbrArgs a, SphConsts sc, QFram
     unsigned n;
     const bool valid = targetOf<B>(a, i, pl, n);
     const auto ld    = coopOf(rec, tile, i, a);
-    const KernelFn kf{wh, nullptr, sc.sincIndex, sc.kernelChoice};
     const SrcPosQ pi = ld(unsigned(i));
     const float hi = h[i], hInv = 1.f / hi, h3Inv = hInv * hInv * hInv;
     // quarter arguments u = r / (4h): the quantum and 1/(4h) folded into one scale per dimension (KernelFn::wq)
     const float sx = q.inv[0] * 0.25f * hInv, sy = q.inv[1] * 0.25f * hInv, sz = q.inv[2] * 0.25f * hInv;
     float rho0 = 0.f;
-    forEachNeighbor<SPHX_BATCH_POS>(&pl, 0, n, ld, [&](unsigned, const SrcPosQ& pj) {
-        const float ux = float(int32_t(pi.x - pj.x)) * sx;
-        const float uy = float(int32_t(pi.y - pj.y)) * sy;
-        const float uz = float(int32_t(pi.z - pj.z)) * sz;
-        rho0 += kf.wqIn(sqrtF(ux * ux + uy * uy + uz * uz)) * pj.m;
+    withKernelFn<kKf>(sc, wh, nullptr, [&](const auto& kf) {
+        float sum = 0.f;
+        forEachNeighbor<SPHX_BATCH_POS>(&pl, 0, n, ld, [&](unsigned, const SrcPosQ& pj) {
+            const float ux = float(int32_t(pi.x - pj.x)) * sx;
+            const float uy = float(int32_t(pi.y - pj.y)) * sy;
+            const float uz = float(int32_t(pi.z - pj.z)) * sz;
+            sum += kf.wqIn(sqrtF(ux * ux + uy * uy + uz * uz)) * pj.m;
+        });
+        rho0 = pi.m + sum / kf.wqScale();
     });
-    rho0 = pi.m + rho0 / kf.wqScale();
     if (!valid) return;
     const float v = pi.m / (rho0 * float(sc.K) * h3Inv);
     xm[i]         = v;
@@ -546,7 +569,7 @@ struct EosOut
     float *prho = nullptr, *c = nullptr, *rho = nullptr, *p = nullptr;
 };
 
-template<class R, class G, int B = kBlock>
+template<class R, class G, int B = kBlock, int kKf = 0>
 __global__ __launch_bounds__(B) void veDefGradhKernel(NbrArgs a, SphConsts sc, G box,
                                                            const float* __restrict__ h, const R* __restrict__ rec,
                                                            const float* __restrict__ wh, const float* __restrict__ whd,
@@ -561,8 +584,8 @@ __global__ __launch_bounds__(B) void veDefGradhKernel(NbrArgs a, SphConsts sc, G
     unsigned n;
     const bool valid = targetOf<B>(a, i, pl, n);
     float k, g;
-    veDefGradhJLoop(unsigned(i), sc.K, box, &pl, 0, n, h[i], coopOf(rec, tile, i, a),
-                    KernelFn{wh, whd, sc.sincIndex, sc.kernelChoice}, k, g, mUniform);
+    withKernelFn<kKf>(sc, wh, whd, [&](const auto& kf)
+                 { veDefGradhJLoop(unsigned(i), sc.K, box, &pl, 0, n, h[i], coopOf(rec, tile, i, a), kf, k, g, mUniform); });
     if (!valid) return;
     kx[i]    = k;
     gradh[i] = g;
@@ -662,7 +685,7 @@ __global__ __launch_bounds__(kBlock) void iadKernel(NbrArgs a, SphConsts sc, Box
 }
 
 //! @brief IAD matrix, then divv/curlv (+ velocity gradient) in the same kernel over the same neighbor list
-template<bool kAvS, class R, class G, int B = kBlock>
+template<bool kAvS, class R, class G, int B = kBlock, int kKf = 0>
 __global__ __launch_bounds__(B) void iadDivvCurlvKernel(NbrArgs a, SphConsts sc, G box,
                                                              const float* __restrict__ h,
                                                              const float* __restrict__ kx,
@@ -681,8 +704,10 @@ __global__ __launch_bounds__(B) void iadDivvCurlvKernel(NbrArgs a, SphConsts sc,
     unsigned n;
     const bool valid = targetOf<B>(a, i, pl, n);
     float c[6], g[6], dvi, cvi, S[3];
-    iadDivvCurlvJLoop<kAvS>(unsigned(i), sc.K, box, &pl, 0, n, h[i], kx[i], coopOf(rec, tile, i, a),
-                            KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, c, dvi, cvi, g, S);
+    withKernelFn<kKf>(sc, wh, nullptr, [&](const auto& kf) {
+        iadDivvCurlvJLoop<kAvS>(unsigned(i), sc.K, box, &pl, 0, n, h[i], kx[i], coopOf(rec, tile, i, a), kf, c, dvi,
+                                cvi, g, S);
+    });
     if (valid)
     {
         for (int k = 0; k < 6; ++k)
@@ -833,7 +858,7 @@ __global__ __launch_bounds__(kBlock) void avSwitchesQKernel(NbrArgs a, SphConsts
 }
 
 //! @brief AV switches on SrcAvV records (vd = vol divv) with the IAD loop's S_i (avSwitchesVJLoop, sph_math.hpp)
-template<int B = kBlock>
+template<int B = kBlock, int kKf = 0>
 __global__ __launch_bounds__(B) void avSwitchesVKernel(NbrArgs a, SphConsts sc, QFrame q,
                                                             const float* __restrict__ h, Six cij,
                                                             const SrcAvV* __restrict__ rec,
@@ -854,9 +879,11 @@ __global__ __launch_bounds__(B) void avSwitchesVKernel(NbrArgs a, SphConsts sc, 
     float ci[6]    = {cij.p[0][i], cij.p[1][i], cij.p[2][i], cij.p[3][i], cij.p[4][i], cij.p[5][i]};
     const float4 s = avS[i - a.first];
     const float S[3] = {s.x, s.y, s.z};
-    float al = avSwitchesVJLoop(unsigned(i), sc.K, q, &pl, 0, n, h[i], ci, divv[i], S,
-                                coopOf(rec, tile, i, a), KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, dt,
-                                sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
+    float al;
+    withKernelFn<kKf>(sc, wh, nullptr, [&](const auto& kf) {
+        al = avSwitchesVJLoop(unsigned(i), sc.K, q, &pl, 0, n, h[i], ci, divv[i], S, coopOf(rec, tile, i, a), kf, dt,
+                              sc.alphamin, sc.alphamax, sc.decayConstant, alpha[i]);
+    });
     if (!valid) return;
     alphaOut[i] = al;
     if (momSide) momSide[i].alpha = al;
@@ -947,7 +974,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 //! @brief the split-record instance (uniform mass, SrcMomQ64 + SrcMomSide), 4 waves per SIMD as above
 //! (kBuf: neighbor gathers as raw buffer loads with 32-bit offsets, MomSplitLoaderT; the launcher takes it while the
 //! records fit 4 GiB)
-template<int B = kBlock, bool kBuf = false>
+template<int B = kBlock, bool kBuf = false, int kKf = 0>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void momentumEnergyVeQ64Kernel(
     NbrArgs a, SphConsts sc, QFrame box, const SrcMomQ64* __restrict__ rec, const SrcMomSide* __restrict__ side,
     float mU, const float* __restrict__ wh, float* __restrict__ ax, float* __restrict__ ay, float* __restrict__ az,
@@ -966,8 +993,10 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void mom
         coopOf(rec, tile, i, a), side, mU,
         __builtin_amdgcn_make_buffer_rsrc(const_cast<SrcMomQ64*>(rec), 0, int(a.ntot * 64u), kBufferFormatWord),
         __builtin_amdgcn_make_buffer_rsrc(const_cast<SrcMomSide*>(side), 0, int(a.ntot * 8u), kBufferFormatWord)};
-    momentumEnergyJLoop<false>(unsigned(i), sc, box, &pl, 0, n, ld, GradVLoader{nullptr},
-                               KernelFn{wh, nullptr, sc.sincIndex, sc.kernelChoice}, axi, ayi, azi, dui, mvs);
+    withKernelFn<kKf>(sc, wh, nullptr, [&](const auto& kf) {
+        momentumEnergyJLoop<false>(unsigned(i), sc, box, &pl, 0, n, ld, GradVLoader{nullptr}, kf, axi, ayi, azi, dui,
+                                   mvs);
+    });
     if (valid)
     {
         ax[i] = axi;
@@ -1270,8 +1299,11 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
         withPairBlock([&](auto bc)
                       {
                           constexpr int B = decltype(bc)::value;
-                          xmassQKernel<B><<<gridT(a, B), B, 0, s>>>(withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec,
-                                                                    wh, xm, (SrcXmQ*)xmOut);
+                          withKf(sc, [&](auto kk)
+                                 {
+                                     xmassQKernel<B, decltype(kk)::value><<<gridT(a, B), B, 0, s>>>(
+                                         withTot(a, ntot), sc, q, h, (const SrcPosQ*)rec, wh, xm, (SrcXmQ*)xmOut);
+                                 });
                       }, 0);
     }
     SPHX_LAUNCH_CHECK();
@@ -1293,9 +1325,12 @@ void veDefGradh(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
         withPairBlockL<SPHX_GRADH_BLOCK>([&](auto bc)
                       {
                           constexpr int B = decltype(bc)::value;
-                          veDefGradhKernel<SrcXmQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
-                              withTot(a, ntot), sc, q, h, (const SrcXmQ*)rec, wh, whd, kx, gradh, mUniform, vx, vy, vz,
-                              (SrcIadQ*)iadOut, eos);
+                          withKf(sc, [&](auto kk)
+                                 {
+                                     veDefGradhKernel<SrcXmQ, QFrame, B, decltype(kk)::value><<<gridT(a, B), B, 0, s>>>(
+                                         withTot(a, ntot), sc, q, h, (const SrcXmQ*)rec, wh, whd, kx, gradh, mUniform,
+                                         vx, vy, vz, (SrcIadQ*)iadOut, eos);
+                                 });
                       }, 1);
     }
     else
@@ -1385,15 +1420,19 @@ void iadDivvCurlv(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t
         withPairBlock([&](auto bc)
                       {
                           constexpr int B = decltype(bc)::value;
-                          if (avS)
-                              iadDivvCurlvKernel<true, SrcIadQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
-                                  withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv, curlv, g,
-                                  dV[0] != nullptr, (float4*)avS, (SrcAvV*)avOut, (SrcMomQ*)momOut, cs, m, prho,
-                                  momSide);
-                          else
-                              iadDivvCurlvKernel<false, SrcIadQ, QFrame, B><<<gridT(a, B), B, 0, s>>>(
-                                  withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv, curlv, g,
-                                  dV[0] != nullptr, nullptr, nullptr, (SrcMomQ*)momOut, cs, m, prho, momSide);
+                          withKf(sc, [&](auto kk)
+                          {
+                              constexpr int KK = decltype(kk)::value;
+                              if (avS)
+                                  iadDivvCurlvKernel<true, SrcIadQ, QFrame, B, KK><<<gridT(a, B), B, 0, s>>>(
+                                      withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv, curlv, g,
+                                      dV[0] != nullptr, (float4*)avS, (SrcAvV*)avOut, (SrcMomQ*)momOut, cs, m, prho,
+                                      momSide);
+                              else
+                                  iadDivvCurlvKernel<false, SrcIadQ, QFrame, B, KK><<<gridT(a, B), B, 0, s>>>(
+                                      withTot(a, ntot), sc, q, h, kx, (const SrcIadQ*)rec, wh, c, divv, curlv, g,
+                                      dV[0] != nullptr, nullptr, nullptr, (SrcMomQ*)momOut, cs, m, prho, momSide);
+                          });
                       }, 2);
     }
     SPHX_LAUNCH_CHECK();
@@ -1429,11 +1468,13 @@ void avSwitches(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t n
         withPairBlockL<SPHX_AV_BLOCK>([&](auto bc)
                       {
                           constexpr int B = decltype(bc)::value;
-                          avSwitchesVKernel<B><<<gridT(a, B), B, 0, s>>>(withTot(a, ntot), sc, q, h, cc,
-                                                                         (const SrcAvV*)rec, divv, (const float4*)avS,
-                                                                         wh, dt, alpha, alphaOut, dtDev,
-                                                                         (SrcMomQ*)momOut,
-                                                                         momSideOf(momOut, ntot, momSplit));
+                          withKf(sc, [&](auto kk)
+                                 {
+                                     avSwitchesVKernel<B, decltype(kk)::value><<<gridT(a, B), B, 0, s>>>(
+                                         withTot(a, ntot), sc, q, h, cc, (const SrcAvV*)rec, divv, (const float4*)avS,
+                                         wh, dt, alpha, alphaOut, dtDev, (SrcMomQ*)momOut,
+                                         momSideOf(momOut, ntot, momSplit));
+                                 });
                       }, 3);
     }
     else
@@ -1464,12 +1505,17 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
                       {
                           constexpr int B = decltype(bc)::value;
                           // 32-bit buffer offsets while the 64-B records fit 4 GiB (Sedov -n 400: 4.1 GB)
-                          if (SPHX_MOM_BUF && uint64_t(ntot) * sizeof(SrcMomQ64) < (uint64_t(1) << 32))
-                              momentumEnergyVeQ64Kernel<B, true><<<gridT(a, B), B, 0, s>>>(
-                                  withTot(a, ntot), sc, q, main, side, mUniform, wh, ax, ay, az, du, minDt);
-                          else
-                              momentumEnergyVeQ64Kernel<B, false><<<gridT(a, B), B, 0, s>>>(
-                                  withTot(a, ntot), sc, q, main, side, mUniform, wh, ax, ay, az, du, minDt);
+                          const bool buf = SPHX_MOM_BUF && uint64_t(ntot) * sizeof(SrcMomQ64) < (uint64_t(1) << 32);
+                          withKf(sc, [&](auto kk)
+                          {
+                              constexpr int KK = decltype(kk)::value;
+                              if (buf)
+                                  momentumEnergyVeQ64Kernel<B, true, KK><<<gridT(a, B), B, 0, s>>>(
+                                      withTot(a, ntot), sc, q, main, side, mUniform, wh, ax, ay, az, du, minDt);
+                              else
+                                  momentumEnergyVeQ64Kernel<B, false, KK><<<gridT(a, B), B, 0, s>>>(
+                                      withTot(a, ntot), sc, q, main, side, mUniform, wh, ax, ay, az, du, minDt);
+                          });
                       }, 4);
         SPHX_LAUNCH_CHECK();
         return;

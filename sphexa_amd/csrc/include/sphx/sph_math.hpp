@@ -92,14 +92,36 @@ SPHX_HD T tableLookup(const T* table, T v)
  * kernel is evaluated analytically from one sin/cos pair instead (the table's interpolation error, ~1e-8
  * relative, is below fp32 rounding). Build with -DSPHX_TABLE_KERNEL to use the tables on the GPU as well.
  */
-struct KernelFn
+template<int kN = 0>
+struct KernelFnT
 {
     const HT* wh;
     const HT* whd;
     HT n;
     int choice;
+    // kN = 6: the default kernel (choice 0, sinc^6) fixed at compile time, so the pair loops carry no per-neighbor
+    // scalar branches on choice and n (KernelFnSinc6, selected per launch by withKernelFn); kN = 0: runtime n, choice
 
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(SPHX_TABLE_KERNEL)
+    //! s^k for a compile-time k as powN forms it (the same products: bit-identical)
+    template<int k>
+    SPHX_HD static HT powC(HT s)
+    {
+        static_assert(k == 5 || k == 6, "the sinc^6 kernel and its derivative");
+        if constexpr (k == 6)
+        {
+            HT s3 = s * s * s;
+            return s3 * s3;
+        }
+        else
+        {
+            HT p = s * s;
+            p *= p;
+            return s * p;
+        }
+    }
+    SPHX_HD bool generic() const { return kN == 0 && choice != 0; }
+    SPHX_HD HT nVal() const { return kN ? HT(kN) : n; }
     //! sinc(x) and d sinc/dv for x = (pi/2) v
     SPHX_HD void sinc(HT v, HT& s, HT& ds) const
     {
@@ -162,15 +184,17 @@ struct KernelFn
     {
         // (in double: once per target, and the fp32 exp2 would add its ulp to every sum)
         constexpr double log2TwoPi = 2.651496129472318798043279295;
-        return choice == 0 ? HT(exp2(double(n) * log2TwoPi)) : HT(1);
+        return (kN || choice == 0) ? HT(exp2(double(nVal()) * log2TwoPi)) : HT(1);
     }
     SPHX_HD HT wq(HT u) const
     {
-        if (choice != 0) return w(HT(4) * u);
+        if (generic()) return w(HT(4) * u);
         constexpr HT twoPi = HT(6.283185307179586);
         HT sq = __builtin_amdgcn_sinf(u) * rcpF(u);
         sq    = u > HT(0) ? sq : twoPi; // (r = 0: sinc = 1)
-        const HT r = powN(sq, n);
+        HT r;
+        if constexpr (kN != 0) r = powC<kN>(sq);
+        else r = powN(sq, n);
         return u < HT(0.5) ? r : HT(0);
     }
     /*! @brief wq for a neighbor of the list of the target whose h defines u: the search's exact fp64 test put it
@@ -178,16 +202,17 @@ struct KernelFn
      *         ~1e-7 and its n-th power below 1e-40, which is the kernel value there. (u = 0 keeps sinc = 1.) */
     SPHX_HD HT wqIn(HT u) const
     {
-        if (choice != 0) return w(HT(4) * u);
+        if (generic()) return w(HT(4) * u);
         constexpr HT twoPi = HT(6.283185307179586);
         HT sq = __builtin_amdgcn_sinf(u) * rcpF(u);
         sq    = u > HT(0) ? sq : twoPi;
-        return powN(sq, n);
+        if constexpr (kN != 0) return powC<kN>(sq);
+        else return powN(sq, n);
     }
     //! @brief S w(4u) and S v dW/dv at v = 4u for a list neighbor (see wq, wqIn: no support test)
     SPHX_HD void wdq(HT u, HT& wS, HT& vdwS) const
     {
-        if (choice != 0)
+        if (generic())
         {
             wS   = w(HT(4) * u);
             vdwS = HT(4) * u * dw(HT(4) * u);
@@ -197,9 +222,11 @@ struct KernelFn
         HT sq = __builtin_amdgcn_sinf(u) * rcpF(u);
         sq    = u > HT(0) ? sq : twoPi;
         const HT cs = __builtin_amdgcn_cosf(u);
-        const HT p  = powN(sq, n - HT(1));
+        HT p;
+        if constexpr (kN != 0) p = powC<kN - 1>(sq);
+        else p = powN(sq, n - HT(1));
         wS   = p * sq;
-        vdwS = n * p * (twoPi * cs - sq);
+        vdwS = nVal() * p * (twoPi * cs - sq);
     }
 #else
     SPHX_HD HT w(HT v) const { return tableLookup(wh, v); }
@@ -215,6 +242,8 @@ struct KernelFn
     }
 #endif
 };
+using KernelFn      = KernelFnT<0>;
+using KernelFnSinc6 = KernelFnT<6>;
 
 //! @brief smoothing length update targeting ng0 neighbors (reference kernels.hpp updateH)
 template<class T>
@@ -1152,9 +1181,9 @@ SPHX_HD void reduceAcrossN(const Ld&, HT*, int)
 }
 
 //! @brief xm_i = m_i / rho0_i, rho0_i = K h^-3 sum_j W_ij m_j including self (reference xmass_kern.hpp)
-template<class Idx, class Ld>
+template<class Idx, class Ld, class KF>
 SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                      const Ld& ld, const KernelFn& kf)
+                      const Ld& ld, const KF& kf)
 {
     SrcPos pi = ld(i);
     HT hInv = HT(1) / hi, h3Inv = hInv * hInv * hInv, hq = HT(0.25) * hInv;
@@ -1170,9 +1199,9 @@ SPHX_HD HT xmassJLoop(unsigned i, double K, const Box& box, const Idx* nbr, int 
 }
 
 //! @brief kx (VE normalization) and grad-h term (reference ve_def_gradh_kern.hpp)
-template<class G, class Idx, class Ld>
+template<class G, class Idx, class Ld, class KF>
 SPHX_HD void veDefGradhJLoop(unsigned i, double K, const G& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                             const Ld& ld, const KernelFn& kf, HT& kxOut, HT& gradhOut,
+                             const Ld& ld, const KF& kf, HT& kxOut, HT& gradhOut,
                              HT mUniform = HT(0))
 {
     const auto pi = ld(i);
@@ -1311,9 +1340,9 @@ SPHX_HD void divvCurlvJLoop(unsigned i, double K, const Box& box, const Idx* nbr
  * M[a][b] = sum_j v_ji[a] xm_j W_ij r_ij[b], so M is accumulated together with tau and the neighbor data is read
  * once. Mathematically identical; rounding differs from the two-pass form at the 1e-7 relative level.
  */
-template<bool kAvS = false, class G, class Idx, class Ld>
+template<bool kAvS = false, class G, class Idx, class Ld, class KF>
 SPHX_HD void iadDivvCurlvJLoop(unsigned i, double K, const G& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                               HT kxi, const Ld& ld, const KernelFn& kf, HT c[6], HT& divvOut, HT& curlvOut, HT* dV,
+                               HT kxi, const Ld& ld, const KF& kf, HT c[6], HT& divvOut, HT& curlvOut, HT* dV,
                                HT* avS = nullptr)
 {
     HT tau[6]  = {0, 0, 0, 0, 0, 0};
@@ -1484,9 +1513,9 @@ __device__ __forceinline__ SrcAvV coopUnpack<SrcAvV>(const float4* o)
 }
 #endif
 
-template<class G, class Idx, class Ld>
+template<class G, class Idx, class Ld, class KF>
 SPHX_HD HT avSwitchesVJLoop(unsigned i, double K, const G& box, const Idx* nbr, int stride, unsigned nc, HT hi,
-                            const HT ci6[6], HT divvi, const HT Si[3], const Ld& ld, const KernelFn& kf, double dt,
+                            const HT ci6[6], HT divvi, const HT Si[3], const Ld& ld, const KF& kf, double dt,
                             HT alphamin, HT alphamax, HT decayConstant, HT alpha_i)
 {
     const auto pi = ld(i);
@@ -1568,9 +1597,9 @@ SPHX_HD HT avRvCorrection(HT rx, HT ry, HT rz, HT eta_ab, HT eta_crit, const HT 
 }
 
 //! @brief VE momentum and energy equations (reference hydro_ve/momentum_energy_kern.hpp)
-template<bool avClean, class G, class Idx, class Ld, class LdG>
+template<bool avClean, class G, class Idx, class Ld, class LdG, class KF>
 SPHX_HD void momentumEnergyJLoop(unsigned i, const SphConsts& sc, const G& box, const Idx* nbr, int stride,
-                                 unsigned nc, const Ld& ld, const LdG& ldg, const KernelFn& kf, HT& axOut, HT& ayOut,
+                                 unsigned nc, const Ld& ld, const LdG& ldg, const KF& kf, HT& axOut, HT& ayOut,
                                  HT& azOut, double& duOut, HT& maxvsignalOut)
 {
     const auto pi = ld(i);
