@@ -66,15 +66,19 @@ def decode_keys(keys: torch.Tensor, box: Box | None = None, kind: int = HILBERT)
     return ix, iy, iz
 
 
-def sort_keys(keys: torch.Tensor):
-    """returns (sorted keys, permutation int32) with sorted[i] = keys[perm[i]]"""
+def sort_keys(keys: torch.Tensor, out: torch.Tensor | None = None):
+    """returns (sorted keys, permutation int32) with sorted[i] = keys[perm[i]]. ``out`` (GPU): the sorted keys' storage
+    (n elements, not overlapping ``keys``), e.g. the particle data's key field, which then needs no copy"""
     n = keys.numel()
     perm = torch.empty(n, dtype=torch.int32, device=keys.device)
     if n == 0:
         return keys.clone(), perm
     if keys.is_cuda:
         h = _lib.hip()
-        out = torch.empty_like(keys)
+        if out is None:
+            out = torch.empty_like(keys)
+        elif out.numel() != n or out.dtype != keys.dtype or not out.is_contiguous():
+            raise ValueError("sort_keys: out must be a contiguous tensor of the keys' size and type")
         tmp = torch.empty(h.sort_temp_bytes(n), dtype=torch.uint8, device=keys.device)
         h.sort_keys(n, keys.data_ptr(), out.data_ptr(), perm.data_ptr(), tmp.data_ptr(), tmp.numel(), _stream())
         return out, perm
