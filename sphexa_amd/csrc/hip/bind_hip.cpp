@@ -389,6 +389,9 @@ PYBIND11_MODULE(_sphx_hip, m)
     m.def("staged_mask", []() { return stagedMask(); });
     m.def("set_list_masks", [](bool on) { setListMasks(on); },
           "store the per-slot staged-source masks in the list tables even without a staged loop (tests)");
+    m.def("set_pair_paths", [](bool kernelFixed, bool momBuf) { setPairPaths(kernelFixed, momBuf); },
+          "pair-loop instances: the compile-time sinc^6 kernel function and the momentum loop's 32-bit buffer gathers "
+          "(defaults on; tests compare them with the generic instances)", py::arg("kernel_fixed"), py::arg("mom_buf"));
     m.def("set_pair_block", [](int block) { setPairBlock(block); },
           "threads per block of the fixed-point pair loops: 512 (8 target groups sharing a CU's L1) or 256");
     m.def("eos_ve", [](int64_t first, int64_t last, const ConstArr& c, Ptr temp, Ptr mm, Ptr kx, Ptr xm, Ptr gradh,

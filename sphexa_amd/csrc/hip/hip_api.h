@@ -183,6 +183,8 @@ void findNeighbors(int64_t first, int64_t last, const double* x, const double* y
                    int testFrontCap, const float* m, int64_t ntot, void* rec, hipStream_t s, const SplitPredict& sp = SplitPredict{});
 //! threads per block of the production pair loops (256 or 512, hydro.hip withPairBlock)
 void setPairBlock(int block);
+//! pair-loop instances: compile-time sinc^6 kernel function, 32-bit buffer gathers of the momentum loop (both default on)
+void setPairPaths(bool kernelFixed, bool momBuf);
 //! pair loops that run LDS-staged (hydro.hip g_staged: bit 0 XMass, 1 Gradh, 2 IAD, 3 AV, 4 momentum)
 void setStaged(unsigned mask);
 unsigned stagedMask();

@@ -107,20 +107,28 @@ __device__ __forceinline__ void withKernelFn(const SphConsts& sc, const float* w
 #ifndef SPHX_KERNEL_FIXED // 0: every pair loop on the runtime kernel function (A/B)
 #define SPHX_KERNEL_FIXED 1
 #endif
+#ifndef SPHX_MOM_BUF // momentum loop gathers as 32-bit-offset buffer loads (momentumEnergyVeQ64Kernel kBuf)
+#define SPHX_MOM_BUF 1
+#endif
+// the instances the launchers may pick (setPairPaths: tests compare them, they must agree bit for bit)
+static bool g_kernelFixed = SPHX_KERNEL_FIXED, g_momBuf = SPHX_MOM_BUF;
+void setPairPaths(bool kernelFixed, bool momBuf)
+{
+    g_kernelFixed = kernelFixed;
+    g_momBuf      = momBuf;
+}
+
 //! f(std::integral_constant<int, kKf>) for the kernel function of these constants (withKernelFn)
 template<class F>
 inline void withKf(const SphConsts& sc, F&& f)
 {
-    if (SPHX_KERNEL_FIXED && sc.kernelChoice == 0 && sc.sincIndex == 6.0f) f(std::integral_constant<int, 6>{});
+    if (g_kernelFixed && sc.kernelChoice == 0 && sc.sincIndex == 6.0f) f(std::integral_constant<int, 6>{});
     else f(std::integral_constant<int, 0>{});
 }
 
 //! descriptor word 3 of the raw buffer loads on gfx9 (32-bit data format; the num-format fields are unused by
 //! untyped loads)
 constexpr int kBufferFormatWord = 0x00020000;
-#ifndef SPHX_MOM_BUF // momentum loop gathers as 32-bit-offset buffer loads (momentumEnergyVeQ64Kernel kBuf)
-#define SPHX_MOM_BUF 1
-#endif
 
 template<class R>
 __device__ __forceinline__ CoopLoader<R> coopOf(const R* rec, float4* blockTile, int64_t self, const NbrArgs& a)
@@ -1505,7 +1513,7 @@ void momentumEnergyVe(const NbrArgs& a, const SphConsts& sc, const Box& box, int
                       {
                           constexpr int B = decltype(bc)::value;
                           // 32-bit buffer offsets while the 64-B records fit 4 GiB (Sedov -n 400: 4.1 GB)
-                          const bool buf = SPHX_MOM_BUF && uint64_t(ntot) * sizeof(SrcMomQ64) < (uint64_t(1) << 32);
+                          const bool buf = g_momBuf && uint64_t(ntot) * sizeof(SrcMomQ64) < (uint64_t(1) << 32);
                           withKf(sc, [&](auto kk)
                           {
                               constexpr int KK = decltype(kk)::value;

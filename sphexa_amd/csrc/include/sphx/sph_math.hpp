@@ -103,7 +103,7 @@ struct KernelFnT
     // scalar branches on choice and n (KernelFnSinc6, selected per launch by withKernelFn); kN = 0: runtime n, choice
 
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(SPHX_TABLE_KERNEL)
-    //! s^k for a compile-time k as powN forms it (the same products: bit-identical)
+    //! s^k for a compile-time k as powN forms it (the same products; inlined, the surrounding FMA contraction may differ)
     template<int k>
     SPHX_HD static HT powC(HT s)
     {

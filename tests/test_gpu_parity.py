@@ -464,6 +464,40 @@ def test_fused_eos_identical(gpu, monkeypatch):
         assert torch.equal(out[0][f], out[1][f]), f
 
 
+def test_pair_loop_instances_agree(gpu):
+    """the pair loops' specialized instances equal the generic ones after three Sedov steps: the momentum gathers as
+    32-bit buffer loads (MomSplitLoaderT) bit for bit; the sinc^6 kernel function fixed at compile time (hydro.hip
+    withKf) to rounding (the same products, but the compiler contracts the inlined constant forms into FMAs
+    differently: 1-ulp differences in kx and the IAD coefficients at step 1)"""
+    from sphexa_amd.ops import _lib
+
+    fields = ("x", "vx", "temp", "c", "prho", "du", "ax", "alpha", "h")
+
+    def run(kernel_fixed, mom_buf):
+        _lib.hip().set_pair_paths(kernel_fixed=kernel_fixed, mom_buf=mom_buf)
+        d = P.ParticlesData(gpu)
+        prop = HydroVeProp(None, 0)
+        prop.activate_fields(d)
+        box = SedovGrid().init(0, 1, 20, d)
+        dom = Domain(Comm(), box)
+        prop.sync(dom, d)
+        for _ in range(3):
+            prop.step(dom, d)
+            d.iteration += 1
+        return {f: d[f].clone().cpu().double() for f in fields}
+
+    try:
+        generic = run(False, False)
+        buf = run(False, True)
+        fixed = run(True, True)
+    finally:
+        _lib.hip().set_pair_paths(kernel_fixed=True, mom_buf=True)
+    for f in fields:
+        assert torch.equal(buf[f], generic[f]), f
+        scale = float(generic[f].abs().max())
+        assert float((fixed[f] - generic[f]).abs().max()) <= 1e-5 * scale, f
+
+
 def test_hilbert_table_keys(gpu):
     """the GPU key kernel's table walk equals the bit-serial hilbertKey kernel on 4 M random points (open and
     periodic boxes, points on the box faces included)"""
