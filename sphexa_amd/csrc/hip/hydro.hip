@@ -149,13 +149,19 @@ inline unsigned gridT(const NbrArgs& a, int block = kBlock) { return gridFor(a.l
  * target groups per block share their sources in the CU's L1 (Sedov -n 400 121.2 -> 118.5 ms/step); 256 where the
  * loops share the GPU with the gravity streams (Evrard -n 200: 21.3 ms at 256, 22.4 at 512). */
 static int g_pairBlock = kBlock;
-// the AV loop (92 VGPRs, 5 waves per SIMD) in blocks of 10 waves: two per CU keep its occupancy (Sedov -n 200 AV
-// 1.814 -> 1.705 ms); Gradh measured 1.119 (512) / 1.171 (448) / 1.354 ms (896), XMass slower at 1024
+// the AV loop (89-92 VGPRs, 5 waves per SIMD) in blocks of 10 waves: two per CU keep its occupancy (Sedov -n 400 AV
+// 13.34 ms at 640, 14.12 at 512). XMass and Gradh (56 / 62 VGPRs with the compile-time kernel function: 8 waves per
+// SIMD) in blocks of 16 waves, 16 consecutive target groups per block: Sedov -n 400 XMass 7.95 -> 7.52 ms, Gradh 8.66
+// -> 8.31 ms against 512 threads (768 and 896 in between; profiles/r6/pairloop_occupancy.md). IAD and momentum (4 waves
+// per SIMD) stay at 512.
 #ifndef SPHX_AV_BLOCK
 #define SPHX_AV_BLOCK 640
 #endif
 #ifndef SPHX_GRADH_BLOCK
-#define SPHX_GRADH_BLOCK 512
+#define SPHX_GRADH_BLOCK 1024
+#endif
+#ifndef SPHX_XMASS_BLOCK
+#define SPHX_XMASS_BLOCK 1024
 #endif
 // loops that take the larger block (bit 0 XMass, 1 Gradh, 2 IAD, 3 AV, 4 momentum); experiment knob SPHX_PAIR_MASK
 static const unsigned kPairMask = []
@@ -1304,7 +1310,7 @@ void xmass(const NbrArgs& a, const SphConsts& sc, const Box& box, int64_t ntot, 
             SPHX_LAUNCH_CHECK();
             return;
         }
-        withPairBlock([&](auto bc)
+        withPairBlockL<SPHX_XMASS_BLOCK>([&](auto bc)
                       {
                           constexpr int B = decltype(bc)::value;
                           withKf(sc, [&](auto kk)
