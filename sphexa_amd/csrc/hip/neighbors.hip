@@ -707,7 +707,8 @@ __device__ __forceinline__ bool searchGroup(int64_t g, int64_t first, int64_t la
 #if SPHX_NS_PREFETCH
             /* the touched leaves' 64-source chunks as one sequence with one chunk of look-ahead: the next chunk's
              * records are in flight while this one is staged and tested (one dependent global-load latency per chunk
-             * before; counters at Sedov -n 400: waves waited on data ~52 % of their lifetime, profiles/r6/search.md) */
+             * before; counters at Sedov -n 400: waves waited on data ~52 % of their lifetime,
+             * profiles/r6/search/README.md) */
             unsigned lc  = 0;
             int32_t nc0  = 0, nb = 0;
             auto leafAt = [&](unsigned k)
